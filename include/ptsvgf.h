@@ -1,0 +1,136 @@
+/* ptsvgf.h — the drop-in boundary: a C ABI into HIP that replaces the
+ * reference's OpenGL plumbing API (layer L2) for the path-tracing + SVGF hot
+ * path. A main.cpp-shaped host issues the SAME call sequence it issues against
+ * the reference classes; each entry point names the reference interface it
+ * replaces (file:line under the reference tree):
+ *
+ *   getShaderProgram(frag, vert)            Utils/shader.h:21-67    -> pt_program_create
+ *   getTextureRGB32F(w, h)                  Utils/help_func.h:22-32 -> pt_texture2d_create
+ *   glTexImage2D(... RGB32F ...)            main.cpp:173-180        -> pt_texture2d_upload
+ *   glTexBuffer(GL_TEXTURE_BUFFER, RGB32F)  main.cpp:136-168        -> pt_texbuffer_create
+ *   glTexStorage3D / glTexSubImage3D        main.cpp:184-205,
+ *                                           Utils/help_func.h:4-20  -> pt_texarray_create / _upload_layer
+ *   RenderPass{program,colorAttachments,width,height}
+ *                                           Utils/render_pass.h:82-90 -> pt_pass_create / _add_color_attachment
+ *   RenderPass::bindData(finalPass)         render_pass.h:92-119    -> pt_pass_bind
+ *   RenderPass::draw()                      render_pass.h:120-140   -> pt_pass_draw
+ *   RenderPass::reset_texture_slot()        render_pass.h:141-143   -> pt_pass_reset_texture_slot
+ *   RenderPass::set_texture_uniform(t,tex,n) render_pass.h:144-150  -> pt_pass_set_texture
+ *   RenderPass::set_uniform_{mat4,float,int,uint,bool,vec3}
+ *                                           render_pass.h:152-180   -> pt_pass_set_uniform_*
+ *   Rasterize_RenderPass::bindData(verts)   render_pass.h:19-62     -> pt_raster_pass_bind
+ *   Rasterize_RenderPass::draw()            render_pass.h:64-79     -> pt_pass_draw
+ *   glUniform*(glGetUniformLocation(...))   main.cpp:223-226,243-247,436-441 -> pt_pass_set_uniform_* (same)
+ *
+ * Conventions:
+ *  - handles are opaque uint32 owned by the library (0 is never a valid handle);
+ *  - every function returns int status: PT_OK (0) or a negative PT_ERR_*;
+ *    pt_last_error() gives the message. Where the reference calls exit(-1)
+ *    (missing shader file, shader.h:8-12) this returns PT_ERR_FILE instead;
+ *  - an unknown uniform name is silently ignored (GL location -1 semantics);
+ *  - textures are RGBA32F, row-major, row 0 = GL window row 0 (bottom);
+ *  - mat4 arguments are 16 floats column-major (glm::value_ptr order);
+ *  - texture targets / formats keep their GL enum values so call sites port 1:1;
+ *  - draws are asynchronous on the library stream (GL orders passes the same
+ *    way); pt_sync() / pt_texture_readback() synchronise.
+ *
+ * MI355X extensions (no GL counterpart): pt_init (device + rank), pt_set_stream
+ * (run on the caller's HIP stream, e.g. torch's), pt_texture2d_wrap (adopt
+ * external device memory), pt_set_band (screen-band sharding across GPUs:
+ * textures hold rows [row0, row0+rows) of the global frame).
+ */
+#ifndef PTSVGF_H
+#define PTSVGF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_OK 0
+#define PT_ERR_INVALID_HANDLE (-1)
+#define PT_ERR_UNKNOWN_PROGRAM (-2)
+#define PT_ERR_FILE (-3)
+#define PT_ERR_MISSING_TEXTURE (-4)
+#define PT_ERR_HIP (-5)
+#define PT_ERR_ARG (-6)
+#define PT_ERR_FORMAT (-7)
+#define PT_ERR_NO_DEVICE (-8)
+#define PT_ERR_STATE (-9)
+
+/* GL enum values (texture targets and formats) */
+#define PT_TEXTURE_2D 0x0DE1
+#define PT_TEXTURE_BUFFER 0x8C2A
+#define PT_TEXTURE_2D_ARRAY 0x8C1A
+#define PT_RGB32F 0x8815
+#define PT_RGBA32F 0x8814
+#define PT_RGB 0x1907
+#define PT_RGBA 0x1908
+
+/* ---- library / device ---------------------------------------------------- */
+int pt_init(int device);                    /* select HIP device, create stream */
+int pt_shutdown(void);                      /* free every handle and the stream */
+int pt_set_stream(void* hip_stream);        /* NULL = library's own stream */
+int pt_sync(void);                          /* wait for all queued draws */
+const char* pt_last_error(void);
+int pt_version(void);
+
+/* Band sharding: this rank renders global rows [y_begin, y_end) of a
+ * frame_w x frame_h frame; every 2-D texture of exactly that size created
+ * afterwards stores global rows [row0, row0 + rows) (band + ghost rows).
+ * Default (never called): one band covering the frame. */
+int pt_set_band(int frame_w, int frame_h, int y_begin, int y_end, int row0, int rows);
+/* Record HIP events around every draw so pt_pass_last_ms can report it. */
+int pt_set_profiling(int on);
+
+/* ---- programs (getShaderProgram) ------------------------------------------- */
+/* The fragment shader's basename selects the HIP kernel: path_tracing.frag,
+ * svgf_reproject.frag, svgf_variance.frag, svgf_Atrous.frag, svgf_modulate.frag,
+ * bilt.frag, save_frame_data.frag, output_pass.frag, taa.frag (full-screen,
+ * vert.vert) and rasterize_frag.frag (rasterize_vert.vert). The shader files are
+ * not read (the kernels are compiled in); an unknown basename or a mismatched
+ * vertex stage returns PT_ERR_UNKNOWN_PROGRAM where the reference exit(-1)s. */
+int pt_program_create(const char* frag_path, const char* vert_path, uint32_t* out_program);
+
+/* ---- textures -------------------------------------------------------------- */
+int pt_texture2d_create(int width, int height, uint32_t* out_tex);                 /* RGBA32F, zeroed */
+int pt_texture2d_upload(uint32_t tex, int width, int height, uint32_t fmt,         /* PT_RGB32F | PT_RGBA32F */
+                        const float* host_data);
+int pt_texture2d_wrap(void* device_ptr, int width, int height, uint32_t* out_tex); /* RGBA32F, not owned */
+int pt_texbuffer_create(const void* host_data, size_t bytes, uint32_t fmt, uint32_t* out_tex); /* RGB32F */
+int pt_texarray_create(int width, int height, int layers, uint32_t* out_tex);     /* RGBA8 2-D array */
+int pt_texarray_upload_layer(uint32_t tex, int layer, int width, int height, int channels,
+                             const uint8_t* host_data);
+int pt_texture_readback(uint32_t tex, float* host_out, size_t bytes);             /* syncs */
+int pt_texture_upload_rgba(uint32_t tex, const float* host_rgba, size_t bytes);   /* raw RGBA32F rows */
+int pt_texture_device_ptr(uint32_t tex, void** out_ptr);
+int pt_texture_info(uint32_t tex, int* width, int* height, int* row0);
+int pt_texture_destroy(uint32_t tex);
+
+/* ---- passes (RenderPass / Rasterize_RenderPass) ---------------------------- */
+int pt_pass_create(uint32_t program, int width, int height, uint32_t* out_pass);
+int pt_pass_add_color_attachment(uint32_t pass, uint32_t tex);
+int pt_pass_bind(uint32_t pass, int final_pass);
+int pt_raster_pass_bind(uint32_t pass, const float* vertices, size_t n_floats);   /* pos3+nrm3 per vertex */
+int pt_pass_reset_texture_slot(uint32_t pass);
+int pt_pass_set_texture(uint32_t pass, uint32_t target, uint32_t tex, const char* name);
+int pt_pass_set_uniform_mat4(uint32_t pass, const char* name, const float* m16);
+int pt_pass_set_uniform_float(uint32_t pass, const char* name, float v);
+int pt_pass_set_uniform_int(uint32_t pass, const char* name, int v);
+int pt_pass_set_uniform_uint(uint32_t pass, const char* name, uint32_t v);
+int pt_pass_set_uniform_bool(uint32_t pass, const char* name, int v);
+int pt_pass_set_uniform_vec3(uint32_t pass, const char* name, const float* v3);
+/* Rows this pass computes (global coords); default = the band. The G-buffer
+ * pass uses it to compute ghost rows locally for multi-GPU halos. */
+int pt_pass_set_rows(uint32_t pass, int y_begin, int y_end);
+int pt_pass_draw(uint32_t pass);
+/* Time the last draw of this pass (ms, HIP events on the library stream; syncs). */
+int pt_pass_last_ms(uint32_t pass, float* ms);
+int pt_pass_destroy(uint32_t pass);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,632 @@
+// oracle_pt.cpp — TEST INFRASTRUCTURE ONLY (see oracle.h header).
+// Statement-by-statement CPU restatement of shaders/path_tracing.frag (live
+// code: 127-515, 520-588, 620-669, 673-687, 699-874, 884-968, 1056-1128).
+// Deliberately naive: per-texel decode of the encoded buffers, the reference's
+// 256-entry stack, no pruning, closest-hit shadow rays — it IS the reference
+// algorithm, so it is also the CPU baseline ("port") for bench.py.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "../path-tracing-svgf_amd/csrc/glsl_builtins.h"
+#include "oracle.h"
+
+using namespace glsl;
+
+namespace {
+
+const float PI = 3.1415926f;      // #define PI 3.1415926 (:52)
+const float INF = 114514.0f;      // #define INF 114514.0 (:53)
+const float epsilon = 1e-6f;      // (:54)
+
+struct Material {
+  v3 emissive, baseColor;
+  float subsurface, metallic, specular, specularTint, roughness, anisotropic, sheen, sheenTint, clearcoat,
+      clearcoatGloss, IOR, transmission;
+};
+struct Triangle {
+  v3 p1, p2, p3, n1, n2, n3;
+  float uv1[2], uv2[2], uv3[2];
+  int objIndex;
+};
+struct BVHNode {
+  int left, right, n, index;
+  v3 AA, BB;
+};
+struct Ray {
+  v3 startPoint, direction;
+};
+struct HitResult {
+  bool isHit, isInside;
+  float distance;
+  v3 hitPoint, normal, viewDir;
+  Material material;
+  int objIndex;
+};
+
+// V[8*32] Sobol direction numbers (:463-472)
+const uint32_t SOBOL_V[8 * 32] = {
+    2147483648u, 1073741824u, 536870912u, 268435456u, 134217728u, 67108864u, 33554432u, 16777216u, 8388608u, 4194304u, 2097152u, 1048576u, 524288u, 262144u, 131072u, 65536u, 32768u, 16384u, 8192u, 4096u, 2048u, 1024u, 512u, 256u, 128u, 64u, 32u, 16u, 8u, 4u, 2u, 1u,
+    2147483648u, 3221225472u, 2684354560u, 4026531840u, 2281701376u, 3422552064u, 2852126720u, 4278190080u, 2155872256u, 3233808384u, 2694840320u, 4042260480u, 2290614272u, 3435921408u, 2863267840u, 4294901760u, 2147516416u, 3221274624u, 2684395520u, 4026593280u, 2281736192u, 3422604288u, 2852170240u, 4278255360u, 2155905152u, 3233857728u, 2694881440u, 4042322160u, 2290649224u, 3435973836u, 2863311530u, 4294967295u,
+    2147483648u, 3221225472u, 1610612736u, 2415919104u, 3892314112u, 1543503872u, 2382364672u, 3305111552u, 1753219072u, 2629828608u, 3999268864u, 1435500544u, 2154299392u, 3231449088u, 1626210304u, 2421489664u, 3900735488u, 1556135936u, 2388680704u, 3314585600u, 1751705600u, 2627492864u, 4008611328u, 1431684352u, 2147543168u, 3221249216u, 1610649184u, 2415969680u, 3892340840u, 1543543964u, 2382425838u, 3305133397u,
+    2147483648u, 3221225472u, 536870912u, 1342177280u, 4160749568u, 1946157056u, 2717908992u, 2466250752u, 3632267264u, 624951296u, 1507852288u, 3872391168u, 2013790208u, 3020685312u, 2181169152u, 3271884800u, 546275328u, 1363623936u, 4226424832u, 1977167872u, 2693105664u, 2437829632u, 3689389568u, 635137280u, 1484783744u, 3846176960u, 2044723232u, 3067084880u, 2148008184u, 3222012020u, 537002146u, 1342505107u,
+    2147483648u, 1073741824u, 536870912u, 2952790016u, 4160749568u, 3690987520u, 2046820352u, 2634022912u, 1518338048u, 801112064u, 2707423232u, 4038066176u, 3666345984u, 1875116032u, 2170683392u, 1085997056u, 579305472u, 3016343552u, 4217741312u, 3719483392u, 2013407232u, 2617981952u, 1510979072u, 755882752u, 2726789248u, 4090085440u, 3680870432u, 1840435376u, 2147625208u, 1074478300u, 537900666u, 2953698205u,
+    2147483648u, 1073741824u, 1610612736u, 805306368u, 2818572288u, 335544320u, 2113929216u, 3472883712u, 2290089984u, 3829399552u, 3059744768u, 1127219200u, 3089629184u, 4199809024u, 3567124480u, 1891565568u, 394297344u, 3988799488u, 920674304u, 4193267712u, 2950604800u, 3977188352u, 3250028032u, 129093376u, 2231568512u, 2963678272u, 4281226848u, 432124720u, 803643432u, 1633613396u, 2672665246u, 3170194367u,
+    2147483648u, 3221225472u, 2684354560u, 3489660928u, 1476395008u, 2483027968u, 1040187392u, 3808428032u, 3196059648u, 599785472u, 505413632u, 4077912064u, 1182269440u, 1736704000u, 2017853440u, 2221342720u, 3329785856u, 2810494976u, 3628507136u, 1416089600u, 2658719744u, 864310272u, 3863387648u, 3076993792u, 553150080u, 272922560u, 4167467040u, 1148698640u, 1719673080u, 2009075780u, 2149644390u, 3222291575u,
+    2147483648u, 1073741824u, 2684354560u, 1342177280u, 2281701376u, 1946157056u, 436207616u, 2566914048u, 2625634304u, 3208642560u, 2720006144u, 2098200576u, 111673344u, 2354315264u, 3464626176u, 4027383808u, 2886631424u, 3770826752u, 1691164672u, 3357462528u, 1993345024u, 3752330240u, 873073152u, 2870150400u, 1700563072u, 87021376u, 1097028000u, 1222351248u, 1560027592u, 2977959924u, 23268898u, 437609937u};
+
+}  // namespace
+
+struct orc_scene {
+  std::vector<float> tri, node, light, hdr, cache;
+  int ntris, nnodes, nlights, hdr_w, hdr_h;
+};
+
+namespace {
+
+// Per-invocation shader state: uniforms + the global `seed` (:433-436).
+struct Shader {
+  const orc_scene* s;
+  uint32_t frameCounter;
+  int width, height, hdrResolution, pointLightSize, max_tracing_depth;
+  float clamp_threshold;
+  bool accumulate;
+  uint32_t seed;
+  int px, py;  // uint((pix*0.5+0.5)*width): the integer pixel coordinate
+
+  float rand() { return u32_to_unit(wang_hash(&seed)); }  // :447-449
+
+  v3 texel3(const std::vector<float>& buf, int texel) const {  // texelFetch on RGB32F buffer
+    return mk(buf[3 * (size_t)texel], buf[3 * (size_t)texel + 1], buf[3 * (size_t)texel + 2]);
+  }
+  // getPointLight (:127-135); out-of-range texelFetch returns 0
+  void getPointLight(int i, v3* pos, v3* rad) const {
+    if (i < 0 || i >= s->nlights) { *pos = splat(0.0f); *rad = splat(0.0f); return; }
+    *pos = texel3(s->light, i * 2 + 0);
+    *rad = texel3(s->light, i * 2 + 1);
+  }
+  Triangle getTriangle(int i) const {  // :139-162
+    int offset = i * 15;
+    Triangle t;
+    t.p1 = texel3(s->tri, offset + 0);
+    t.p2 = texel3(s->tri, offset + 1);
+    t.p3 = texel3(s->tri, offset + 2);
+    t.n1 = texel3(s->tri, offset + 3);
+    t.n2 = texel3(s->tri, offset + 4);
+    t.n3 = texel3(s->tri, offset + 5);
+    v3 uvPacked1 = texel3(s->tri, offset + 12);
+    v3 uvPacked2 = texel3(s->tri, offset + 13);
+    t.uv1[0] = uvPacked1.x; t.uv1[1] = uvPacked1.y;
+    t.uv2[0] = uvPacked1.z; t.uv2[1] = uvPacked2.x;
+    t.uv3[0] = uvPacked2.y; t.uv3[1] = uvPacked2.z;
+    t.objIndex = (int)texel3(s->tri, offset + 14).x;
+    return t;
+  }
+  Material getMaterial(int i) const {  // :165-190
+    Material m;
+    int offset = i * 15;
+    v3 param1 = texel3(s->tri, offset + 8), param2 = texel3(s->tri, offset + 9);
+    v3 param3 = texel3(s->tri, offset + 10), param4 = texel3(s->tri, offset + 11);
+    m.emissive = texel3(s->tri, offset + 6);
+    m.baseColor = texel3(s->tri, offset + 7);
+    m.subsurface = param1.x; m.metallic = param1.y; m.specular = param1.z;
+    m.specularTint = param2.x; m.roughness = param2.y; m.anisotropic = param2.z;
+    m.sheen = param3.x; m.sheenTint = param3.y; m.clearcoat = param3.z;
+    m.clearcoatGloss = param4.x; m.IOR = param4.y; m.transmission = param4.z;
+    return m;
+  }
+  BVHNode getBVHNode(int i) const {  // :193-210
+    BVHNode node;
+    int offset = i * 4;
+    v3 childs = texel3(s->node, offset + 0), leafInfo = texel3(s->node, offset + 1);
+    node.left = (int)childs.x;
+    node.right = (int)childs.y;
+    node.n = (int)leafInfo.x;
+    node.index = (int)leafInfo.y;
+    node.AA = texel3(s->node, offset + 2);
+    node.BB = texel3(s->node, offset + 3);
+    return node;
+  }
+
+  // :215-272
+  HitResult hitTriangle(const Triangle& triangle, const Ray& ray) const {
+    HitResult res;
+    res.distance = INF;
+    res.isHit = false;
+    res.isInside = false;
+    v3 p1 = triangle.p1, p2 = triangle.p2, p3 = triangle.p3;
+    v3 S = ray.startPoint, d = ray.direction;
+    v3 N = normalize(cross(sub(p2, p1), sub(p3, p1)));
+    if (dot(N, d) > 0.0f) {
+      N = neg(N);
+      res.isInside = true;
+    }
+    if (f_abs(dot(N, d)) < 0.00001f) return res;
+    float t = (dot(N, p1) - dot(S, N)) / dot(d, N);
+    if (t < 0.0005f) return res;
+    v3 P = add(S, muls(d, t));
+    v3 c1 = cross(sub(p2, p1), sub(P, p1));
+    v3 c2 = cross(sub(p3, p2), sub(P, p2));
+    v3 c3 = cross(sub(p1, p3), sub(P, p3));
+    bool r1 = (dot(c1, N) > 0.0f && dot(c2, N) > 0.0f && dot(c3, N) > 0.0f);
+    bool r2 = (dot(c1, N) < 0.0f && dot(c2, N) < 0.0f && dot(c3, N) < 0.0f);
+    if (r1 || r2) {
+      res.isHit = true;
+      res.hitPoint = P;
+      res.distance = t;
+      res.normal = N;
+      res.viewDir = d;
+      float alpha = ((-(P.x - p2.x)) * (p3.y - p2.y) + (P.y - p2.y) * (p3.x - p2.x)) /
+                    ((-(p1.x - p2.x)) * (p3.y - p2.y) + (p1.y - p2.y) * (p3.x - p2.x) + 1e-7f);
+      float beta = ((-(P.x - p3.x)) * (p1.y - p3.y) + (P.y - p3.y) * (p1.x - p3.x)) /
+                   ((-(p2.x - p3.x)) * (p1.y - p3.y) + (p2.y - p3.y) * (p1.x - p3.x) + 1e-7f);
+      float gama = (1.0f - alpha) - beta;
+      v3 Nsmooth = add(add(muls(triangle.n1, alpha), muls(triangle.n2, beta)), muls(triangle.n3, gama));
+      Nsmooth = normalize(Nsmooth);
+      res.normal = res.isInside ? neg(Nsmooth) : Nsmooth;
+    }
+    return res;
+  }
+
+  // :275-288
+  static float hitAABB(const Ray& r, v3 AA, v3 BB) {
+    v3 invdir = divv(splat(1.0f), r.direction);
+    v3 f = mul(sub(BB, r.startPoint), invdir);
+    v3 n = mul(sub(AA, r.startPoint), invdir);
+    v3 tmax = vmax(f, n);
+    v3 tmin = vmin(f, n);
+    float t1 = f_min(tmax.x, f_min(tmax.y, tmax.z));
+    float t0 = f_max(tmin.x, f_max(tmin.y, tmin.z));
+    return (t1 >= t0) ? ((t0 > 0.0f) ? (t0) : (t1)) : (-1.0f);
+  }
+
+  static bool under_zero(v3 c) { return c.x < 0.0f || c.y < 0.0f || c.z < 0.0f; }
+
+  // :298-369 (the texture-array branch reads 0: no material array bound)
+  HitResult hitArray(const Ray& ray, int l, int r) const {
+    HitResult res;
+    res.isHit = false;
+    res.distance = INF;
+    for (int i = l; i <= r; ++i) {
+      Triangle triangle = getTriangle(i);
+      HitResult hr = hitTriangle(triangle, ray);
+      if (hr.isHit && hr.distance < res.distance) {
+        res = hr;
+        res.material = getMaterial(i);
+      }
+    }
+    if (res.isHit) {
+      if (under_zero(res.material.baseColor)) res.material.baseColor = splat(0.0f);
+      if (res.material.metallic < 0.0f) res.material.metallic = 0.0f;
+      if (res.material.roughness < 0.0f) res.material.roughness = 0.0f;
+    }
+    return res;
+  }
+
+  // :372-424
+  HitResult hitBVH(const Ray& ray) const {
+    HitResult res;
+    res.isHit = false;
+    res.distance = INF;
+    int stack[256];
+    int sp = 0;
+    stack[sp++] = 1;
+    while (sp > 0) {
+      int top = stack[--sp];
+      BVHNode node = getBVHNode(top);
+      if (node.n > 0) {
+        int L = node.index, R = node.index + node.n - 1;
+        HitResult r = hitArray(ray, L, R);
+        if (r.isHit && r.distance < res.distance) res = r;
+        continue;
+      }
+      float d1 = INF, d2 = INF;
+      if (node.left > 0) {
+        BVHNode leftNode = getBVHNode(node.left);
+        d1 = hitAABB(ray, leftNode.AA, leftNode.BB);
+      }
+      if (node.right > 0) {
+        BVHNode rightNode = getBVHNode(node.right);
+        d2 = hitAABB(ray, rightNode.AA, rightNode.BB);
+      }
+      if (d1 > 0.0f && d2 > 0.0f) {
+        if (d1 < d2) { stack[sp++] = node.right; stack[sp++] = node.left; }
+        else { stack[sp++] = node.left; stack[sp++] = node.right; }
+      } else if (d1 > 0.0f) {
+        stack[sp++] = node.left;
+      } else if (d2 > 0.0f) {
+        stack[sp++] = node.right;
+      }
+    }
+    return res;
+  }
+
+  // ---------------------------------------------------------------- QMC ---
+  static uint32_t grayCode(uint32_t i) { return i ^ (i >> 1); }  // :475-477
+  static float sobol(uint32_t d, uint32_t i) {                   // :480-488
+    uint32_t result = 0u;
+    uint32_t offset = d * 32u;
+    for (uint32_t j = 0u; i > 0u; i >>= 1u, j++)
+      if ((i & 1u) == 1u) result ^= SOBOL_V[j + offset];
+    return (float)result * (1.0f / (float)0xFFFFFFFFu);
+  }
+  static void sobolVec2(uint32_t i, uint32_t b, float* u, float* v) {  // :491-495
+    *u = sobol(b * 2u, grayCode(i));
+    *v = sobol(b * 2u + 1u, grayCode(i));
+  }
+  void CranleyPattersonRotation(float* px_, float* py_) const {  // :497-515
+    uint32_t pseed = ((uint32_t)px * 1973u + (uint32_t)py * 9277u + (uint32_t)(114514 / 1919) * 26699u) | 1u;
+    float u = u32_to_unit(wang_hash(&pseed));
+    float v = u32_to_unit(wang_hash(&pseed));
+    float x = *px_ + u;
+    if (x > 1.0f) x -= 1.0f;
+    if (x < 0.0f) x += 1.0f;
+    float y = *py_ + v;
+    if (y > 1.0f) y -= 1.0f;
+    if (y < 0.0f) y += 1.0f;
+    *px_ = x;
+    *py_ = y;
+  }
+
+  // --------------------------------------------------------------- BRDF ---
+  static float sqr(float x) { return x * x; }
+  static float SchlickFresnel(float u) {  // :524-528
+    float m = f_clamp(1.0f - u, 0.0f, 1.0f);
+    float m2 = m * m;
+    return (m2 * m2) * m;
+  }
+  static float GTR1(float NdotH, float a) {  // :530-535
+    if (a >= 1.0f) return 1.0f / PI;
+    float a2 = a * a;
+    float t = 1.0f + ((a2 - 1.0f) * NdotH) * NdotH;
+    return (a2 - 1.0f) / ((PI * g_log(a2)) * t);
+  }
+  static float GTR2(float NdotH, float a) {  // :537-541
+    float a2 = a * a;
+    float t = 1.0f + ((a2 - 1.0f) * NdotH) * NdotH;
+    return a2 / ((PI * t) * t);
+  }
+  static float smithG_GGX(float NdotV, float alphaG) {  // :547-551
+    float a = alphaG * alphaG;
+    float b = NdotV * NdotV;
+    return 1.0f / (NdotV + f_sqrt((a + b) - a * b));
+  }
+  static v3 BRDF_Evaluate(v3 V, v3 N, v3 L, const Material& m) {  // :620-669
+    float NdotL = dot(N, L);
+    float NdotV = dot(N, V);
+    if (NdotL < 0.0f || NdotV < 0.0f) return splat(0.0f);
+    v3 H = normalize(add(L, V));
+    float NdotH = dot(N, H);
+    float LdotH = dot(L, H);
+    v3 Cdlin = m.baseColor;
+    float Cdlum = (0.3f * Cdlin.x + 0.6f * Cdlin.y) + 0.1f * Cdlin.z;
+    v3 Ctint = (Cdlum > 0.0f) ? divs(Cdlin, Cdlum) : splat(1.0f);
+    v3 Cspec = muls(mixv(splat(1.0f), Ctint, m.specularTint), m.specular);
+    v3 Cspec0 = mixv(muls(Cspec, 0.08f), Cdlin, m.metallic);
+    v3 Csheen = mixv(splat(1.0f), Ctint, m.sheenTint);
+    float Fd90 = 0.5f + ((2.0f * LdotH) * LdotH) * m.roughness;
+    float FL = SchlickFresnel(NdotL), FV = SchlickFresnel(NdotV);
+    float Fd = f_mix(1.0f, Fd90, FL) * f_mix(1.0f, Fd90, FV);
+    float Fss90 = (LdotH * LdotH) * m.roughness;
+    float Fss = f_mix(1.0f, Fss90, FL) * f_mix(1.0f, Fss90, FV);
+    float ss = 1.25f * (Fss * (1.0f / (NdotL + NdotV) - 0.5f) + 0.5f);
+    float alpha = f_max(0.001f, sqr(m.roughness));
+    float Ds = GTR2(NdotH, alpha);
+    float FH = SchlickFresnel(LdotH);
+    v3 Fs = mixv(Cspec0, splat(1.0f), FH);
+    float Gs = smithG_GGX(NdotL, m.roughness);
+    Gs *= smithG_GGX(NdotV, m.roughness);
+    float Dr = GTR1(NdotH, f_mix(0.1f, 0.001f, m.clearcoatGloss));
+    float Fr = f_mix(0.04f, 1.0f, FH);
+    float Gr = smithG_GGX(NdotL, 0.25f) * smithG_GGX(NdotV, 0.25f);
+    v3 Fsheen = muls(Csheen, FH * m.sheen);
+    v3 diffuse = add(muls(Cdlin, (1.0f / PI) * f_mix(Fd, ss, m.subsurface)), Fsheen);
+    v3 specular = muls(muls(Fs, Gs), Ds);
+    v3 clearcoat = splat((((0.25f * Gr) * Fr) * Dr) * m.clearcoat);
+    return add(add(muls(diffuse, 1.0f - m.metallic), specular), clearcoat);
+  }
+  static float BRDF_Pdf(v3 V, v3 N, v3 L, const Material& m) {  // :837-874
+    float NdotL = dot(N, L);
+    float NdotV = dot(N, V);
+    if (NdotL < 0.0f || NdotV < 0.0f) return 0.0f;
+    v3 H = normalize(add(L, V));
+    float NdotH = dot(N, H);
+    float LdotH = dot(L, H);
+    float alpha = f_max(0.001f, sqr(m.roughness));
+    float Ds = GTR2(NdotH, alpha);
+    float Dr = GTR1(NdotH, f_mix(0.1f, 0.001f, m.clearcoatGloss));
+    float pdf_diffuse = NdotL / PI;
+    float pdf_specular = (Ds * NdotH) / (4.0f * LdotH);
+    float pdf_clearcoat = (Dr * NdotH) / (4.0f * LdotH);
+    float r_diffuse = 1.0f - m.metallic;
+    float r_specular = 1.0f;
+    float r_clearcoat = 0.25f * m.clearcoat;
+    float r_sum = (r_diffuse + r_specular) + r_clearcoat;
+    float p_diffuse = r_diffuse / r_sum, p_specular = r_specular / r_sum, p_clearcoat = r_clearcoat / r_sum;
+    float pdf = (p_diffuse * pdf_diffuse + p_specular * pdf_specular) + p_clearcoat * pdf_clearcoat;
+    return f_max(1e-10f, pdf);
+  }
+
+  // ----------------------------------------------------------- sampling ---
+  static v3 toNormalHemisphere(v3 v, v3 N) {  // :681-687
+    v3 helper = mk(1, 0, 0);
+    if (f_abs(N.x) > 0.999f) helper = mk(0, 0, 1);
+    v3 tangent = normalize(cross(N, helper));
+    v3 bitangent = normalize(cross(N, tangent));
+    return add(add(muls(tangent, v.x), muls(bitangent, v.y)), muls(N, v.z));
+  }
+  static v3 SampleCosineHemisphere(float xi_1, float xi_2, v3 N) {  // :699-710
+    float r = f_sqrt(xi_1);
+    float theta = (xi_2 * 2.0f) * PI;
+    float x = r * g_cos(theta);
+    float y = r * g_sin(theta);
+    float z = f_sqrt((1.0f - x * x) - y * y);
+    return toNormalHemisphere(mk(x, y, z), N);
+  }
+  static v3 SampleGTR2(float xi_1, float xi_2, v3 V, v3 N, float alpha) {  // :713-730
+    float phi_h = (2.0f * PI) * xi_1;
+    float sin_phi_h = g_sin(phi_h), cos_phi_h = g_cos(phi_h);
+    float cos_theta_h = f_sqrt((1.0f - xi_2) / (1.0f + (alpha * alpha - 1.0f) * xi_2));
+    float sin_theta_h = f_sqrt(f_max(0.0f, 1.0f - cos_theta_h * cos_theta_h));
+    v3 H = mk(sin_theta_h * cos_phi_h, sin_theta_h * sin_phi_h, cos_theta_h);
+    H = toNormalHemisphere(H, N);
+    return reflect(neg(V), H);
+  }
+  static v3 SampleGTR1(float xi_1, float xi_2, v3 V, v3 N, float alpha) {  // :733-750
+    float phi_h = (2.0f * PI) * xi_1;
+    float sin_phi_h = g_sin(phi_h), cos_phi_h = g_cos(phi_h);
+    float cos_theta_h = f_sqrt((1.0f - g_pow(alpha * alpha, 1.0f - xi_2)) / (1.0f - alpha * alpha));
+    float sin_theta_h = f_sqrt(f_max(0.0f, 1.0f - cos_theta_h * cos_theta_h));
+    v3 H = mk(sin_theta_h * cos_phi_h, sin_theta_h * sin_phi_h, cos_theta_h);
+    H = toNormalHemisphere(H, N);
+    return reflect(neg(V), H);
+  }
+  static v3 SampleBRDF(float xi_1, float xi_2, float xi_3, v3 V, v3 N, const Material& m) {  // :753-784
+    float alpha_GTR1 = f_mix(0.1f, 0.001f, m.clearcoatGloss);
+    float alpha_GTR2 = f_max(0.001f, sqr(m.roughness));
+    float r_diffuse = 1.0f - m.metallic;
+    float r_specular = 1.0f;
+    float r_clearcoat = 0.25f * m.clearcoat;
+    float r_sum = (r_diffuse + r_specular) + r_clearcoat;
+    float p_diffuse = r_diffuse / r_sum, p_specular = r_specular / r_sum;
+    float rd = xi_3;
+    if (rd <= p_diffuse) return SampleCosineHemisphere(xi_1, xi_2, N);
+    else if (p_diffuse < rd && rd <= p_diffuse + p_specular) return SampleGTR2(xi_1, xi_2, V, N, alpha_GTR2);
+    else if (p_diffuse + p_specular < rd) return SampleGTR1(xi_1, xi_2, V, N, alpha_GTR1);
+    return mk(0, 1, 0);
+  }
+
+  // --------------------------------------------------------- environment ---
+  void hdrTex(const std::vector<float>& img, float u, float v, float* out) const {
+    tex2d_linear(img.data(), s->hdr_w, s->hdr_h, 3, u, v, out, 3);
+  }
+  v3 SampleHdr(float xi_1, float xi_2) const {  // :787-799
+    float xy[3];
+    hdrTex(s->cache, xi_1, xi_2, xy);
+    xy[1] = 1.0f - xy[1];
+    float phi = (2.0f * PI) * (xy[0] - 0.5f);
+    float theta = PI * (xy[1] - 0.5f);
+    return mk(g_cos(theta) * g_cos(phi), g_sin(theta), g_cos(theta) * g_sin(phi));
+  }
+  static void toSphericalCoord(v3 v, float* u, float* w) {  // :804-810
+    float a = g_atan2(v.z, v.x), b = g_asin(v.y);
+    a /= (2.0f * PI);
+    b /= PI;
+    a += 0.5f;
+    b += 0.5f;
+    *u = a;
+    *w = 1.0f - b;
+  }
+  v3 hdrColor(v3 L) const {  // :813-817
+    float u, v, c[3];
+    toSphericalCoord(normalize(L), &u, &v);
+    hdrTex(s->hdr, u, v, c);
+    return mk(c[0], c[1], c[2]);
+  }
+  float hdrPdf(v3 L, int hdrRes) const {  // :821-832
+    float u, v, c[3];
+    toSphericalCoord(normalize(L), &u, &v);
+    hdrTex(s->cache, u, v, c);
+    float pdf = c[2];
+    float theta = PI * (0.5f - v);
+    float sin_theta = f_max(g_sin(theta), 1e-10f);
+    float p_convert = (float)(hdrRes * hdrRes / 2) / (((2.0f * PI) * PI) * sin_theta);
+    return pdf * p_convert;
+  }
+
+  // ------------------------------------------------------------ lights ---
+  v3 calculatePointLight(const HitResult& hit, float* pdf) {  // :884-919
+    if (pointLightSize == 0) {
+      *pdf = 0.0f;
+      return splat(0.0f);
+    }
+    *pdf = (2.0f * PI) / (float)pointLightSize;
+    v3 lpos, lrad;
+    getPointLight((int)(rand() * (float)pointLightSize), &lpos, &lrad);
+    v3 newDir = normalize(sub(lpos, hit.hitPoint));
+    float dist = length(sub(lpos, hit.hitPoint));
+    Ray shadowRay{hit.hitPoint, newDir};
+    HitResult shadowHit = hitBVH(shadowRay);
+    if (shadowHit.isHit) {
+      float shadowDist = length(sub(shadowHit.hitPoint, hit.hitPoint));
+      if (shadowDist < dist) return splat(0.0f);
+    }
+    v3 pointLightValue = divs(lrad, dist * dist);
+    v3 brdf = BRDF_Evaluate(neg(hit.viewDir), hit.normal, newDir, hit.material);
+    return divs(muls(mul(pointLightValue, brdf), f_abs(dot(newDir, hit.normal))), *pdf);
+  }
+  v3 hdriLight(const HitResult& hit, float* pdf) {  // :922-946
+    float r1 = rand();
+    float r2 = rand();
+    v3 newDir = SampleHdr(r1, r2);
+    Ray shadowRay{hit.hitPoint, newDir};
+    HitResult shadowHit = hitBVH(shadowRay);
+    if (shadowHit.isHit) {
+      *pdf = 0.0f;
+      return splat(0.0f);
+    }
+    v3 hdriValue = hdrColor(newDir);
+    v3 brdf = BRDF_Evaluate(neg(hit.viewDir), hit.normal, newDir, hit.material);
+    *pdf = hdrPdf(shadowRay.direction, hdrResolution);
+    return divs(mul(muls(brdf, f_abs(dot(newDir, hit.normal))), hdriValue), *pdf);
+  }
+  void shade(const HitResult& hit, v3 newDir, v3* hitLight, v3* reduction) {  // :948-968
+    v3 brdf = BRDF_Evaluate(neg(hit.viewDir), hit.normal, newDir, hit.material);
+    float brdfPdf = BRDF_Pdf(neg(hit.viewDir), hit.normal, newDir, hit.material);
+    float hdriPdf = 0.0f, pointPdf = 0.0f;
+    v3 hdriLightCalc = hdriLight(hit, &hdriPdf);
+    v3 pointLightCalc = calculatePointLight(hit, &pointPdf);
+    v3 cosb = muls(brdf, f_abs(dot(newDir, hit.normal)));
+    v3 brdfLightCalc = divs(mul(hit.material.emissive, cosb), brdfPdf);
+    float sum_weight = ((hdriPdf + pointPdf) + brdfPdf) + epsilon;
+    float w1 = hdriPdf / sum_weight, w2 = pointPdf / sum_weight, w3 = brdfPdf / sum_weight;
+    v3 mixc = add(add(muls(hdriLightCalc, w1), muls(pointLightCalc, w2)), muls(brdfLightCalc, w3));
+    *hitLight = mul(*reduction, mixc);
+    *reduction = mul(*reduction, divs(cosb, brdfPdf));
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+orc_scene* orc_scene_create(const float* tri, int ntris, const float* node, int nnodes, const float* lights,
+                            int nlights, const float* hdr, const float* cache, int hdr_w, int hdr_h) {
+  orc_scene* s = new orc_scene();
+  s->tri.assign(tri, tri + (size_t)ntris * 45);
+  s->node.assign(node, node + (size_t)nnodes * 12);
+  if (nlights > 0) s->light.assign(lights, lights + (size_t)nlights * 6);
+  s->hdr.assign(hdr, hdr + (size_t)hdr_w * hdr_h * 3);
+  s->cache.assign(cache, cache + (size_t)hdr_w * hdr_h * 3);
+  s->ntris = ntris;
+  s->nnodes = nnodes;
+  s->nlights = nlights;
+  s->hdr_w = hdr_w;
+  s->hdr_h = hdr_h;
+  return s;
+}
+void orc_scene_destroy(orc_scene* s) { delete s; }
+
+int orc_path_trace(const orc_scene* s, const orc_pt_params* p, const float* last_frame, float* out_color,
+                   float* out_emission, float* out_albedo, int threads) {
+  const int W = p->width, H = p->height;
+  if (p->max_tracing_depth > 4) return -1;  // sobol dims 0..7 only (:463)
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads > 0 ? threads : 1)
+  for (int y = p->y_begin; y < p->y_end; ++y) {
+    for (int x = 0; x < W; ++x) {
+      Shader sh;
+      sh.s = s;
+      sh.frameCounter = p->frameCounter;
+      sh.width = W;
+      sh.height = H;
+      sh.hdrResolution = s->hdr_w;
+      sh.pointLightSize = s->nlights;
+      sh.max_tracing_depth = p->max_tracing_depth;
+      sh.clamp_threshold = p->clamp_threshold;
+      sh.accumulate = p->accumulate != 0;
+      sh.px = x;
+      sh.py = y;
+      sh.seed = ((uint32_t)x * 1973u + (uint32_t)y * 9277u + p->frameCounter * 26699u) | 1u;  // :433-436
+      // main() (:1056-1128)
+      float pixx = (float)(2 * x + 1) / (float)W - 1.0f;
+      float pixy = (float)(2 * y + 1) / (float)H - 1.0f;
+      if (p->aspect_corrected) pixx = pixx * ((float)W / (float)H);
+      Ray ray;
+      ray.startPoint = mk(p->eye[0], p->eye[1], p->eye[2]);
+      (void)sh.rand();  // AA jitter: computed, never applied (:1060)
+      (void)sh.rand();
+      const float* m = p->cameraRotate;
+      float dv[3];
+      for (int r = 0; r < 3; ++r) dv[r] = (m[0 + r] * pixx + m[4 + r] * pixy) + (m[8 + r] * -1.0f + m[12 + r] * 0.0f);
+      ray.direction = normalize(mk(dv[0], dv[1], dv[2]));
+      v3 color = splat(0.0f), light = splat(0.0f), reduction = splat(1.0f);
+      HitResult firstHit;
+      firstHit.isHit = false;
+      firstHit.material.emissive = splat(0.0f);   // uninitialised in GLSL when the primary ray misses
+      firstHit.material.baseColor = splat(0.0f);  // (the build defines it as 0)
+      for (int i = 0; i < sh.max_tracing_depth; ++i) {
+        HitResult nearestHit = sh.hitBVH(ray);
+        if (i == 0) firstHit = nearestHit.isHit ? nearestHit : firstHit;
+        if (!nearestHit.isHit) {
+          light = add(light, mul(sh.hdrColor(ray.direction), reduction));
+          break;
+        }
+        float xi_1, xi_2;
+        Shader::sobolVec2(p->frameCounter + 1u, (uint32_t)i, &xi_1, &xi_2);
+        sh.CranleyPattersonRotation(&xi_1, &xi_2);
+        float xi_3 = sh.rand();
+        v3 L = Shader::SampleBRDF(xi_1, xi_2, xi_3, neg(nearestHit.viewDir), nearestHit.normal, nearestHit.material);
+        float NdotL = dot(nearestHit.normal, L);
+        if (NdotL <= 0.0f) break;
+        v3 hitLight;
+        sh.shade(nearestHit, L, &hitLight, &reduction);
+        light = add(light, hitLight);
+        ray.startPoint = nearestHit.hitPoint;
+        ray.direction = L;
+      }
+      light = vclamp(light, 0.0f, sh.clamp_threshold);
+      if (!f_isnan(light.x) && !f_isnan(light.y) && !f_isnan(light.z)) color = light;
+      size_t o = ((size_t)y * W + x) * 4;
+      if (sh.accumulate && last_frame) {  // :1116-1119
+        v3 last = mk(last_frame[o], last_frame[o + 1], last_frame[o + 2]);
+        color = mixv(last, color, 1.0f / (float)(p->frameCounter + 1u));
+      }
+      out_color[o] = color.x; out_color[o + 1] = color.y; out_color[o + 2] = color.z; out_color[o + 3] = 1.0f;
+      v3 em = firstHit.material.emissive, al = firstHit.material.baseColor;
+      out_emission[o] = em.x; out_emission[o + 1] = em.y; out_emission[o + 2] = em.z; out_emission[o + 3] = 1.0f;
+      out_albedo[o] = al.x; out_albedo[o + 1] = al.y; out_albedo[o + 2] = al.z; out_albedo[o + 3] = 1.0f;
+    }
+  }
+  return 0;
+}
+
+// ---- unit-test entry points --------------------------------------------------
+uint32_t orc_wang_hash(uint32_t seed) { return wang_hash(&seed); }
+float orc_sobol(uint32_t d, uint32_t i) { return Shader::sobol(d, i); }
+static Material mat14(const float* m) {
+  Material r;
+  r.emissive = mk(0, 0, 0);
+  r.baseColor = mk(m[0], m[1], m[2]);
+  r.subsurface = m[3]; r.metallic = m[4]; r.specular = m[5]; r.specularTint = m[6]; r.roughness = m[7];
+  r.anisotropic = m[8]; r.sheen = m[9]; r.sheenTint = m[10]; r.clearcoat = m[11]; r.clearcoatGloss = m[12];
+  r.IOR = m[13]; r.transmission = 0.0f;
+  return r;
+}
+void orc_brdf_eval(const float* V, const float* N, const float* L, const float* m, float* out3) {
+  v3 r = Shader::BRDF_Evaluate(mk(V[0], V[1], V[2]), mk(N[0], N[1], N[2]), mk(L[0], L[1], L[2]), mat14(m));
+  out3[0] = r.x; out3[1] = r.y; out3[2] = r.z;
+}
+float orc_brdf_pdf(const float* V, const float* N, const float* L, const float* m) {
+  return Shader::BRDF_Pdf(mk(V[0], V[1], V[2]), mk(N[0], N[1], N[2]), mk(L[0], L[1], L[2]), mat14(m));
+}
+float orc_hit_aabb(const float* S, const float* d, const float* AA, const float* BB) {
+  Ray r{mk(S[0], S[1], S[2]), mk(d[0], d[1], d[2])};
+  return Shader::hitAABB(r, mk(AA[0], AA[1], AA[2]), mk(BB[0], BB[1], BB[2]));
+}
+int orc_hit_triangle(const float* S, const float* d, const float* t9, const float* n9, float* out5) {
+  Shader sh;
+  Triangle t;
+  t.p1 = mk(t9[0], t9[1], t9[2]); t.p2 = mk(t9[3], t9[4], t9[5]); t.p3 = mk(t9[6], t9[7], t9[8]);
+  t.n1 = mk(n9[0], n9[1], n9[2]); t.n2 = mk(n9[3], n9[4], n9[5]); t.n3 = mk(n9[6], n9[7], n9[8]);
+  Ray r{mk(S[0], S[1], S[2]), mk(d[0], d[1], d[2])};
+  HitResult h = sh.hitTriangle(t, r);
+  out5[0] = h.distance;
+  out5[1] = h.isHit ? h.normal.x : 0.0f; out5[2] = h.isHit ? h.normal.y : 0.0f; out5[3] = h.isHit ? h.normal.z : 0.0f;
+  out5[4] = h.isInside ? 1.0f : 0.0f;
+  return h.isHit ? 1 : 0;
+}
+void orc_math(int fn, const float* in, int n, float* out) {
+  for (int i = 0; i < n; ++i) {
+    switch (fn) {
+      case 0: out[i] = g_sin(in[i]); break;
+      case 1: out[i] = g_cos(in[i]); break;
+      case 2: out[i] = g_atan2(in[i], in[n + i]); break;
+      case 3: out[i] = g_asin(in[i]); break;
+      case 4: out[i] = g_log(in[i]); break;
+      case 5: out[i] = g_exp(in[i]); break;
+      default: out[i] = 0.0f;
+    }
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,1068 @@
+// capi.hip — implementation of include/ptsvgf.h: the GL-plumbing-shaped C ABI
+// (Utils/render_pass.h:82-182, Utils/shader.h:21-67, Utils/help_func.h:22-32)
+// over HIP device memory and the gfx950 kernels.
+//
+// GL semantics kept:
+//  * RenderPass uniforms are set by name; an unknown name is silently ignored;
+//  * set_texture_uniform binds to the pass's next texture slot; a sampler that
+//    was never bound reads texture unit 0, i.e. the texture most recently bound
+//    to slot 0 by any pass (GL's global unit state);
+//  * draw() is ordered after every previous draw (one in-order HIP stream);
+//  * scene texture buffers are decoded once per (buffer, version) into the
+//    kernels' SoA records (pt_device.h) on first use, like a driver upload.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/ptsvgf.h"
+#include "../../include/ptsvgf_scene.h"
+#include "glsl_builtins.h"
+#include "pt_device.h"
+
+namespace {
+
+using namespace ptk;
+
+enum ProgKind {
+  PK_PATHTRACE = 1,
+  PK_REPROJECT,
+  PK_VARIANCE,
+  PK_ATROUS,
+  PK_MODULATE,
+  PK_BLIT,
+  PK_SAVE,
+  PK_OUTPUT,
+  PK_TAA,
+  PK_RASTER
+};
+
+struct Texture {
+  uint32_t target = PT_TEXTURE_2D;
+  int W = 0, H = 0;      // logical (global) size
+  int row0 = 0, rows = 0;  // stored rows (band)
+  int layers = 0;
+  bool owned = true;
+  void* dev = nullptr;
+  size_t bytes = 0;
+  std::vector<uint8_t> host;  // buffers: host copy for decoding
+  uint64_t version = 1;
+  float* aux = nullptr;  // compact depth-fwidth side plane
+  bool aux_valid = false;
+};
+
+struct Uniform {
+  int type = 0;  // 1 float 2 int 3 uint 4 bool 5 vec3 6 mat4
+  float f[16] = {0};
+  int i = 0;
+  uint32_t u = 0;
+};
+
+struct RasterScene {
+  float4* geom = nullptr;
+  float4* bvh = nullptr;
+  int root_ref = 0;
+  int ntris = 0;
+};
+
+struct Pass {
+  uint32_t program = 0;
+  int W = 0, H = 0;
+  std::vector<uint32_t> att;
+  bool bound = false, final_pass = false;
+  int slot = 0;
+  std::unordered_map<std::string, uint32_t> tex;
+  std::unordered_map<std::string, Uniform> uni;
+  int y_begin = -1, y_end = -1;
+  RasterScene raster;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+};
+
+struct SceneGPU {
+  float4* geom = nullptr;
+  float4* shade = nullptr;
+  float4* bvh = nullptr;
+  int root_ref = 0;
+  int ntris = 0;
+  uint64_t tri_ver = 0, node_ver = 0;
+};
+
+struct Lib {
+  bool init = false;
+  int device = 0;
+  hipStream_t own = nullptr, stream = nullptr;
+  uint32_t next = 1;
+  std::map<uint32_t, int> programs;
+  std::map<uint32_t, std::unique_ptr<Texture>> textures;
+  std::map<uint32_t, std::unique_ptr<Pass>> passes;
+  std::map<std::pair<uint32_t, uint32_t>, SceneGPU> scenes;
+  uint32_t unit0 = 0;  // GL texture unit 0 binding (global)
+  int band_w = 0, band_h = 0, band_y0 = 0, band_y1 = 0, band_row0 = 0, band_rows = 0;
+  bool profiling = false;
+};
+
+Lib g;
+thread_local std::string g_err;
+std::recursive_mutex g_mu;
+
+int err(int code, const std::string& m) {
+  g_err = m;
+  return code;
+}
+int hip_err(hipError_t e, const char* what) {
+  return err(PT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HIPCHK(x)                                    \
+  do {                                               \
+    hipError_t e_ = (x);                             \
+    if (e_ != hipSuccess) return hip_err(e_, #x);    \
+  } while (0)
+
+std::string basename_of(const char* p) {
+  std::string s(p ? p : "");
+  size_t k = s.find_last_of("/\\");
+  return k == std::string::npos ? s : s.substr(k + 1);
+}
+
+Texture* tex_of(uint32_t h) {
+  auto it = g.textures.find(h);
+  return it == g.textures.end() ? nullptr : it->second.get();
+}
+Pass* pass_of(uint32_t h) {
+  auto it = g.passes.find(h);
+  return it == g.passes.end() ? nullptr : it->second.get();
+}
+
+int ensure_init() {
+  if (g.init) return PT_OK;
+  return err(PT_ERR_STATE, "pt_init() has not been called");
+}
+
+// ---------------------------------------------------------------- packing ---
+struct NodeRaw {
+  int left, right, n, index;
+  float AA[3], BB[3];
+};
+
+int pack_bvh(const float* node_enc, int nnodes, std::vector<float4>& out, int* root_ref, int ntris) {
+  if (nnodes < 2) return err(PT_ERR_FORMAT, "BVH needs the dummy node 0 and a root node 1");
+  std::vector<NodeRaw> nd(nnodes);
+  for (int i = 0; i < nnodes; ++i) {
+    const float* f = node_enc + (size_t)i * 12;
+    nd[i].left = (int)f[0];
+    nd[i].right = (int)f[1];
+    nd[i].n = (int)f[3];
+    nd[i].index = (int)f[4];
+    for (int k = 0; k < 3; ++k) { nd[i].AA[k] = f[6 + k]; nd[i].BB[k] = f[9 + k]; }
+  }
+  std::vector<int> idx(nnodes, -1);
+  std::vector<int> order;
+  // iterative DFS (depth check: stack needs one slot per interior level)
+  struct Item { int id, depth; };
+  std::vector<Item> st;
+  auto leaf_ref = [&](int id, int* ref) -> int {
+    const NodeRaw& n = nd[id];
+    if (n.n > 15) return err(PT_ERR_FORMAT, "BVH leaf holds more than 15 triangles");
+    if (n.index < 0 || n.index + n.n > ntris) return err(PT_ERR_FORMAT, "BVH leaf range out of bounds");
+    *ref = -(n.index * 16 + n.n) - 1;
+    return PT_OK;
+  };
+  if (nd[1].n > 0) {
+    int r;
+    if (leaf_ref(1, &r) != PT_OK) return PT_ERR_FORMAT;
+    *root_ref = r;
+    out.clear();
+    return PT_OK;
+  }
+  st.push_back({1, 1});
+  while (!st.empty()) {
+    Item it = st.back();
+    st.pop_back();
+    if (it.depth >= kStack) return err(PT_ERR_FORMAT, "BVH deeper than the traversal stack");
+    idx[it.id] = (int)order.size();
+    order.push_back(it.id);
+    const NodeRaw& n = nd[it.id];
+    if (n.left <= 0 || n.right <= 0 || n.left >= nnodes || n.right >= nnodes)
+      return err(PT_ERR_FORMAT, "BVH interior node with an invalid child");
+    if (nd[n.right].n <= 0) st.push_back({n.right, it.depth + 1});
+    if (nd[n.left].n <= 0) st.push_back({n.left, it.depth + 1});
+  }
+  out.assign(order.size() * 4, float4{0, 0, 0, 0});
+  for (size_t k = 0; k < order.size(); ++k) {
+    const NodeRaw& n = nd[order[k]];
+    const NodeRaw& L = nd[n.left];
+    const NodeRaw& R = nd[n.right];
+    int rl, rr;
+    if (L.n > 0) { if (leaf_ref(n.left, &rl) != PT_OK) return PT_ERR_FORMAT; } else rl = idx[n.left];
+    if (R.n > 0) { if (leaf_ref(n.right, &rr) != PT_OK) return PT_ERR_FORMAT; } else rr = idx[n.right];
+    float4* q = &out[4 * k];
+    q[0] = float4{L.AA[0], L.AA[1], L.AA[2], L.BB[0]};
+    q[1] = float4{L.BB[1], L.BB[2], R.AA[0], R.AA[1]};
+    q[2] = float4{R.AA[2], R.BB[0], R.BB[1], R.BB[2]};
+    float a, b;
+    memcpy(&a, &rl, 4);
+    memcpy(&b, &rr, 4);
+    q[3] = float4{a, b, 0, 0};
+  }
+  *root_ref = 0;
+  return PT_OK;
+}
+
+template <class T>
+int upload_vec(const std::vector<T>& v, T** dst) {
+  if (*dst) { (void)hipFree(*dst); *dst = nullptr; }
+  if (v.empty()) return PT_OK;
+  HIPCHK(hipMalloc((void**)dst, v.size() * sizeof(T)));
+  HIPCHK(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return PT_OK;
+}
+
+int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU** out) {
+  SceneGPU& sg = g.scenes[{th, nh}];
+  if (sg.geom && sg.tri_ver == tris->version && sg.node_ver == nodes->version) {
+    *out = &sg;
+    return PT_OK;
+  }
+  using namespace glsl;
+  size_t ntris = tris->host.size() / (45 * sizeof(float));
+  size_t nnodes = nodes->host.size() / (12 * sizeof(float));
+  const float* te = (const float*)tris->host.data();
+  std::vector<float4> geom(ntris * 4), shade(ntris * 9);
+  for (size_t i = 0; i < ntris; ++i) {
+    const float* f = te + i * 45;
+    v3 p1 = mk(f[0], f[1], f[2]), p2 = mk(f[3], f[4], f[5]), p3 = mk(f[6], f[7], f[8]);
+    v3 N = normalize(cross(sub(p2, p1), sub(p3, p1)));  // hitTriangle :227, same built-ins
+    geom[4 * i + 0] = float4{p1.x, p1.y, p1.z, dot(N, p1)};
+    geom[4 * i + 1] = float4{p2.x, p2.y, p2.z, 0.0f};
+    geom[4 * i + 2] = float4{p3.x, p3.y, p3.z, 0.0f};
+    geom[4 * i + 3] = float4{N.x, N.y, N.z, 0.0f};
+    float4* s = &shade[9 * i];
+    s[0] = float4{f[9], f[10], f[11], f[12]};
+    s[1] = float4{f[13], f[14], f[15], f[16]};
+    s[2] = float4{f[17], f[18], f[19], f[20]};
+    s[3] = float4{f[21], f[22], f[23], f[24]};
+    s[4] = float4{f[25], f[26], f[27], f[28]};
+    s[5] = float4{f[29], f[30], f[31], f[32]};
+    s[6] = float4{f[33], f[34], f[35], f[42]};
+    s[7] = float4{f[36], f[37], f[38], f[39]};
+    s[8] = float4{f[40], f[41], 0.0f, 0.0f};
+  }
+  std::vector<float4> bvh;
+  int root = 0;
+  int rc = pack_bvh((const float*)nodes->host.data(), (int)nnodes, bvh, &root, (int)ntris);
+  if (rc != PT_OK) return rc;
+  if ((rc = upload_vec(geom, &sg.geom)) != PT_OK) return rc;
+  if ((rc = upload_vec(shade, &sg.shade)) != PT_OK) return rc;
+  if (bvh.empty()) bvh.push_back(float4{0, 0, 0, 0});
+  if ((rc = upload_vec(bvh, &sg.bvh)) != PT_OK) return rc;
+  sg.root_ref = root;
+  sg.ntris = (int)ntris;
+  sg.tri_ver = tris->version;
+  sg.node_ver = nodes->version;
+  *out = &sg;
+  return PT_OK;
+}
+
+// -------------------------------------------------------------- bindings ---
+const Uniform* U(Pass* p, const char* name, int type) {
+  auto it = p->uni.find(name);
+  if (it == p->uni.end()) return nullptr;
+  return it->second.type == type ? &it->second : nullptr;
+}
+float uf(Pass* p, const char* n, float def) {
+  const Uniform* u = U(p, n, 1);
+  return u ? u->f[0] : def;
+}
+int ui(Pass* p, const char* n, int def) {
+  auto it = p->uni.find(n);
+  if (it == p->uni.end()) return def;
+  if (it->second.type == 2 || it->second.type == 4) return it->second.i;
+  if (it->second.type == 3) return (int)it->second.u;
+  return def;
+}
+uint32_t uu(Pass* p, const char* n, uint32_t def) {
+  auto it = p->uni.find(n);
+  if (it == p->uni.end()) return def;
+  if (it->second.type == 3) return it->second.u;
+  if (it->second.type == 2 || it->second.type == 4) return (uint32_t)it->second.i;
+  return def;
+}
+
+Texture* sampler(Pass* p, const char* name, uint32_t* handle = nullptr) {
+  auto it = p->tex.find(name);
+  uint32_t h = it != p->tex.end() ? it->second : g.unit0;
+  if (handle) *handle = h;
+  return tex_of(h);
+}
+
+int plane_of(Texture* t, Pass* p, Plane* out, const char* what) {
+  if (!t || t->target != PT_TEXTURE_2D || !t->dev)
+    return err(PT_ERR_MISSING_TEXTURE, std::string("pass needs 2-D texture '") + what + "'");
+  if (t->W != p->W || t->H != p->H)
+    return err(PT_ERR_ARG, std::string("texture '") + what + "' size differs from the pass size");
+  out->p = (float4*)t->dev;
+  out->aux = t->aux_valid ? t->aux : nullptr;
+  out->W = t->W;
+  out->row0 = t->row0;
+  out->rows = t->rows;
+  return PT_OK;
+}
+int att_plane(Pass* p, int k, Plane* out) {
+  if ((int)p->att.size() <= k) return err(PT_ERR_ARG, "pass has too few color attachments");
+  Texture* t = tex_of(p->att[k]);
+  int rc = plane_of(t, p, out, "color attachment");
+  if (rc != PT_OK) return rc;
+  t->version++;
+  t->aux_valid = false;
+  return PT_OK;
+}
+#define TRY(x)                    \
+  do {                            \
+    int rc_ = (x);                \
+    if (rc_ != PT_OK) return rc_; \
+  } while (0)
+
+void rows_of(Pass* p, int* y0, int* y1) {
+  if (p->y_begin >= 0) {
+    *y0 = p->y_begin;
+    *y1 = p->y_end;
+  } else if (g.band_h > 0 && p->W == g.band_w && p->H == g.band_h) {
+    *y0 = g.band_y0;
+    *y1 = g.band_y1;
+  } else {
+    *y0 = 0;
+    *y1 = p->H;
+  }
+}
+
+// sobol (path_tracing.frag:480-495): a per-frame uniform value
+float sobol_host(uint32_t d, uint32_t i) {
+  static const uint32_t V[8 * 32] = {
+#include "sobol_v.inc"
+  };
+  uint32_t r = 0u;
+  for (uint32_t j = 0u; i > 0u; i >>= 1u, j++)
+    if ((i & 1u) == 1u) r ^= V[j + d * 32u];
+  return (float)r * (1.0f / (float)0xFFFFFFFFu);
+}
+
+int copy_plane(Texture* dst, Texture* src, Pass* p, int y0, int y1) {
+  if (!src || !dst || !src->dev || !dst->dev) return err(PT_ERR_MISSING_TEXTURE, "copy: unbound texture");
+  if (src->W != dst->W || src->H != dst->H) return err(PT_ERR_ARG, "copy: size mismatch");
+  (void)p;
+  int a = std::max(y0, std::max(src->row0, dst->row0));
+  int b = std::min(y1, std::min(src->row0 + src->rows, dst->row0 + dst->rows));
+  if (b > a) {
+    size_t rowb = (size_t)src->W * 16;
+    HIPCHK(hipMemcpyAsync((char*)dst->dev + (size_t)(a - dst->row0) * rowb,
+                          (char*)src->dev + (size_t)(a - src->row0) * rowb, (size_t)(b - a) * rowb,
+                          hipMemcpyDeviceToDevice, g.stream));
+  }
+  dst->version++;
+  dst->aux_valid = false;
+  if (src->aux_valid && src->aux) {  // keep the compact side plane in step with its texture
+    if (!dst->aux) HIPCHK(hipMalloc((void**)&dst->aux, (size_t)dst->W * dst->rows * 4));
+    if (b > a) {
+      size_t rb = (size_t)src->W * 4;
+      HIPCHK(hipMemcpyAsync((char*)dst->aux + (size_t)(a - dst->row0) * rb, (char*)src->aux + (size_t)(a - src->row0) * rb,
+                            (size_t)(b - a) * rb, hipMemcpyDeviceToDevice, g.stream));
+    }
+    dst->aux_valid = true;
+  }
+  return PT_OK;
+}
+
+// ------------------------------------------------------------- draw calls ---
+int draw_pathtrace(Pass* p) {
+  PTParams k;
+  memset(&k, 0, sizeof(k));
+  k.W = p->W;
+  k.H = p->H;
+  rows_of(p, &k.y0, &k.y1);
+  TRY(att_plane(p, 0, &k.color));
+  TRY(att_plane(p, 1, &k.emission));
+  TRY(att_plane(p, 2, &k.albedo));
+  uint32_t th, nh, lh;
+  Texture* tt = sampler(p, "triangles", &th);
+  Texture* nt = sampler(p, "nodes", &nh);
+  Texture* lt = sampler(p, "pointLights", &lh);
+  if (!tt || tt->target != PT_TEXTURE_BUFFER || !nt || nt->target != PT_TEXTURE_BUFFER)
+    return err(PT_ERR_MISSING_TEXTURE, "path_tracing needs the 'triangles' and 'nodes' texture buffers");
+  SceneGPU* sg;
+  TRY(get_scene(tt, th, nt, nh, &sg));
+  k.scene.tri_geom = sg->geom;
+  k.scene.tri_shade = sg->shade;
+  k.scene.bvh = sg->bvh;
+  k.scene.root_ref = sg->root_ref;
+  k.scene.ntris = sg->ntris;
+  if (lt && lt->target == PT_TEXTURE_BUFFER) {
+    k.scene.lights = (const float*)lt->dev;
+    k.scene.nlights_buf = (int)(lt->bytes / (6 * sizeof(float)));
+  }
+  Texture* hm = sampler(p, "hdrMap");
+  Texture* hc = sampler(p, "hdrCache");
+  if (!hm || !hc || !hm->dev || !hc->dev) return err(PT_ERR_MISSING_TEXTURE, "path_tracing needs hdrMap and hdrCache");
+  k.hdr = Tex{(const float4*)hm->dev, hm->W, hm->H};
+  k.cache = Tex{(const float4*)hc->dev, hc->W, hc->H};
+  k.hdrResolution = ui(p, "hdrResolution", hm->W);
+  k.pointLightSize = ui(p, "pointLightSize", 0);
+  k.frameCounter = uu(p, "frameCounter", 0);
+  const Uniform* e = U(p, "eye", 5);
+  if (e) memcpy(k.eye, e->f, 12);
+  const Uniform* cr = U(p, "cameraRotate", 6);
+  if (cr) memcpy(k.camRot, cr->f, 64);
+  else { k.camRot[0] = k.camRot[5] = k.camRot[10] = k.camRot[15] = 1.0f; }
+  k.accumulate = ui(p, "accumulate", 0);
+  k.clamp_threshold = uf(p, "clamp_threshold", 0.0f);
+  k.max_depth = ui(p, "max_tracing_depth", 0);
+  if (k.max_depth > 4) return err(PT_ERR_ARG, "max_tracing_depth > 4 indexes past the 8 Sobol dimensions (:463)");
+  k.aspect_corrected = ui(p, "aspect_corrected", 0);
+  k.prune = ui(p, "prune", 1);
+  for (int b = 0; b < 4; ++b) {
+    uint32_t i = k.frameCounter + 1u;
+    uint32_t gc = i ^ (i >> 1);
+    k.sobol_u[b] = sobol_host(2u * b, gc);
+    k.sobol_v[b] = sobol_host(2u * b + 1u, gc);
+  }
+  if (k.accumulate) {
+    Texture* lf = sampler(p, "lastFrame");
+    if (lf) TRY(plane_of(lf, p, &k.last, "lastFrame"));
+  }
+  int rc = launch_pathtrace(k, g.stream);
+  return rc ? hip_err((hipError_t)rc, "pathtrace launch") : PT_OK;
+}
+
+int draw_raster(Pass* p) {
+  if (!p->raster.geom && p->raster.ntris > 0) return err(PT_ERR_STATE, "raster pass not bound");
+  GBufParams k;
+  memset(&k, 0, sizeof(k));
+  k.W = p->W;
+  k.H = p->H;
+  rows_of(p, &k.y0, &k.y1);
+  TRY(att_plane(p, 0, &k.world));
+  TRY(att_plane(p, 1, &k.normal_depth));
+  TRY(att_plane(p, 2, &k.motion));
+  TRY(att_plane(p, 3, &k.fwidth));
+  Texture* fwt = tex_of(p->att[3]);
+  if (!fwt->aux) HIPCHK(hipMalloc((void**)&fwt->aux, (size_t)fwt->W * fwt->rows * 4));
+  k.fwidth_aux = fwt->aux;
+  k.geom = p->raster.geom;
+  k.bvh = p->raster.bvh;
+  k.root_ref = p->raster.root_ref;
+  float V[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1}, P[16], PV[16];
+  memcpy(P, V, 64);
+  memcpy(PV, V, 64);
+  if (const Uniform* u = U(p, "view", 6)) memcpy(V, u->f, 64);
+  if (const Uniform* u = U(p, "projection", 6)) memcpy(P, u->f, 64);
+  if (const Uniform* u = U(p, "pre_viewproj", 6)) memcpy(PV, u->f, 64);
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) k.invR[r * 3 + c] = V[r * 4 + c];
+  for (int r = 0; r < 3; ++r)
+    k.eye[r] = -((k.invR[r * 3] * V[12] + k.invR[r * 3 + 1] * V[13]) + k.invR[r * 3 + 2] * V[14]);
+  k.P00 = P[0];
+  k.P11 = P[5];
+  for (int c = 0; c < 4; ++c)
+    for (int r = 0; r < 4; ++r)
+      k.M[c * 4 + r] = ((P[0 * 4 + r] * V[c * 4 + 0] + P[1 * 4 + r] * V[c * 4 + 1]) + P[2 * 4 + r] * V[c * 4 + 2]) +
+                       P[3 * 4 + r] * V[c * 4 + 3];
+  memcpy(k.PV, PV, 64);
+  if (p->raster.ntris == 0) k.root_ref = -1;  // empty leaf
+  int rc = launch_gbuffer(k, g.stream);
+  if (rc) return hip_err((hipError_t)rc, "gbuffer launch");
+  fwt->aux_valid = true;
+  return PT_OK;
+}
+
+int draw_svgf(Pass* p, int kind) {
+  int y0, y1;
+  rows_of(p, &y0, &y1);
+  int rc = 0;
+  if (kind == PK_REPROJECT) {
+    ReprojParams k;
+    memset(&k, 0, sizeof(k));
+    k.W = p->W; k.H = p->H; k.y0 = y0; k.y1 = y1;
+    TRY(plane_of(sampler(p, "gMotion"), p, &k.motion, "gMotion"));
+    TRY(plane_of(sampler(p, "gColor"), p, &k.color, "gColor"));
+    TRY(plane_of(sampler(p, "gAlbedo"), p, &k.albedo, "gAlbedo"));
+    TRY(plane_of(sampler(p, "gEmission"), p, &k.emission, "gEmission"));
+    TRY(plane_of(sampler(p, "gPrevIllum"), p, &k.prev_illum, "gPrevIllum"));
+    TRY(plane_of(sampler(p, "gPrevMoments_HistoryLength"), p, &k.prev_moments, "gPrevMoments_HistoryLength"));
+    TRY(plane_of(sampler(p, "gNormalAndLinearZ"), p, &k.nd, "gNormalAndLinearZ"));
+    TRY(plane_of(sampler(p, "gPrevNormalAndLinearZ"), p, &k.prev_nd, "gPrevNormalAndLinearZ"));
+    TRY(plane_of(sampler(p, "gNormalDepthFwidth"), p, &k.fwidth, "gNormalDepthFwidth"));
+    TRY(att_plane(p, 0, &k.out_illum));
+    TRY(att_plane(p, 1, &k.out_moments));
+    k.inv_w = uf(p, "inv_screen_width", 0.0f);
+    k.inv_h = uf(p, "inv_screen_height", 0.0f);
+    k.depth_thr = uf(p, "depth_threshold", 0.0f);
+    k.normal_thr = uf(p, "normal_threshold", 0.0f);
+    rc = launch_reproject(k, g.stream);
+  } else if (kind == PK_VARIANCE) {
+    VarianceParams k;
+    memset(&k, 0, sizeof(k));
+    k.W = p->W; k.H = p->H; k.y0 = y0; k.y1 = y1;
+    TRY(plane_of(sampler(p, "gIllumination"), p, &k.illum, "gIllumination"));
+    TRY(plane_of(sampler(p, "gMoments_HistoryLength"), p, &k.moments, "gMoments_HistoryLength"));
+    TRY(plane_of(sampler(p, "gNormalAndLinearZ"), p, &k.nd, "gNormalAndLinearZ"));
+    TRY(plane_of(sampler(p, "gNormalDepthFwidth"), p, &k.fwidth, "gNormalDepthFwidth"));
+    TRY(att_plane(p, 0, &k.out));
+    k.phi_color = uf(p, "gPhiColor", 0.0f);
+    k.phi_normal = uf(p, "gPhiNormal", 0.0f);
+    rc = launch_variance(k, g.stream);
+  } else if (kind == PK_ATROUS) {
+    AtrousParams k;
+    memset(&k, 0, sizeof(k));
+    k.W = p->W; k.H = p->H; k.y0 = y0; k.y1 = y1;
+    TRY(plane_of(sampler(p, "gIllumination"), p, &k.illum, "gIllumination"));
+    TRY(plane_of(sampler(p, "gNormalAndLinearZ"), p, &k.nd, "gNormalAndLinearZ"));
+    TRY(plane_of(sampler(p, "gNormalDepthFwidth"), p, &k.fwidth, "gNormalDepthFwidth"));
+    TRY(att_plane(p, 0, &k.out));
+    if (k.out.p == k.illum.p) return err(PT_ERR_ARG, "a-trous output aliases its input (GL feedback loop)");
+    k.step = ui(p, "gStepSize", 1);
+    k.phi_color = uf(p, "gPhiColor", 0.0f);
+    k.phi_normal = uf(p, "gPhiNormal", 0.0f);
+    rc = ui(p, "exact", 0) ? launch_atrous_exact(k, g.stream) : launch_atrous_fast(k, g.stream);
+  } else if (kind == PK_MODULATE) {
+    ModulateParams k;
+    memset(&k, 0, sizeof(k));
+    k.W = p->W; k.H = p->H; k.y0 = y0; k.y1 = y1;
+    TRY(plane_of(sampler(p, "gAlbedo"), p, &k.albedo, "gAlbedo"));
+    TRY(plane_of(sampler(p, "gEmission"), p, &k.emission, "gEmission"));
+    TRY(plane_of(sampler(p, "gIllumination"), p, &k.illum, "gIllumination"));
+    TRY(plane_of(sampler(p, "gNormalAndLinearZ"), p, &k.nd, "gNormalAndLinearZ"));
+    TRY(att_plane(p, 0, &k.out));
+    rc = launch_modulate(k, g.stream);
+  } else if (kind == PK_OUTPUT) {
+    OutputParams k;
+    memset(&k, 0, sizeof(k));
+    k.W = p->W; k.H = p->H; k.y0 = y0; k.y1 = y1;
+    TRY(plane_of(sampler(p, "texPass0"), p, &k.in, "texPass0"));
+    if (p->att.empty()) return PT_OK;  // default framebuffer: nothing to keep
+    TRY(att_plane(p, 0, &k.out));
+    rc = launch_output(k, g.stream);
+  } else if (kind == PK_TAA) {
+    TAAParams k;
+    memset(&k, 0, sizeof(k));
+    k.W = p->W; k.H = p->H; k.y0 = y0; k.y1 = y1;
+    TRY(plane_of(sampler(p, "currentColor"), p, &k.cur, "currentColor"));
+    TRY(plane_of(sampler(p, "previousColor"), p, &k.prev, "previousColor"));
+    TRY(plane_of(sampler(p, "velocityTexture"), p, &k.vel, "velocityTexture"));
+    TRY(plane_of(sampler(p, "normal_depth"), p, &k.nd, "normal_depth"));
+    TRY(att_plane(p, 0, &k.out));
+    k.frameCounter = uu(p, "frameCounter", 0);
+    rc = launch_taa(k, g.stream);
+  } else if (kind == PK_BLIT) {
+    if (p->att.empty()) return err(PT_ERR_ARG, "bilt pass without attachment");
+    TRY(copy_plane(tex_of(p->att[0]), sampler(p, "in_texture"), p, y0, y1));
+  } else if (kind == PK_SAVE) {
+    const char* names[5] = {"texPass0", "texPass1", "texPass2", "accColor", "taaOutput"};
+    for (int i = 0; i < 5 && i < (int)p->att.size(); ++i)
+      TRY(copy_plane(tex_of(p->att[i]), sampler(p, names[i]), p, y0, y1));
+  }
+  return rc ? hip_err((hipError_t)rc, "kernel launch") : PT_OK;
+}
+
+Uniform* set_u(uint32_t pass, const char* name, int type, int* rc) {
+  *rc = ensure_init();
+  if (*rc != PT_OK) return nullptr;
+  Pass* p = pass_of(pass);
+  if (!p) { *rc = err(PT_ERR_INVALID_HANDLE, "invalid pass"); return nullptr; }
+  if (!name) { *rc = err(PT_ERR_ARG, "null uniform name"); return nullptr; }
+  Uniform& u = p->uni[name];
+  u.type = type;
+  return &u;
+}
+
+}  // namespace
+
+// ================================================================= C ABI ===
+extern "C" {
+
+const char* pt_last_error(void) { return g_err.c_str(); }
+int pt_version(void) { return 1; }
+
+int pt_init(int device) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (g.init) return PT_OK;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return err(PT_ERR_NO_DEVICE, "no HIP device visible");
+  if (device < 0 || device >= n) return err(PT_ERR_ARG, "device index out of range");
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipStreamCreateWithFlags(&g.own, hipStreamNonBlocking));
+  g.stream = g.own;
+  g.device = device;
+  g.init = true;
+  return PT_OK;
+}
+
+int pt_shutdown(void) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!g.init) return PT_OK;
+  (void)hipDeviceSynchronize();
+  for (auto& kv : g.textures) {
+    Texture* t = kv.second.get();
+    if (t->owned && t->dev) (void)hipFree(t->dev);
+    if (t->aux) (void)hipFree(t->aux);
+  }
+  for (auto& kv : g.passes) {
+    Pass* p = kv.second.get();
+    if (p->raster.geom) (void)hipFree(p->raster.geom);
+    if (p->raster.bvh) (void)hipFree(p->raster.bvh);
+    if (p->ev0) (void)hipEventDestroy(p->ev0);
+    if (p->ev1) (void)hipEventDestroy(p->ev1);
+  }
+  for (auto& kv : g.scenes) {
+    if (kv.second.geom) (void)hipFree(kv.second.geom);
+    if (kv.second.shade) (void)hipFree(kv.second.shade);
+    if (kv.second.bvh) (void)hipFree(kv.second.bvh);
+  }
+  if (g.own) (void)hipStreamDestroy(g.own);
+  g = Lib();
+  return PT_OK;
+}
+
+int pt_set_stream(void* s) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  g.stream = s ? (hipStream_t)s : g.own;
+  return PT_OK;
+}
+
+int pt_sync(void) {
+  TRY(ensure_init());
+  HIPCHK(hipStreamSynchronize(g.stream));
+  return PT_OK;
+}
+
+int pt_set_band(int fw, int fh, int y0, int y1, int row0, int rows) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (fw <= 0 || fh <= 0 || y0 < 0 || y1 > fh || y0 >= y1 || row0 < 0 || rows <= 0 || row0 + rows > fh ||
+      row0 > y0 || row0 + rows < y1)
+    return err(PT_ERR_ARG, "pt_set_band: inconsistent band");
+  g.band_w = fw; g.band_h = fh; g.band_y0 = y0; g.band_y1 = y1; g.band_row0 = row0; g.band_rows = rows;
+  return PT_OK;
+}
+
+int pt_set_profiling(int on) {
+  g.profiling = on != 0;
+  return PT_OK;
+}
+
+int pt_program_create(const char* frag, const char* vert, uint32_t* out) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  if (!out) return err(PT_ERR_ARG, "null out pointer");
+  std::string f = basename_of(frag), v = basename_of(vert);
+  static const std::map<std::string, int> kinds = {
+      {"path_tracing.frag", PK_PATHTRACE}, {"svgf_reproject.frag", PK_REPROJECT},
+      {"svgf_variance.frag", PK_VARIANCE}, {"svgf_Atrous.frag", PK_ATROUS},
+      {"svgf_modulate.frag", PK_MODULATE}, {"bilt.frag", PK_BLIT},
+      {"save_frame_data.frag", PK_SAVE},   {"output_pass.frag", PK_OUTPUT},
+      {"taa.frag", PK_TAA},                {"rasterize_frag.frag", PK_RASTER}};
+  auto it = kinds.find(f);
+  if (it == kinds.end()) return err(PT_ERR_UNKNOWN_PROGRAM, "no HIP kernel for fragment shader '" + f + "'");
+  const char* want = it->second == PK_RASTER ? "rasterize_vert.vert" : "vert.vert";
+  if (v != want) return err(PT_ERR_UNKNOWN_PROGRAM, "'" + f + "' must be linked with '" + want + "'");
+  uint32_t h = g.next++;
+  g.programs[h] = it->second;
+  *out = h;
+  return PT_OK;
+}
+
+static int new_texture(std::unique_ptr<Texture> t, uint32_t* out) {
+  uint32_t h = g.next++;
+  g.textures[h] = std::move(t);
+  *out = h;
+  return PT_OK;
+}
+
+int pt_texture2d_create(int w, int h, uint32_t* out) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  if (w <= 0 || h <= 0 || !out) return err(PT_ERR_ARG, "pt_texture2d_create: bad size");
+  auto t = std::make_unique<Texture>();
+  t->W = w;
+  t->H = h;
+  if (g.band_h > 0 && w == g.band_w && h == g.band_h) {
+    t->row0 = g.band_row0;
+    t->rows = g.band_rows;
+  } else {
+    t->row0 = 0;
+    t->rows = h;
+  }
+  t->bytes = (size_t)w * t->rows * 16;
+  HIPCHK(hipMalloc(&t->dev, t->bytes));
+  HIPCHK(hipMemsetAsync(t->dev, 0, t->bytes, g.stream));  // GL leaves it undefined; the build zeroes
+  return new_texture(std::move(t), out);
+}
+
+int pt_texture2d_wrap(void* ptr, int w, int h, uint32_t* out) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  if (!ptr || w <= 0 || h <= 0 || !out) return err(PT_ERR_ARG, "pt_texture2d_wrap: bad argument");
+  auto t = std::make_unique<Texture>();
+  t->W = w;
+  t->H = h;
+  if (g.band_h > 0 && w == g.band_w && h == g.band_h) {
+    t->row0 = g.band_row0;
+    t->rows = g.band_rows;
+  } else {
+    t->rows = h;
+  }
+  t->bytes = (size_t)w * t->rows * 16;
+  t->dev = ptr;
+  t->owned = false;
+  return new_texture(std::move(t), out);
+}
+
+int pt_texture2d_upload(uint32_t tex, int w, int h, uint32_t fmt, const float* data) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  Texture* t = tex_of(tex);
+  if (!t || t->target != PT_TEXTURE_2D) return err(PT_ERR_INVALID_HANDLE, "invalid 2-D texture");
+  if (!data) return err(PT_ERR_ARG, "null data");
+  if (fmt != PT_RGB32F && fmt != PT_RGBA32F && fmt != PT_RGB && fmt != PT_RGBA)
+    return err(PT_ERR_FORMAT, "upload format must be RGB32F or RGBA32F");
+  int nch = (fmt == PT_RGB32F || fmt == PT_RGB) ? 3 : 4;
+  if (w != t->W || h != t->H) {  // glTexImage2D respecifies the image
+    if (t->owned && t->dev) HIPCHK(hipFree(t->dev));
+    if (!t->owned) return err(PT_ERR_ARG, "cannot resize a wrapped texture");
+    t->W = w; t->H = h; t->row0 = 0; t->rows = h;
+    if (g.band_h > 0 && w == g.band_w && h == g.band_h) { t->row0 = g.band_row0; t->rows = g.band_rows; }
+    t->bytes = (size_t)w * t->rows * 16;
+    HIPCHK(hipMalloc(&t->dev, t->bytes));
+  }
+  std::vector<float4> buf((size_t)w * t->rows);
+  for (int r = 0; r < t->rows; ++r) {
+    const float* src = data + ((size_t)(t->row0 + r) * w) * nch;
+    for (int x = 0; x < w; ++x) {
+      const float* q = src + (size_t)x * nch;
+      buf[(size_t)r * w + x] = float4{q[0], q[1], q[2], nch == 4 ? q[3] : 1.0f};
+    }
+  }
+  HIPCHK(hipMemcpyAsync(t->dev, buf.data(), t->bytes, hipMemcpyHostToDevice, g.stream));
+  HIPCHK(hipStreamSynchronize(g.stream));
+  t->version++;
+  t->aux_valid = false;
+  return PT_OK;
+}
+
+int pt_texture_upload_rgba(uint32_t tex, const float* data, size_t bytes) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  Texture* t = tex_of(tex);
+  if (!t || t->target != PT_TEXTURE_2D) return err(PT_ERR_INVALID_HANDLE, "invalid 2-D texture");
+  if (!data || bytes != t->bytes) return err(PT_ERR_ARG, "upload size must equal the stored rows");
+  HIPCHK(hipMemcpyAsync(t->dev, data, bytes, hipMemcpyHostToDevice, g.stream));
+  HIPCHK(hipStreamSynchronize(g.stream));
+  t->version++;
+  t->aux_valid = false;
+  return PT_OK;
+}
+
+int pt_texbuffer_create(const void* data, size_t bytes, uint32_t fmt, uint32_t* out) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  if (fmt != PT_RGB32F) return err(PT_ERR_FORMAT, "texture buffers are RGB32F (main.cpp:142,151,168)");
+  if ((!data && bytes) || bytes % 12 || !out) return err(PT_ERR_ARG, "texbuffer size must be whole RGB32F texels");
+  auto t = std::make_unique<Texture>();
+  t->target = PT_TEXTURE_BUFFER;
+  t->bytes = bytes;
+  t->W = (int)(bytes / 12);
+  t->H = 1;
+  t->rows = 1;
+  if (bytes) {
+    t->host.assign((const uint8_t*)data, (const uint8_t*)data + bytes);
+    HIPCHK(hipMalloc(&t->dev, bytes));
+    HIPCHK(hipMemcpy(t->dev, data, bytes, hipMemcpyHostToDevice));
+  }
+  return new_texture(std::move(t), out);
+}
+
+int pt_texarray_create(int w, int h, int layers, uint32_t* out) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  if (w <= 0 || h <= 0 || layers <= 0 || !out) return err(PT_ERR_ARG, "pt_texarray_create: bad size");
+  auto t = std::make_unique<Texture>();
+  t->target = PT_TEXTURE_2D_ARRAY;
+  t->W = w; t->H = h; t->rows = h; t->layers = layers;
+  t->bytes = (size_t)w * h * layers * 4;
+  HIPCHK(hipMalloc(&t->dev, t->bytes));
+  HIPCHK(hipMemset(t->dev, 0, t->bytes));
+  return new_texture(std::move(t), out);
+}
+
+int pt_texarray_upload_layer(uint32_t tex, int layer, int w, int h, int ch, const uint8_t* data) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  Texture* t = tex_of(tex);
+  if (!t || t->target != PT_TEXTURE_2D_ARRAY) return err(PT_ERR_INVALID_HANDLE, "invalid texture array");
+  if (!data || layer < 0 || layer >= t->layers || w > t->W || h > t->H || (ch != 3 && ch != 4))
+    return err(PT_ERR_ARG, "pt_texarray_upload_layer: bad argument");
+  // glTexSubImage3D at the origin (help_func.h:12): a w x h sub-rectangle of the layer
+  std::vector<uint8_t> row((size_t)w * 4);
+  for (int y = 0; y < h; ++y) {
+    for (int x = 0; x < w; ++x) {
+      const uint8_t* q = data + ((size_t)y * w + x) * ch;
+      row[4 * x] = q[0]; row[4 * x + 1] = q[1]; row[4 * x + 2] = q[2]; row[4 * x + 3] = ch == 4 ? q[3] : 255;
+    }
+    HIPCHK(hipMemcpy((char*)t->dev + (((size_t)layer * t->H + y) * t->W) * 4, row.data(), row.size(),
+                     hipMemcpyHostToDevice));
+  }
+  t->version++;
+  return PT_OK;
+}
+
+int pt_texture_readback(uint32_t tex, float* out, size_t bytes) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  Texture* t = tex_of(tex);
+  if (!t || !t->dev) return err(PT_ERR_INVALID_HANDLE, "invalid texture");
+  if (!out || bytes < t->bytes) return err(PT_ERR_ARG, "readback buffer too small");
+  HIPCHK(hipStreamSynchronize(g.stream));
+  HIPCHK(hipMemcpy(out, t->dev, t->bytes, hipMemcpyDeviceToHost));
+  return PT_OK;
+}
+
+int pt_texture_device_ptr(uint32_t tex, void** out) {
+  Texture* t = tex_of(tex);
+  if (!t || !out) return err(PT_ERR_INVALID_HANDLE, "invalid texture");
+  *out = t->dev;
+  return PT_OK;
+}
+
+int pt_texture_info(uint32_t tex, int* w, int* h, int* row0) {
+  Texture* t = tex_of(tex);
+  if (!t) return err(PT_ERR_INVALID_HANDLE, "invalid texture");
+  if (w) *w = t->W;
+  if (h) *h = t->rows;
+  if (row0) *row0 = t->row0;
+  return PT_OK;
+}
+
+int pt_texture_destroy(uint32_t tex) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  auto it = g.textures.find(tex);
+  if (it == g.textures.end()) return err(PT_ERR_INVALID_HANDLE, "invalid texture");
+  (void)hipStreamSynchronize(g.stream);
+  if (it->second->owned && it->second->dev) (void)hipFree(it->second->dev);
+  if (it->second->aux) (void)hipFree(it->second->aux);
+  g.textures.erase(it);
+  return PT_OK;
+}
+
+int pt_pass_create(uint32_t program, int w, int h, uint32_t* out) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  if (!g.programs.count(program)) return err(PT_ERR_INVALID_HANDLE, "invalid program");
+  if (w <= 0 || h <= 0 || !out) return err(PT_ERR_ARG, "pt_pass_create: bad size");
+  auto p = std::make_unique<Pass>();
+  p->program = program;
+  p->W = w;
+  p->H = h;
+  uint32_t hnd = g.next++;
+  g.passes[hnd] = std::move(p);
+  *out = hnd;
+  return PT_OK;
+}
+
+int pt_pass_add_color_attachment(uint32_t pass, uint32_t tex) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  Pass* p = pass_of(pass);
+  if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
+  if (!tex_of(tex)) return err(PT_ERR_INVALID_HANDLE, "invalid texture");
+  p->att.push_back(tex);
+  return PT_OK;
+}
+
+int pt_pass_bind(uint32_t pass, int final_pass) {
+  Pass* p = pass_of(pass);
+  if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
+  p->bound = true;
+  p->final_pass = final_pass != 0;
+  return PT_OK;
+}
+
+int pt_raster_pass_bind(uint32_t pass, const float* verts, size_t n_floats) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  Pass* p = pass_of(pass);
+  if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
+  if (g.programs[p->program] != PK_RASTER) return err(PT_ERR_ARG, "not a rasterize pass");
+  if (n_floats % 18) return err(PT_ERR_ARG, "vertex list must be whole triangles of pos3+nrm3");
+  int ntris = (int)(n_floats / 18);
+  p->raster.ntris = ntris;
+  p->bound = true;
+  if (ntris == 0) return PT_OK;
+  // SAH BVH over the raster triangles (same builder as the scene), objIndex = original index
+  const float mat[PTS_MATERIAL_FLOATS] = {0};
+  pts_scene* s = pts_scene_create();
+  if (pts_scene_add_raw(s, verts, ntris, mat, -1) != 0 || pts_scene_build_bvh(s, 8) != 0) {
+    std::string m = pts_last_error();
+    pts_scene_destroy(s);
+    return err(PT_ERR_ARG, "raster BVH: " + m);
+  }
+  int64_t cnt[6];
+  pts_scene_counts(s, cnt);
+  std::vector<float> te((size_t)cnt[0] * 45), ne((size_t)cnt[1] * 12);
+  pts_scene_encode(s, te.data(), ne.data(), nullptr);
+  pts_scene_destroy(s);
+  using namespace glsl;
+  std::vector<float4> geom((size_t)ntris * 7);
+  for (int i = 0; i < ntris; ++i) {
+    const float* f = &te[(size_t)i * 45];
+    v3 p1 = mk(f[0], f[1], f[2]), p2 = mk(f[3], f[4], f[5]), p3 = mk(f[6], f[7], f[8]);
+    v3 e1 = sub(p2, p1), e2 = sub(p3, p1), ng = cross(e1, e2);
+    int oi = (int)f[42];
+    float oif;
+    memcpy(&oif, &oi, 4);
+    float4* q = &geom[(size_t)i * 7];
+    q[0] = float4{p1.x, p1.y, p1.z, oif};
+    q[1] = float4{e1.x, e1.y, e1.z, 0};
+    q[2] = float4{e2.x, e2.y, e2.z, 0};
+    q[3] = float4{ng.x, ng.y, ng.z, 0};
+    q[4] = float4{f[9], f[10], f[11], 0};
+    q[5] = float4{f[12], f[13], f[14], 0};
+    q[6] = float4{f[15], f[16], f[17], 0};
+  }
+  std::vector<float4> bvh;
+  int root = 0;
+  TRY(pack_bvh(ne.data(), (int)cnt[1], bvh, &root, ntris));
+  if (bvh.empty()) bvh.push_back(float4{0, 0, 0, 0});
+  TRY(upload_vec(geom, &p->raster.geom));
+  TRY(upload_vec(bvh, &p->raster.bvh));
+  p->raster.root_ref = root;
+  return PT_OK;
+}
+
+int pt_pass_reset_texture_slot(uint32_t pass) {
+  Pass* p = pass_of(pass);
+  if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
+  p->slot = 0;
+  return PT_OK;
+}
+
+int pt_pass_set_texture(uint32_t pass, uint32_t target, uint32_t tex, const char* name) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  Pass* p = pass_of(pass);
+  if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
+  Texture* t = tex_of(tex);
+  if (!t) return err(PT_ERR_INVALID_HANDLE, "invalid texture");
+  if (!name) return err(PT_ERR_ARG, "null sampler name");
+  if (target != t->target) return err(PT_ERR_FORMAT, "texture bound to the wrong target");
+  if (p->slot == 0) g.unit0 = tex;  // glActiveTexture(GL_TEXTURE0 + slot) is global state
+  p->slot++;
+  p->tex[name] = tex;
+  return PT_OK;
+}
+
+int pt_pass_set_uniform_mat4(uint32_t pass, const char* name, const float* m) {
+  int rc;
+  Uniform* u = set_u(pass, name, 6, &rc);
+  if (!u) return rc;
+  if (!m) return err(PT_ERR_ARG, "null matrix");
+  memcpy(u->f, m, 64);
+  return PT_OK;
+}
+int pt_pass_set_uniform_float(uint32_t pass, const char* name, float v) {
+  int rc;
+  Uniform* u = set_u(pass, name, 1, &rc);
+  if (!u) return rc;
+  u->f[0] = v;
+  return PT_OK;
+}
+int pt_pass_set_uniform_int(uint32_t pass, const char* name, int v) {
+  int rc;
+  Uniform* u = set_u(pass, name, 2, &rc);
+  if (!u) return rc;
+  u->i = v;
+  return PT_OK;
+}
+int pt_pass_set_uniform_uint(uint32_t pass, const char* name, uint32_t v) {
+  int rc;
+  Uniform* u = set_u(pass, name, 3, &rc);
+  if (!u) return rc;
+  u->u = v;
+  return PT_OK;
+}
+int pt_pass_set_uniform_bool(uint32_t pass, const char* name, int v) {
+  int rc;
+  Uniform* u = set_u(pass, name, 4, &rc);
+  if (!u) return rc;
+  u->i = v != 0;
+  return PT_OK;
+}
+int pt_pass_set_uniform_vec3(uint32_t pass, const char* name, const float* v) {
+  int rc;
+  Uniform* u = set_u(pass, name, 5, &rc);
+  if (!u) return rc;
+  if (!v) return err(PT_ERR_ARG, "null vector");
+  memcpy(u->f, v, 12);
+  return PT_OK;
+}
+
+int pt_pass_set_rows(uint32_t pass, int y0, int y1) {
+  Pass* p = pass_of(pass);
+  if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
+  if (y0 < 0 && y1 < 0) { p->y_begin = p->y_end = -1; return PT_OK; }
+  if (y0 < 0 || y1 > p->H || y0 > y1) return err(PT_ERR_ARG, "pt_pass_set_rows: bad range");
+  p->y_begin = y0;
+  p->y_end = y1;
+  return PT_OK;
+}
+
+int pt_pass_draw(uint32_t pass) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  Pass* p = pass_of(pass);
+  if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
+  if (!p->bound) return err(PT_ERR_STATE, "pass drawn before bindData");
+  int kind = g.programs[p->program];
+  if (g.profiling) {
+    if (!p->ev0) { HIPCHK(hipEventCreate(&p->ev0)); HIPCHK(hipEventCreate(&p->ev1)); }
+    HIPCHK(hipEventRecord(p->ev0, g.stream));
+  }
+  int rc;
+  if (kind == PK_PATHTRACE) rc = draw_pathtrace(p);
+  else if (kind == PK_RASTER) rc = draw_raster(p);
+  else rc = draw_svgf(p, kind);
+  if (rc != PT_OK) return rc;
+  if (g.profiling) {
+    HIPCHK(hipEventRecord(p->ev1, g.stream));
+    p->timed = true;
+  }
+  return PT_OK;
+}
+
+int pt_pass_last_ms(uint32_t pass, float* ms) {
+  Pass* p = pass_of(pass);
+  if (!p || !ms) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
+  if (!p->timed) return err(PT_ERR_STATE, "pass has no timed draw (pt_set_profiling(1))");
+  HIPCHK(hipEventSynchronize(p->ev1));
+  HIPCHK(hipEventElapsedTime(ms, p->ev0, p->ev1));
+  return PT_OK;
+}
+
+int pt_pass_destroy(uint32_t pass) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  auto it = g.passes.find(pass);
+  if (it == g.passes.end()) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
+  (void)hipStreamSynchronize(g.stream);
+  Pass* p = it->second.get();
+  if (p->raster.geom) (void)hipFree(p->raster.geom);
+  if (p->raster.bvh) (void)hipFree(p->raster.bvh);
+  if (p->ev0) (void)hipEventDestroy(p->ev0);
+  if (p->ev1) (void)hipEventDestroy(p->ev1);
+  g.passes.erase(it);
+  return PT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,138 @@
+// pt_device.h — parameter blocks and HBM layouts shared by the C-ABI layer
+// (capi.hip) and the kernels. Everything here is plain data; no torch types.
+//
+// HBM layout (DESIGN.md "Data layout"):
+//  * frame planes: RGBA32F (float4) row-major, one plane per GL texture, holding
+//    global rows [row0, row0+rows) of a W x H frame (row0 = 0, rows = H on 1 GPU);
+//  * optional compact side plane `aux` (float, 4 B/px) next to a plane whose only
+//    consumer-visible channel is .y (the depth fwidth of gNormalDepthFwidth):
+//    written by the G-buffer kernel, read by the a-trous kernel instead of the
+//    16-B texel (52 B/px/iteration instead of 64);
+//  * scene: tri_geom  4 x float4 / triangle  (p1,N.p1)(p2,-)(p3,-)(N,-)  intersection
+//           tri_shade 9 x float4 / triangle  normals, material, uv, objIndex  closest hit only
+//           bvh       4 x float4 / interior node: both children's AABBs + child refs
+//    (children refs >= 0: interior index; < 0: leaf = -(first*16 + count) - 1);
+//  * HDR map / importance cache: float4 per texel (RGB32F padded), row-major.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#else
+struct float4 {
+  float x, y, z, w;
+};
+#endif
+
+namespace ptk {
+
+constexpr int kStack = 32;       // traversal stack depth (host checks BVH depth < kStack)
+constexpr int kBlock = 256;      // threads per block for per-pixel kernels
+
+struct Plane {          // banded RGBA32F plane
+  float4* p;
+  const float* aux;     // optional compact channel (see above), may be null
+  int W;                // row width (pixels)
+  int row0;             // global row of local row 0
+  int rows;             // allocated rows
+};
+
+struct Tex {            // non-banded float4 image (HDR map / cache)
+  const float4* p;
+  int W, H;
+};
+
+struct SceneDev {
+  const float4* tri_geom;
+  const float4* tri_shade;
+  const float4* bvh;
+  int root_ref;         // >= 0 interior node index, < 0 leaf ref
+  int ntris;
+  const float* lights;  // 6 floats per light (PointLight: position, radiance)
+  int nlights_buf;      // lights actually present in the buffer
+};
+
+struct PTParams {
+  int W, H, y0, y1;     // frame size (global) and rows to compute
+  Plane color, emission, albedo, last;  // outputs (+ lastFrame input)
+  SceneDev scene;
+  Tex hdr, cache;
+  int hdrResolution;
+  int pointLightSize;
+  uint32_t frameCounter;
+  float eye[3];
+  float camRot[16];     // column-major inverse(view)
+  int accumulate;
+  float clamp_threshold;
+  int max_depth;
+  int aspect_corrected;
+  int prune;            // closest-hit pruning (parity-safe margin)
+  float sobol_u[4], sobol_v[4];  // sobolVec2(frameCounter+1, b): uniform across pixels
+};
+
+struct GBufParams {
+  int W, H, y0, y1;
+  Plane world, normal_depth, motion, fwidth;
+  float* fwidth_aux;    // compact depth-fwidth plane (rows of fwidth), may be null
+  const float4* geom;   // 7 x float4 per raster triangle: (p1,idx)(e1,-)(e2,-)(Ng,-)(n1)(n2)(n3)
+  const float4* bvh;
+  int root_ref;
+  float eye[3];
+  float invR[9];        // row-major R^T (camera-to-world rotation)
+  float P00, P11;       // projection diagonal (pixel ray scale)
+  float M[16];          // projection * view (column-major)
+  float PV[16];         // pre_viewproj
+};
+
+struct ReprojParams {
+  int W, H, y0, y1;
+  Plane motion, color, albedo, emission, prev_illum, prev_moments, nd, prev_nd, fwidth;
+  Plane out_illum, out_moments;
+  float inv_w, inv_h, depth_thr, normal_thr;
+};
+
+struct VarianceParams {
+  int W, H, y0, y1;
+  Plane illum, moments, nd, fwidth, out;
+  float phi_color, phi_normal;
+};
+
+struct AtrousParams {
+  int W, H, y0, y1;
+  Plane illum, nd, fwidth, out;
+  int step;
+  float phi_color, phi_normal;
+};
+
+struct ModulateParams {
+  int W, H, y0, y1;
+  Plane albedo, emission, illum, nd, out;
+};
+
+struct OutputParams {
+  int W, H, y0, y1;
+  Plane in, out;
+};
+
+struct TAAParams {
+  int W, H, y0, y1;
+  Plane cur, prev, vel, nd, out;
+  uint32_t frameCounter;
+};
+
+}  // namespace ptk
+
+#if defined(__HIPCC__)
+namespace ptk {
+// Launchers (kernels_*.hip). Return hipError_t as int.
+int launch_pathtrace(const PTParams& p, hipStream_t s);
+int launch_gbuffer(const GBufParams& p, hipStream_t s);
+int launch_reproject(const ReprojParams& p, hipStream_t s);
+int launch_variance(const VarianceParams& p, hipStream_t s);
+int launch_atrous_exact(const AtrousParams& p, hipStream_t s);
+int launch_atrous_fast(const AtrousParams& p, hipStream_t s);
+int launch_modulate(const ModulateParams& p, hipStream_t s);
+int launch_output(const OutputParams& p, hipStream_t s);
+int launch_taa(const TAAParams& p, hipStream_t s);
+}  // namespace ptk
+#endif

@@ -1,0 +1,386 @@
+"""Headless ``main.cpp``: the reference's startup (main.cpp:65-338) and frame
+loop (main.cpp:436-602) driven through the drop-in C ABI.
+
+Two drivers over the same kernels:
+
+* :class:`Renderer` (``mode="reference"``) issues the reference's exact call
+  sequence — every pass, every ping-pong ``bilt`` copy, the iteration-1 history
+  copy and the 5-target ``save_frame_data`` copy (main.cpp:499-553). This is
+  what a C++ ``main.cpp`` linked against libptsvgf.so does.
+* ``mode="fast"`` keeps the identical math but replaces the copies with
+  double-buffered targets (pointer swaps, SURVEY.md §2 "build replaces with
+  pointer swaps"): same outputs bit for bit (tests/test_gpu_frame.py), fewer
+  HBM bytes per frame. This is the benchmarked path.
+
+TAA and the output tonemap run in both modes (main.cpp:537-590).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import gl
+from .camera import Camera, mat_mul, parameter_config, rigid_inverse
+from .gl import GL_TEXTURE_2D, GL_TEXTURE_BUFFER, RenderPass, Rasterize_RenderPass, getShaderProgram, getTextureRGB32F
+from .scene import Scene
+
+SHADERS = "./shaders/"
+
+
+def _prog(frag: str, vert: str = "vert.vert") -> int:
+    return getShaderProgram(SHADERS + frag, SHADERS + vert)
+
+
+class Renderer:
+    def __init__(self, scene: Scene, width: int, height: int, config: parameter_config | None = None,
+                 mode: str = "fast", aspect_corrected: bool | None = None, band=None, prune: bool = True,
+                 atrous_exact: bool = False, run_taa: bool = True, run_output: bool = True):
+        """band = (y0, y1, row0, rows) for screen-band sharding (see ptsvgf.dist)."""
+        if mode not in ("fast", "reference"):
+            raise ValueError(mode)
+        if mode == "fast" and config is not None and config.accumulate_color:
+            raise NotImplementedError("accumulate mode runs through mode='reference' (SURVEY.md §8(f) item 3)")
+        self.mode = mode
+        self.W, self.H = int(width), int(height)
+        self.cfg = config or parameter_config()
+        self.camera = Camera(self.W, self.H)
+        self.aspect_corrected = (self.W != self.H) if aspect_corrected is None else bool(aspect_corrected)
+        self.prune = prune
+        self.atrous_exact = atrous_exact
+        self.run_taa = run_taa
+        self.run_output = run_output
+        self.scene = scene
+        if band is not None:
+            y0, y1, row0, rows = band
+            gl.set_band(self.W, self.H, y0, y1, row0, rows)
+        self.band = band
+        W, H = self.W, self.H
+        tex = getTextureRGB32F
+
+        # scene buffers (main.cpp:136-181)
+        self.trianglesTextureBuffer = gl.texture_buffer(scene.tri_enc)
+        self.nodesTextureBuffer = gl.texture_buffer(scene.node_enc)
+        self.pointLightBuffer = gl.texture_buffer(scene.lights)
+        hh, hw, _ = scene.hdr.shape
+        self.hdrMap = tex(hw, hh)
+        gl.upload_rgb32f(self.hdrMap, scene.hdr)
+        self.hdrCache = tex(hw, hh)
+        gl.upload_rgb32f(self.hdrCache, scene.cache)
+        self.hdrResolution = hw
+
+        nbuf = 2 if mode == "fast" else 1
+        # G-buffer (main.cpp:208-226); fast mode double-buffers it (prev normal/depth = other parity)
+        self.init_pass = []
+        self.gbuf = []
+        raster_prog = _prog("rasterize_frag.frag", "rasterize_vert.vert")
+        for b in range(nbuf):
+            g = dict(world=tex(W, H), normal_depth=tex(W, H), velocity=tex(W, H), fwidth=tex(W, H))
+            p = Rasterize_RenderPass(raster_prog, W, H)
+            p.colorAttachments += [g["world"], g["normal_depth"], g["velocity"], g["fwidth"]]
+            p.bindData(scene.raster)
+            p.set_uniform_int("screen_width", W)
+            p.set_uniform_int("screen_height", H)
+            self.init_pass.append(p)
+            self.gbuf.append(g)
+
+        # path tracer (main.cpp:229-248)
+        self.pass_path_tracing = RenderPass(_prog("path_tracing.frag"), W, H)
+        self.curColor, self.Emission, self.Albedo = tex(W, H), tex(W, H), tex(W, H)
+        self.pass_path_tracing.colorAttachments += [self.curColor, self.Emission, self.Albedo]
+        self.pass_path_tracing.bindData(False)
+        pt = self.pass_path_tracing
+        pt.set_uniform_int("nTriangles", scene.ntris)
+        pt.set_uniform_int("nNodes", scene.node_enc.shape[0])
+        pt.set_uniform_int("width", W)
+        pt.set_uniform_int("height", H)
+        pt.set_uniform_int("pointLightSize", scene.lights.shape[0])
+        pt.set_uniform_int("aspect_corrected", int(self.aspect_corrected))
+        pt.set_uniform_int("prune", int(prune))
+
+        # SVGF targets
+        if mode == "reference":
+            self._build_reference_passes()
+        else:
+            self._build_fast_passes()
+        # output / tonemap (main.cpp:336-338); a readable target instead of the default framebuffer
+        self.output_tex = tex(W, H)
+        self.output_pass = RenderPass(_prog("output_pass.frag"), W, H)
+        self.output_pass.colorAttachments.append(self.output_tex)
+        self.output_pass.bindData(True)
+        self.pre_viewproj = mat_mul(self.camera.cam_proj_mat, self.camera.cam_view_mat)  # main.h:48
+        self.frame_index = 0
+
+    # ------------------------------------------------------------ passes ---
+    def _svgf_pass(self, frag: str, atts) -> RenderPass:
+        p = RenderPass(_prog(frag), self.W, self.H)
+        p.colorAttachments += list(atts)
+        p.bindData(False)
+        return p
+
+    def _build_reference_passes(self):
+        W, H, tex = self.W, self.H, getTextureRGB32F
+        self.tmp_atrous_result = tex(W, H)
+        self.bilt_pass = self._svgf_pass("bilt.frag", [self.tmp_atrous_result])
+        self.next_frame_color_input = tex(W, H)
+        self.save_next_frame_pass = self._svgf_pass("bilt.frag", [self.next_frame_color_input])
+        self.taa_output = tex(W, H)
+        self.pass_taa = self._svgf_pass("taa.frag", [self.taa_output])
+        self.pass_taa.set_uniform_int("screen_width", W)
+        self.pass_taa.set_uniform_int("screen_height", H)
+        self.curIllumination, self.curMomentHistory = tex(W, H), tex(W, H)
+        self.reproject_pass = self._svgf_pass("svgf_reproject.frag", [self.curIllumination, self.curMomentHistory])
+        self.variance_compute_illumination = tex(W, H)
+        self.variance_compute_pass = self._svgf_pass("svgf_variance.frag", [self.variance_compute_illumination])
+        self.atrous_output = tex(W, H)
+        self.atrous_pass = self._svgf_pass("svgf_Atrous.frag", [self.atrous_output])
+        self.modulate_color = tex(W, H)
+        self.svgf_modulate_pass = self._svgf_pass("svgf_modulate.frag", [self.modulate_color])
+        self.lastIllumination, self.last_normal_depth = tex(W, H), tex(W, H)
+        self.last_Moments_HistoryLength, self.last_acc_color, self.last_taa_color = tex(W, H), tex(W, H), tex(W, H)
+        self.next_frame_input = self._svgf_pass("save_frame_data.frag", [
+            self.lastIllumination, self.last_normal_depth, self.last_Moments_HistoryLength, self.last_acc_color,
+            self.last_taa_color])
+        for p in (self.reproject_pass, self.variance_compute_pass, self.atrous_pass):
+            p.set_uniform_float("inv_screen_width", 1.0 / W)
+            p.set_uniform_float("inv_screen_height", 1.0 / H)
+
+    def _build_fast_passes(self):
+        W, H, tex = self.W, self.H, getTextureRGB32F
+        self.illum = tex(W, H)                                  # reproject out 0
+        self.moments = [tex(W, H), tex(W, H)]                   # reproject out 1 (history, by parity)
+        self.hist_illum = [tex(W, H), tex(W, H)]                # a-trous iteration 1 output (history)
+        self.var_out = tex(W, H)
+        self.ping, self.pong = tex(W, H), tex(W, H)
+        self.modulate_color = tex(W, H)
+        self.taa = [tex(W, H), tex(W, H)]
+        self.acc = [tex(W, H), tex(W, H)] if self.cfg.accumulate_color else None
+        self.reproject = [self._svgf_pass("svgf_reproject.frag", [self.illum, self.moments[b]]) for b in (0, 1)]
+        self.variance_compute_pass = self._svgf_pass("svgf_variance.frag", [self.var_out])
+        self.atrous_to = {"ping": self._svgf_pass("svgf_Atrous.frag", [self.ping]),
+                          "pong": self._svgf_pass("svgf_Atrous.frag", [self.pong]),
+                          "hist0": self._svgf_pass("svgf_Atrous.frag", [self.hist_illum[0]]),
+                          "hist1": self._svgf_pass("svgf_Atrous.frag", [self.hist_illum[1]])}
+        self.svgf_modulate_pass = self._svgf_pass("svgf_modulate.frag", [self.modulate_color])
+        self.pass_taa = [self._svgf_pass("taa.frag", [self.taa[b]]) for b in (0, 1)]
+        for p in self.pass_taa:
+            p.set_uniform_int("screen_width", W)
+            p.set_uniform_int("screen_height", H)
+        for p in self.reproject + [self.variance_compute_pass, *self.atrous_to.values()]:
+            p.set_uniform_float("inv_screen_width", 1.0 / W)
+            p.set_uniform_float("inv_screen_height", 1.0 / H)
+
+    # ------------------------------------------------------------- frame ---
+    def _gbuffer_and_pt(self, b: int):
+        cam, cfg = self.camera, self.cfg
+        view, proj = cam.cam_view_mat, cam.cam_proj_mat
+        ip = self.init_pass[b]
+        ip.set_uniform_mat4("view", view)                      # main.cpp:436-443
+        ip.set_uniform_mat4("projection", proj)
+        ip.set_uniform_mat4("pre_viewproj", self.pre_viewproj)
+        ip.set_uniform_uint("frameCounter", cam.frameCounter)
+        ip.draw()
+        self.cameraRotate = rigid_inverse(view)                # main.cpp:445
+        pt = self.pass_path_tracing                            # main.cpp:447-470
+        pt.set_uniform_vec3("eye", cam.cam_position)
+        pt.set_uniform_mat4("cameraRotate", self.cameraRotate)
+        pt.set_uniform_uint("frameCounter", cam.frameCounter)
+        pt.set_uniform_int("hdrResolution", self.hdrResolution)
+        pt.set_uniform_bool("use_normal_map", cfg.use_normal_texture)
+        pt.set_uniform_bool("accumulate", cfg.accumulate_color)
+        pt.set_uniform_float("clamp_threshold", cfg.clamp_threshold)
+        pt.set_uniform_int("max_tracing_depth", cfg.max_tracing_depth)
+        pt.reset_texture_slot()
+        pt.set_texture_uniform(GL_TEXTURE_BUFFER, self.trianglesTextureBuffer, "triangles")
+        pt.set_texture_uniform(GL_TEXTURE_BUFFER, self.nodesTextureBuffer, "nodes")
+        if cfg.accumulate_color:
+            last_acc = self.last_acc_color if self.mode == "reference" else self.acc[1 - b]
+            pt.set_texture_uniform(GL_TEXTURE_2D, last_acc, "lastFrame")
+        pt.set_texture_uniform(GL_TEXTURE_2D, self.hdrMap, "hdrMap")
+        pt.set_texture_uniform(GL_TEXTURE_2D, self.hdrCache, "hdrCache")
+        pt.set_texture_uniform(GL_TEXTURE_BUFFER, self.pointLightBuffer, "pointLights")
+        pt.draw()
+
+    def _frame_reference(self):
+        cfg = self.cfg
+        g = self.gbuf[0]
+        self._gbuffer_and_pt(0)
+        rp = self.reproject_pass                               # main.cpp:474-486
+        rp.reset_texture_slot()
+        rp.set_uniform_float("depth_threshold", cfg.reproj_depth_threshold)
+        rp.set_uniform_float("normal_threshold", cfg.reproj_normal_threshold)
+        rp.set_texture_uniform(GL_TEXTURE_2D, g["velocity"], "gMotion")
+        rp.set_texture_uniform(GL_TEXTURE_2D, self.curColor, "gColor")
+        rp.set_texture_uniform(GL_TEXTURE_2D, self.Albedo, "gAlbedo")
+        rp.set_texture_uniform(GL_TEXTURE_2D, self.Emission, "gEmission")
+        rp.set_texture_uniform(GL_TEXTURE_2D, self.lastIllumination, "gPrevIllum")
+        rp.set_texture_uniform(GL_TEXTURE_2D, self.last_Moments_HistoryLength, "gPrevMoments_HistoryLength")
+        rp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
+        rp.set_texture_uniform(GL_TEXTURE_2D, self.last_normal_depth, "gPrevNormalAndLinearZ")
+        rp.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
+        rp.draw()
+        vp = self.variance_compute_pass                        # main.cpp:488-495
+        vp.reset_texture_slot()
+        vp.set_uniform_float("gPhiColor", cfg.sigma_l)
+        vp.set_uniform_float("gPhiNormal", cfg.sigma_n)
+        vp.set_texture_uniform(GL_TEXTURE_2D, self.curIllumination, "gIllumination")
+        vp.set_texture_uniform(GL_TEXTURE_2D, self.curMomentHistory, "gMoments_HistoryLength")
+        vp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
+        vp.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
+        vp.draw()
+        ap = self.atrous_pass                                  # main.cpp:499-526
+        for i in range(cfg.num_atrous_iterations):
+            ap.reset_texture_slot()
+            ap.set_uniform_float("gPhiColor", cfg.sigma_l)
+            ap.set_uniform_float("gPhiNormal", cfg.sigma_n)
+            ap.set_uniform_int("gStepSize", 1 << i)
+            ap.set_uniform_int("exact", int(self.atrous_exact))
+            ap.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
+            ap.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
+            src = self.variance_compute_illumination if i == 0 else self.tmp_atrous_result
+            ap.set_texture_uniform(GL_TEXTURE_2D, src, "gIllumination")
+            ap.draw()
+            self.bilt_pass.reset_texture_slot()
+            self.bilt_pass.set_texture_uniform(GL_TEXTURE_2D, self.atrous_output, "in_texture")
+            self.bilt_pass.draw()
+            if i == 1:
+                self.save_next_frame_pass.reset_texture_slot()
+                self.save_next_frame_pass.set_texture_uniform(GL_TEXTURE_2D, self.atrous_output, "in_texture")
+                self.save_next_frame_pass.draw()
+        mp = self.svgf_modulate_pass                           # main.cpp:530-535
+        mp.reset_texture_slot()
+        mp.set_texture_uniform(GL_TEXTURE_2D, self.Albedo, "gAlbedo")
+        mp.set_texture_uniform(GL_TEXTURE_2D, self.Emission, "gEmission")
+        mp.set_texture_uniform(GL_TEXTURE_2D, self.atrous_output, "gIllumination")
+        mp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
+        mp.draw()
+        if self.run_taa:                                       # main.cpp:537-544
+            tp = self.pass_taa
+            tp.reset_texture_slot()
+            tp.set_texture_uniform(GL_TEXTURE_2D, self.modulate_color, "currentColor")
+            tp.set_texture_uniform(GL_TEXTURE_2D, self.last_taa_color, "previousColor")
+            tp.set_texture_uniform(GL_TEXTURE_2D, g["velocity"], "velocityTexture")
+            tp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "normal_depth")
+            tp.set_uniform_uint("frameCounter", self.camera.frameCounter)
+            tp.draw()
+        nf = self.next_frame_input                             # main.cpp:546-553
+        nf.reset_texture_slot()
+        nf.set_texture_uniform(GL_TEXTURE_2D, self.next_frame_color_input, "texPass0")
+        nf.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "texPass1")
+        nf.set_texture_uniform(GL_TEXTURE_2D, self.curMomentHistory, "texPass2")
+        nf.set_texture_uniform(GL_TEXTURE_2D, self.curColor, "accColor")
+        nf.set_texture_uniform(GL_TEXTURE_2D, self.taa_output, "taaOutput")
+        nf.draw()
+        self.final = self.taa_output if self.run_taa else self.modulate_color
+
+    def _frame_fast(self):
+        cfg = self.cfg
+        b = self.frame_index & 1
+        pb = 1 - b
+        g, gp = self.gbuf[b], self.gbuf[pb]
+        self._gbuffer_and_pt(b)
+        rp = self.reproject[b]
+        rp.reset_texture_slot()
+        rp.set_uniform_float("depth_threshold", cfg.reproj_depth_threshold)
+        rp.set_uniform_float("normal_threshold", cfg.reproj_normal_threshold)
+        rp.set_texture_uniform(GL_TEXTURE_2D, g["velocity"], "gMotion")
+        rp.set_texture_uniform(GL_TEXTURE_2D, self.curColor, "gColor")
+        rp.set_texture_uniform(GL_TEXTURE_2D, self.Albedo, "gAlbedo")
+        rp.set_texture_uniform(GL_TEXTURE_2D, self.Emission, "gEmission")
+        rp.set_texture_uniform(GL_TEXTURE_2D, self.hist_illum[pb], "gPrevIllum")
+        rp.set_texture_uniform(GL_TEXTURE_2D, self.moments[pb], "gPrevMoments_HistoryLength")
+        rp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
+        rp.set_texture_uniform(GL_TEXTURE_2D, gp["normal_depth"], "gPrevNormalAndLinearZ")
+        rp.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
+        rp.draw()
+        vp = self.variance_compute_pass
+        vp.reset_texture_slot()
+        vp.set_uniform_float("gPhiColor", cfg.sigma_l)
+        vp.set_uniform_float("gPhiNormal", cfg.sigma_n)
+        vp.set_texture_uniform(GL_TEXTURE_2D, self.illum, "gIllumination")
+        vp.set_texture_uniform(GL_TEXTURE_2D, self.moments[b], "gMoments_HistoryLength")
+        vp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
+        vp.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
+        vp.draw()
+        # a-trous chain without copies: i0 var->ping, i1 ping->hist[b] (next frame's history),
+        # then alternate through ping/pong
+        src = self.var_out
+        hist_key = "hist0" if b == 0 else "hist1"
+        dests = []
+        n = cfg.num_atrous_iterations
+        for i in range(n):
+            if i == 1:
+                dests.append(hist_key)
+            else:
+                prev_tex = None if not dests else self._atrous_tex(dests[-1])
+                dests.append("pong" if prev_tex == self.ping else "ping")
+        for i in range(n):
+            ap = self.atrous_to[dests[i]]
+            ap.reset_texture_slot()
+            ap.set_uniform_float("gPhiColor", cfg.sigma_l)
+            ap.set_uniform_float("gPhiNormal", cfg.sigma_n)
+            ap.set_uniform_int("gStepSize", 1 << i)
+            ap.set_uniform_int("exact", int(self.atrous_exact))
+            ap.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
+            ap.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
+            ap.set_texture_uniform(GL_TEXTURE_2D, src, "gIllumination")
+            ap.draw()
+            src = self._atrous_tex(dests[i])
+        if n < 2:  # history = iteration-1 output never produced; the reference keeps the old one
+            pass
+        self.atrous_final = src
+        mp = self.svgf_modulate_pass
+        mp.reset_texture_slot()
+        mp.set_texture_uniform(GL_TEXTURE_2D, self.Albedo, "gAlbedo")
+        mp.set_texture_uniform(GL_TEXTURE_2D, self.Emission, "gEmission")
+        mp.set_texture_uniform(GL_TEXTURE_2D, src, "gIllumination")
+        mp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
+        mp.draw()
+        if self.run_taa:
+            tp = self.pass_taa[b]
+            tp.reset_texture_slot()
+            tp.set_texture_uniform(GL_TEXTURE_2D, self.modulate_color, "currentColor")
+            tp.set_texture_uniform(GL_TEXTURE_2D, self.taa[pb], "previousColor")
+            tp.set_texture_uniform(GL_TEXTURE_2D, g["velocity"], "velocityTexture")
+            tp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "normal_depth")
+            tp.set_uniform_uint("frameCounter", self.camera.frameCounter)
+            tp.draw()
+        self.final = self.taa[b] if self.run_taa else self.modulate_color
+
+    def _atrous_tex(self, key: str) -> int:
+        return {"ping": self.ping, "pong": self.pong, "hist0": self.hist_illum[0], "hist1": self.hist_illum[1]}[key]
+
+    def frame(self) -> None:
+        """One iteration of main.cpp's while-loop body (436-602), headless."""
+        self.camera.update()
+        if self.mode == "reference":
+            self._frame_reference()
+        else:
+            self._frame_fast()
+        if self.run_output:                                    # main.cpp:556-590 (final view)
+            op = self.output_pass
+            op.reset_texture_slot()
+            op.set_uniform_bool("accumulate", self.cfg.accumulate_color)
+            op.set_texture_uniform(GL_TEXTURE_2D, self.final, "texPass0")
+            op.draw()
+        # main.cpp:599-600: pre_viewproj = projection * inverse(cameraRotate) = projection * view
+        self.pre_viewproj = mat_mul(self.camera.cam_proj_mat, self.camera.cam_view_mat)
+        self.camera.frameCounter += 1
+        self.frame_index += 1
+
+    # --------------------------------------------------------- accessors ---
+    def planes(self) -> dict:
+        """Handles of this frame's per-pass outputs (for readback / tests)."""
+        if self.mode == "reference":
+            g = self.gbuf[0]
+            return dict(world=g["world"], normal_depth=g["normal_depth"], velocity=g["velocity"], fwidth=g["fwidth"],
+                        color=self.curColor, emission=self.Emission, albedo=self.Albedo,
+                        reproj_illum=self.curIllumination, reproj_moments=self.curMomentHistory,
+                        variance=self.variance_compute_illumination, atrous=self.atrous_output,
+                        history_illum=self.lastIllumination, modulate=self.modulate_color, final=self.final,
+                        output=self.output_tex)
+        b = (self.frame_index - 1) & 1
+        g = self.gbuf[b]
+        return dict(world=g["world"], normal_depth=g["normal_depth"], velocity=g["velocity"], fwidth=g["fwidth"],
+                    color=self.curColor, emission=self.Emission, albedo=self.Albedo, reproj_illum=self.illum,
+                    reproj_moments=self.moments[b], variance=self.var_out, atrous=self.atrous_final,
+                    history_illum=self.hist_illum[b], modulate=self.modulate_color, final=self.final,
+                    output=self.output_tex)
