@@ -108,6 +108,8 @@ class Renderer:
         self.output_pass.bindData(True)
         self.pre_viewproj = mat_mul(self.camera.cam_proj_mat, self.camera.cam_view_mat)  # main.h:48
         self.frame_index = 0
+        self._profile = False
+        self._times: dict = {}
 
     # ------------------------------------------------------------ passes ---
     def _svgf_pass(self, frag: str, atts) -> RenderPass:
@@ -177,7 +179,7 @@ class Renderer:
         ip.set_uniform_mat4("projection", proj)
         ip.set_uniform_mat4("pre_viewproj", self.pre_viewproj)
         ip.set_uniform_uint("frameCounter", cam.frameCounter)
-        ip.draw()
+        self._draw(ip, "gbuffer")
         self.cameraRotate = rigid_inverse(view)                # main.cpp:445
         pt = self.pass_path_tracing                            # main.cpp:447-470
         pt.set_uniform_vec3("eye", cam.cam_position)
@@ -197,7 +199,7 @@ class Renderer:
         pt.set_texture_uniform(GL_TEXTURE_2D, self.hdrMap, "hdrMap")
         pt.set_texture_uniform(GL_TEXTURE_2D, self.hdrCache, "hdrCache")
         pt.set_texture_uniform(GL_TEXTURE_BUFFER, self.pointLightBuffer, "pointLights")
-        pt.draw()
+        self._draw(pt, "pathtrace")
 
     def _frame_reference(self):
         cfg = self.cfg
@@ -216,7 +218,7 @@ class Renderer:
         rp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
         rp.set_texture_uniform(GL_TEXTURE_2D, self.last_normal_depth, "gPrevNormalAndLinearZ")
         rp.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
-        rp.draw()
+        self._draw(rp, "reproject")
         vp = self.variance_compute_pass                        # main.cpp:488-495
         vp.reset_texture_slot()
         vp.set_uniform_float("gPhiColor", cfg.sigma_l)
@@ -225,7 +227,7 @@ class Renderer:
         vp.set_texture_uniform(GL_TEXTURE_2D, self.curMomentHistory, "gMoments_HistoryLength")
         vp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
         vp.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
-        vp.draw()
+        self._draw(vp, "variance")
         ap = self.atrous_pass                                  # main.cpp:499-526
         for i in range(cfg.num_atrous_iterations):
             ap.reset_texture_slot()
@@ -237,21 +239,21 @@ class Renderer:
             ap.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
             src = self.variance_compute_illumination if i == 0 else self.tmp_atrous_result
             ap.set_texture_uniform(GL_TEXTURE_2D, src, "gIllumination")
-            ap.draw()
+            self._draw(ap, "atrous")
             self.bilt_pass.reset_texture_slot()
             self.bilt_pass.set_texture_uniform(GL_TEXTURE_2D, self.atrous_output, "in_texture")
-            self.bilt_pass.draw()
+            self._draw(self.bilt_pass, "copy")
             if i == 1:
                 self.save_next_frame_pass.reset_texture_slot()
                 self.save_next_frame_pass.set_texture_uniform(GL_TEXTURE_2D, self.atrous_output, "in_texture")
-                self.save_next_frame_pass.draw()
+                self._draw(self.save_next_frame_pass, "copy")
         mp = self.svgf_modulate_pass                           # main.cpp:530-535
         mp.reset_texture_slot()
         mp.set_texture_uniform(GL_TEXTURE_2D, self.Albedo, "gAlbedo")
         mp.set_texture_uniform(GL_TEXTURE_2D, self.Emission, "gEmission")
         mp.set_texture_uniform(GL_TEXTURE_2D, self.atrous_output, "gIllumination")
         mp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
-        mp.draw()
+        self._draw(mp, "modulate")
         if self.run_taa:                                       # main.cpp:537-544
             tp = self.pass_taa
             tp.reset_texture_slot()
@@ -260,7 +262,7 @@ class Renderer:
             tp.set_texture_uniform(GL_TEXTURE_2D, g["velocity"], "velocityTexture")
             tp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "normal_depth")
             tp.set_uniform_uint("frameCounter", self.camera.frameCounter)
-            tp.draw()
+            self._draw(tp, "taa")
         nf = self.next_frame_input                             # main.cpp:546-553
         nf.reset_texture_slot()
         nf.set_texture_uniform(GL_TEXTURE_2D, self.next_frame_color_input, "texPass0")
@@ -268,7 +270,7 @@ class Renderer:
         nf.set_texture_uniform(GL_TEXTURE_2D, self.curMomentHistory, "texPass2")
         nf.set_texture_uniform(GL_TEXTURE_2D, self.curColor, "accColor")
         nf.set_texture_uniform(GL_TEXTURE_2D, self.taa_output, "taaOutput")
-        nf.draw()
+        self._draw(nf, "copy")
         self.final = self.taa_output if self.run_taa else self.modulate_color
 
     def _frame_fast(self):
@@ -290,7 +292,7 @@ class Renderer:
         rp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
         rp.set_texture_uniform(GL_TEXTURE_2D, gp["normal_depth"], "gPrevNormalAndLinearZ")
         rp.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
-        rp.draw()
+        self._draw(rp, "reproject")
         vp = self.variance_compute_pass
         vp.reset_texture_slot()
         vp.set_uniform_float("gPhiColor", cfg.sigma_l)
@@ -299,7 +301,7 @@ class Renderer:
         vp.set_texture_uniform(GL_TEXTURE_2D, self.moments[b], "gMoments_HistoryLength")
         vp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
         vp.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
-        vp.draw()
+        self._draw(vp, "variance")
         # a-trous chain without copies: i0 var->ping, i1 ping->hist[b] (next frame's history),
         # then alternate through ping/pong
         src = self.var_out
@@ -322,7 +324,7 @@ class Renderer:
             ap.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
             ap.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
             ap.set_texture_uniform(GL_TEXTURE_2D, src, "gIllumination")
-            ap.draw()
+            self._draw(ap, "atrous")
             src = self._atrous_tex(dests[i])
         if n < 2:  # history = iteration-1 output never produced; the reference keeps the old one
             pass
@@ -333,7 +335,7 @@ class Renderer:
         mp.set_texture_uniform(GL_TEXTURE_2D, self.Emission, "gEmission")
         mp.set_texture_uniform(GL_TEXTURE_2D, src, "gIllumination")
         mp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
-        mp.draw()
+        self._draw(mp, "modulate")
         if self.run_taa:
             tp = self.pass_taa[b]
             tp.reset_texture_slot()
@@ -342,8 +344,27 @@ class Renderer:
             tp.set_texture_uniform(GL_TEXTURE_2D, g["velocity"], "velocityTexture")
             tp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "normal_depth")
             tp.set_uniform_uint("frameCounter", self.camera.frameCounter)
-            tp.draw()
+            self._draw(tp, "taa")
         self.final = self.taa[b] if self.run_taa else self.modulate_color
+
+    def _draw(self, p: RenderPass, name: str) -> None:
+        p.draw()
+        if self._profile:
+            self._times.setdefault(name, []).append(p.last_ms())
+
+    def profile(self, on: bool) -> None:
+        """Time every draw with HIP events (synchronises after each draw: diagnostics only)."""
+        gl.set_profiling(on)
+        self._profile = on
+        self._times = {}
+
+    def pass_times(self) -> dict:
+        """Per-pass ms of the profiled frames (sum per frame) + the a-trous per-launch average."""
+        out = {k: float(np.sum(v)) for k, v in self._times.items()}
+        if self._times.get("atrous"):
+            out["atrous_avg_ms"] = float(np.mean(self._times["atrous"]))
+        out["frame_sum_ms"] = float(sum(np.sum(v) for k, v in self._times.items()))
+        return out
 
     def _atrous_tex(self, key: str) -> int:
         return {"ping": self.ping, "pong": self.pong, "hist0": self.hist_illum[0], "hist1": self.hist_illum[1]}[key]
@@ -360,7 +381,7 @@ class Renderer:
             op.reset_texture_slot()
             op.set_uniform_bool("accumulate", self.cfg.accumulate_color)
             op.set_texture_uniform(GL_TEXTURE_2D, self.final, "texPass0")
-            op.draw()
+            self._draw(op, "output")
         # main.cpp:599-600: pre_viewproj = projection * inverse(cameraRotate) = projection * view
         self.pre_viewproj = mat_mul(self.camera.cam_proj_mat, self.camera.cam_view_mat)
         self.camera.frameCounter += 1
