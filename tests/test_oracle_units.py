@@ -1,0 +1,159 @@
+"""The oracle's building blocks against independent hand-derived values.
+
+Parity for the GLSL passes is unpinned (no reference outputs exist, SURVEY.md
+§8(c)); these tests pin each restated GLSL helper to values derived here
+independently (numpy float64, closed forms, the shader text's own constants).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_ref as O
+
+
+def _f(a):
+    return O.f32(a)
+
+
+def _math(fn, x, y=None):
+    x = _f(x)
+    inp = x if y is None else _f(np.concatenate([x, _f(y)]))
+    out = np.zeros(x.size, np.float32)
+    O.lib().orc_math(fn, O.fp(inp), x.size, O.fp(out))
+    return out
+
+
+def _ulps(a, b):
+    a = a.astype(np.float64)
+    b32 = b.astype(np.float32)
+    ulp = np.spacing(np.abs(b32)).astype(np.float64)
+    return np.abs(a - b) / np.maximum(ulp, np.finfo(np.float32).tiny)
+
+
+def test_builtin_transcendentals_accuracy():
+    rng = np.random.default_rng(0)
+    x = rng.uniform(-7, 7, 20000).astype(np.float32)
+    for fn, ref in ((0, np.sin), (1, np.cos)):
+        got = _math(fn, x)
+        err = np.abs(got.astype(np.float64) - ref(x.astype(np.float64)))
+        assert err.max() < 4e-7, (fn, err.max())
+    y = rng.uniform(-3, 3, 20000).astype(np.float32)
+    got = _math(2, y, x)
+    assert np.abs(got - np.arctan2(y.astype(np.float64), x.astype(np.float64))).max() < 8e-7
+    a = rng.uniform(-1, 1, 20000).astype(np.float32)
+    assert _ulps(_math(3, a), np.arcsin(a.astype(np.float64))).max() <= 4
+    p = np.exp(rng.uniform(-30, 30, 20000)).astype(np.float32)
+    assert np.abs(_math(4, p) - np.log(p.astype(np.float64))).max() < 4e-6
+    e = rng.uniform(-80, 80, 20000).astype(np.float32)
+    assert _ulps(_math(5, e), np.exp(e.astype(np.float64))).max() <= 4
+
+
+def _wang(seed):  # path_tracing.frag:438-445, independently restated
+    s = seed & 0xFFFFFFFF
+    s = (s ^ 61) ^ (s >> 16)
+    s = (s * 9) & 0xFFFFFFFF
+    s = s ^ (s >> 4)
+    s = (s * 0x27D4EB2D) & 0xFFFFFFFF
+    return s ^ (s >> 15)
+
+
+@pytest.mark.parametrize("seed", [1, 3, 1973, 26699 | 1, 0xFFFFFFFF, 123456789])
+def test_wang_hash(seed):
+    assert O.lib().orc_wang_hash(seed) == _wang(seed)
+
+
+def test_sobol_known_values():
+    L = O.lib()
+    # dimension 0 is the van der Corput sequence: bit-reversed index / 2^32
+    for i in range(1, 64):
+        rev = int(f"{i:032b}"[::-1], 2)
+        assert L.orc_sobol(0, i) == np.float32(np.float32(rev) * np.float32(2.0 ** -32))
+    # dimension 1 direction numbers (path_tracing.frag:465): V[1][0]=2^31, V[1][1]=3*2^30
+    assert L.orc_sobol(1, 1) == 0.5
+    assert L.orc_sobol(1, 2) == 0.75
+    assert L.orc_sobol(1, 3) == 0.25
+
+
+def _aabb(S, d, lo, hi):
+    return O.lib().orc_hit_aabb(O.fp(_f(S)), O.fp(_f(d)), O.fp(_f(lo)), O.fp(_f(hi)))
+
+
+def test_hit_aabb_semantics():
+    lo, hi = [-1, -1, -1], [1, 1, 1]
+    assert _aabb([0, 0, -5], [0, 0, 1], lo, hi) == 4.0            # entry distance t0
+    assert _aabb([0, 0, 0], [0, 0, 1], lo, hi) == 1.0             # origin inside -> exit t1
+    assert _aabb([0, 3, -5], [0, 0, 1], lo, hi) == -1.0           # miss
+    assert _aabb([0, 0, 5], [0, 0, 1], lo, hi) <= 0.0             # behind: caller treats d<=0 as miss
+
+
+def _tri(S, d, p, n=None):
+    n = n if n is not None else np.tile([0, 0, 1], 3)
+    out = np.zeros(5, np.float32)
+    hit = O.lib().orc_hit_triangle(O.fp(_f(S)), O.fp(_f(d)), O.fp(_f(p)), O.fp(_f(n)), O.fp(out))
+    return hit, out
+
+
+def test_hit_triangle_semantics():
+    P = [-1, -1, 0, 1, -1, 0, 0, 1, 0]  # CCW seen from +z: geometric N = +z
+    hit, o = _tri([0, 0, 5], [0, 0, -1], P)
+    assert hit and o[0] == 5.0 and o[4] == 0.0 and o[3] > 0        # front hit, smooth normal +z
+    hit, o = _tri([0, 0, -5], [0, 0, 1], P)
+    assert hit and o[4] == 1.0 and o[3] < 0                        # from behind: isInside, normal flipped
+    hit, _ = _tri([0, 0, 5], [1, 0, 0], P)
+    assert not hit                                                 # parallel (|N.d| < 1e-5)
+    hit, _ = _tri([0, 0, 0.0001], [0, 0, -1], P)
+    assert not hit                                                 # t < 0.0005
+    hit, _ = _tri([5, 5, 5], [0, 0, -1], P)
+    assert not hit                                                 # outside the edges
+
+
+def _brdf(V, N, L, m):
+    out = np.zeros(3, np.float32)
+    O.lib().orc_brdf_eval(O.fp(_f(V)), O.fp(_f(N)), O.fp(_f(L)), O.fp(_f(m)), O.fp(out))
+    return out
+
+
+def _pdf(V, N, L, m):
+    return O.lib().orc_brdf_pdf(O.fp(_f(V)), O.fp(_f(N)), O.fp(_f(L)), O.fp(_f(m)))
+
+
+MAT = [0.8, 0.5, 0.3, 0.0, 0.2, 0.5, 0.0, 0.4, 0.0, 0.2, 0.5, 0.3, 0.7, 1.0]  # baseColor, subsurface, ...
+
+
+def _unit(v):
+    v = np.asarray(v, np.float64)
+    return (v / np.linalg.norm(v)).astype(np.float32)
+
+
+def test_brdf_zero_below_horizon_and_reciprocal():
+    N = [0, 0, 1]
+    V, L = _unit([0.3, 0.1, 0.9]), _unit([-0.5, 0.2, 0.6])
+    assert (_brdf(V, N, _unit([0.1, 0, -1]), MAT) == 0).all()       # NdotL < 0 -> 0 (:623)
+    assert _pdf(V, N, _unit([0.1, 0, -1]), MAT) == 0.0
+    np.testing.assert_allclose(_brdf(V, N, L, MAT), _brdf(L, N, V, MAT), rtol=1e-5)  # Disney is reciprocal
+
+
+def test_brdf_lambert_limit():
+    """metallic 0, specular 0, roughness 1, no clearcoat/sheen/subsurface at normal incidence:
+    f = baseColor/pi * Fd with Fd = mix(1,Fd90,FL)*mix(1,Fd90,FV); at L=V=N: FL=FV=0 -> f = baseColor/pi."""
+    m = [0.5, 0.25, 1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.5, 0.0, 1.0, 1.0]
+    N = [0, 0, 1]
+    f = _brdf(N, N, N, m)
+    # specular=0 keeps Fs = mix(0, 1, FH) with FH=SchlickFresnel(1)=0 -> no spec term
+    np.testing.assert_allclose(f, np.float32([0.5, 0.25, 1.0]) / np.float32(3.1415926), rtol=1e-6)
+
+
+def test_brdf_pdf_normalised():
+    """BRDF_Pdf integrates to ~1 over the hemisphere (lobe mixture of normalised pdfs)."""
+    rng = np.random.default_rng(1)
+    n = 6000
+    u1, u2 = rng.random(n), rng.random(n)
+    z = u1                                           # uniform hemisphere sampling, pdf 1/(2pi)
+    r = np.sqrt(1 - z * z)
+    Ls = np.stack([r * np.cos(2 * np.pi * u2), r * np.sin(2 * np.pi * u2), z], 1).astype(np.float32)
+    V = _unit([0.2, 0.1, 0.95])
+    m = [0.7, 0.7, 0.7, 0.0, 0.0, 0.5, 0.0, 0.6, 0.0, 0.0, 0.5, 0.0, 1.0, 1.0]
+    vals = np.array([_pdf(V, [0, 0, 1], L, m) for L in Ls])
+    est = vals.mean() * 2 * np.pi
+    assert 0.85 < est < 1.15, est

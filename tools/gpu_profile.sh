@@ -1,0 +1,15 @@
+#!/bin/bash
+# rocprofv3 passes for the 4K frame: kernel trace + stats, then separate PMC passes.
+# usage: bash tools/gpu_profile.sh <tag>
+set -o pipefail
+TAG=${1:-r01}
+R="$GRAFT_REPO_ROOT"
+OUT="$R/gpurun_out/prof_$TAG"
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+B="$R/bench.py --steps 5 --warmup 2 --no-cpu-baseline"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $B > "$OUT/trace.log" 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $B > "$OUT/fetch.log" 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 $B > "$OUT/write.log" 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --output-format csv -d "$OUT/sq" -o run -- python3 $B > "$OUT/sq.log" 2>&1 || exit $?
+echo profile-done
