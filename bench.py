@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default="480x270", help="oracle sample frame size for cpu_baseline")
     ap.add_argument("--breakdown", action="store_true", help="print per-pass ms to stderr")
+    ap.add_argument("--pt-kernel", type=int, default=0, help="0 wavefront (production), 1 megakernel (A/B)")
     return ap.parse_args()
 
 
@@ -104,6 +105,7 @@ def main():
     else:
         from ptsvgf.renderer import Renderer
         r = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, run_taa=False, run_output=False)
+    r.pass_path_tracing.set_uniform_int("pt_kernel", args.pt_kernel)
 
     def step():
         if args.moving:

@@ -72,7 +72,8 @@ extern "C" {
 /* ---- library / device ---------------------------------------------------- */
 int pt_init(int device);                    /* select HIP device, create stream */
 int pt_shutdown(void);                      /* free every handle and the stream */
-int pt_set_stream(void* hip_stream);        /* NULL = library's own stream */
+int pt_set_stream(void* hip_stream);        /* run on this stream; NULL = HIP default (null) stream */
+int pt_use_own_stream(void);                /* back to the library's own stream (the pt_init default) */
 int pt_sync(void);                          /* wait for all queued draws */
 const char* pt_last_error(void);
 int pt_version(void);

@@ -101,8 +101,8 @@ extern "C" int orc_reproject(int W, int H, const float* motion_p, const float* c
       }
       if (valid) {
         float sumw = 0.0f;
-        float bx = ipx - (float)(int)(ipx / inv_w) * inv_w;  // :84-85 (UV units)
-        float by = ipy - (float)(int)(ipy / inv_h) * inv_h;
+        float bx = ipx - (float)f2i(ipx / inv_w) * inv_w;  // :84-85 (UV units); int(NaN) defined, glsl_builtins.h
+        float by = ipy - (float)f2i(ipy / inv_h) * inv_h;
         const float w[4] = {(1.0f - bx) * (1.0f - by), bx * (1.0f - by), (1.0f - bx) * by, bx * by};
         for (int k = 0; k < 4; ++k) {
           if (!v[k]) continue;

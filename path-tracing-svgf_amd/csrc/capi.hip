@@ -72,8 +72,37 @@ struct RasterScene {
   int ntris = 0;
 };
 
+struct WFBuffers {
+  void* base = nullptr;  // one allocation carved into the WFState arrays
+  size_t n = 0;          // pixels covered
+  WFState st{};
+};
+
+int wf_alloc(WFBuffers& b, size_t n) {
+  if (b.base && b.n == n) return PT_OK;
+  if (b.base) { (void)hipFree(b.base); b.base = nullptr; }
+  const size_t f4 = n * 16, al = 256;
+  auto up = [&](size_t v) { return (v + al - 1) / al * al; };
+  size_t total = up(f4) * 10 + up(n * 8) + up(n * 4) + up(n) * 2 + up(n * 4) * 2 + up(64);
+  if (hipMalloc(&b.base, total) != hipSuccess) { b.base = nullptr; return PT_ERR_HIP; }
+  char* c = (char*)b.base;
+  float4** f4p[10] = {&b.st.ray_o, &b.st.ray_d, &b.st.light, &b.st.red, &b.st.pend0,
+                      &b.st.pend1, &b.st.pend2, &b.st.pend3, &b.st.sh_h, &b.st.sh_p};
+  for (auto q : f4p) { *q = (float4*)c; c += up(f4); }
+  b.st.hit = (int2*)c; c += up(n * 8);
+  b.st.seed = (uint32_t*)c; c += up(n * 4);
+  b.st.occ_h = (uint8_t*)c; c += up(n);
+  b.st.occ_p = (uint8_t*)c; c += up(n);
+  b.st.list0 = (int*)c; c += up(n * 4);
+  b.st.list1 = (int*)c; c += up(n * 4);
+  b.st.counters = (int*)c;
+  b.n = n;
+  return PT_OK;
+}
+
 struct Pass {
   uint32_t program = 0;
+  WFBuffers wf;
   int W = 0, H = 0;
   std::vector<uint32_t> att;
   bool bound = false, final_pass = false;
@@ -436,7 +465,14 @@ int draw_pathtrace(Pass* p) {
     Texture* lf = sampler(p, "lastFrame");
     if (lf) TRY(plane_of(lf, p, &k.last, "lastFrame"));
   }
-  int rc = launch_pathtrace(k, g.stream);
+  int rc;
+  if (ui(p, "pt_kernel", 0) == 1) {  // 1: single megakernel (kernels_pt.hip), kept for A/B
+    rc = launch_pathtrace(k, g.stream);
+  } else {                            // 0: wavefront (kernels_wavefront.hip), production
+    TRY(wf_alloc(p->wf, (size_t)k.W * (size_t)std::max(0, k.y1 - k.y0)));
+    k.wf = p->wf.st;
+    rc = launch_pathtrace_wavefront(k, g.stream);
+  }
   return rc ? hip_err((hipError_t)rc, "pathtrace launch") : PT_OK;
 }
 
@@ -616,6 +652,7 @@ int pt_shutdown(void) {
     Pass* p = kv.second.get();
     if (p->raster.geom) (void)hipFree(p->raster.geom);
     if (p->raster.bvh) (void)hipFree(p->raster.bvh);
+    if (p->wf.base) (void)hipFree(p->wf.base);
     if (p->ev0) (void)hipEventDestroy(p->ev0);
     if (p->ev1) (void)hipEventDestroy(p->ev1);
   }
@@ -632,7 +669,15 @@ int pt_shutdown(void) {
 int pt_set_stream(void* s) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   TRY(ensure_init());
-  g.stream = s ? (hipStream_t)s : g.own;
+  // s is used as given: NULL is the HIP default (null) stream, which is torch's default stream.
+  g.stream = (hipStream_t)s;
+  return PT_OK;
+}
+
+int pt_use_own_stream(void) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  g.stream = g.own;
   return PT_OK;
 }
 
@@ -1059,6 +1104,7 @@ int pt_pass_destroy(uint32_t pass) {
   Pass* p = it->second.get();
   if (p->raster.geom) (void)hipFree(p->raster.geom);
   if (p->raster.bvh) (void)hipFree(p->raster.bvh);
+  if (p->wf.base) (void)hipFree(p->wf.base);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
   g.passes.erase(it);

@@ -43,6 +43,14 @@ GL_HD float f_mix(float x, float y, float a) { return x * (1.0f - a) + y * a; } 
 GL_HD float f_sqrt(float x) { return sqrtf(x); }
 GL_HD float f_floor(float x) { return floorf(x); }
 GL_HD bool f_isnan(float x) { return x != x; }
+// int(float): GLSL leaves NaN / out-of-range undefined (and C makes it UB). Defined here
+// as gfx950's v_cvt_i32_f32: NaN -> 0, saturate to the int range, else truncate.
+GL_HD int f2i(float x) {
+  if (x != x) return 0;
+  if (x >= 2147483648.0f) return 2147483647;
+  if (x <= -2147483648.0f) return (int)0x80000000;
+  return (int)x;
+}
 
 GL_HD uint32_t f_bits(float f) {
 #if defined(__HIPCC__)
@@ -80,7 +88,7 @@ GL_HD float g_sin(float xx) {
   float x = xx;
   int sign = 1;
   if (x < 0.0f) { sign = -1; x = -x; }
-  int j = (int)(1.27323954473516f * x);
+  int j = f2i(1.27323954473516f * x);
   float y = (float)j;
   if (j & 1) { j += 1; y += 1.0f; }
   j &= 7;
@@ -94,7 +102,7 @@ GL_HD float g_sin(float xx) {
 GL_HD float g_cos(float xx) {
   float x = xx < 0.0f ? -xx : xx;
   int sign = 1;
-  int j = (int)(1.27323954473516f * x);
+  int j = f2i(1.27323954473516f * x);
   float y = (float)j;
   if (j & 1) { j += 1; y += 1.0f; }
   j &= 7;

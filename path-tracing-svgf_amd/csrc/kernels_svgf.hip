@@ -102,8 +102,8 @@ __global__ void __launch_bounds__(256) reproject_kernel(ReprojParams p) {
   }
   if (valid) {
     float sumw = 0.0f;
-    float bx = ipx - (float)(int)(ipx / p.inv_w) * p.inv_w;
-    float by = ipy - (float)(int)(ipy / p.inv_h) * p.inv_h;
+    float bx = ipx - (float)f2i(ipx / p.inv_w) * p.inv_w;
+    float by = ipy - (float)f2i(ipy / p.inv_h) * p.inv_h;
     const float w[4] = {(1.0f - bx) * (1.0f - by), bx * (1.0f - by), (1.0f - bx) * by, bx * by};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {

@@ -1,0 +1,282 @@
+// kernels_wavefront.hip — the production path tracer: path_tracing.frag's main()
+// (:1056-1128) split into stages so that BVH traversal runs in small,
+// high-occupancy kernels and shading runs without a traversal stack:
+//
+//   per bounce i:  trace_closest -> shade -> trace_shadow (HDR + point light) -> finish
+//   then          finalize (clamp / NaN / accumulate / store)
+//
+// Rays that stay alive are compacted into a list with one wave-ballot atomic per
+// wave, so traversal waves carry only live rays (58 % of the 4K frame is sky).
+// The arithmetic per pixel is exactly the megakernel's (and the reference's):
+// shade() evaluates both light contributions as if unoccluded, finish() applies
+// the shadow verdicts with the reference's selection (hdriLight :934-937 zeroes
+// pdf and value; calculatePointLight :905-909 zeroes the value only), so outputs
+// stay bit-identical to the CPU oracle. RNG consumption order per pixel is
+// unchanged: AA x2, then per bounce xi_3, r1, r2, light pick.
+#include <hip/hip_runtime.h>
+
+#include "glsl_builtins.h"
+#include "pt_device.h"
+#include "pt_shading.h"
+
+using namespace glsl;
+
+namespace ptk {
+
+constexpr int kTB = 128;  // threads per traversal block (LDS stack: kStack*kTB*4 = 16 KiB)
+
+__device__ __forceinline__ void pix_xy(const PTParams& p, int pid, int* x, int* y) {
+  *x = pid % p.W;
+  *y = p.y0 + pid / p.W;
+}
+
+// wave-aggregated append: one atomic per wave
+__device__ __forceinline__ void wave_push(bool push, int value, int* __restrict__ list, int* counter) {
+  unsigned long long mask = __ballot(push);
+  if (mask == 0ull) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)mask) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(counter, __popcll(mask));
+  base = __shfl(base, leader);
+  if (push) list[base + __popcll(mask & ((1ull << lane) - 1ull))] = value;
+}
+
+__device__ __forceinline__ v3 primary_dir(const PTParams& p, int x, int y) {
+  float pixx = (float)(2 * x + 1) / (float)p.W - 1.0f;
+  float pixy = (float)(2 * y + 1) / (float)p.H - 1.0f;
+  if (p.aspect_corrected) pixx = pixx * ((float)p.W / (float)p.H);
+  const float* m = p.camRot;
+  return normalize(mk((m[0] * pixx + m[4] * pixy) + (m[8] * -1.0f + m[12] * 0.0f),
+                      (m[1] * pixx + m[5] * pixy) + (m[9] * -1.0f + m[13] * 0.0f),
+                      (m[2] * pixx + m[6] * pixy) + (m[10] * -1.0f + m[14] * 0.0f)));
+}
+
+// ------------------------------------------------------------ primaries ---
+// 16x16 screen tiles, each wave an 8x8 sub-tile: coherent camera rays.
+__global__ void __launch_bounds__(256) wf_primary(PTParams p) {
+  __shared__ int stk[kStack * 256];
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  const int x = blockIdx.x * 16 + (wv & 1) * 8 + (ln & 7);
+  const int y = p.y0 + blockIdx.y * 16 + (wv >> 1) * 8 + (ln >> 3);
+  if (x >= p.W || y >= p.y1) return;
+  const int pid = (y - p.y0) * p.W + x;
+  v3 S = mk(p.eye[0], p.eye[1], p.eye[2]);
+  v3 d = primary_dir(p, x, y);
+  float t;
+  int tri = traverse<0, 256>(p.scene, stk + threadIdx.x, S, d, 0.0f, p.prune, &t);
+  p.wf.hit[pid] = make_int2(tri, __float_as_int(t));
+}
+
+// ----------------------------------------------------------- bounce trace ---
+__global__ void __launch_bounds__(kTB) wf_trace_closest(PTParams p, const int* __restrict__ list,
+                                                        const int* __restrict__ count) {
+  __shared__ int stk[kStack * kTB];
+  const int k = blockIdx.x * kTB + threadIdx.x;
+  if (k >= *count) return;
+  const int pid = list[k];
+  float4 o = p.wf.ray_o[pid], dd = p.wf.ray_d[pid];
+  float t;
+  int tri = traverse<0, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dd), 0.0f, p.prune, &t);
+  p.wf.hit[pid] = make_int2(tri, __float_as_int(t));
+}
+
+// HDR shadow rays in the first half of the grid, point-light shadow rays in the second.
+__global__ void __launch_bounds__(kTB) wf_trace_shadow(PTParams p, const int* __restrict__ list,
+                                                       const int* __restrict__ count) {
+  __shared__ int stk[kStack * kTB];
+  const int n = *count;
+  const int k = blockIdx.x * kTB + threadIdx.x;
+  if (k >= 2 * n) return;
+  const bool point = k >= n;
+  const int pid = list[point ? k - n : k];
+  float4 o = p.wf.ray_o[pid];
+  float ts;
+  if (!point) {
+    float4 hd = p.wf.sh_h[pid];
+    p.wf.occ_h[pid] = traverse<1, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(hd), 0.0f, 0, &ts) >= 0;
+  } else {
+    float4 ld = p.wf.sh_p[pid];
+    if (ld.w < 0.0f) return;  // pointLightSize == 0: no ray
+    p.wf.occ_p[pid] = traverse<2, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(ld), ld.w, 0, &ts) >= 0;
+  }
+}
+
+// ------------------------------------------------------------------ shade ---
+// Bounce i: consume the closest hit of the ray in (ray_o, ray_d); on a hit,
+// sample the next direction and prepare both NEE contributions (:948-968).
+__global__ void __launch_bounds__(256) wf_shade(PTParams p, int bounce, const int* __restrict__ list_in,
+                                                const int* __restrict__ count_in, int* __restrict__ list_out,
+                                                int* __restrict__ count_out) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  int pid;
+  bool valid;
+  if (bounce == 0) {
+    valid = k < p.W * (p.y1 - p.y0);
+    pid = k;
+  } else {
+    valid = k < *count_in;
+    pid = valid ? list_in[k] : 0;
+  }
+  bool push = false;
+  if (valid) {
+    int x, y;
+    pix_xy(p, pid, &x, &y);
+    int2 hr = p.wf.hit[pid];
+    v3 S, d;
+    uint32_t seed;
+    v3 light, red;
+    if (bounce == 0) {
+      S = mk(p.eye[0], p.eye[1], p.eye[2]);
+      d = primary_dir(p, x, y);
+      seed = ((uint32_t)x * 1973u + (uint32_t)y * 9277u + p.frameCounter * 26699u) | 1u;  // :433-436
+      wang_hash(&seed);  // AA jitter rand() x2 (:1060), never applied
+      wang_hash(&seed);
+      light = splat(0.0f);
+      red = splat(1.0f);
+    } else {
+      S = xyz(p.wf.ray_o[pid]);
+      d = xyz(p.wf.ray_d[pid]);
+      seed = p.wf.seed[pid];
+      light = xyz(p.wf.light[pid]);
+      red = xyz(p.wf.red[pid]);
+    }
+    if (hr.x < 0) {  // miss (:1084-1087)
+      light = add(light, mul(hdr_color(p, d), red));
+      if (bounce == 0) {
+        pst(p.emission, x, y, f4(0.0f, 0.0f, 0.0f, 1.0f));
+        pst(p.albedo, x, y, f4(0.0f, 0.0f, 0.0f, 1.0f));
+      }
+    } else {
+      Hit h = decode_hit(p.scene, hr.x, __int_as_float(hr.y), S, d);
+      if (bounce == 0) {
+        pst(p.emission, x, y, f4(h.m.emissive.x, h.m.emissive.y, h.m.emissive.z, 1.0f));
+        pst(p.albedo, x, y, f4(h.m.baseColor.x, h.m.baseColor.y, h.m.baseColor.z, 1.0f));
+      }
+      uint32_t ps = ((uint32_t)x * 1973u + (uint32_t)y * 9277u + (uint32_t)(114514 / 1919) * 26699u) | 1u;
+      float cpu = u32_to_unit(wang_hash(&ps));
+      float cpv = u32_to_unit(wang_hash(&ps));
+      float xi1 = p.sobol_u[bounce] + cpu;
+      if (xi1 > 1.0f) xi1 -= 1.0f;
+      if (xi1 < 0.0f) xi1 += 1.0f;
+      float xi2 = p.sobol_v[bounce] + cpv;
+      if (xi2 > 1.0f) xi2 -= 1.0f;
+      if (xi2 < 0.0f) xi2 += 1.0f;
+      float xi3 = u32_to_unit(wang_hash(&seed));
+      v3 V = neg(h.viewDir);
+      v3 L = sample_brdf(xi1, xi2, xi3, V, h.normal, h.m);
+      if (dot(h.normal, L) > 0.0f) {
+        push = true;
+        v3 brdf = brdf_eval(V, h.normal, L, h.m);
+        float bpdf = brdf_pdf(V, h.normal, L, h.m);
+        // hdriLight, evaluated as if unoccluded (:922-946)
+        float r1 = u32_to_unit(wang_hash(&seed));
+        float r2 = u32_to_unit(wang_hash(&seed));
+        v3 hd = sample_hdr(p, r1, r2);
+        v3 hv = hdr_color(p, hd);
+        v3 hb = brdf_eval(V, h.normal, hd, h.m);
+        float hpdf = hdr_pdf(p, hd);
+        v3 hcalc = divs(mul(muls(hb, f_abs(dot(hd, h.normal))), hv), hpdf);
+        // calculatePointLight, as if unoccluded (:884-919)
+        v3 pcalc = splat(0.0f);
+        float4 shp = f4(0.0f, 0.0f, 0.0f, -1.0f);
+        if (p.pointLightSize != 0) {
+          float ppdf = (2.0f * PT_PI) / (float)p.pointLightSize;
+          int li = (int)(u32_to_unit(wang_hash(&seed)) * (float)p.pointLightSize);
+          v3 lpos = splat(0.0f), lrad = splat(0.0f);
+          if (li >= 0 && li < p.scene.nlights_buf) {
+            const float* lp = p.scene.lights + 6 * li;
+            lpos = mk(lp[0], lp[1], lp[2]);
+            lrad = mk(lp[3], lp[4], lp[5]);
+          }
+          v3 ld = normalize(sub(lpos, h.P));
+          float dist = length(sub(lpos, h.P));
+          v3 plv = divs(lrad, dist * dist);
+          v3 pb = brdf_eval(V, h.normal, ld, h.m);
+          pcalc = divs(muls(mul(plv, pb), f_abs(dot(ld, h.normal))), ppdf);
+          shp = f4(ld.x, ld.y, ld.z, dist);
+        }
+        v3 cosb = muls(brdf, f_abs(dot(L, h.normal)));
+        v3 bcalc = divs(mul(h.m.emissive, cosb), bpdf);
+        p.wf.pend0[pid] = f4(hcalc.x, hcalc.y, hcalc.z, hpdf);
+        p.wf.pend1[pid] = f4(pcalc.x, pcalc.y, pcalc.z, bpdf);
+        p.wf.pend2[pid] = f4(bcalc.x, bcalc.y, bcalc.z, 0.0f);
+        p.wf.pend3[pid] = f4(cosb.x, cosb.y, cosb.z, 0.0f);
+        p.wf.sh_h[pid] = f4(hd.x, hd.y, hd.z, 0.0f);
+        p.wf.sh_p[pid] = shp;
+        p.wf.ray_o[pid] = f4(h.P.x, h.P.y, h.P.z, 0.0f);
+        p.wf.ray_d[pid] = f4(L.x, L.y, L.z, 0.0f);
+        p.wf.red[pid] = f4(red.x, red.y, red.z, 0.0f);
+        p.wf.occ_h[pid] = 0;
+        p.wf.occ_p[pid] = 0;
+      }
+    }
+    p.wf.seed[pid] = seed;
+    p.wf.light[pid] = f4(light.x, light.y, light.z, 0.0f);
+  }
+  wave_push(push, pid, list_out, count_out);
+}
+
+// ----------------------------------------------------------------- finish ---
+__global__ void __launch_bounds__(256) wf_finish(PTParams p, const int* __restrict__ list,
+                                                 const int* __restrict__ count) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= *count) return;
+  const int pid = list[k];
+  float4 q0 = p.wf.pend0[pid], q1 = p.wf.pend1[pid], q2 = p.wf.pend2[pid], q3 = p.wf.pend3[pid];
+  v3 hcalc = xyz(q0), pcalc = xyz(q1), bcalc = xyz(q2), cosb = xyz(q3);
+  float hpdf = q0.w, bpdf = q1.w;
+  float ppdf = p.pointLightSize != 0 ? (2.0f * PT_PI) / (float)p.pointLightSize : 0.0f;
+  if (p.wf.occ_h[pid]) { hpdf = 0.0f; hcalc = splat(0.0f); }  // :934-937
+  if (p.wf.occ_p[pid]) pcalc = splat(0.0f);                   // :905-909 (pdf kept)
+  v3 red = xyz(p.wf.red[pid]), light = xyz(p.wf.light[pid]);
+  float sw = ((hpdf + ppdf) + bpdf) + 1e-6f;
+  float w1 = hpdf / sw, w2 = ppdf / sw, w3 = bpdf / sw;
+  v3 hitLight = mul(red, add(add(muls(hcalc, w1), muls(pcalc, w2)), muls(bcalc, w3)));
+  red = mul(red, divs(cosb, bpdf));
+  light = add(light, hitLight);
+  p.wf.red[pid] = f4(red.x, red.y, red.z, 0.0f);
+  p.wf.light[pid] = f4(light.x, light.y, light.z, 0.0f);
+}
+
+// --------------------------------------------------------------- finalize ---
+__global__ void __launch_bounds__(256) wf_finalize(PTParams p) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= p.W * (p.y1 - p.y0)) return;
+  int x, y;
+  pix_xy(p, k, &x, &y);
+  v3 light = vclamp(xyz(p.wf.light[k]), 0.0f, p.clamp_threshold);  // :1110-1113
+  v3 color = splat(0.0f);
+  if (!f_isnan(light.x) && !f_isnan(light.y) && !f_isnan(light.z)) color = light;
+  if (p.accumulate && p.last.p) {  // :1116-1119
+    float4 lc = pld(p.last, x, y);
+    color = mixv(xyz(lc), color, 1.0f / (float)(p.frameCounter + 1u));
+  }
+  pst(p.color, x, y, f4(color.x, color.y, color.z, 1.0f));
+}
+
+int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s) {
+  const int rows = p.y1 - p.y0;
+  if (rows <= 0) return 0;
+  const int N = p.W * rows;
+  hipError_t e = hipMemsetAsync(p.wf.counters, 0, 8 * sizeof(int), s);
+  if (e != hipSuccess) return (int)e;
+  dim3 tiles((p.W + 15) / 16, (rows + 15) / 16);
+  hipLaunchKernelGGL(wf_primary, tiles, dim3(256), 0, s, p);
+  const int gN = (N + 255) / 256, gT = (N + kTB - 1) / kTB, gT2 = (2 * N + kTB - 1) / kTB;
+  int* lists[2] = {p.wf.list0, p.wf.list1};
+  for (int i = 0; i < p.max_depth; ++i) {
+    const int* lin = lists[(i + 1) & 1];
+    int* lout = lists[i & 1];
+    const int* cin = p.wf.counters + (i > 0 ? i - 1 : 0);
+    int* cout = p.wf.counters + i;
+    if (i > 0) hipLaunchKernelGGL(wf_trace_closest, dim3(gT), dim3(kTB), 0, s, p, lin, cin);
+    hipLaunchKernelGGL(wf_shade, dim3(gN), dim3(256), 0, s, p, i, lin, cin, lout, cout);
+    hipLaunchKernelGGL(wf_trace_shadow, dim3(gT2), dim3(kTB), 0, s, p, (const int*)lout, (const int*)cout);
+    hipLaunchKernelGGL(wf_finish, dim3(gN), dim3(256), 0, s, p, (const int*)lout, (const int*)cout);
+  }
+  hipLaunchKernelGGL(wf_finalize, dim3(gN), dim3(256), 0, s, p);
+  return (int)hipGetLastError();
+}
+
+}  // namespace ptk

@@ -22,6 +22,9 @@
 struct float4 {
   float x, y, z, w;
 };
+struct int2 {
+  int x, y;
+};
 #endif
 
 namespace ptk {
@@ -52,6 +55,19 @@ struct SceneDev {
   int nlights_buf;      // lights actually present in the buffer
 };
 
+// Wavefront path-tracer state (kernels_wavefront.hip): SoA per band pixel.
+struct WFState {
+  float4 *ray_o, *ray_d;        // current ray (origin, direction)
+  float4 *light, *red;          // radiance accumulator, path throughput ("reduction")
+  float4 *pend0, *pend1, *pend2, *pend3;  // NEE terms awaiting the shadow verdicts
+  float4 *sh_h, *sh_p;          // shadow directions (HDR; point light + distance in .w)
+  int2* hit;                    // closest hit (triangle, t bits)
+  uint32_t* seed;               // RNG state (path_tracing.frag:433)
+  uint8_t *occ_h, *occ_p;       // shadow verdicts
+  int *list0, *list1;           // compacted live-ray lists (ping-pong)
+  int* counters;                // list lengths per bounce
+};
+
 struct PTParams {
   int W, H, y0, y1;     // frame size (global) and rows to compute
   Plane color, emission, albedo, last;  // outputs (+ lastFrame input)
@@ -68,6 +84,7 @@ struct PTParams {
   int aspect_corrected;
   int prune;            // closest-hit pruning (parity-safe margin)
   float sobol_u[4], sobol_v[4];  // sobolVec2(frameCounter+1, b): uniform across pixels
+  WFState wf;
 };
 
 struct GBufParams {
@@ -126,6 +143,7 @@ struct TAAParams {
 namespace ptk {
 // Launchers (kernels_*.hip). Return hipError_t as int.
 int launch_pathtrace(const PTParams& p, hipStream_t s);
+int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s);
 int launch_gbuffer(const GBufParams& p, hipStream_t s);
 int launch_reproject(const ReprojParams& p, hipStream_t s);
 int launch_variance(const VarianceParams& p, hipStream_t s);

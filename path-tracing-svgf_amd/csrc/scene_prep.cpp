@@ -570,18 +570,30 @@ struct Lcg {
   }
 };
 // Surface of revolution: profile (r_k, y_k), k = 0..np-1, `seg` segments, outward winding.
+// A zero radius is a pole: one vertex and a triangle fan (no zero-area faces).
 void lathe(MeshOut& m, const float* r, const float* y, int np, int seg) {
-  int base = (int)(m.pos.size() / 3);
-  for (int k = 0; k < np; ++k)
+  std::vector<int> start(np);
+  for (int k = 0; k < np; ++k) {
+    start[k] = (int)(m.pos.size() / 3);
+    if (r[k] == 0.0f) {
+      m.vert(0.0f, y[k], 0.0f);
+      continue;
+    }
     for (int s = 0; s < seg; ++s) {
       float a = 2.0f * glsl::kPI * (float)s / (float)seg;
       m.vert(r[k] * glsl::g_cos(a), y[k], r[k] * glsl::g_sin(a));
     }
-  for (int k = 0; k + 1 < np; ++k)
+  }
+  for (int k = 0; k + 1 < np; ++k) {
+    bool pa = r[k] == 0.0f, pb = r[k + 1] == 0.0f;
+    if (pa && pb) continue;
     for (int s = 0; s < seg; ++s) {
       int s1 = (s + 1) % seg;
-      m.quad(base + k * seg + s, base + (k + 1) * seg + s, base + (k + 1) * seg + s1, base + k * seg + s1);
+      if (pa) m.tri(start[k], start[k + 1] + s, start[k + 1] + s1);
+      else if (pb) m.tri(start[k] + s, start[k + 1], start[k] + s1);
+      else m.quad(start[k] + s, start[k + 1] + s, start[k + 1] + s1, start[k] + s1);
     }
+  }
 }
 // Tube along a polyline (centres c, radius rad), `seg` segments around.
 void tube(MeshOut& m, const std::vector<v3>& c, float rad, int seg) {
@@ -638,7 +650,7 @@ int pts_gen_plant(uint32_t seed, int leaves, int* nv, int* nt, float* positions,
     int base = (int)(m.pos.size() / 3);
     for (int a = 0; a <= nu; ++a) {
       float u = (float)a / nu;
-      float half = Wd * glsl::g_sin(glsl::kPI * u);
+      float half = Wd * (0.15f + 0.85f * glsl::g_sin(glsl::kPI * u));  // never zero width: no degenerate faces
       for (int b = 0; b <= nvv; ++b) {
         float v = (float)b / nvv * 2.0f - 1.0f;
         v3 p = glsl::add(tip, glsl::muls(fwd, L * u));

@@ -63,6 +63,7 @@ _PT_SIGS = [
     ("pt_init", C.c_int, [C.c_int]),
     ("pt_shutdown", C.c_int, []),
     ("pt_set_stream", C.c_int, [_vp]),
+    ("pt_use_own_stream", C.c_int, []),
     ("pt_sync", C.c_int, []),
     ("pt_last_error", C.c_char_p, []),
     ("pt_version", C.c_int, []),

@@ -1,0 +1,137 @@
+"""Screen-band sharding of one frame across GPUs.
+
+One process per GPU; rank r renders the horizontal band of global rows
+[y0, y1). The path tracer is embarrassingly parallel (RNG seeds use global pixel
+coordinates, path_tracing.frag:433-436), so it runs on owned rows only. The SVGF
+passes are bounded stencils; before each one the ranks swap halo rows with
+their up/down neighbours (torch.distributed P2P: RCCL over xGMI on the GPU,
+gloo on the CPU tests). The G-buffer ghost rows are recomputed locally (a
+primary-ray cast is cheaper than shipping 2 planes).
+
+Every frame-sized plane is stored with GHOST rows either side of the band:
+rows [row0, row1) = [y0 - GHOST, y1 + GHOST) clipped to the frame.
+
+HALO_SCHEDULE is the single source of truth for which planes are exchanged
+before which pass and how many rows; BandRenderer (GPU) and
+tests/test_dist_gloo.py (CPU, oracle) both execute it.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+# a-trous radius 2*step (svgf_Atrous.frag:92-97) up to step 16; variance radius 3
+# (svgf_variance.frag:273); reprojection taps within |motion|+2 rows (svgf_reproject.frag:63,116)
+ATROUS_HALO = [2 * (1 << i) for i in range(8)]
+VARIANCE_HALO = 3
+GHOST = 34
+
+# (stage, planes, rows): executed before `stage`
+HALO_SCHEDULE = (
+    ("reproject", ("prev_illum", "prev_moments"), "reproj"),
+    ("variance", ("illum", "moments"), VARIANCE_HALO),
+    *((f"atrous{i}", ("atrous_in",), ATROUS_HALO[i]) for i in range(8)),
+)
+
+
+@dataclass
+class BandPlan:
+    W: int
+    H: int
+    rank: int
+    world: int
+    ghost: int = GHOST
+    reproj_halo: int = 8
+
+    def __post_init__(self):
+        b = [(self.H * k) // self.world for k in range(self.world + 1)]
+        self.y0, self.y1 = b[self.rank], b[self.rank + 1]
+        if self.y1 - self.y0 < max(ATROUS_HALO[4], self.reproj_halo):
+            raise ValueError(f"band of {self.y1 - self.y0} rows is thinner than the largest halo")
+        if self.reproj_halo + 1 > self.ghost:
+            raise ValueError("reprojection halo exceeds the ghost rows")
+        self.row0 = max(0, self.y0 - self.ghost)
+        self.row1 = min(self.H, self.y1 + self.ghost)
+        self.rows = self.row1 - self.row0
+        self.up = self.rank - 1 if self.rank > 0 else None
+        self.down = self.rank + 1 if self.rank < self.world - 1 else None
+
+    def rows_for(self, n) -> int:
+        return self.reproj_halo if n == "reproj" else int(n)
+
+
+def halo_exchange(tensors, plan: BandPlan, n: int, dist, group=None) -> None:
+    """Swap n halo rows with both neighbours for each (rows, W, C) tensor holding rows [row0, row1)."""
+    if plan.world == 1 or n <= 0:
+        return
+    if tensors and tensors[0].is_cuda and dist.get_backend(group) == "gloo":
+        # gloo has no device P2P: stage through host memory (tests run 2 ranks on one GPU this way)
+        host = [t.cpu() for t in tensors]
+        halo_exchange(host, plan, n, dist, group)
+        for t, h in zip(tensors, host):
+            t.copy_(h)
+        return
+    ops = []
+    lo = plan.y0 - plan.row0  # local index of the first owned row
+    hi = plan.y1 - plan.row0  # one past the last owned row
+    for t in tensors:
+        if plan.up is not None:
+            k = min(n, lo)
+            ops.append(dist.P2POp(dist.isend, t[lo:lo + k], plan.up, group))  # row slices are contiguous
+            ops.append(dist.P2POp(dist.irecv, t[lo - k:lo], plan.up, group))
+        if plan.down is not None:
+            k = min(n, plan.rows - hi)
+            ops.append(dist.P2POp(dist.isend, t[hi - k:hi], plan.down, group))
+            ops.append(dist.P2POp(dist.irecv, t[hi:hi + k], plan.down, group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+
+
+class BandRenderer:
+    """One rank's share of a frame: the fast Renderer on band storage + HALO_SCHEDULE exchanges."""
+
+    def __init__(self, scene, W, H, cfg, rank, world, dist, reproj_halo: int = 8, **kw):
+        import torch
+
+        from . import gl
+        from .renderer import Renderer
+
+        self.plan = BandPlan(W, H, rank, world, reproj_halo=reproj_halo)
+        self.dist = dist
+        self._tensors = {}
+        gl.set_band(W, H, self.plan.y0, self.plan.y1, self.plan.row0, self.plan.rows)
+        dev = torch.device("cuda", torch.cuda.current_device())
+
+        def factory(w, h):
+            t = torch.zeros((self.plan.rows, w, 4), dtype=torch.float32, device=dev)
+            handle = gl.wrap_device_texture(t.data_ptr(), w, h)
+            self._tensors[handle] = t
+            return handle
+
+        kw.setdefault("run_taa", False)
+        kw.setdefault("run_output", False)
+        self.r = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, tex_factory=factory,
+                          halo=self._halo, gbuffer_rows=(self.plan.row0, self.plan.row1), **kw)
+        self.camera = self.r.camera
+        self.pass_path_tracing = self.r.pass_path_tracing
+
+    def _halo(self, stage: str, handles) -> None:
+        for st, _, n in HALO_SCHEDULE:
+            if st == stage:
+                halo_exchange([self._tensors[h] for h in handles], self.plan, self.plan.rows_for(n), self.dist)
+                return
+
+    def frame(self) -> None:
+        self.r.frame()
+
+    def profile(self, on: bool) -> None:
+        self.r.profile(on)
+
+    def pass_times(self) -> dict:
+        return self.r.pass_times()
+
+    def rows_rendered(self) -> int:
+        return self.plan.y1 - self.plan.y0
+
+    def planes(self) -> dict:
+        return self.r.planes()

@@ -33,8 +33,12 @@ def _prog(frag: str, vert: str = "vert.vert") -> int:
 class Renderer:
     def __init__(self, scene: Scene, width: int, height: int, config: parameter_config | None = None,
                  mode: str = "fast", aspect_corrected: bool | None = None, band=None, prune: bool = True,
-                 atrous_exact: bool = False, run_taa: bool = True, run_output: bool = True):
-        """band = (y0, y1, row0, rows) for screen-band sharding (see ptsvgf.dist)."""
+                 atrous_exact: bool = False, run_taa: bool = True, run_output: bool = True, tex_factory=None,
+                 halo=None, gbuffer_rows=None):
+        """band = (y0, y1, row0, rows) for screen-band sharding; tex_factory(w, h) -> handle allocates the
+        frame-sized planes (ptsvgf.dist wraps torch tensors); halo(stage, handles) is called before the
+        SVGF passes that read neighbour rows (dist.HALO_SCHEDULE); gbuffer_rows = (row0, row1) ghost rows
+        the G-buffer recomputes locally."""
         if mode not in ("fast", "reference"):
             raise ValueError(mode)
         if mode == "fast" and config is not None and config.accumulate_color:
@@ -53,17 +57,19 @@ class Renderer:
             y0, y1, row0, rows = band
             gl.set_band(self.W, self.H, y0, y1, row0, rows)
         self.band = band
+        self._halo_cb = halo
         W, H = self.W, self.H
-        tex = getTextureRGB32F
+        self._tex = tex_factory or getTextureRGB32F
+        tex = self._tex
 
         # scene buffers (main.cpp:136-181)
         self.trianglesTextureBuffer = gl.texture_buffer(scene.tri_enc)
         self.nodesTextureBuffer = gl.texture_buffer(scene.node_enc)
         self.pointLightBuffer = gl.texture_buffer(scene.lights)
         hh, hw, _ = scene.hdr.shape
-        self.hdrMap = tex(hw, hh)
+        self.hdrMap = getTextureRGB32F(hw, hh)
         gl.upload_rgb32f(self.hdrMap, scene.hdr)
-        self.hdrCache = tex(hw, hh)
+        self.hdrCache = getTextureRGB32F(hw, hh)
         gl.upload_rgb32f(self.hdrCache, scene.cache)
         self.hdrResolution = hw
 
@@ -79,6 +85,8 @@ class Renderer:
             p.bindData(scene.raster)
             p.set_uniform_int("screen_width", W)
             p.set_uniform_int("screen_height", H)
+            if gbuffer_rows is not None:
+                p.set_rows(*gbuffer_rows)
             self.init_pass.append(p)
             self.gbuf.append(g)
 
@@ -119,7 +127,7 @@ class Renderer:
         return p
 
     def _build_reference_passes(self):
-        W, H, tex = self.W, self.H, getTextureRGB32F
+        W, H, tex = self.W, self.H, self._tex
         self.tmp_atrous_result = tex(W, H)
         self.bilt_pass = self._svgf_pass("bilt.frag", [self.tmp_atrous_result])
         self.next_frame_color_input = tex(W, H)
@@ -146,7 +154,7 @@ class Renderer:
             p.set_uniform_float("inv_screen_height", 1.0 / H)
 
     def _build_fast_passes(self):
-        W, H, tex = self.W, self.H, getTextureRGB32F
+        W, H, tex = self.W, self.H, self._tex
         self.illum = tex(W, H)                                  # reproject out 0
         self.moments = [tex(W, H), tex(W, H)]                   # reproject out 1 (history, by parity)
         self.hist_illum = [tex(W, H), tex(W, H)]                # a-trous iteration 1 output (history)
@@ -279,6 +287,7 @@ class Renderer:
         pb = 1 - b
         g, gp = self.gbuf[b], self.gbuf[pb]
         self._gbuffer_and_pt(b)
+        self._halo("reproject", [self.hist_illum[pb], self.moments[pb]])
         rp = self.reproject[b]
         rp.reset_texture_slot()
         rp.set_uniform_float("depth_threshold", cfg.reproj_depth_threshold)
@@ -293,6 +302,7 @@ class Renderer:
         rp.set_texture_uniform(GL_TEXTURE_2D, gp["normal_depth"], "gPrevNormalAndLinearZ")
         rp.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
         self._draw(rp, "reproject")
+        self._halo("variance", [self.illum, self.moments[b]])
         vp = self.variance_compute_pass
         vp.reset_texture_slot()
         vp.set_uniform_float("gPhiColor", cfg.sigma_l)
@@ -315,6 +325,7 @@ class Renderer:
                 prev_tex = None if not dests else self._atrous_tex(dests[-1])
                 dests.append("pong" if prev_tex == self.ping else "ping")
         for i in range(n):
+            self._halo(f"atrous{i}", [src])
             ap = self.atrous_to[dests[i]]
             ap.reset_texture_slot()
             ap.set_uniform_float("gPhiColor", cfg.sigma_l)
@@ -326,8 +337,6 @@ class Renderer:
             ap.set_texture_uniform(GL_TEXTURE_2D, src, "gIllumination")
             self._draw(ap, "atrous")
             src = self._atrous_tex(dests[i])
-        if n < 2:  # history = iteration-1 output never produced; the reference keeps the old one
-            pass
         self.atrous_final = src
         mp = self.svgf_modulate_pass
         mp.reset_texture_slot()
@@ -346,6 +355,10 @@ class Renderer:
             tp.set_uniform_uint("frameCounter", self.camera.frameCounter)
             self._draw(tp, "taa")
         self.final = self.taa[b] if self.run_taa else self.modulate_color
+
+    def _halo(self, stage: str, handles) -> None:
+        if self._halo_cb is not None:
+            self._halo_cb(stage, handles)
 
     def _draw(self, p: RenderPass, name: str) -> None:
         p.draw()

@@ -32,6 +32,25 @@ def scene_small():
 
 
 @pytest.fixture(scope="session")
+def scene_nan():
+    """Clock + a quad fan holding one zero-area face: readObj's normal accumulation turns it into
+    NaN vertex normals on the neighbouring faces (obj_loader.h:101-110), exercising NaN paths."""
+    import numpy as np
+
+    from ptsvgf.scene import POINT_LIGHTS, Scene, SceneBuilder, env_map, hdr_cache, material, transform
+    b = SceneBuilder()
+    b.add_obj(os.path.join(REPO, "assets", "models", "clock.obj"), material(baseColor=(0.8, 0.6, 0.3)),
+              transform(), True, 0)
+    pos = np.array([[-0.6, -0.6, 0.2], [0.6, -0.6, 0.2], [0.6, 0.1, 0.2], [-0.6, 0.1, 0.2]], np.float32)
+    idx = np.array([[0, 1, 2], [0, 2, 3], [0, 0, 2]], np.int32)  # last face has zero area
+    b.add_mesh(pos, idx, material(baseColor=(0.3, 0.6, 0.8)), transform(), True, 1)
+    b.build(8)
+    tri, node, raster = b.encode()
+    hdr = env_map(128, 64)
+    return Scene("nan_probe", tri, node, raster, POINT_LIGHTS.copy(), hdr, hdr_cache(hdr), b.counts())
+
+
+@pytest.fixture(scope="session")
 def scene_cornell():
     from ptsvgf.scene import build_scene
 

@@ -1,0 +1,120 @@
+"""Multi-GPU band decomposition, validated on the CPU with gloo (world 2 and 3).
+
+Each rank holds only its band (+ ghost rows) of every plane; everything outside
+is poisoned with NaN. The ranks run the SVGF passes (CPU oracle) following
+ptsvgf.dist.HALO_SCHEDULE and exchange halos with ptsvgf.dist.halo_exchange —
+the same plan/schedule/exchange code the GPU BandRenderer runs over RCCL. The
+owned rows must equal the single-process full-frame result bit for bit: a
+missing or short halo lets NaN poison into the band.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, W, H, frames, moving):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "path-tracing-svgf_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle_ref as O
+        from ptsvgf.camera import rigid_inverse
+        from ptsvgf.dist import HALO_SCHEDULE, BandPlan, halo_exchange
+        from ptsvgf.scene import build_scene
+
+        scene = build_scene("table_clock_plant", hdr_size=(128, 64), plant_leaves=20)
+        plan = BandPlan(W, H, rank, world, ghost=34, reproj_halo=8)
+        full = O.OracleFrameLoop(scene, W, H, threads=2)
+        band = O.OracleFrameLoop(scene, W, H, threads=2)  # same camera path, band-restricted execution
+        sched = {st: n for st, _, n in HALO_SCHEDULE}
+
+        def poison(a, lo, hi):
+            a[:lo] = np.nan
+            a[hi:] = np.nan
+            return a
+
+        def halo(stage, arrays):
+            ts = [torch.from_numpy(a)[plan.row0:plan.row1] for a in arrays]
+            halo_exchange(ts, plan, plan.rows_for(sched[stage]), dist)
+
+        nan = lambda: np.full((H, W, 4), np.nan, np.float32)  # noqa: E731
+        prev_illum, prev_moments, prev_nd = nan(), nan(), nan()
+        for q in (prev_illum, prev_moments, prev_nd):  # history starts as zeros (the build zero-fills)
+            q[plan.row0:plan.row1] = 0.0
+        for f in range(frames):
+            if moving and f:
+                full.camera.orbit(1.5, 0.5)
+                band.camera.orbit(1.5, 0.5)
+            want = full.frame()
+            cam, cfg = band.camera, band.cfg
+            cam.update()
+            view, proj = cam.cam_view_mat, cam.cam_proj_mat
+            g = O.gbuffer(scene.raster, W, H, view, proj, band.pre_viewproj, 2)
+            for k in g:
+                poison(g[k], plan.row0, plan.row1)
+            col, em, al = band.os.path_trace(W, H, cam.frameCounter, cam.cam_position, rigid_inverse(view),
+                                             cfg.clamp_threshold, cfg.max_tracing_depth, band.aspect_corrected,
+                                             rows=(plan.y0, plan.y1), threads=2)
+            for a in (col, em, al):
+                poison(a, plan.y0, plan.y1)
+            halo("reproject", [prev_illum, prev_moments])
+            ri, rm = O.reproject(g["velocity"], col, al, em, prev_illum, prev_moments, g["normal_depth"], prev_nd,
+                                 g["fwidth"], np.float32(1.0 / W), np.float32(1.0 / H), 10.0, 16.0, 2)
+            poison(ri, plan.y0, plan.y1)
+            poison(rm, plan.y0, plan.y1)
+            halo("variance", [ri, rm])
+            a = poison(O.variance(ri, rm, g["normal_depth"], g["fwidth"], 4.0, 128.0, 2), plan.y0, plan.y1)
+            hist = None
+            for i in range(cfg.num_atrous_iterations):
+                halo(f"atrous{i}", [a])
+                a = poison(O.atrous(a, g["normal_depth"], g["fwidth"], 1 << i, 4.0, 128.0, 2), plan.y0, plan.y1)
+                if i == 1:
+                    hist = a
+            m = poison(O.modulate(al, em, a, g["normal_depth"], 2), plan.y0, plan.y1)
+            band.pre_viewproj = band._mat_mul(proj, view)
+            cam.frameCounter += 1
+            prev_illum, prev_moments, prev_nd = hist, rm, g["normal_depth"]
+            got = dict(color=col, reproj_illum=ri, reproj_moments=rm, variance=None, atrous=a, modulate=m)
+            for k, v in got.items():
+                if v is None:
+                    continue
+                o, w = v[plan.y0:plan.y1], want[k][plan.y0:plan.y1]
+                assert np.array_equal(np.isnan(o), np.isnan(w)), (rank, f, k, "NaN leaked into the band")
+                assert np.array_equal(np.nan_to_num(o), np.nan_to_num(w)), (rank, f, k)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,moving", [(2, False), (3, True)])
+def test_band_halo_schedule_gloo(world, moving):
+    W, H = 48, 108  # bands of 54 / 36 rows (>= the 32-row a-trous halo)
+    mp.spawn(_worker, args=(world, _free_port(), W, H, 3, moving), nprocs=world, join=True)
+
+
+def test_band_plan_properties():
+    from ptsvgf.dist import GHOST, BandPlan
+    for world in (1, 2, 4, 8):
+        plans = [BandPlan(3840, 2160, r, world) for r in range(world)]
+        assert plans[0].y0 == 0 and plans[-1].y1 == 2160
+        for a, b in zip(plans, plans[1:]):
+            assert a.y1 == b.y0 and a.down == b.rank and b.up == a.rank
+        for p in plans:
+            assert p.row0 == max(0, p.y0 - GHOST) and p.row1 == min(2160, p.y1 + GHOST)
+    with pytest.raises(ValueError):
+        BandPlan(64, 40, 0, 4)  # bands thinner than the a-trous halo

@@ -86,6 +86,21 @@ def test_cornell_teapot_matches_oracle(gpu, scene_cornell):
         _cmp(key, got[key], want[key], rel=True)
 
 
+def test_nan_normals_match_oracle(gpu, scene_nan):
+    """Degenerate faces -> NaN vertex normals: both sides propagate NaN identically."""
+    gl = gpu
+    W = H = 64
+    r = _renderer(scene_nan, W, H, mode="reference", atrous_exact=True, run_taa=False, run_output=False)
+    ref = O.OracleFrameLoop(scene_nan, W, H)
+    for f in range(2):
+        r.frame()
+        want = ref.frame()
+        got = _readback(gl, r)
+        assert np.isnan(want["normal_depth"]).any(), "probe scene must produce NaN normals"
+        for key in ("normal_depth", "color", "emission", "albedo", "reproj_illum", "variance", "atrous", "modulate"):
+            _cmp(f"f{f}/{key}", got[key], want[key], rel=True)
+
+
 def test_prune_is_result_preserving(gpu, scene_small):
     """Closest-hit box pruning (kernels_pt.hip) changes no pixel versus the reference's full traversal."""
     gl = gpu
@@ -96,6 +111,21 @@ def test_prune_is_result_preserving(gpu, scene_small):
         r.frame()
         outs.append(gl.readback(r.planes()["color"]))
     assert np.array_equal(outs[0], outs[1])
+
+
+def test_wavefront_equals_megakernel(gpu, scene_small):
+    """The staged (wavefront) path tracer and the single-kernel form give identical bits."""
+    gl = gpu
+    W, H = 96, 64
+    outs = []
+    for kern in (0, 1):
+        r = _renderer(scene_small, W, H, mode="fast", run_taa=False, run_output=False)
+        r.pass_path_tracing.set_uniform_int("pt_kernel", kern)
+        for _ in range(2):
+            r.frame()
+        outs.append({k: gl.readback(r.planes()[k]) for k in ("color", "emission", "albedo")})
+    for k in outs[0]:
+        assert np.array_equal(outs[0][k], outs[1][k]), k
 
 
 def test_fast_driver_equals_reference_driver(gpu, scene_small):

@@ -1,9 +1,9 @@
 #!/bin/bash
+# GPU session: all GPU tests, then the 4K bench.
 cd "$GRAFT_REPO_ROOT"
-echo "host: $(hostname) nproc=$(nproc)"; rocm-smi --showproductname 2>/dev/null | grep -i -E "card|series" | head -3
-timeout -k 10 900 python -m pytest tests/test_gpu_parity.py -x -q -m gpu -s > gpurun_out/t1.log 2>&1
+timeout -k 10 900 python -m pytest tests -x -q -m gpu -s > gpurun_out/t.log 2>&1
 rc=$?
-echo "pytest rc=$rc"
+echo "pytest rc=$rc"; grep -E "passed|failed|Error" gpurun_out/t.log | tail -5
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping (rc=$rc)"; exit $rc; fi
-timeout -k 10 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/b1.log 2>&1
-echo "bench rc=$?"
+timeout -k 10 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/b.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -c 1200 gpurun_out/b.log
