@@ -53,7 +53,8 @@ def cpu_baseline(scene, W, H, sample: str):
 
     sw, sh = (int(v) for v in sample.split("x"))
     threads = min(16, os.cpu_count() or 1)
-    loop = O.OracleFrameLoop(scene, sw, sh, parameter_config(), aspect_corrected=True, threads=threads)
+    loop = O.OracleFrameLoop(scene, sw, sh, parameter_config(), aspect_corrected=True, threads=threads,
+                              run_taa=False)
     loop.frame()  # warm (first frame: young history, full 7x7 variance)
     t0 = time.perf_counter()
     n = 0

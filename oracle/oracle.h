@@ -76,6 +76,10 @@ int orc_atrous(int W, int H, const float* illum, const float* normal_depth, cons
 int orc_modulate(int W, int H, const float* albedo, const float* emission, const float* illum,
                  const float* normal_depth, float* out, int threads);
 
+/* taa.frag:123-153 — history clip in YCoCg-R, velocity-weighted blend */
+int orc_taa(int W, int H, const float* cur, const float* prev, const float* velocity, const float* normal_depth,
+            uint32_t frameCounter, float* out, int threads);
+
 /* output_pass.frag:18-24 — Reinhard-like tonemap (limit 1.5) + gamma 1/2.2 */
 int orc_output(int W, int H, const float* color, float* out, int threads);
 

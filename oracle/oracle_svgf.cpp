@@ -318,3 +318,95 @@ extern "C" int orc_output(int W, int H, const float* color, float* out, int thre
     }
   return 0;
 }
+
+// ----------------------------------------------------------------- TAA ---
+// taa.frag restated with every fetch a full LINEAR-sampler fetch at the
+// shader's own float uv (the GPU kernel reads texels directly at the integer
+// offsets; agreement checks that shortcut too).
+namespace {
+// taa.frag:41-51
+inline v3 taa_rgb2ycocgr(v3 c) {
+  v3 r;
+  r.y = c.x - c.z;
+  float temp = c.z + r.y / 2.0f;
+  r.z = c.y - temp;
+  r.x = temp + r.z / 2.0f;
+  return r;
+}
+// taa.frag:53-63
+inline v3 taa_ycocgr2rgb(v3 c) {
+  v3 r;
+  float temp = c.x - c.z / 2.0f;
+  r.y = c.z + temp;
+  r.z = temp - c.y / 2.0f;
+  r.x = r.z + c.y;
+  return r;
+}
+// taa.frag:65-78
+inline float taa_luminance(v3 c) { return (0.25f * c.x + 0.5f * c.y) + 0.25f * c.z; }
+inline v3 taa_tonemap(v3 c) { return divs(c, 1.0f + taa_luminance(c)); }
+inline v3 taa_untonemap(v3 c) { return divs(c, 1.0f - taa_luminance(c)); }
+inline v3 taa_rgb(const Img& im, float u, float v) {
+  float o[3];
+  im.lin(u, v, o, 3);
+  return mk(o[0], o[1], o[2]);
+}
+}  // namespace
+
+extern "C" int orc_taa(int W, int H, const float* cur_p, const float* prev_p, const float* vel_p, const float* nd_p,
+                       uint32_t frameCounter, float* out, int threads) {
+  Img currentColor{cur_p, W, H}, previousColor{prev_p, W, H}, velocityTexture{vel_p, W, H}, normal_depth{nd_p, W, H};
+#pragma omp parallel for schedule(dynamic, 4) num_threads(threads > 0 ? threads : 1)
+  for (int y = 0; y < H; ++y)
+    for (int x = 0; x < W; ++x) {
+      float* o = out + ((size_t)y * W + x) * 4;
+      const float dX = 1.0f / (float)W, dY = 1.0f / (float)H;  // deltaRes (:17, :83)
+      float su = uv_of(x, W), sv = uv_of(y, H);                 // screenPosition (:124)
+      v3 nowColor = taa_rgb(currentColor, su, sv);               // :125
+      float t4[4];
+      normal_depth.lin(su, sv, t4, 4);
+      if (frameCounter == 0u || t4[3] == 1.0f) {                 // :126-135
+        o[0] = nowColor.x; o[1] = nowColor.y; o[2] = nowColor.z; o[3] = 1.0f;
+        continue;
+      }
+      // getClosestOffset (:15-39)
+      float closestDepth = 1.0f, cu = su, cv = sv;
+      for (int i = -1; i <= 1; ++i)
+        for (int j = -1; j <= 1; ++j) {
+          float nu = su + dX * (float)i, nv = sv + dY * (float)j;
+          normal_depth.lin(nu, nv, t4, 4);
+          if (t4[3] < closestDepth) { closestDepth = t4[3]; cu = nu; cv = nv; }
+        }
+      float vel[2];
+      velocityTexture.lin(cu, cv, vel, 2);                        // :137
+      float ou = f_clamp(su - vel[0], 0.0f, 1.0f), ov = f_clamp(sv - vel[1], 0.0f, 1.0f);  // :138
+      v3 preColor = taa_rgb(previousColor, ou, ov);               // :139
+      nowColor = taa_rgb2ycocgr(taa_tonemap(nowColor));           // :141
+      preColor = taa_rgb2ycocgr(taa_tonemap(preColor));           // :142
+      // clipAABB (:80-121)
+      v3 m1 = splat(0.0f), m2 = splat(0.0f);
+      for (int i = -1; i <= 1; ++i)
+        for (int j = -1; j <= 1; ++j) {
+          v3 C = taa_rgb2ycocgr(taa_tonemap(taa_rgb(currentColor, su + dX * (float)i, sv + dY * (float)j)));
+          m1 = add(m1, C);
+          m2 = add(m2, mul(C, C));
+        }
+      v3 mu = divs(m1, 9.0f);
+      v3 d = sub(divs(m2, 9.0f), mul(mu, mu));
+      v3 sigma = mk(f_sqrt(f_abs(d.x)), f_sqrt(f_abs(d.y)), f_sqrt(f_abs(d.z)));
+      v3 aabbMin = sub(mu, muls(sigma, 1.0f)), aabbMax = add(mu, muls(sigma, 1.0f));
+      v3 p_clip = muls(add(aabbMax, aabbMin), 0.5f), e_clip = muls(sub(aabbMax, aabbMin), 0.5f);
+      v3 v_clip = sub(preColor, p_clip);
+      v3 v_unit = divv(v_clip, e_clip);
+      float ma_unit = f_max(f_abs(v_unit.x), f_max(f_abs(v_unit.y), f_abs(v_unit.z)));
+      if (ma_unit > 1.0f) preColor = add(p_clip, divs(v_clip, ma_unit));
+      preColor = taa_untonemap(taa_ycocgr2rgb(preColor));         // :146
+      nowColor = taa_untonemap(taa_ycocgr2rgb(nowColor));         // :147
+      float blend = f_clamp(0.05f + f_sqrt(vel[0] * vel[0] + vel[1] * vel[1]) * 100.0f, 0.0f, 1.0f);  // :149
+      o[0] = blend * nowColor.x + (1.0f - blend) * preColor.x;    // :151
+      o[1] = blend * nowColor.y + (1.0f - blend) * preColor.y;
+      o[2] = blend * nowColor.z + (1.0f - blend) * preColor.z;
+      o[3] = 1.0f;
+    }
+  return 0;
+}

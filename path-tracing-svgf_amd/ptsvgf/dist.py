@@ -30,6 +30,8 @@ HALO_SCHEDULE = (
     ("reproject", ("prev_illum", "prev_moments"), "reproj"),
     ("variance", ("illum", "moments"), VARIANCE_HALO),
     *((f"atrous{i}", ("atrous_in",), ATROUS_HALO[i]) for i in range(8)),
+    # taa.frag: 3x3 neighbourhood of the current colour, history fetched at uv - velocity (:88-98, :137-139)
+    ("taa", ("modulate", "prev_taa"), "reproj"),
 )
 
 

@@ -346,6 +346,7 @@ class Renderer:
         mp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
         self._draw(mp, "modulate")
         if self.run_taa:
+            self._halo("taa", [self.modulate_color, self.taa[pb]])
             tp = self.pass_taa[b]
             tp.reset_texture_slot()
             tp.set_texture_uniform(GL_TEXTURE_2D, self.modulate_color, "currentColor")

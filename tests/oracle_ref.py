@@ -44,6 +44,7 @@ def lib() -> C.CDLL:
                                  C.c_float, _fp, C.c_int]
         L.orc_modulate.argtypes = [C.c_int, C.c_int, _fp, _fp, _fp, _fp, _fp, C.c_int]
         L.orc_output.argtypes = [C.c_int, C.c_int, _fp, _fp, C.c_int]
+        L.orc_taa.argtypes = [C.c_int, C.c_int, _fp, _fp, _fp, _fp, C.c_uint32, _fp, C.c_int]
         L.orc_wang_hash.restype = C.c_uint32
         L.orc_wang_hash.argtypes = [C.c_uint32]
         L.orc_sobol.restype = C.c_float
@@ -150,6 +151,14 @@ def modulate(albedo, emission, illum, nd, threads=THREADS):
     return o
 
 
+def taa(cur, prev, velocity, nd, frame_counter, threads=THREADS):
+    H, W, _ = cur.shape
+    ins = [f32(a) for a in (cur, prev, velocity, nd)]
+    o = frame(H, W)
+    lib().orc_taa(W, H, *[fp(a) for a in ins], int(frame_counter), fp(o), threads)
+    return o
+
+
 def output(color, threads=THREADS):
     H, W, _ = color.shape
     c = f32(color)
@@ -162,7 +171,8 @@ class OracleFrameLoop:
     """main.cpp:436-553 on the oracle: G-buffer -> PT -> reproject -> variance -> a-trous x N -> modulate,
     with the reference's history plumbing (iteration-1 a-trous output becomes next frame's gPrevIllum)."""
 
-    def __init__(self, scene, W, H, cfg=None, aspect_corrected=None, threads=THREADS):
+    def __init__(self, scene, W, H, cfg=None, aspect_corrected=None, threads=THREADS, run_taa=True,
+                 run_output=False):
         from ptsvgf.camera import Camera, mat_mul, parameter_config
         self.scene = scene
         self.os = OracleScene(scene)
@@ -171,9 +181,10 @@ class OracleFrameLoop:
         self.camera = Camera(W, H)
         self.aspect_corrected = (W != H) if aspect_corrected is None else aspect_corrected
         self.threads = threads
+        self.run_taa, self.run_output = run_taa, run_output
         self.pre_viewproj = mat_mul(self.camera.cam_proj_mat, self.camera.cam_view_mat)
         z = lambda: frame(H, W)  # noqa: E731
-        self.prev_illum, self.prev_moments, self.prev_nd = z(), z(), z()
+        self.prev_illum, self.prev_moments, self.prev_nd, self.prev_taa = z(), z(), z(), z()
         self._mat_mul = mat_mul
 
     def frame(self):
@@ -198,6 +209,11 @@ class OracleFrameLoop:
         m = modulate(al, em, a, g["normal_depth"], self.threads)
         out = dict(g, color=col, emission=em, albedo=al, reproj_illum=ri, reproj_moments=rm, variance=v, atrous=a,
                    history_illum=hist, modulate=m)
+        if self.run_taa:                                                  # main.cpp:537-544
+            out["final"] = self.prev_taa = taa(m, self.prev_taa, g["velocity"], g["normal_depth"], cam.frameCounter,
+                                               self.threads)
+            if self.run_output:                                           # main.cpp:555-591
+                out["output"] = output(out["final"], self.threads)
         self.prev_illum, self.prev_moments, self.prev_nd = hist, rm, g["normal_depth"]
         self.pre_viewproj = self._mat_mul(proj, view)
         cam.frameCounter += 1

@@ -54,8 +54,8 @@ def _worker(rank, world, port, W, H, frames, moving):
             halo_exchange(ts, plan, plan.rows_for(sched[stage]), dist)
 
         nan = lambda: np.full((H, W, 4), np.nan, np.float32)  # noqa: E731
-        prev_illum, prev_moments, prev_nd = nan(), nan(), nan()
-        for q in (prev_illum, prev_moments, prev_nd):  # history starts as zeros (the build zero-fills)
+        prev_illum, prev_moments, prev_nd, prev_taa = nan(), nan(), nan(), nan()
+        for q in (prev_illum, prev_moments, prev_nd, prev_taa):  # history starts as zeros (the build zero-fills)
             q[plan.row0:plan.row1] = 0.0
         for f in range(frames):
             if moving and f:
@@ -87,10 +87,13 @@ def _worker(rank, world, port, W, H, frames, moving):
                 if i == 1:
                     hist = a
             m = poison(O.modulate(al, em, a, g["normal_depth"], 2), plan.y0, plan.y1)
+            halo("taa", [m, prev_taa])
+            t = poison(O.taa(m, prev_taa, g["velocity"], g["normal_depth"], cam.frameCounter, 2), plan.y0, plan.y1)
+            prev_taa = t
             band.pre_viewproj = band._mat_mul(proj, view)
             cam.frameCounter += 1
             prev_illum, prev_moments, prev_nd = hist, rm, g["normal_depth"]
-            got = dict(color=col, reproj_illum=ri, reproj_moments=rm, variance=None, atrous=a, modulate=m)
+            got = dict(color=col, reproj_illum=ri, reproj_moments=rm, variance=None, atrous=a, modulate=m, final=t)
             for k, v in got.items():
                 if v is None:
                     continue

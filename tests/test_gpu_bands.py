@@ -12,7 +12,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 W, H, FRAMES = 64, 96, 3
-KEYS = ("color", "albedo", "reproj_illum", "variance", "atrous", "modulate")
+KEYS = ("color", "albedo", "reproj_illum", "variance", "atrous", "modulate", "final")
 
 
 def _port():
@@ -40,7 +40,7 @@ def _worker(rank, world, port, outdir, moving):
     gl.init(0)
     check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
     scene = build_scene("table_clock_plant", hdr_size=(256, 128), plant_leaves=40)
-    r = BandRenderer(scene, W, H, parameter_config(), rank, world, dist)
+    r = BandRenderer(scene, W, H, parameter_config(), rank, world, dist, run_taa=True)
     for f in range(FRAMES):
         if moving and f:
             r.camera.orbit(1.5, 0.5)
@@ -66,7 +66,7 @@ def test_two_bands_equal_full_frame(gpu, moving):
         mp.spawn(_worker, args=(2, _port(), d, moving), nprocs=2, join=True)
         bands = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(2)]
     scene = build_scene("table_clock_plant", hdr_size=(256, 128), plant_leaves=40)
-    full = Renderer(scene, W, H, parameter_config(), mode="fast", aspect_corrected=True, run_taa=False,
+    full = Renderer(scene, W, H, parameter_config(), mode="fast", aspect_corrected=True, run_taa=True,
                     run_output=False)
     for f in range(FRAMES):
         if moving and f:

@@ -157,3 +157,22 @@ def test_fast_atrous_within_tolerance(gpu, scene_small):
     got = _readback(gl, r)
     for key in ("atrous", "modulate"):
         _cmp(key, got[key], want[key], rel=True)
+
+
+@pytest.mark.parametrize("mode", ["reference", "fast"])
+def test_taa_and_output_match_oracle(gpu, scene_small, mode):
+    """taa.frag + output_pass.frag under an orbiting camera: the TAA history (last_taa_color)
+    goes through save_frame_data in the reference driver and a ping-pong pair in the fast driver."""
+    gl = gpu
+    W, H = 80, 64
+    r = _renderer(scene_small, W, H, mode=mode, atrous_exact=True, run_taa=True, run_output=True)
+    ref = O.OracleFrameLoop(scene_small, W, H, run_taa=True, run_output=True)
+    for f in range(4):
+        if f >= 2:
+            r.camera.orbit(1.5, -0.5)
+            ref.camera.orbit(1.5, -0.5)
+        r.frame()
+        want = ref.frame()
+        got = _readback(gl, r)
+        for key in ("modulate", "final", "output"):
+            _cmp(f"{mode}/f{f}/{key}", got[key], want[key], rel=True)

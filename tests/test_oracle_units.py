@@ -157,3 +157,25 @@ def test_brdf_pdf_normalised():
     vals = np.array([_pdf(V, [0, 0, 1], L, m) for L in Ls])
     est = vals.mean() * 2 * np.pi
     assert 0.85 < est < 1.15, est
+
+
+def test_taa_oracle_properties():
+    """taa.frag:126-135 pass-through cases and the steady state of the history clip."""
+    rng = np.random.default_rng(7)
+    H, W = 12, 16
+    cur = rng.uniform(0.0, 2.0, (H, W, 4)).astype(np.float32)
+    prev = rng.uniform(0.0, 2.0, (H, W, 4)).astype(np.float32)
+    vel = np.zeros((H, W, 4), np.float32)
+    nd = np.full((H, W, 4), 0.5, np.float32)
+    nd[:3, :, 3] = 1.0                                   # background rows (clear colour .w == 1)
+    out0 = O.taa(cur, prev, vel, nd, 0)                  # frameCounter 0: current colour
+    assert np.array_equal(out0[..., :3], cur[..., :3]) and (out0[..., 3] == 1).all()
+    out1 = O.taa(cur, prev, vel, nd, 5)
+    assert np.array_equal(out1[:3, :, :3], cur[:3, :, :3])  # background: current colour
+    # static history equal to a constant current image: clip box collapses, result is that colour
+    c = np.broadcast_to(np.float32([0.3, 0.6, 0.9, 1.0]), (H, W, 4)).copy()
+    out2 = O.taa(c, c, vel, nd, 5)
+    assert np.allclose(out2[3:, :, :3], c[3:, :, :3], rtol=1e-5)
+    # blend factor 0.05 with zero velocity: the result sits between the clipped history and the current colour
+    lo = np.minimum(cur, prev)[3:, :, :3] - 1e-3
+    assert np.isfinite(out1).all() and (out1[3:, :, :3] >= lo.min()).all()
