@@ -27,6 +27,23 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 ATROUS_BYTES_PER_PX = 52  # illum 16 + normal/z 16 + depth-fwidth 4 + write 16
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8 TB/s spec
+METRIC = "frames/sec @1spp+SVGF, 1080p & 4K; \u00e0-trous HBM GB/s vs peak"  # BASELINE.json "metric"
+ATROUS_KERNEL = "atrous_step_kernel"
+# HBM bytes per a-trous launch measured with rocprofv3 PMC passes (tools/gpu_profile.sh), committed under profiles/
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "atrous_traffic.json")
+
+
+def atrous_traffic(W, rows):
+    """PMC-measured HBM bytes per a-trous launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, in KB units as the
+    guide prescribes) from the committed profile, when it was taken for this kernel at this frame size."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if t.get("kernel") != ATROUS_KERNEL or t.get("pixels") != W * rows:
+        return None
+    return t.get("bytes_per_launch")
 
 
 def parse():
@@ -40,6 +57,8 @@ def parse():
     ap.add_argument("--moving", action="store_true", help="orbit the camera 1 deg/frame (configs[4])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default="480x270", help="oracle sample frame size for cpu_baseline")
+    ap.add_argument("--no-1080p", action="store_true", help="skip the secondary 1080p measurement")
+    ap.add_argument("--equal-bands", action="store_true", help="multi-GPU: equal band heights (no cost balancing)")
     ap.add_argument("--breakdown", action="store_true", help="print per-pass ms to stderr")
     ap.add_argument("--pt-kernel", type=int, default=0, help="0 wavefront (production), 1 megakernel (A/B)")
     return ap.parse_args()
@@ -92,7 +111,6 @@ def main():
     from ptsvgf.camera import parameter_config
     from ptsvgf.scene import build_scene
 
-    W, H = args.width, args.height
     scene = build_scene(args.scene)
     cfg = parameter_config()
     gl.init(local)
@@ -100,54 +118,65 @@ def main():
     from ptsvgf._lib import check, pt
     check(pt().pt_set_stream(stream.cuda_stream))
 
-    if world > 1:
-        from ptsvgf.dist import BandRenderer
-        r = BandRenderer(scene, W, H, cfg, rank, world, dist)
-    else:
-        from ptsvgf.renderer import Renderer
-        r = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, run_taa=False, run_output=False)
-    r.pass_path_tracing.set_uniform_int("pt_kernel", args.pt_kernel)
+    def run(W, H):
+        """Warm up, time exactly args.steps frames (barrier + sync on both sides, max over ranks), then one
+        profiled frame for the per-pass HIP-event breakdown."""
+        if world > 1:
+            from ptsvgf.dist import make_band_renderer
+            r = make_band_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands)
+        else:
+            from ptsvgf.renderer import Renderer
+            r = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, run_taa=False, run_output=False)
+        r.pass_path_tracing.set_uniform_int("pt_kernel", args.pt_kernel)
 
-    def step():
-        if args.moving:
-            r.camera.orbit(1.0, 0.0)
-        r.frame()
+        def step():
+            if args.moving:
+                r.camera.orbit(1.0, 0.0)
+            r.frame()
 
-    for _ in range(args.warmup):
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([dt], device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        r.profile(True)
         step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([dt], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        torch.cuda.synchronize()
+        per_pass = r.pass_times()
+        r.profile(False)
+        rows = r.rows_rendered() if hasattr(r, "rows_rendered") else H
+        r.close() if hasattr(r, "close") else None
+        return dt, per_pass, rows
+
+    W, H = args.width, args.height
+    dt, per_pass, rows = run(W, H)
     ms = dt / args.steps * 1e3
     fps = args.steps / dt  # whole frames per second (all ranks together render one frame)
+    extra = {}
+    if not args.no_1080p and (W, H) == (3840, 2160):
+        dt2, _, _ = run(1920, 1080)
+        extra = {"fps_1080p": round(args.steps / dt2, 3), "ms_per_step_1080p": round(dt2 / args.steps * 1e3, 3)}
 
-    # per-pass timing (HIP events on the library stream), after the timed region
-    r.profile(True)
-    step()
-    torch.cuda.synchronize()
-    per_pass = r.pass_times()
-    r.profile(False)
     atrous_ms = per_pass.get("atrous_avg_ms")
-    rows = r.rows_rendered() if hasattr(r, "rows_rendered") else H
     roof = None
     if atrous_ms:
         achieved = ATROUS_BYTES_PER_PX * W * rows / (atrous_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "atrous_fast_kernel", "avg_launch_ms": round(atrous_ms, 4),
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": atrous_traffic(W, rows),
+                "kernel": ATROUS_KERNEL, "avg_launch_ms": round(atrous_ms, 4),
                 "algorithmic_bytes_per_launch": ATROUS_BYTES_PER_PX * W * rows}
 
     cpu = None
@@ -158,7 +187,7 @@ def main():
             cpu = {"value": None, "error": str(e)}
 
     if rank == 0:
-        line = {"metric": "frames/sec @1spp+SVGF (4K); a-trous HBM GB/s vs peak", "value": round(fps, 3),
+        line = {"metric": METRIC, "value": round(fps, 3),
                 "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
                 "dtype": "f32", "data": "synthetic",
@@ -167,7 +196,7 @@ def main():
                            "resolution": [W, H], "spp": 1, "max_tracing_depth": cfg.max_tracing_depth,
                            "atrous_iterations": cfg.num_atrous_iterations, "triangles": scene.ntris,
                            "parallelism": f"bands{world}"},
-                "roofline": roof, "cpu_baseline": cpu,
+                "roofline": roof, "cpu_baseline": cpu, **extra,
                 "passes_ms": {k: round(v, 4) for k, v in per_pass.items()}}
         print(json.dumps(line), flush=True)
     gl.shutdown()

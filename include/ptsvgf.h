@@ -126,6 +126,11 @@ int pt_pass_set_uniform_vec3(uint32_t pass, const char* name, const float* v3);
 /* Rows this pass computes (global coords); default = the band. The G-buffer
  * pass uses it to compute ghost rows locally for multi-GPU halos. */
 int pt_pass_set_rows(uint32_t pass, int y_begin, int y_end);
+/* Load-balancing probe (path-tracing pass, wavefront kernel): while set, every
+ * draw ADDS the BVH node + triangle visits of each pixel's rays into
+ * device_counts[row - y_begin] (uint32 per computed row; caller zeroes it).
+ * NULL disables. No reference counterpart (multi-GPU band planning). */
+int pt_pass_set_row_cost(uint32_t pass, void* device_counts);
 int pt_pass_draw(uint32_t pass);
 /* Time the last draw of this pass (ms, HIP events on the library stream; syncs). */
 int pt_pass_last_ms(uint32_t pass, float* ms);

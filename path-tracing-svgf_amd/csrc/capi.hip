@@ -113,6 +113,7 @@ struct Pass {
   RasterScene raster;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
+  uint32_t* row_cost = nullptr;  // pt_pass_set_row_cost (not owned)
 };
 
 struct SceneGPU {
@@ -471,6 +472,7 @@ int draw_pathtrace(Pass* p) {
   } else {                            // 0: wavefront (kernels_wavefront.hip), production
     TRY(wf_alloc(p->wf, (size_t)k.W * (size_t)std::max(0, k.y1 - k.y0)));
     k.wf = p->wf.st;
+    k.wf.row_cost = p->row_cost;
     rc = launch_pathtrace_wavefront(k, g.stream);
   }
   return rc ? hip_err((hipError_t)rc, "pathtrace launch") : PT_OK;
@@ -565,7 +567,9 @@ int draw_svgf(Pass* p, int kind) {
     k.step = ui(p, "gStepSize", 1);
     k.phi_color = uf(p, "gPhiColor", 0.0f);
     k.phi_normal = uf(p, "gPhiNormal", 0.0f);
-    rc = ui(p, "exact", 0) ? launch_atrous_exact(k, g.stream) : launch_atrous_fast(k, g.stream);
+    if (ui(p, "exact", 0)) rc = launch_atrous_exact(k, g.stream);          // bit-exact form (tests)
+    else if (ui(p, "atrous_variant", 0) == 1) rc = launch_atrous_simple(k, g.stream);  // A/B
+    else rc = launch_atrous_fast(k, g.stream);                             // step-specialised
   } else if (kind == PK_MODULATE) {
     ModulateParams k;
     memset(&k, 0, sizeof(k));
@@ -1061,6 +1065,14 @@ int pt_pass_set_rows(uint32_t pass, int y0, int y1) {
   if (y0 < 0 || y1 > p->H || y0 > y1) return err(PT_ERR_ARG, "pt_pass_set_rows: bad range");
   p->y_begin = y0;
   p->y_end = y1;
+  return PT_OK;
+}
+
+int pt_pass_set_row_cost(uint32_t pass, void* device_counts) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  Pass* p = pass_of(pass);
+  if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
+  p->row_cost = (uint32_t*)device_counts;
   return PT_OK;
 }
 

@@ -10,6 +10,9 @@
 //  * the per-tap divisions by phiIllum / phiDepth*|offset| become multiplies by
 //    per-pixel reciprocals (5 distinct |offset| values);
 //  * depth fwidth comes from the compact 4-B side plane when present.
+// Built with -ffp-contract=off and explicit FMAs: the checked (border) and
+// unchecked (interior) instantiations must give identical bits, or a pixel's
+// result would depend on which band or block it falls in.
 #include <hip/hip_runtime.h>
 
 #include "glsl_builtins.h"
@@ -67,8 +70,9 @@ __global__ void __launch_bounds__(256) atrous_fast_kernel(AtrousParams p) {
       float4 q = ND[rn + px];
       float lp = (0.2125f * ip.x + 0.7154f * ip.y) + 0.0721f * ip.z;
       float dn = fminf(fmaxf((nd.x * q.x + nd.y * q.y) + nd.z * q.z, 0.0f), 1.0f);
+      // fmaxf: 0 * inf (phiIllumination == 0, equal luminance) is NaN, which the shader's max(., 0) zeroes
       float e = p.phi_normal * __builtin_amdgcn_logf(dn) -
-                (fabsf(lc - lp) * kL + fabsf(nd.w - q.w) * (kD * invlen));
+                (fmaxf(fabsf(lc - lp) * kL, 0.0f) + fabsf(nd.w - q.w) * (kD * invlen));
       float w = __builtin_amdgcn_exp2f(e) * kern;
       sumW += w;
       s0 += w * ip.x;
@@ -86,7 +90,152 @@ __global__ void __launch_bounds__(256) atrous_fast_kernel(AtrousParams p) {
   *out = o;
 }
 
+// ---------------------------------------------------------------------------
+// Step-specialised form (production). The simple kernel above is VALU-bound, not
+// HBM-bound: per tap it spends ~39 VALU instructions, a third of them 64-bit
+// address arithmetic and bounds tests. Here the step is a template constant, so
+// for blocks whose 5x5 dilated footprint lies inside the frame and the band
+// (all but the border blocks) every tap is a load from a wave-uniform row
+// pointer (SGPR base) at a constant column offset (immediate), with no tests;
+// the 1/|offset| and kernel weights fold into per-pixel constants and the
+// exponent. Border blocks run the checked path with the same arithmetic.
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+struct AtrousCentre {
+  float4 ic, nd;
+  float wLr, wLg, wLb, cL;      // kL * luminance weights, -(lc * kL)
+  float lc, kD1, kD2, kD4, kD5, kD8, phiN;
+};
+
+// The 24 taps of one pixel. FLAT: phiIllumination == 0 (variance <= -1e-10 or NaN),
+// where the shader's |lc - lp| / phiIllumination is +inf (weight 0) unless
+// lp == lc (0/0 = NaN, which max(., 0) turns into 0): handled exactly, apart.
+template <int S, bool EDGE, bool FLAT>
+__device__ __forceinline__ void atrous_taps(const AtrousParams& p, const AtrousCentre& c, int x, int y, int ly,
+                                            float& sumW, f2v& s01, f2v& s23) {
+  const int W = p.illum.W;
+  const float4* __restrict__ I = p.illum.p;
+  const float4* __restrict__ ND = p.nd.p;
+#pragma unroll
+  for (int yy = -2; yy <= 2; ++yy) {
+    const int py = y + yy * S;
+    if (EDGE && (py < 0 || py >= p.H)) continue;
+    const float4* __restrict__ Ir = I + (size_t)(EDGE ? arow(p.illum, py) : ly + yy * S) * W;
+    const float4* __restrict__ Nr = ND + (size_t)(EDGE ? arow(p.nd, py) : ly + yy * S) * W;
+#pragma unroll
+    for (int xx = -2; xx <= 2; ++xx) {
+      if (xx == 0 && yy == 0) continue;
+      const int px = x + xx * S;
+      if (EDGE && (px < 0 || px >= p.W)) continue;
+      const int r2 = xx * xx + yy * yy;
+      const float kDl = r2 == 1 ? c.kD1 : r2 == 2 ? c.kD2 : r2 == 4 ? c.kD4 : r2 == 5 ? c.kD5 : c.kD8;
+      const int ax = xx < 0 ? -xx : xx, ay = yy < 0 ? -yy : yy;
+      const float kern = (ax == 0 ? 1.0f : ax == 1 ? 2.0f / 3.0f : 1.0f / 6.0f) *
+                         (ay == 0 ? 1.0f : ay == 1 ? 2.0f / 3.0f : 1.0f / 6.0f);
+      const float4 ip = Ir[px];
+      const float4 q = Nr[px];
+      const float dn = fminf(fmaxf(__builtin_fmaf(c.nd.z, q.z, __builtin_fmaf(c.nd.y, q.y, c.nd.x * q.x)), 0.0f),
+                             1.0f);
+      float a;
+      if (FLAT) {
+        const float lp = (0.2125f * ip.x + 0.7154f * ip.y) + 0.0721f * ip.z;
+        a = lp == c.lc ? fabsf(c.nd.w - q.w) * kDl : __builtin_inff();
+      } else {
+        const float tl = __builtin_fmaf(ip.z, c.wLb, __builtin_fmaf(ip.y, c.wLg, __builtin_fmaf(ip.x, c.wLr, c.cL)));
+        a = __builtin_fmaf(fabsf(c.nd.w - q.w), kDl, fabsf(tl));
+      }
+      const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(c.phiN, __builtin_amdgcn_logf(dn), -a)) * kern;
+      sumW += w;
+      s01 = __builtin_elementwise_fma(f2v{w, w}, f2v{ip.x, ip.y}, s01);
+      s23 = __builtin_elementwise_fma(f2v{w, w * w}, f2v{ip.z, ip.w}, s23);
+    }
+  }
+}
+
+template <int S, bool EDGE>
+__device__ __forceinline__ void atrous_pixel(const AtrousParams& p, int x, int y) {
+  const int W = p.illum.W;
+  const int ly = EDGE ? arow(p.illum, y) : y - p.illum.row0;
+  AtrousCentre c;
+  c.ic = p.illum.p[(size_t)ly * W + x];
+  c.nd = p.nd.p[(size_t)ly * W + x];
+  float4* out = p.out.p + (size_t)ly * W + x;
+  if (c.nd.w == 1.0f) {
+    *out = c.ic;
+    return;
+  }
+  const float LOG2E = 1.4426950408889634f;
+  c.lc = (0.2125f * c.ic.x + 0.7154f * c.ic.y) + 0.0721f * c.ic.z;
+  const float phiL = p.phi_color * __builtin_sqrtf(fmaxf(0.0f, 1e-10f + c.ic.w));
+  const float fwz = p.fwidth.aux ? p.fwidth.aux[(size_t)ly * W + x] : p.fwidth.p[(size_t)ly * W + x].y;
+  const float kL = LOG2E / phiL;
+  // |lc - lp| * kL = |lp*kL - lc*kL|: luminance weights pre-scaled, centre folded into the first FMA
+  c.wLr = 0.2125f * kL;
+  c.wLg = 0.7154f * kL;
+  c.wLb = 0.0721f * kL;
+  c.cL = -(c.lc * kL);
+  const float kD = LOG2E / (fmaxf(fwz, 1e-8f) * (float)S);
+  // kD / |offset| for |offset|^2 = 1, 2, 4, 5, 8
+  c.kD1 = kD;
+  c.kD2 = kD * 0.70710678f;
+  c.kD4 = kD * 0.5f;
+  c.kD5 = kD * 0.44721360f;
+  c.kD8 = kD * 0.35355339f;
+  c.phiN = p.phi_normal;
+  float sumW = 1.0f;
+  f2v s01 = {c.ic.x, c.ic.y}, s23 = {c.ic.z, c.ic.w};  // packed accumulators (v_pk_fma_f32)
+  if (__builtin_expect(phiL > 0.0f, 1)) atrous_taps<S, EDGE, false>(p, c, x, y, ly, sumW, s01, s23);
+  else atrous_taps<S, EDGE, true>(p, c, x, y, ly, sumW, s01, s23);
+  const float inv = 1.0f / sumW;
+  float4 o;
+  o.x = s01.x * inv;
+  o.y = s01.y * inv;
+  o.z = s23.x * inv;
+  o.w = s23.y * (inv * inv);
+  *out = o;
+}
+
+// Block = 4 waves, each one row of 64 pixels; the row index is wave-uniform so
+// the compiler keeps row pointers in SGPRs. Every plane of the pass must hold the
+// same rows (always true for frame planes; the launcher checks).
+template <int S>
+__global__ void __launch_bounds__(256) atrous_step_kernel(AtrousParams p) {
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int x0 = blockIdx.x * 64;
+  const int y = p.y0 + blockIdx.y * 4 + wv;
+  if (y >= p.y1) return;
+  const int x = x0 + (threadIdx.x & 63);
+  const int yb = p.y0 + blockIdx.y * 4;
+  const int lo = max(0, p.illum.row0), hi = min(p.H, p.illum.row0 + p.illum.rows);
+  const bool interior = x0 - 2 * S >= 0 && x0 + 63 + 2 * S < p.W && yb - 2 * S >= lo &&
+                        yb + 3 + 2 * S < hi;
+  if (interior) {
+    atrous_pixel<S, false>(p, x, y);
+  } else if (x < p.W) {
+    atrous_pixel<S, true>(p, x, y);
+  }
+}
+
 int launch_atrous_fast(const AtrousParams& p, hipStream_t s) {
+  if (p.y1 <= p.y0) return 0;
+  const Plane* planes[3] = {&p.nd, &p.out, &p.fwidth};
+  int same = 1;
+  for (const Plane* q : planes)
+    if (q->row0 != p.illum.row0 || q->rows != p.illum.rows || q->W != p.illum.W) same = 0;
+  if (!same) return launch_atrous_simple(p, s);
+  dim3 grid((p.W + 63) / 64, (p.y1 - p.y0 + 3) / 4);
+  switch (p.step) {
+    case 1: hipLaunchKernelGGL(atrous_step_kernel<1>, grid, dim3(256), 0, s, p); break;
+    case 2: hipLaunchKernelGGL(atrous_step_kernel<2>, grid, dim3(256), 0, s, p); break;
+    case 4: hipLaunchKernelGGL(atrous_step_kernel<4>, grid, dim3(256), 0, s, p); break;
+    case 8: hipLaunchKernelGGL(atrous_step_kernel<8>, grid, dim3(256), 0, s, p); break;
+    case 16: hipLaunchKernelGGL(atrous_step_kernel<16>, grid, dim3(256), 0, s, p); break;
+    default: return launch_atrous_simple(p, s);  // other steps (iterations > 5): generic kernel
+  }
+  return (int)hipGetLastError();
+}
+
+int launch_atrous_simple(const AtrousParams& p, hipStream_t s) {
   if (p.y1 <= p.y0) return 0;
   dim3 grid((p.W + 63) / 64, (p.y1 - p.y0 + 3) / 4);
   hipLaunchKernelGGL(atrous_fast_kernel, grid, dim3(256), 0, s, p);

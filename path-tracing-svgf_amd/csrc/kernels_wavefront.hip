@@ -42,6 +42,11 @@ __device__ __forceinline__ void wave_push(bool push, int value, int* __restrict_
   if (push) list[base + __popcll(mask & ((1ull << lane) - 1ull))] = value;
 }
 
+// load-balancing probe: accumulate traversal steps per band row (only when requested)
+__device__ __forceinline__ void add_row_cost(const PTParams& p, int local_row, uint32_t steps) {
+  if (p.wf.row_cost) atomicAdd(p.wf.row_cost + local_row, steps);
+}
+
 __device__ __forceinline__ v3 primary_dir(const PTParams& p, int x, int y) {
   float pixx = (float)(2 * x + 1) / (float)p.W - 1.0f;
   float pixy = (float)(2 * y + 1) / (float)p.H - 1.0f;
@@ -64,8 +69,10 @@ __global__ void __launch_bounds__(256) wf_primary(PTParams p) {
   v3 S = mk(p.eye[0], p.eye[1], p.eye[2]);
   v3 d = primary_dir(p, x, y);
   float t;
-  int tri = traverse<0, 256>(p.scene, stk + threadIdx.x, S, d, 0.0f, p.prune, &t);
+  uint32_t steps;
+  int tri = traverse<0, 256>(p.scene, stk + threadIdx.x, S, d, 0.0f, p.prune, &t, &steps);
   p.wf.hit[pid] = make_int2(tri, __float_as_int(t));
+  add_row_cost(p, y - p.y0, steps);
 }
 
 // ----------------------------------------------------------- bounce trace ---
@@ -77,8 +84,10 @@ __global__ void __launch_bounds__(kTB) wf_trace_closest(PTParams p, const int* _
   const int pid = list[k];
   float4 o = p.wf.ray_o[pid], dd = p.wf.ray_d[pid];
   float t;
-  int tri = traverse<0, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dd), 0.0f, p.prune, &t);
+  uint32_t steps;
+  int tri = traverse<0, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dd), 0.0f, p.prune, &t, &steps);
   p.wf.hit[pid] = make_int2(tri, __float_as_int(t));
+  add_row_cost(p, pid / p.W, steps);
 }
 
 // HDR shadow rays in the first half of the grid, point-light shadow rays in the second.
@@ -92,14 +101,16 @@ __global__ void __launch_bounds__(kTB) wf_trace_shadow(PTParams p, const int* __
   const int pid = list[point ? k - n : k];
   float4 o = p.wf.ray_o[pid];
   float ts;
+  uint32_t steps;
   if (!point) {
     float4 hd = p.wf.sh_h[pid];
-    p.wf.occ_h[pid] = traverse<1, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(hd), 0.0f, 0, &ts) >= 0;
+    p.wf.occ_h[pid] = traverse<1, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(hd), 0.0f, 0, &ts, &steps) >= 0;
   } else {
     float4 ld = p.wf.sh_p[pid];
     if (ld.w < 0.0f) return;  // pointLightSize == 0: no ray
-    p.wf.occ_p[pid] = traverse<2, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(ld), ld.w, 0, &ts) >= 0;
+    p.wf.occ_p[pid] = traverse<2, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(ld), ld.w, 0, &ts, &steps) >= 0;
   }
+  add_row_cost(p, pid / p.W, steps);
 }
 
 // ------------------------------------------------------------------ shade ---

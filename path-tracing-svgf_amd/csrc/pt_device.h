@@ -66,6 +66,7 @@ struct WFState {
   uint8_t *occ_h, *occ_p;       // shadow verdicts
   int *list0, *list1;           // compacted live-ray lists (ping-pong)
   int* counters;                // list lengths per bounce
+  uint32_t* row_cost;           // optional: traversal steps per band row (load-balancing probe), may be null
 };
 
 struct PTParams {
@@ -149,6 +150,7 @@ int launch_reproject(const ReprojParams& p, hipStream_t s);
 int launch_variance(const VarianceParams& p, hipStream_t s);
 int launch_atrous_exact(const AtrousParams& p, hipStream_t s);
 int launch_atrous_fast(const AtrousParams& p, hipStream_t s);
+int launch_atrous_simple(const AtrousParams& p, hipStream_t s);
 int launch_modulate(const ModulateParams& p, hipStream_t s);
 int launch_output(const OutputParams& p, hipStream_t s);
 int launch_taa(const TAAParams& p, hipStream_t s);

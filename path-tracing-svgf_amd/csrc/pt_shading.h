@@ -80,18 +80,21 @@ __device__ __forceinline__ int ref_leaf_count(int ref) { return (-(ref + 1)) & 1
 // `stk` points at this lane's first slot; slots are STRIDE ints apart (LDS column).
 constexpr int kNone = (int)0x80000000;  // "no node" (leaf refs are >= -(2^31 - 1))
 
+// `steps` (optional) receives the node + triangle visits (load-balancing probe).
 template <int MODE, int STRIDE>
 __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, float maxd, int prune,
-                        float* t_best_out) {
+                        float* t_best_out, uint32_t* steps = nullptr) {
   v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   float tbest = PT_INF;
   int best = -1;
   int sp = 0;
   int node = sc.root_ref;
   int leaf = kNone;
+  uint32_t nvis = 0;
   if (node < 0) { leaf = node; node = kNone; }
   while (node != kNone || leaf != kNone) {
     while (node >= 0) {  // interior nodes (kNone and leaf refs are negative)
+      ++nvis;
       const float4* nd = sc.bvh + 4 * node;
       float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
       float t0l, t0r;
@@ -128,17 +131,18 @@ __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
     }
     while (leaf != kNone) {
       int first = ref_leaf_first(leaf), cnt = ref_leaf_count(leaf);
+      nvis += (uint32_t)cnt;
       for (int i = first; i < first + cnt; ++i) {
         float t;
         if (!tri_hit(sc.tri_geom, i, S, d, &t)) continue;
         if (MODE == 0) {
           if (t < tbest) { tbest = t; best = i; }
         } else if (MODE == 1) {
-          if (t < PT_INF) { *t_best_out = t; return i; }
+          if (t < PT_INF) { *t_best_out = t; if (steps) *steps = nvis; return i; }
         } else {
           if (t < PT_INF) {
             float sd = length(sub(add(S, muls(d, t)), S));
-            if (sd < maxd) { *t_best_out = t; return i; }
+            if (sd < maxd) { *t_best_out = t; if (steps) *steps = nvis; return i; }
           }
         }
       }
@@ -150,6 +154,7 @@ __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
     }
   }
   *t_best_out = tbest;
+  if (steps) *steps = nvis;
   return best;
 }
 

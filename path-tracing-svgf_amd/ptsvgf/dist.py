@@ -43,9 +43,12 @@ class BandPlan:
     world: int
     ghost: int = GHOST
     reproj_halo: int = 8
+    bounds: tuple | None = None  # world+1 row boundaries (balanced_bounds); None = equal bands
 
     def __post_init__(self):
-        b = [(self.H * k) // self.world for k in range(self.world + 1)]
+        b = list(self.bounds) if self.bounds is not None else [(self.H * k) // self.world for k in range(self.world + 1)]
+        if len(b) != self.world + 1 or b[0] != 0 or b[-1] != self.H or any(x >= y for x, y in zip(b, b[1:])):
+            raise ValueError(f"bad band bounds {b}")
         self.y0, self.y1 = b[self.rank], b[self.rank + 1]
         if self.y1 - self.y0 < max(ATROUS_HALO[4], self.reproj_halo):
             raise ValueError(f"band of {self.y1 - self.y0} rows is thinner than the largest halo")
@@ -59,6 +62,34 @@ class BandPlan:
 
     def rows_for(self, n) -> int:
         return self.reproj_halo if n == "reproj" else int(n)
+
+
+MIN_BAND_ROWS = max(ATROUS_HALO[4], 8) + 4  # a band must hold the widest halo it ships (5-iteration a-trous)
+
+
+def balanced_bounds(row_cost, world: int, min_rows: int = MIN_BAND_ROWS, align: int = 2) -> tuple:
+    """Row boundaries splitting a frame into `world` bands of equal summed cost.
+
+    row_cost[y] is the estimated time of row y (measure_row_cost). Boundary k is the first row where the
+    cumulative cost reaches k/world of the total, rounded to `align` rows and pushed so that every band keeps
+    at least `min_rows` rows. Pure function of its inputs, so every rank computes the same plan."""
+    import numpy as np
+
+    c = np.asarray(row_cost, dtype=np.float64)
+    H = c.size
+    if world * min_rows > H:
+        raise ValueError(f"{world} bands of >= {min_rows} rows do not fit {H} rows")
+    cum = np.concatenate([[0.0], np.cumsum(np.maximum(c, 0.0))])
+    total = cum[-1]
+    b = [0]
+    for k in range(1, world):
+        y = int(np.searchsorted(cum, total * k / world)) if total > 0 else (H * k) // world
+        y = int(round(y / align) * align)
+        lo = b[-1] + min_rows                   # previous band keeps min_rows
+        hi = H - (world - k) * min_rows         # the remaining bands still fit
+        b.append(min(max(y, lo), hi))
+    b.append(H)
+    return tuple(b)
 
 
 def halo_exchange(tensors, plan: BandPlan, n: int, dist, group=None) -> None:
@@ -92,13 +123,13 @@ def halo_exchange(tensors, plan: BandPlan, n: int, dist, group=None) -> None:
 class BandRenderer:
     """One rank's share of a frame: the fast Renderer on band storage + HALO_SCHEDULE exchanges."""
 
-    def __init__(self, scene, W, H, cfg, rank, world, dist, reproj_halo: int = 8, **kw):
+    def __init__(self, scene, W, H, cfg, rank, world, dist, reproj_halo: int = 8, bounds=None, **kw):
         import torch
 
         from . import gl
         from .renderer import Renderer
 
-        self.plan = BandPlan(W, H, rank, world, reproj_halo=reproj_halo)
+        self.plan = BandPlan(W, H, rank, world, reproj_halo=reproj_halo, bounds=bounds)
         self.dist = dist
         self._tensors = {}
         gl.set_band(W, H, self.plan.y0, self.plan.y1, self.plan.row0, self.plan.rows)
@@ -137,3 +168,69 @@ class BandRenderer:
 
     def planes(self) -> dict:
         return self.r.planes()
+
+    def close(self) -> None:
+        self.r.close()
+        self._tensors.clear()
+
+    def measure_row_cost(self):
+        """Estimated time (ms) of every frame row, identical on all ranks: one probed frame counts each row's
+        BVH visits (pt_pass_set_row_cost) and times every pass; the per-rank frame times are fitted as
+        T_k = a * visits_k + b * rows_k over the ranks (least squares, a, b >= 0) and spread back onto rows."""
+        import numpy as np
+        import torch
+
+        p, W, H = self.plan, self.r.W, self.r.H
+        dev = torch.device("cuda", torch.cuda.current_device())
+        counts = torch.zeros(p.y1 - p.y0, dtype=torch.int32, device=dev)
+        self.pass_path_tracing.set_row_cost(counts.data_ptr())
+        self.r.profile(True)
+        self.r.frame()
+        torch.cuda.synchronize()
+        times = self.r.pass_times()
+        self.r.profile(False)
+        self.pass_path_tracing.set_row_cost(0)
+        frame_ms = times["frame_sum_ms"]
+        visits = torch.zeros(H, dtype=torch.float64, device=dev)
+        visits[p.y0:p.y1] = counts.to(torch.float64)
+        per_rank = torch.zeros(3 * p.world, dtype=torch.float64, device=dev)
+        per_rank[3 * p.rank:3 * p.rank + 3] = torch.tensor([counts.sum().item(), p.y1 - p.y0, frame_ms],
+                                                           dtype=torch.float64)
+        self.dist.all_reduce(visits)
+        self.dist.all_reduce(per_rank)
+        v = visits.cpu().numpy()
+        m = per_rank.cpu().numpy().reshape(p.world, 3)
+        a, b = fit_row_cost(m[:, 0], m[:, 1], m[:, 2])
+        return a * v + b
+
+
+def fit_row_cost(visits, rows, ms):
+    """Least-squares T = a*visits + b*rows with a, b >= 0 (falls back to a single term when the 2-term fit
+    goes negative or is singular)."""
+    import numpy as np
+
+    A = np.stack([np.asarray(visits, np.float64), np.asarray(rows, np.float64)], 1)
+    t = np.asarray(ms, np.float64)
+    try:
+        (a, b), *_ = np.linalg.lstsq(A, t, rcond=None)
+    except np.linalg.LinAlgError:
+        a = b = -1.0
+    if a >= 0 and b >= 0 and a + b > 0:
+        return float(a), float(b)
+    if A[:, 0].sum() > 0:
+        return float(t.sum() / A[:, 0].sum()), 0.0
+    return 0.0, float(t.sum() / max(A[:, 1].sum(), 1.0))
+
+
+def make_band_renderer(scene, W, H, cfg, rank, world, dist, balance: bool = True, **kw):
+    """BandRenderer whose band heights equalise the measured per-row cost (sky rows are cheap, the plant
+    and clock rows expensive). Calibration renders two frames on equal bands (warm-up + probe), then the
+    renderer is rebuilt on the balanced plan; every rank derives the same bounds from all-reduced data."""
+    r = BandRenderer(scene, W, H, cfg, rank, world, dist, **kw)
+    if not balance or world == 1:
+        return r
+    r.frame()
+    cost = r.measure_row_cost()
+    bounds = balanced_bounds(cost, world)
+    r.close()
+    return BandRenderer(scene, W, H, cfg, rank, world, dist, bounds=bounds, **kw)

@@ -181,6 +181,15 @@ class RenderPass:
     def set_rows(self, y0: int, y1: int) -> None:
         check(pt().pt_pass_set_rows(self._handle(), y0, y1))
 
+    def set_row_cost(self, device_ptr: int) -> None:
+        """Accumulate per-row BVH visits into a device uint32 array (path tracer; 0 disables)."""
+        check(pt().pt_pass_set_row_cost(self._handle(), C.c_void_p(device_ptr or None)))
+
+    def destroy(self) -> None:
+        if self._h is not None:
+            check(pt().pt_pass_destroy(self._h))
+            self._h = None
+
     def last_ms(self) -> float:
         v = C.c_float()
         check(pt().pt_pass_last_ms(self._handle(), C.byref(v)))

@@ -59,8 +59,15 @@ class Renderer:
         self.band = band
         self._halo_cb = halo
         W, H = self.W, self.H
-        self._tex = tex_factory or getTextureRGB32F
-        tex = self._tex
+        self._owned: list[int] = []   # every texture this renderer created (close() destroys them)
+        make = tex_factory or getTextureRGB32F
+
+        def tex(w, h):
+            t = make(w, h)
+            self._owned.append(t)
+            return t
+
+        self._tex = tex
 
         # scene buffers (main.cpp:136-181)
         self.trianglesTextureBuffer = gl.texture_buffer(scene.tri_enc)
@@ -71,6 +78,8 @@ class Renderer:
         gl.upload_rgb32f(self.hdrMap, scene.hdr)
         self.hdrCache = getTextureRGB32F(hw, hh)
         gl.upload_rgb32f(self.hdrCache, scene.cache)
+        self._owned += [self.trianglesTextureBuffer, self.nodesTextureBuffer, self.pointLightBuffer, self.hdrMap,
+                        self.hdrCache]
         self.hdrResolution = hw
 
         nbuf = 2 if mode == "fast" else 1
@@ -402,6 +411,16 @@ class Renderer:
         self.frame_index += 1
 
     # --------------------------------------------------------- accessors ---
+    def close(self) -> None:
+        """Release every pass and texture this renderer created (the GL objects main.cpp never frees)."""
+        for v in list(vars(self).values()):
+            for q in (v if isinstance(v, list) else list(v.values()) if isinstance(v, dict) else [v]):
+                if isinstance(q, RenderPass):
+                    q.destroy()
+        for t in self._owned:
+            gl.destroy_texture(t)
+        self._owned = []
+
     def planes(self) -> dict:
         """Handles of this frame's per-pass outputs (for readback / tests)."""
         if self.mode == "reference":

@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, W, H, frames, moving):
+def _worker(rank, world, port, W, H, frames, moving, bounds=None):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, here)
@@ -39,7 +39,7 @@ def _worker(rank, world, port, W, H, frames, moving):
         from ptsvgf.scene import build_scene
 
         scene = build_scene("table_clock_plant", hdr_size=(128, 64), plant_leaves=20)
-        plan = BandPlan(W, H, rank, world, ghost=34, reproj_halo=8)
+        plan = BandPlan(W, H, rank, world, ghost=34, reproj_halo=8, bounds=bounds)
         full = O.OracleFrameLoop(scene, W, H, threads=2)
         band = O.OracleFrameLoop(scene, W, H, threads=2)  # same camera path, band-restricted execution
         sched = {st: n for st, _, n in HALO_SCHEDULE}
@@ -104,10 +104,10 @@ def _worker(rank, world, port, W, H, frames, moving):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,moving", [(2, False), (3, True)])
-def test_band_halo_schedule_gloo(world, moving):
-    W, H = 48, 108  # bands of 54 / 36 rows (>= the 32-row a-trous halo)
-    mp.spawn(_worker, args=(world, _free_port(), W, H, 3, moving), nprocs=world, join=True)
+@pytest.mark.parametrize("world,moving,bounds", [(2, False, None), (3, True, None), (2, True, (0, 38, 108))])
+def test_band_halo_schedule_gloo(world, moving, bounds):
+    W, H = 48, 108  # bands of 54 / 36 rows (>= the 32-row a-trous halo); uneven (balanced) split 38 / 70
+    mp.spawn(_worker, args=(world, _free_port(), W, H, 3, moving, bounds), nprocs=world, join=True)
 
 
 def test_band_plan_properties():
@@ -121,3 +121,29 @@ def test_band_plan_properties():
             assert p.row0 == max(0, p.y0 - GHOST) and p.row1 == min(2160, p.y1 + GHOST)
     with pytest.raises(ValueError):
         BandPlan(64, 40, 0, 4)  # bands thinner than the a-trous halo
+
+
+def test_balanced_bounds_properties():
+    from ptsvgf.dist import MIN_BAND_ROWS, balanced_bounds, fit_row_cost
+    rng = np.random.default_rng(3)
+    for world in (2, 3, 4, 8):
+        cost = rng.uniform(0.0, 1.0, 2160)
+        cost[:700] *= 6.0                              # an expensive region
+        b = balanced_bounds(cost, world)
+        assert b[0] == 0 and b[-1] == 2160 and len(b) == world + 1
+        sizes = np.diff(b)
+        assert (sizes >= MIN_BAND_ROWS).all() and all(x % 2 == 0 for x in b)
+        sums = [cost[x:y].sum() for x, y in zip(b, b[1:])]
+        assert max(sums) <= cost.sum() / world * 1.05   # equal cost within row granularity
+    # zero cost degenerates to equal bands; a band never shrinks below the halo
+    assert balanced_bounds(np.zeros(200), 4) == (0, 50, 100, 150, 200)
+    spike = np.zeros(400)
+    spike[10] = 1.0
+    b = balanced_bounds(spike, 4)
+    assert (np.diff(b) >= MIN_BAND_ROWS).all()
+    with pytest.raises(ValueError):
+        balanced_bounds(np.ones(100), 4)
+    a, c = fit_row_cost([10.0, 30.0], [100, 100], [2.0, 4.0])
+    assert abs(a - 0.1) < 1e-9 and abs(c - 0.01) < 1e-9
+    a, c = fit_row_cost([10.0, 30.0], [100, 100], [5.0, 1.0])   # negative slope -> single-term fallback
+    assert a >= 0 and c >= 0

@@ -1,0 +1,76 @@
+"""Production a-trous kernels (kernels_atrous.hip) against the exact oracle on
+synthetic planes large enough that every step (1..16) runs both the interior
+(unchecked) and the border (checked) code paths, with the special cases the
+shader's arithmetic has: background pixels (z == 1), phiIllumination == 0
+(variance <= -1e-10) next to neighbours of exactly equal luminance, zero depth
+fwidth, NaN normals. Bar: north_star's 1e-3 per channel (relative above 1)."""
+import numpy as np
+import pytest
+
+import oracle_ref as O
+
+pytestmark = pytest.mark.gpu
+
+W, H = 320, 200
+
+
+def _planes(seed=11):
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+    illum = np.empty((H, W, 4), np.float32)
+    illum[..., :3] = rng.uniform(0.0, 3.0, (H, W, 3))
+    illum[..., 3] = rng.uniform(0.0, 0.5, (H, W))
+    illum[40:60, 100:140, 3] = -1.0                 # phiIllumination == 0 ...
+    illum[40:60, 100:140, :3] = 0.5                 # ... with neighbours of equal luminance
+    illum[45, 120, :3] = 0.75
+    n = np.stack([0.2 * np.sin(xx * 0.05), 0.2 * np.cos(yy * 0.07), np.ones_like(xx)], -1)
+    n += rng.normal(0.0, 0.02, n.shape)
+    n /= np.linalg.norm(n, axis=-1, keepdims=True)
+    nd = np.empty((H, W, 4), np.float32)
+    nd[..., :3] = n
+    nd[..., 3] = 2.0 + 0.01 * xx + 0.02 * yy + rng.normal(0.0, 0.01, (H, W))
+    bg = rng.uniform(size=(H, W)) < 0.08
+    nd[bg] = (0.2, 0.3, 0.3, 1.0)                   # clear colour: background sentinel
+    nd[150:152, 30:34, :3] = np.nan                 # NaN normals (degenerate faces)
+    fw = np.zeros((H, W, 4), np.float32)
+    fw[..., 1] = rng.uniform(0.0, 0.05, (H, W))
+    fw[80:90, :, 1] = 0.0
+    return illum, nd, fw
+
+
+def _run(gl, illum, nd, fw, step, variant):
+    from ptsvgf.gl import GL_TEXTURE_2D, RenderPass, getShaderProgram, getTextureRGB32F
+    ti, tn, tf, to = (getTextureRGB32F(W, H) for _ in range(4))
+    gl.upload_rgba(ti, illum)
+    gl.upload_rgba(tn, nd)
+    gl.upload_rgba(tf, fw)
+    p = RenderPass(getShaderProgram("shaders/svgf_Atrous.frag", "shaders/vert.vert"), W, H)
+    p.colorAttachments.append(to)
+    p.bindData(False)
+    p.set_uniform_float("gPhiColor", 4.0)
+    p.set_uniform_float("gPhiNormal", 128.0)
+    p.set_uniform_int("gStepSize", step)
+    p.set_uniform_int("atrous_variant", variant)
+    p.set_texture_uniform(GL_TEXTURE_2D, ti, "gIllumination")
+    p.set_texture_uniform(GL_TEXTURE_2D, tn, "gNormalAndLinearZ")
+    p.set_texture_uniform(GL_TEXTURE_2D, tf, "gNormalDepthFwidth")
+    p.draw()
+    out = gl.readback(to)
+    p.destroy()
+    for t in (ti, tn, tf, to):
+        gl.destroy_texture(t)
+    return out
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("step", [1, 2, 4, 8, 16])
+def test_atrous_kernel_vs_oracle(gpu, step, variant):
+    illum, nd, fw = _planes()
+    want = O.atrous(illum, nd, fw, step)
+    got = _run(gpu, illum, nd, fw, step, variant)
+    assert np.array_equal(np.isnan(got), np.isnan(want)), \
+        f"NaN pattern differs: gpu {int(np.isnan(got).sum())} oracle {int(np.isnan(want).sum())}"
+    d = np.abs(got.astype(np.float64) - want) / np.maximum(1.0, np.abs(want))
+    mx = float(np.nanmax(d))
+    print(f"step {step} variant {variant}: max rel diff {mx:.3e}")
+    assert mx <= 1e-3

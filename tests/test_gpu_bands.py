@@ -23,7 +23,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, outdir, moving):
+def _worker(rank, world, port, outdir, moving, balance):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(os.path.dirname(here), "path-tracing-svgf_amd"))
@@ -34,13 +34,13 @@ def _worker(rank, world, port, outdir, moving):
     from ptsvgf import gl
     from ptsvgf._lib import check, pt
     from ptsvgf.camera import parameter_config
-    from ptsvgf.dist import BandRenderer
+    from ptsvgf.dist import make_band_renderer
     from ptsvgf.scene import build_scene
     torch.cuda.set_device(0)
     gl.init(0)
     check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
     scene = build_scene("table_clock_plant", hdr_size=(256, 128), plant_leaves=40)
-    r = BandRenderer(scene, W, H, parameter_config(), rank, world, dist, run_taa=True)
+    r = make_band_renderer(scene, W, H, parameter_config(), rank, world, dist, balance=balance, run_taa=True)
     for f in range(FRAMES):
         if moving and f:
             r.camera.orbit(1.5, 0.5)
@@ -53,8 +53,8 @@ def _worker(rank, world, port, outdir, moving):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("moving", [False, True])
-def test_two_bands_equal_full_frame(gpu, moving):
+@pytest.mark.parametrize("moving,balance", [(False, False), (True, False), (True, True)])
+def test_two_bands_equal_full_frame(gpu, moving, balance):
     import torch.multiprocessing as mp
 
     from ptsvgf.camera import parameter_config
@@ -63,7 +63,7 @@ def test_two_bands_equal_full_frame(gpu, moving):
 
     gl = gpu
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(2, _port(), d, moving), nprocs=2, join=True)
+        mp.spawn(_worker, args=(2, _port(), d, moving, balance), nprocs=2, join=True)
         bands = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(2)]
     scene = build_scene("table_clock_plant", hdr_size=(256, 128), plant_leaves=40)
     full = Renderer(scene, W, H, parameter_config(), mode="fast", aspect_corrected=True, run_taa=True,

@@ -7,7 +7,7 @@ R="$GRAFT_REPO_ROOT"
 OUT="$R/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-B="$R/bench.py --steps 5 --warmup 2 --no-cpu-baseline"
+B="$R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-1080p"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $B > "$OUT/trace.log" 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $B > "$OUT/fetch.log" 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 $B > "$OUT/write.log" 2>&1 || exit $?
