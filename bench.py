@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--scene", default="table_clock_plant")
     ap.add_argument("--moving", action="store_true", help="orbit the camera 1 deg/frame (configs[4])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", default="480x270", help="oracle sample frame size for cpu_baseline")
+    ap.add_argument("--cpu-sample", default="960x540", help="oracle sample frame size for cpu_baseline")
     ap.add_argument("--no-1080p", action="store_true", help="skip the secondary 1080p measurement")
     ap.add_argument("--equal-bands", action="store_true", help="multi-GPU: equal band heights (no cost balancing)")
     ap.add_argument("--breakdown", action="store_true", help="print per-pass ms to stderr")
@@ -80,7 +80,7 @@ def cpu_baseline(scene, W, H, sample: str):
     while True:
         loop.frame()
         n += 1
-        if time.perf_counter() - t0 > 10.0 or n >= 20:
+        if time.perf_counter() - t0 > 10.0 and n >= 3:  # ~10 s of CPU work
             break
     dt = (time.perf_counter() - t0) / n
     scale = (W * H) / (sw * sh)
