@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--equal-bands", action="store_true", help="multi-GPU: equal band heights (no cost balancing)")
     ap.add_argument("--breakdown", action="store_true", help="print per-pass ms to stderr")
     ap.add_argument("--pt-kernel", type=int, default=0, help="0 wavefront (production), 1 megakernel (A/B)")
+    ap.add_argument("--pt-uniform", action="append", default=[], metavar="NAME=INT",
+                    help="extra int uniform on the path-tracing pass (A/B switches, e.g. shadow_bvh4=0)")
     return ap.parse_args()
 
 
@@ -128,6 +130,9 @@ def main():
             from ptsvgf.renderer import Renderer
             r = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, run_taa=False, run_output=False)
         r.pass_path_tracing.set_uniform_int("pt_kernel", args.pt_kernel)
+        for kv in args.pt_uniform:
+            name, val = kv.split("=")
+            r.pass_path_tracing.set_uniform_int(name, int(val))
 
         def step():
             if args.moving:

@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -120,6 +121,9 @@ struct SceneGPU {
   float4* geom = nullptr;
   float4* shade = nullptr;
   float4* bvh = nullptr;
+  float4* bvh4 = nullptr;
+  bool has4 = false;
+  int root4 = 0;
   int root_ref = 0;
   int ntris = 0;
   uint64_t tri_ver = 0, node_ver = 0;
@@ -246,6 +250,69 @@ int pack_bvh(const float* node_enc, int nnodes, std::vector<float4>& out, int* r
   return PT_OK;
 }
 
+// 4-wide BVH for any-hit (shadow) rays, collapsed from the same binary SAH tree:
+// each 4-wide node holds up to four descendants of one binary node, opened
+// largest-surface-area first. Any-hit answers do not depend on visiting order,
+// and a box nested in a passing parent box passes the same slab test (rounding
+// is monotone), so skipping the intermediate levels changes no verdict.
+// Layout (7 x float4 = 112 B): lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] refs[4];
+// refs: >= 0 node index, < 0 leaf (binary encoding), kNone = empty slot.
+int pack_bvh4(const float* node_enc, int nnodes, int ntris, std::vector<float4>& out, int* root_ref) {
+  std::vector<NodeRaw> nd(nnodes);
+  for (int i = 0; i < nnodes; ++i) {
+    const float* f = node_enc + (size_t)i * 12;
+    nd[i].left = (int)f[0];
+    nd[i].right = (int)f[1];
+    nd[i].n = (int)f[3];
+    nd[i].index = (int)f[4];
+    for (int k = 0; k < 3; ++k) { nd[i].AA[k] = f[6 + k]; nd[i].BB[k] = f[9 + k]; }
+  }
+  out.clear();
+  auto leaf = [&](int id) { return -(nd[id].index * 16 + nd[id].n) - 1; };
+  if (nd[1].n > 0) { *root_ref = leaf(1); return PT_OK; }
+  auto area = [&](int id) {
+    const NodeRaw& n = nd[id];
+    float dx = n.BB[0] - n.AA[0], dy = n.BB[1] - n.AA[1], dz = n.BB[2] - n.AA[2];
+    return dx * dy + dy * dz + dz * dx;
+  };
+  int depth4 = 0;
+  std::string bad;
+  std::function<int(int, int)> build = [&](int bin, int depth) -> int {
+    depth4 = std::max(depth4, depth);
+    std::vector<int> ch{nd[bin].left, nd[bin].right};
+    while (ch.size() < 4) {  // open the largest interior child
+      int best = -1;
+      float ba = -1.0f;
+      for (size_t c = 0; c < ch.size(); ++c)
+        if (nd[ch[c]].n <= 0 && area(ch[c]) > ba) { ba = area(ch[c]); best = (int)c; }
+      if (best < 0) break;
+      const int b = ch[best];
+      ch[best] = nd[b].left;
+      ch.insert(ch.begin() + best + 1, nd[b].right);
+    }
+    const int k = (int)(out.size() / 7);
+    out.resize(out.size() + 7, float4{0, 0, 0, 0});
+    int refs[4] = {kNoneRef, kNoneRef, kNoneRef, kNoneRef};
+    for (size_t c = 0; c < ch.size(); ++c) {
+      const NodeRaw& n = nd[ch[c]];
+      float* q = (float*)&out[7 * (size_t)k];
+      for (int a = 0; a < 3; ++a) { q[8 * a + c] = n.AA[a]; q[8 * a + 4 + c] = n.BB[a]; }
+      if (n.n > 15) bad = "BVH leaf holds more than 15 triangles";
+      else if (n.n > 0 && (n.index < 0 || n.index + n.n > ntris)) bad = "BVH leaf range out of bounds";
+      if (n.n > 0) refs[c] = leaf(ch[c]);
+      else refs[c] = build(ch[c], depth + 1);  // may reallocate `out`
+    }
+    memcpy(&out[7 * (size_t)k + 6], refs, 16);
+    return k;
+  };
+  build(1, 1);
+  if (!bad.empty()) return err(PT_ERR_FORMAT, bad);
+  // traversal continues into one hit child and pushes the other (up to 3) per level
+  if (3 * depth4 + 1 > kStack) return err(PT_ERR_FORMAT, "4-wide BVH deeper than the traversal stack");
+  *root_ref = 0;
+  return PT_OK;
+}
+
 template <class T>
 int upload_vec(const std::vector<T>& v, T** dst) {
   if (*dst) { (void)hipFree(*dst); *dst = nullptr; }
@@ -285,10 +352,15 @@ int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU*
     s[7] = float4{f[36], f[37], f[38], f[39]};
     s[8] = float4{f[40], f[41], 0.0f, 0.0f};
   }
-  std::vector<float4> bvh;
-  int root = 0;
+  std::vector<float4> bvh, bvh4;
+  int root = 0, root4 = 0;
   int rc = pack_bvh((const float*)nodes->host.data(), (int)nnodes, bvh, &root, (int)ntris);
   if (rc != PT_OK) return rc;
+  // the 4-wide any-hit tree is optional: a scene too deep for it keeps the binary walk
+  sg.has4 = pack_bvh4((const float*)nodes->host.data(), (int)nnodes, (int)ntris, bvh4, &root4) == PT_OK;
+  if (sg.has4 && (rc = upload_vec(bvh4.empty() ? std::vector<float4>{float4{0, 0, 0, 0}} : bvh4, &sg.bvh4)) != PT_OK)
+    return rc;
+  sg.root4 = root4;
   if ((rc = upload_vec(geom, &sg.geom)) != PT_OK) return rc;
   if ((rc = upload_vec(shade, &sg.shade)) != PT_OK) return rc;
   if (bvh.empty()) bvh.push_back(float4{0, 0, 0, 0});
@@ -432,6 +504,8 @@ int draw_pathtrace(Pass* p) {
   k.scene.tri_shade = sg->shade;
   k.scene.bvh = sg->bvh;
   k.scene.root_ref = sg->root_ref;
+  k.scene.bvh4 = (sg->has4 && ui(p, "shadow_bvh4", 1)) ? sg->bvh4 : nullptr;  // 0: binary walk (A/B)
+  k.scene.root4 = sg->root4;
   k.scene.ntris = sg->ntris;
   if (lt && lt->target == PT_TEXTURE_BUFFER) {
     k.scene.lights = (const float*)lt->dev;
@@ -664,6 +738,7 @@ int pt_shutdown(void) {
     if (kv.second.geom) (void)hipFree(kv.second.geom);
     if (kv.second.shade) (void)hipFree(kv.second.shade);
     if (kv.second.bvh) (void)hipFree(kv.second.bvh);
+    if (kv.second.bvh4) (void)hipFree(kv.second.bvh4);
   }
   if (g.own) (void)hipStreamDestroy(g.own);
   g = Lib();

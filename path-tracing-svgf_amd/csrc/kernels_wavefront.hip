@@ -104,11 +104,15 @@ __global__ void __launch_bounds__(kTB) wf_trace_shadow(PTParams p, const int* __
   uint32_t steps;
   if (!point) {
     float4 hd = p.wf.sh_h[pid];
-    p.wf.occ_h[pid] = traverse<1, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(hd), 0.0f, 0, &ts, &steps) >= 0;
+    p.wf.occ_h[pid] = p.scene.bvh4
+                          ? anyhit4<1, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(hd), 0.0f, &steps)
+                          : traverse<1, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(hd), 0.0f, 0, &ts, &steps) >= 0;
   } else {
     float4 ld = p.wf.sh_p[pid];
     if (ld.w < 0.0f) return;  // pointLightSize == 0: no ray
-    p.wf.occ_p[pid] = traverse<2, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(ld), ld.w, 0, &ts, &steps) >= 0;
+    p.wf.occ_p[pid] = p.scene.bvh4
+                          ? anyhit4<2, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(ld), ld.w, &steps)
+                          : traverse<2, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(ld), ld.w, 0, &ts, &steps) >= 0;
   }
   add_row_cost(p, pid / p.W, steps);
 }

@@ -12,6 +12,8 @@
 //           tri_shade 9 x float4 / triangle  normals, material, uv, objIndex  closest hit only
 //           bvh       4 x float4 / interior node: both children's AABBs + child refs
 //    (children refs >= 0: interior index; < 0: leaf = -(first*16 + count) - 1);
+//           bvh4      7 x float4 / node: the 4-wide collapse for any-hit (shadow) rays,
+//                     lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] refs[4];
 //  * HDR map / importance cache: float4 per texel (RGB32F padded), row-major.
 #pragma once
 #include <stdint.h>
@@ -31,6 +33,7 @@ namespace ptk {
 
 constexpr int kStack = 32;       // traversal stack depth (host checks BVH depth < kStack)
 constexpr int kBlock = 256;      // threads per block for per-pixel kernels
+constexpr int kNoneRef = (int)0x80000000;  // "no node" (leaf refs are >= -(2^31 - 1))
 
 struct Plane {          // banded RGBA32F plane
   float4* p;
@@ -50,6 +53,8 @@ struct SceneDev {
   const float4* tri_shade;
   const float4* bvh;
   int root_ref;         // >= 0 interior node index, < 0 leaf ref
+  const float4* bvh4;   // 4-wide collapse of bvh for any-hit rays (7 x float4 / node), may be null
+  int root4;
   int ntris;
   const float* lights;  // 6 floats per light (PointLight: position, radiance)
   int nlights_buf;      // lights actually present in the buffer

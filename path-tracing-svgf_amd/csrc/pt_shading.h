@@ -78,7 +78,7 @@ __device__ __forceinline__ int ref_leaf_count(int ref) { return (-(ref + 1)) & 1
 // intersected in the order the depth-first walk reaches them, so the strict '<'
 // tie rule of hitArray/hitBVH picks the same triangle.
 // `stk` points at this lane's first slot; slots are STRIDE ints apart (LDS column).
-constexpr int kNone = (int)0x80000000;  // "no node" (leaf refs are >= -(2^31 - 1))
+constexpr int kNone = kNoneRef;
 
 // `steps` (optional) receives the node + triangle visits (load-balancing probe).
 template <int MODE, int STRIDE>
@@ -156,6 +156,75 @@ __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
   *t_best_out = tbest;
   if (steps) *steps = nvis;
   return best;
+}
+
+// Any-hit traversal of the 4-wide BVH (shadow rays): MODE 1 any hit, MODE 2 any
+// hit nearer than `maxd` by length(P - S) — the same triangle tests as
+// traverse<1|2>, whose verdict does not depend on the order leaves are visited.
+// Per node: the four child boxes are slab-tested (same hitAABB arithmetic); the
+// walk continues into one hit child and pushes the others; leaves are postponed
+// one per lane (while-while) so the wave intersects together.
+template <int MODE, int STRIDE>
+__device__ bool anyhit4(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, float maxd, uint32_t* steps) {
+  v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const float lim = maxd * 1.0002f + 2.0e-4f;
+  int sp = 0;
+  int node = sc.root4;
+  int leaf = kNone;
+  uint32_t nvis = 0;
+  if (node < 0) { leaf = node; node = kNone; }
+  while (node != kNone || leaf != kNone) {
+    while (node >= 0) {
+      ++nvis;
+      const float4* q = sc.bvh4 + 7 * node;
+      const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5], rf = q[6];
+      const float alx[4] = {lx.x, lx.y, lx.z, lx.w}, ahx[4] = {hx.x, hx.y, hx.z, hx.w};
+      const float aly[4] = {ly.x, ly.y, ly.z, ly.w}, ahy[4] = {hy.x, hy.y, hy.z, hy.w};
+      const float alz[4] = {lz.x, lz.y, lz.z, lz.w}, ahz[4] = {hz.x, hz.y, hz.z, hz.w};
+      const int ref[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
+      int next = kNone;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float t0;
+        float dist = slab(S, inv, alx[c], aly[c], alz[c], ahx[c], ahy[c], ahz[c], &t0);
+        bool hit = ref[c] != kNone && dist > 0.0f;
+        if (MODE == 2) hit = hit && !(t0 > lim);
+        if (hit) {
+          if (next == kNone) next = ref[c];
+          else stk[sp++ * STRIDE] = ref[c];
+        }
+      }
+      node = next != kNone ? next : (sp > 0 ? stk[--sp * STRIDE] : kNone);
+      if (node < 0 && node != kNone && leaf == kNone) {  // postpone this leaf, keep walking
+        leaf = node;
+        node = sp > 0 ? stk[--sp * STRIDE] : kNone;
+      }
+      if (!__any(leaf == kNone)) break;
+    }
+    while (leaf != kNone) {
+      int first = ref_leaf_first(leaf), cnt = ref_leaf_count(leaf);
+      nvis += (uint32_t)cnt;
+      for (int i = first; i < first + cnt; ++i) {
+        float t;
+        if (!tri_hit(sc.tri_geom, i, S, d, &t)) continue;
+        if (MODE == 1) {
+          if (t < PT_INF) { if (steps) *steps = nvis; return true; }
+        } else {
+          if (t < PT_INF) {
+            float sdist = length(sub(add(S, muls(d, t)), S));
+            if (sdist < maxd) { if (steps) *steps = nvis; return true; }
+          }
+        }
+      }
+      leaf = kNone;
+      if (node < 0 && node != kNone) {
+        leaf = node;
+        node = sp > 0 ? stk[--sp * STRIDE] : kNone;
+      }
+    }
+  }
+  if (steps) *steps = nvis;
+  return false;
 }
 
 struct Hit {

@@ -113,6 +113,23 @@ def test_prune_is_result_preserving(gpu, scene_small):
     assert np.array_equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("scene_name", ["scene_small", "scene_cornell", "scene_nan"])
+def test_bvh4_shadows_are_result_preserving(gpu, scene_name, request):
+    """Shadow rays on the 4-wide BVH give the same verdicts as the binary walk (any-hit is order-free)."""
+    gl = gpu
+    scene = request.getfixturevalue(scene_name)
+    W, H = 96, 64
+    outs = []
+    for wide in (1, 0):
+        r = _renderer(scene, W, H, mode="fast", run_taa=False, run_output=False)
+        r.pass_path_tracing.set_uniform_int("shadow_bvh4", wide)
+        for _ in range(2):
+            r.frame()
+        outs.append({k: gl.readback(r.planes()[k]) for k in ("color", "emission", "albedo")})
+    for k in outs[0]:
+        assert np.array_equal(outs[0][k], outs[1][k], equal_nan=True), k
+
+
 def test_wavefront_equals_megakernel(gpu, scene_small):
     """The staged (wavefront) path tracer and the single-kernel form give identical bits."""
     gl = gpu
