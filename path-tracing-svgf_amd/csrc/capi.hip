@@ -83,8 +83,10 @@ int wf_alloc(WFBuffers& b, size_t n) {
   if (b.base && b.n == n) return PT_OK;
   if (b.base) { (void)hipFree(b.base); b.base = nullptr; }
   const size_t f4 = n * 16, al = 256;
+  const size_t nl = (size_t)wf_list_capacity((int)n) * 8;  // 8 list segments
   auto up = [&](size_t v) { return (v + al - 1) / al * al; };
-  size_t total = up(f4) * 10 + up(n * 8) + up(n * 4) + up(n) * 2 + up(n * 4) * 2 + up(64);
+  size_t total = up(f4) * 10 + up(n * 8) + up(n * 4) + up(n) * 2 + up(nl * 4) * 2 + up(nl * 8) +
+                 up(kWfCounters * 4);
   if (hipMalloc(&b.base, total) != hipSuccess) { b.base = nullptr; return PT_ERR_HIP; }
   char* c = (char*)b.base;
   float4** f4p[10] = {&b.st.ray_o, &b.st.ray_d, &b.st.light, &b.st.red, &b.st.pend0,
@@ -94,8 +96,9 @@ int wf_alloc(WFBuffers& b, size_t n) {
   b.st.seed = (uint32_t*)c; c += up(n * 4);
   b.st.occ_h = (uint8_t*)c; c += up(n);
   b.st.occ_p = (uint8_t*)c; c += up(n);
-  b.st.list0 = (int*)c; c += up(n * 4);
-  b.st.list1 = (int*)c; c += up(n * 4);
+  b.st.list0 = (int*)c; c += up(nl * 4);
+  b.st.list1 = (int*)c; c += up(nl * 4);
+  b.st.shadow_list = (int*)c; c += up(nl * 8);
   b.st.counters = (int*)c;
   b.n = n;
   return PT_OK;

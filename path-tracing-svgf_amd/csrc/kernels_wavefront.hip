@@ -24,22 +24,81 @@ using namespace glsl;
 namespace ptk {
 
 constexpr int kTB = 128;  // threads per traversal block (LDS stack: kStack*kTB*4 = 16 KiB)
+#ifdef PT_TRACE_WAVES_PER_EU
+#define PT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(PT_TRACE_WAVES_PER_EU)))
+#else
+#define PT_TRACE_ATTR
+#endif
 
 __device__ __forceinline__ void pix_xy(const PTParams& p, int pid, int* x, int* y) {
   *x = pid % p.W;
   *y = p.y0 + pid / p.W;
 }
 
-// wave-aggregated append: one atomic per wave
-__device__ __forceinline__ void wave_push(bool push, int value, int* __restrict__ list, int* counter) {
-  unsigned long long mask = __ballot(push);
-  if (mask == 0ull) return;
-  const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((long long)mask) - 1;
+// ---------------------------------------------------------- ray lists ---
+// Compacted ray lists are split into kSeg segments, one per XCD group of
+// blocks (blockIdx % kSeg), each with its own counter: a producer block makes
+// ONE atomic per list (block-aggregated through LDS), and the 8 counters spread
+// those atomics over 8 addresses (one word saturates near 90 atomics/us,
+// MI355X_MICROARCH.md "dequeue"). Consumers map a dense index onto the
+// segments with the 8 counts (scalar loads).
+constexpr int kSeg = 8;
+
+__device__ __forceinline__ int seg_total(const int* __restrict__ counts) {
+  int t = 0;
+#pragma unroll
+  for (int s = 0; s < kSeg; ++s) t += counts[s];
+  return t;
+}
+__device__ __forceinline__ bool seg_get(const int* __restrict__ items, const int* __restrict__ counts, int cap, int k,
+                                        int* v) {
   int base = 0;
-  if (lane == leader) base = atomicAdd(counter, __popcll(mask));
-  base = __shfl(base, leader);
-  if (push) list[base + __popcll(mask & ((1ull << lane) - 1ull))] = value;
+#pragma unroll
+  for (int s = 0; s < kSeg; ++s) {
+    const int c = counts[s];
+    if (k < base + c) {
+      *v = items[s * cap + (k - base)];
+      return true;
+    }
+    base += c;
+  }
+  return false;
+}
+
+// Block-wide append of up to one item to each of three lists (live rays, HDR
+// shadow rays, point-light shadow rays). Every thread of the 256-thread block
+// must call it.
+__device__ __forceinline__ void block_push3(bool p0, int v0, int* __restrict__ items0, int* counts0, int cap0,
+                                            bool p1, int v1, int* __restrict__ items1, int* counts1, int cap1,
+                                            bool p2, int v2, int* __restrict__ items2, int* counts2, int cap2) {
+  __shared__ int wc[3][4];
+  __shared__ int base[3];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const unsigned long long m0 = __ballot(p0), m1 = __ballot(p1), m2 = __ballot(p2);
+  if (lane == 0) {
+    wc[0][wv] = __popcll(m0);
+    wc[1][wv] = __popcll(m1);
+    wc[2][wv] = __popcll(m2);
+  }
+  __syncthreads();
+  const int seg = blockIdx.x % kSeg;
+  if (threadIdx.x < 3) {
+    const int l = threadIdx.x;
+    const int t = (wc[l][0] + wc[l][1]) + (wc[l][2] + wc[l][3]);
+    int* c = l == 0 ? counts0 : (l == 1 ? counts1 : counts2);
+    base[l] = t ? atomicAdd(c + seg, t) : 0;
+  }
+  __syncthreads();
+  int o0 = base[0], o1 = base[1], o2 = base[2];
+  for (int w = 0; w < wv; ++w) {
+    o0 += wc[0][w];
+    o1 += wc[1][w];
+    o2 += wc[2][w];
+  }
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  if (p0) items0[seg * cap0 + o0 + __popcll(m0 & lt)] = v0;
+  if (p1) items1[seg * cap1 + o1 + __popcll(m1 & lt)] = v1;
+  if (p2) items2[seg * cap2 + o2 + __popcll(m2 & lt)] = v2;
 }
 
 // load-balancing probe: accumulate traversal steps per band row (only when requested)
@@ -59,7 +118,7 @@ __device__ __forceinline__ v3 primary_dir(const PTParams& p, int x, int y) {
 
 // ------------------------------------------------------------ primaries ---
 // 16x16 screen tiles, each wave an 8x8 sub-tile: coherent camera rays.
-__global__ void __launch_bounds__(256) wf_primary(PTParams p) {
+__global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
   __shared__ int stk[kStack * 256];
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   const int x = blockIdx.x * 16 + (wv & 1) * 8 + (ln & 7);
@@ -76,12 +135,12 @@ __global__ void __launch_bounds__(256) wf_primary(PTParams p) {
 }
 
 // ----------------------------------------------------------- bounce trace ---
-__global__ void __launch_bounds__(kTB) wf_trace_closest(PTParams p, const int* __restrict__ list,
-                                                        const int* __restrict__ count) {
+__global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest(PTParams p, const int* __restrict__ list,
+                                                                       const int* __restrict__ counts, int cap) {
   __shared__ int stk[kStack * kTB];
   const int k = blockIdx.x * kTB + threadIdx.x;
-  if (k >= *count) return;
-  const int pid = list[k];
+  int pid;
+  if (!seg_get(list, counts, cap, k, &pid)) return;
   float4 o = p.wf.ray_o[pid], dd = p.wf.ray_d[pid];
   float t;
   uint32_t steps;
@@ -90,50 +149,73 @@ __global__ void __launch_bounds__(kTB) wf_trace_closest(PTParams p, const int* _
   add_row_cost(p, pid / p.W, steps);
 }
 
-// HDR shadow rays in the first half of the grid, point-light shadow rays in the second.
-__global__ void __launch_bounds__(kTB) wf_trace_shadow(PTParams p, const int* __restrict__ list,
-                                                       const int* __restrict__ count) {
+// Shadow rays from the compacted lists wf_shade queued: HDR rays, then point-light rays.
+__global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p, const int* __restrict__ list,
+                                                                      const int* __restrict__ counts, int cap) {
   __shared__ int stk[kStack * kTB];
-  const int n = *count;
   const int k = blockIdx.x * kTB + threadIdx.x;
-  if (k >= 2 * n) return;
-  const bool point = k >= n;
-  const int pid = list[point ? k - n : k];
+  const int nh = seg_total(counts);  // HDR list first, then the point-light list
+  const bool point = k >= nh;
+  int pid;
+  if (!point) {
+    seg_get(list, counts, cap, k, &pid);
+  } else if (!seg_get(list + kSeg * cap, counts + kSeg, cap, k - nh, &pid)) {
+    return;
+  }
   float4 o = p.wf.ray_o[pid];
   float ts;
   uint32_t steps;
-  if (!point) {
-    float4 hd = p.wf.sh_h[pid];
-    p.wf.occ_h[pid] = p.scene.bvh4
-                          ? anyhit4<1, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(hd), 0.0f, &steps)
-                          : traverse<1, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(hd), 0.0f, 0, &ts, &steps) >= 0;
+  const float4 dir = point ? p.wf.sh_p[pid] : p.wf.sh_h[pid];  // point: (direction, distance)
+  bool occ;
+  if (p.scene.bvh4) {
+    occ = anyhit4<kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps);
+  } else if (!point) {
+    occ = traverse<1, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), 0.0f, 0, &ts, &steps) >= 0;
   } else {
-    float4 ld = p.wf.sh_p[pid];
-    if (ld.w < 0.0f) return;  // pointLightSize == 0: no ray
-    p.wf.occ_p[pid] = p.scene.bvh4
-                          ? anyhit4<2, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(ld), ld.w, &steps)
-                          : traverse<2, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(ld), ld.w, 0, &ts, &steps) >= 0;
+    occ = traverse<2, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), dir.w, 0, &ts, &steps) >= 0;
   }
+  (point ? p.wf.occ_p : p.wf.occ_h)[pid] = occ;
   add_row_cost(p, pid / p.W, steps);
+}
+
+// shade()'s MIS combination (:950-966) for given shadow verdicts: hdriLight zeroes
+// its value and pdf when occluded, calculatePointLight only its value.
+struct NeeTerms {
+  v3 hcalc, pcalc, bcalc;
+  float hpdf, ppdf, bpdf;
+};
+__device__ __forceinline__ v3 nee_hit_light(v3 red, const NeeTerms& t, bool occ_h, bool occ_p) {
+  v3 hcalc = t.hcalc, pcalc = t.pcalc;
+  float hpdf = t.hpdf;
+  if (occ_h) { hpdf = 0.0f; hcalc = splat(0.0f); }  // :934-937
+  if (occ_p) pcalc = splat(0.0f);                   // :905-909 (pdf kept)
+  float sw = ((hpdf + t.ppdf) + t.bpdf) + 1e-6f;
+  float w1 = hpdf / sw, w2 = t.ppdf / sw, w3 = t.bpdf / sw;
+  return mul(red, add(add(muls(hcalc, w1), muls(pcalc, w2)), muls(t.bcalc, w3)));
+}
+__device__ __forceinline__ bool zero_bits(v3 a) {  // all three exactly +0.0f
+  return (__float_as_uint(a.x) | __float_as_uint(a.y) | __float_as_uint(a.z)) == 0u;
 }
 
 // ------------------------------------------------------------------ shade ---
 // Bounce i: consume the closest hit of the ray in (ray_o, ray_d); on a hit,
 // sample the next direction and prepare both NEE contributions (:948-968).
+// Shadow rays whose verdict cannot change a bit of the result (a light below the
+// surface: zero BRDF) are not queued; the others go to one compacted list.
 __global__ void __launch_bounds__(256) wf_shade(PTParams p, int bounce, const int* __restrict__ list_in,
-                                                const int* __restrict__ count_in, int* __restrict__ list_out,
-                                                int* __restrict__ count_out) {
+                                                const int* __restrict__ counts_in, int* __restrict__ list_out,
+                                                int* __restrict__ counts_out, int* __restrict__ shadow_out,
+                                                int* __restrict__ shadow_counts, int cap) {
   const int k = blockIdx.x * 256 + threadIdx.x;
-  int pid;
+  int pid = 0;
   bool valid;
   if (bounce == 0) {
     valid = k < p.W * (p.y1 - p.y0);
     pid = k;
   } else {
-    valid = k < *count_in;
-    pid = valid ? list_in[k] : 0;
+    valid = seg_get(list_in, counts_in, cap, k, &pid);
   }
-  bool push = false;
+  bool push = false, need_h = false, need_p = false;
   if (valid) {
     int x, y;
     pix_xy(p, pid, &x, &y);
@@ -213,6 +295,12 @@ __global__ void __launch_bounds__(256) wf_shade(PTParams p, int bounce, const in
         }
         v3 cosb = muls(brdf, f_abs(dot(L, h.normal)));
         v3 bcalc = divs(mul(h.m.emissive, cosb), bpdf);
+        // A verdict only zeroes terms: with the point value exactly +0 (light below the
+        // surface: zero BRDF) its ray cannot change a bit; the HDR verdict also moves the
+        // MIS weights, so it is dropped only when every term is +0 and every pdf finite.
+        const bool pz = zero_bits(pcalc);
+        need_p = shp.w >= 0.0f && !pz;
+        need_h = !(pz && zero_bits(hcalc) && zero_bits(bcalc) && __builtin_isfinite(hpdf) && __builtin_isfinite(bpdf));
         p.wf.pend0[pid] = f4(hcalc.x, hcalc.y, hcalc.z, hpdf);
         p.wf.pend1[pid] = f4(pcalc.x, pcalc.y, pcalc.z, bpdf);
         p.wf.pend2[pid] = f4(bcalc.x, bcalc.y, bcalc.z, 0.0f);
@@ -229,26 +317,26 @@ __global__ void __launch_bounds__(256) wf_shade(PTParams p, int bounce, const in
     p.wf.seed[pid] = seed;
     p.wf.light[pid] = f4(light.x, light.y, light.z, 0.0f);
   }
-  wave_push(push, pid, list_out, count_out);
+  // HDR and point-light shadow rays go to separate lists so trace waves stay homogeneous
+  block_push3(push, pid, list_out, counts_out, cap, need_h, pid, shadow_out, shadow_counts, cap, need_p, pid,
+              shadow_out + kSeg * cap, shadow_counts + kSeg, cap);
 }
 
 // ----------------------------------------------------------------- finish ---
 __global__ void __launch_bounds__(256) wf_finish(PTParams p, const int* __restrict__ list,
-                                                 const int* __restrict__ count) {
+                                                 const int* __restrict__ counts, int cap) {
   const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= *count) return;
-  const int pid = list[k];
+  int pid;
+  if (!seg_get(list, counts, cap, k, &pid)) return;
   float4 q0 = p.wf.pend0[pid], q1 = p.wf.pend1[pid], q2 = p.wf.pend2[pid], q3 = p.wf.pend3[pid];
-  v3 hcalc = xyz(q0), pcalc = xyz(q1), bcalc = xyz(q2), cosb = xyz(q3);
-  float hpdf = q0.w, bpdf = q1.w;
-  float ppdf = p.pointLightSize != 0 ? (2.0f * PT_PI) / (float)p.pointLightSize : 0.0f;
-  if (p.wf.occ_h[pid]) { hpdf = 0.0f; hcalc = splat(0.0f); }  // :934-937
-  if (p.wf.occ_p[pid]) pcalc = splat(0.0f);                   // :905-909 (pdf kept)
+  NeeTerms nt;
+  nt.hcalc = xyz(q0); nt.pcalc = xyz(q1); nt.bcalc = xyz(q2);
+  nt.hpdf = q0.w; nt.bpdf = q1.w;
+  nt.ppdf = p.pointLightSize != 0 ? (2.0f * PT_PI) / (float)p.pointLightSize : 0.0f;
+  v3 cosb = xyz(q3);
   v3 red = xyz(p.wf.red[pid]), light = xyz(p.wf.light[pid]);
-  float sw = ((hpdf + ppdf) + bpdf) + 1e-6f;
-  float w1 = hpdf / sw, w2 = ppdf / sw, w3 = bpdf / sw;
-  v3 hitLight = mul(red, add(add(muls(hcalc, w1), muls(pcalc, w2)), muls(bcalc, w3)));
-  red = mul(red, divs(cosb, bpdf));
+  v3 hitLight = nee_hit_light(red, nt, p.wf.occ_h[pid] != 0, p.wf.occ_p[pid] != 0);
+  red = mul(red, divs(cosb, nt.bpdf));
   light = add(light, hitLight);
   p.wf.red[pid] = f4(red.x, red.y, red.z, 0.0f);
   p.wf.light[pid] = f4(light.x, light.y, light.z, 0.0f);
@@ -270,11 +358,14 @@ __global__ void __launch_bounds__(256) wf_finalize(PTParams p) {
   pst(p.color, x, y, f4(color.x, color.y, color.z, 1.0f));
 }
 
+int wf_list_capacity(int npix) { return ((npix + 255) / 256 + kSeg - 1) / kSeg * 256; }
+
 int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s) {
   const int rows = p.y1 - p.y0;
   if (rows <= 0) return 0;
   const int N = p.W * rows;
-  hipError_t e = hipMemsetAsync(p.wf.counters, 0, 8 * sizeof(int), s);
+  const int cap = wf_list_capacity(N);  // per segment; the host sized the lists with the same function
+  hipError_t e = hipMemsetAsync(p.wf.counters, 0, kWfCounters * sizeof(int), s);
   if (e != hipSuccess) return (int)e;
   dim3 tiles((p.W + 15) / 16, (rows + 15) / 16);
   hipLaunchKernelGGL(wf_primary, tiles, dim3(256), 0, s, p);
@@ -283,12 +374,15 @@ int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s) {
   for (int i = 0; i < p.max_depth; ++i) {
     const int* lin = lists[(i + 1) & 1];
     int* lout = lists[i & 1];
-    const int* cin = p.wf.counters + (i > 0 ? i - 1 : 0);
-    int* cout = p.wf.counters + i;
-    if (i > 0) hipLaunchKernelGGL(wf_trace_closest, dim3(gT), dim3(kTB), 0, s, p, lin, cin);
-    hipLaunchKernelGGL(wf_shade, dim3(gN), dim3(256), 0, s, p, i, lin, cin, lout, cout);
-    hipLaunchKernelGGL(wf_trace_shadow, dim3(gT2), dim3(kTB), 0, s, p, (const int*)lout, (const int*)cout);
-    hipLaunchKernelGGL(wf_finish, dim3(gN), dim3(256), 0, s, p, (const int*)lout, (const int*)cout);
+    int* live = p.wf.counters + 32 * i;        // kSeg live-list counts of bounce i
+    int* shadow = p.wf.counters + 32 * i + 8;  // kSeg HDR + kSeg point-light shadow-list counts
+    const int* live_in = p.wf.counters + 32 * (i > 0 ? i - 1 : 0);
+    if (i > 0) hipLaunchKernelGGL(wf_trace_closest, dim3(gT), dim3(kTB), 0, s, p, lin, live_in, cap);
+    hipLaunchKernelGGL(wf_shade, dim3(gN), dim3(256), 0, s, p, i, lin, live_in, lout, live, p.wf.shadow_list, shadow,
+                       cap);
+    hipLaunchKernelGGL(wf_trace_shadow, dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
+                       (const int*)shadow, cap);
+    hipLaunchKernelGGL(wf_finish, dim3(gN), dim3(256), 0, s, p, (const int*)lout, (const int*)live, cap);
   }
   hipLaunchKernelGGL(wf_finalize, dim3(gN), dim3(256), 0, s, p);
   return (int)hipGetLastError();

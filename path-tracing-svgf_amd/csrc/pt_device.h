@@ -31,9 +31,13 @@ struct int2 {
 
 namespace ptk {
 
-constexpr int kStack = 32;       // traversal stack depth (host checks BVH depth < kStack)
+#ifndef PT_KSTACK
+#define PT_KSTACK 32
+#endif
+constexpr int kStack = PT_KSTACK;  // traversal stack depth (host checks BVH depth < kStack)
 constexpr int kBlock = 256;      // threads per block for per-pixel kernels
-constexpr int kNoneRef = (int)0x80000000;  // "no node" (leaf refs are >= -(2^31 - 1))
+constexpr int kNoneRef = (int)0x80000000;
+constexpr int kWfCounters = 128;  // wavefront list counters (4 bounces x 32)  // "no node" (leaf refs are >= -(2^31 - 1))
 
 struct Plane {          // banded RGBA32F plane
   float4* p;
@@ -70,7 +74,9 @@ struct WFState {
   uint32_t* seed;               // RNG state (path_tracing.frag:433)
   uint8_t *occ_h, *occ_p;       // shadow verdicts
   int *list0, *list1;           // compacted live-ray lists (ping-pong)
-  int* counters;                // list lengths per bounce
+  int* shadow_list;             // compacted shadow rays of one bounce: HDR list, then point-light list
+  int* counters;                // per bounce i: [32i, 32i+8) live-list, [32i+8, 32i+16) HDR and
+                                // [32i+16, 32i+24) point-light segment counts (kWfCounters ints)
   uint32_t* row_cost;           // optional: traversal steps per band row (load-balancing probe), may be null
 };
 
@@ -150,6 +156,7 @@ namespace ptk {
 // Launchers (kernels_*.hip). Return hipError_t as int.
 int launch_pathtrace(const PTParams& p, hipStream_t s);
 int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s);
+int wf_list_capacity(int npix);  // per-segment capacity of the compacted ray lists (8 segments)
 int launch_gbuffer(const GBufParams& p, hipStream_t s);
 int launch_reproject(const ReprojParams& p, hipStream_t s);
 int launch_variance(const VarianceParams& p, hipStream_t s);

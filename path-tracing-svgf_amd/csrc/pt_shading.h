@@ -158,16 +158,20 @@ __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
   return best;
 }
 
-// Any-hit traversal of the 4-wide BVH (shadow rays): MODE 1 any hit, MODE 2 any
-// hit nearer than `maxd` by length(P - S) — the same triangle tests as
-// traverse<1|2>, whose verdict does not depend on the order leaves are visited.
+// Any-hit traversal of the 4-wide BVH (shadow rays): HDR rays take any hit,
+// point-light rays any hit nearer than `maxd` by length(P - S) — the same
+// triangle tests as traverse<1|2>, whose verdict does not depend on the order
+// leaves are visited.
 // Per node: the four child boxes are slab-tested (same hitAABB arithmetic); the
 // walk continues into one hit child and pushes the others; leaves are postponed
 // one per lane (while-while) so the wave intersects together.
-template <int MODE, int STRIDE>
-__device__ bool anyhit4(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, float maxd, uint32_t* steps) {
+// `point` is a runtime flag so HDR and point-light rays share one instruction
+// stream in a wave (they differ only in the pruning bound and the hit predicate).
+template <int STRIDE>
+__device__ bool anyhit4(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, bool point, float maxd,
+                        uint32_t* steps) {
   v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-  const float lim = maxd * 1.0002f + 2.0e-4f;
+  const float lim = point ? maxd * 1.0002f + 2.0e-4f : __builtin_inff();
   int sp = 0;
   int node = sc.root4;
   int leaf = kNone;
@@ -187,8 +191,7 @@ __device__ bool anyhit4(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
       for (int c = 0; c < 4; ++c) {
         float t0;
         float dist = slab(S, inv, alx[c], aly[c], alz[c], ahx[c], ahy[c], ahz[c], &t0);
-        bool hit = ref[c] != kNone && dist > 0.0f;
-        if (MODE == 2) hit = hit && !(t0 > lim);
+        const bool hit = ref[c] != kNone && dist > 0.0f && !(t0 > lim);
         if (hit) {
           if (next == kNone) next = ref[c];
           else stk[sp++ * STRIDE] = ref[c];
@@ -206,14 +209,10 @@ __device__ bool anyhit4(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
       nvis += (uint32_t)cnt;
       for (int i = first; i < first + cnt; ++i) {
         float t;
-        if (!tri_hit(sc.tri_geom, i, S, d, &t)) continue;
-        if (MODE == 1) {
-          if (t < PT_INF) { if (steps) *steps = nvis; return true; }
-        } else {
-          if (t < PT_INF) {
-            float sdist = length(sub(add(S, muls(d, t)), S));
-            if (sdist < maxd) { if (steps) *steps = nvis; return true; }
-          }
+        if (!tri_hit(sc.tri_geom, i, S, d, &t) || !(t < PT_INF)) continue;
+        if (!point || length(sub(add(S, muls(d, t)), S)) < maxd) {  // :905-909 for point lights
+          if (steps) *steps = nvis;
+          return true;
         }
       }
       leaf = kNone;

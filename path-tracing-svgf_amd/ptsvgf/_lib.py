@@ -44,7 +44,8 @@ class PtError(RuntimeError):
 
 
 def _load(name: str) -> C.CDLL:
-    path = os.path.join(LIB_DIR, name)
+    # PTSVGF_LIB_DIR: an alternative in-tree build (A/B experiments, tools/exp_*.sh)
+    path = os.path.join(os.environ.get("PTSVGF_LIB_DIR", LIB_DIR), name)
     if not os.path.exists(path):
         raise ImportError(
             f"{path} is missing: build it with `make -C {PKG_ROOT}` "
