@@ -310,8 +310,8 @@ int pack_bvh4(const float* node_enc, int nnodes, int ntris, std::vector<float4>&
   };
   build(1, 1);
   if (!bad.empty()) return err(PT_ERR_FORMAT, bad);
-  // traversal continues into one hit child and pushes the other (up to 3) per level
-  if (3 * depth4 + 1 > kStack) return err(PT_ERR_FORMAT, "4-wide BVH deeper than the traversal stack");
+  // no depth bound: a ray whose 4-wide walk would overflow the stack falls back to the binary walk
+  (void)depth4;
   *root_ref = 0;
   return PT_OK;
 }
@@ -507,7 +507,7 @@ int draw_pathtrace(Pass* p) {
   k.scene.tri_shade = sg->shade;
   k.scene.bvh = sg->bvh;
   k.scene.root_ref = sg->root_ref;
-  k.scene.bvh4 = (sg->has4 && ui(p, "shadow_bvh4", 1)) ? sg->bvh4 : nullptr;  // 0: binary walk (A/B)
+  k.scene.bvh4 = (sg->has4 && ui(p, "shadow_bvh4", 0)) ? sg->bvh4 : nullptr;  // 1: 4-wide any-hit (A/B; slower here)
   k.scene.root4 = sg->root4;
   k.scene.ntris = sg->ntris;
   if (lt && lt->target == PT_TEXTURE_BUFFER) {

@@ -166,13 +166,10 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p,
   float ts;
   uint32_t steps;
   const float4 dir = point ? p.wf.sh_p[pid] : p.wf.sh_h[pid];  // point: (direction, distance)
-  bool occ;
-  if (p.scene.bvh4) {
-    occ = anyhit4<kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps);
-  } else if (!point) {
-    occ = traverse<1, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), 0.0f, 0, &ts, &steps) >= 0;
-  } else {
-    occ = traverse<2, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), dir.w, 0, &ts, &steps) >= 0;
+  int occ = p.scene.bvh4 ? anyhit4<kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps) : -1;
+  if (occ < 0) {  // no 4-wide tree, or its stack overflowed: binary walk
+    occ = (point ? traverse<2, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), dir.w, 0, &ts, &steps)
+                 : traverse<1, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), 0.0f, 0, &ts, &steps)) >= 0;
   }
   (point ? p.wf.occ_p : p.wf.occ_h)[pid] = occ;
   add_row_cost(p, pid / p.W, steps);

@@ -167,9 +167,11 @@ __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
 // one per lane (while-while) so the wave intersects together.
 // `point` is a runtime flag so HDR and point-light rays share one instruction
 // stream in a wave (they differ only in the pruning bound and the hit predicate).
+// Returns 1 occluded, 0 visible, -1 when the stack would overflow (the caller
+// re-traces that ray on the binary tree, whose depth the host bounds by kStack).
 template <int STRIDE>
-__device__ bool anyhit4(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, bool point, float maxd,
-                        uint32_t* steps) {
+__device__ int anyhit4(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, bool point, float maxd,
+                       uint32_t* steps) {
   v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   const float lim = point ? maxd * 1.0002f + 2.0e-4f : __builtin_inff();
   int sp = 0;
@@ -193,8 +195,12 @@ __device__ bool anyhit4(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, b
         float dist = slab(S, inv, alx[c], aly[c], alz[c], ahx[c], ahy[c], ahz[c], &t0);
         const bool hit = ref[c] != kNone && dist > 0.0f && !(t0 > lim);
         if (hit) {
-          if (next == kNone) next = ref[c];
-          else stk[sp++ * STRIDE] = ref[c];
+          if (next == kNone) {
+            next = ref[c];
+          } else {
+            if (sp == kStack) return -1;
+            stk[sp++ * STRIDE] = ref[c];
+          }
         }
       }
       node = next != kNone ? next : (sp > 0 ? stk[--sp * STRIDE] : kNone);
@@ -212,7 +218,7 @@ __device__ bool anyhit4(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, b
         if (!tri_hit(sc.tri_geom, i, S, d, &t) || !(t < PT_INF)) continue;
         if (!point || length(sub(add(S, muls(d, t)), S)) < maxd) {  // :905-909 for point lights
           if (steps) *steps = nvis;
-          return true;
+          return 1;
         }
       }
       leaf = kNone;
@@ -223,7 +229,7 @@ __device__ bool anyhit4(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, b
     }
   }
   if (steps) *steps = nvis;
-  return false;
+  return 0;
 }
 
 struct Hit {
