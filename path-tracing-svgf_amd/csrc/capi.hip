@@ -70,6 +70,7 @@ struct RasterScene {
   float4* geom = nullptr;
   float4* bvh = nullptr;
   int root_ref = 0;
+  int stack_need = 0;
   int ntris = 0;
 };
 
@@ -127,6 +128,7 @@ struct SceneGPU {
   float4* bvh4 = nullptr;
   bool has4 = false;
   int root4 = 0;
+  int stack_need = 0;
   int root_ref = 0;
   int ntris = 0;
   uint64_t tri_ver = 0, node_ver = 0;
@@ -189,7 +191,8 @@ struct NodeRaw {
   float AA[3], BB[3];
 };
 
-int pack_bvh(const float* node_enc, int nnodes, std::vector<float4>& out, int* root_ref, int ntris) {
+// *need: deepest interior level (root = 1) = the most stack entries a walk holds
+int pack_bvh(const float* node_enc, int nnodes, std::vector<float4>& out, int* root_ref, int ntris, int* need) {
   if (nnodes < 2) return err(PT_ERR_FORMAT, "BVH needs the dummy node 0 and a root node 1");
   std::vector<NodeRaw> nd(nnodes);
   for (int i = 0; i < nnodes; ++i) {
@@ -212,6 +215,7 @@ int pack_bvh(const float* node_enc, int nnodes, std::vector<float4>& out, int* r
     *ref = -(n.index * 16 + n.n) - 1;
     return PT_OK;
   };
+  *need = 0;
   if (nd[1].n > 0) {
     int r;
     if (leaf_ref(1, &r) != PT_OK) return PT_ERR_FORMAT;
@@ -224,6 +228,7 @@ int pack_bvh(const float* node_enc, int nnodes, std::vector<float4>& out, int* r
     Item it = st.back();
     st.pop_back();
     if (it.depth >= kStack) return err(PT_ERR_FORMAT, "BVH deeper than the traversal stack");
+    *need = std::max(*need, it.depth);
     idx[it.id] = (int)order.size();
     order.push_back(it.id);
     const NodeRaw& n = nd[it.id];
@@ -357,7 +362,7 @@ int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU*
   }
   std::vector<float4> bvh, bvh4;
   int root = 0, root4 = 0;
-  int rc = pack_bvh((const float*)nodes->host.data(), (int)nnodes, bvh, &root, (int)ntris);
+  int rc = pack_bvh((const float*)nodes->host.data(), (int)nnodes, bvh, &root, (int)ntris, &sg.stack_need);
   if (rc != PT_OK) return rc;
   // the 4-wide any-hit tree is optional: a scene too deep for it keeps the binary walk
   sg.has4 = pack_bvh4((const float*)nodes->host.data(), (int)nnodes, (int)ntris, bvh4, &root4) == PT_OK;
@@ -507,6 +512,7 @@ int draw_pathtrace(Pass* p) {
   k.scene.tri_shade = sg->shade;
   k.scene.bvh = sg->bvh;
   k.scene.root_ref = sg->root_ref;
+  k.stack_need = sg->stack_need;
   k.scene.bvh4 = (sg->has4 && ui(p, "shadow_bvh4", 0)) ? sg->bvh4 : nullptr;  // 1: 4-wide any-hit (A/B; slower here)
   k.scene.root4 = sg->root4;
   k.scene.ntris = sg->ntris;
@@ -572,6 +578,7 @@ int draw_raster(Pass* p) {
   k.geom = p->raster.geom;
   k.bvh = p->raster.bvh;
   k.root_ref = p->raster.root_ref;
+  k.stack_need = p->raster.stack_need;
   float V[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1}, P[16], PV[16];
   memcpy(P, V, 64);
   memcpy(PV, V, 64);
@@ -1062,7 +1069,7 @@ int pt_raster_pass_bind(uint32_t pass, const float* verts, size_t n_floats) {
   }
   std::vector<float4> bvh;
   int root = 0;
-  TRY(pack_bvh(ne.data(), (int)cnt[1], bvh, &root, ntris));
+  TRY(pack_bvh(ne.data(), (int)cnt[1], bvh, &root, ntris, &p->raster.stack_need));
   if (bvh.empty()) bvh.push_back(float4{0, 0, 0, 0});
   TRY(upload_vec(geom, &p->raster.geom));
   TRY(upload_vec(bvh, &p->raster.bvh));

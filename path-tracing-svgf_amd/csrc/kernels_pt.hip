@@ -200,8 +200,9 @@ __device__ __forceinline__ float lin_z(const GBufParams& p, v3 P) {
   return zw / fw;
 }
 
+template <int KS>
 __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
-  __shared__ int stk[kStack * kBlock];
+  __shared__ int stk[KS * kBlock];
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   const int x = blockIdx.x * 16 + (wv & 1) * 8 + (ln & 7);
   const int y = p.y0 + blockIdx.y * 16 + (wv >> 1) * 8 + (ln >> 3);
@@ -306,7 +307,8 @@ int launch_pathtrace(const PTParams& p, hipStream_t s) {
 int launch_gbuffer(const GBufParams& p, hipStream_t s) {
   if (p.y1 <= p.y0) return 0;
   dim3 grid((p.W + 15) / 16, (p.y1 - p.y0 + 15) / 16);
-  hipLaunchKernelGGL(gbuffer_kernel, grid, dim3(kBlock), 0, s, p);
+  if (p.stack_need <= kStackSmall) hipLaunchKernelGGL(gbuffer_kernel<kStackSmall>, grid, dim3(kBlock), 0, s, p);
+  else hipLaunchKernelGGL(gbuffer_kernel<kStack>, grid, dim3(kBlock), 0, s, p);
   return (int)hipGetLastError();
 }
 

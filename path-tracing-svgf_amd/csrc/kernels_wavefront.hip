@@ -118,8 +118,9 @@ __device__ __forceinline__ v3 primary_dir(const PTParams& p, int x, int y) {
 
 // ------------------------------------------------------------ primaries ---
 // 16x16 screen tiles, each wave an 8x8 sub-tile: coherent camera rays.
+template <int KS>
 __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
-  __shared__ int stk[kStack * 256];
+  __shared__ int stk[KS * 256];
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   const int x = blockIdx.x * 16 + (wv & 1) * 8 + (ln & 7);
   const int y = p.y0 + blockIdx.y * 16 + (wv >> 1) * 8 + (ln >> 3);
@@ -135,9 +136,10 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
 }
 
 // ----------------------------------------------------------- bounce trace ---
+template <int KS>
 __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest(PTParams p, const int* __restrict__ list,
                                                                        const int* __restrict__ counts, int cap) {
-  __shared__ int stk[kStack * kTB];
+  __shared__ int stk[KS * kTB];
   const int k = blockIdx.x * kTB + threadIdx.x;
   int pid;
   if (!seg_get(list, counts, cap, k, &pid)) return;
@@ -150,9 +152,10 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest(PTParams p
 }
 
 // Shadow rays from the compacted lists wf_shade queued: HDR rays, then point-light rays.
+template <int KS>
 __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p, const int* __restrict__ list,
                                                                       const int* __restrict__ counts, int cap) {
-  __shared__ int stk[kStack * kTB];
+  __shared__ int stk[KS * kTB];
   const int k = blockIdx.x * kTB + threadIdx.x;
   const int nh = seg_total(counts);  // HDR list first, then the point-light list
   const bool point = k >= nh;
@@ -166,7 +169,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p,
   float ts;
   uint32_t steps;
   const float4 dir = point ? p.wf.sh_p[pid] : p.wf.sh_h[pid];  // point: (direction, distance)
-  int occ = p.scene.bvh4 ? anyhit4<kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps) : -1;
+  int occ = p.scene.bvh4 ? anyhit4<kTB, KS>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps) : -1;
   if (occ < 0) {  // no 4-wide tree, or its stack overflowed: binary walk
     occ = (point ? traverse<2, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), dir.w, 0, &ts, &steps)
                  : traverse<1, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), 0.0f, 0, &ts, &steps)) >= 0;
@@ -357,7 +360,8 @@ __global__ void __launch_bounds__(256) wf_finalize(PTParams p) {
 
 int wf_list_capacity(int npix) { return ((npix + 255) / 256 + kSeg - 1) / kSeg * 256; }
 
-int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s) {
+template <int KS>
+int launch_wavefront(const PTParams& p, hipStream_t s) {
   const int rows = p.y1 - p.y0;
   if (rows <= 0) return 0;
   const int N = p.W * rows;
@@ -365,7 +369,7 @@ int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s) {
   hipError_t e = hipMemsetAsync(p.wf.counters, 0, kWfCounters * sizeof(int), s);
   if (e != hipSuccess) return (int)e;
   dim3 tiles((p.W + 15) / 16, (rows + 15) / 16);
-  hipLaunchKernelGGL(wf_primary, tiles, dim3(256), 0, s, p);
+  hipLaunchKernelGGL(wf_primary<KS>, tiles, dim3(256), 0, s, p);
   const int gN = (N + 255) / 256, gT = (N + kTB - 1) / kTB, gT2 = (2 * N + kTB - 1) / kTB;
   int* lists[2] = {p.wf.list0, p.wf.list1};
   for (int i = 0; i < p.max_depth; ++i) {
@@ -374,15 +378,20 @@ int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s) {
     int* live = p.wf.counters + 32 * i;        // kSeg live-list counts of bounce i
     int* shadow = p.wf.counters + 32 * i + 8;  // kSeg HDR + kSeg point-light shadow-list counts
     const int* live_in = p.wf.counters + 32 * (i > 0 ? i - 1 : 0);
-    if (i > 0) hipLaunchKernelGGL(wf_trace_closest, dim3(gT), dim3(kTB), 0, s, p, lin, live_in, cap);
+    if (i > 0) hipLaunchKernelGGL(wf_trace_closest<KS>, dim3(gT), dim3(kTB), 0, s, p, lin, live_in, cap);
     hipLaunchKernelGGL(wf_shade, dim3(gN), dim3(256), 0, s, p, i, lin, live_in, lout, live, p.wf.shadow_list, shadow,
                        cap);
-    hipLaunchKernelGGL(wf_trace_shadow, dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
+    hipLaunchKernelGGL(wf_trace_shadow<KS>, dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
                        (const int*)shadow, cap);
     hipLaunchKernelGGL(wf_finish, dim3(gN), dim3(256), 0, s, p, (const int*)lout, (const int*)live, cap);
   }
   hipLaunchKernelGGL(wf_finalize, dim3(gN), dim3(256), 0, s, p);
   return (int)hipGetLastError();
+}
+
+int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s) {
+  // the LDS stack bounds resident waves: a tree that fits the small stack gets more of them
+  return p.stack_need <= kStackSmall ? launch_wavefront<kStackSmall>(p, s) : launch_wavefront<kStack>(p, s);
 }
 
 }  // namespace ptk

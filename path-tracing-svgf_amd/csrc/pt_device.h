@@ -35,6 +35,7 @@ namespace ptk {
 #define PT_KSTACK 32
 #endif
 constexpr int kStack = PT_KSTACK;  // traversal stack depth (host checks BVH depth < kStack)
+constexpr int kStackSmall = 24;    // smaller LDS stack (more resident waves) for trees that fit it
 constexpr int kBlock = 256;      // threads per block for per-pixel kernels
 constexpr int kNoneRef = (int)0x80000000;
 constexpr int kWfCounters = 128;  // wavefront list counters (4 bounces x 32)  // "no node" (leaf refs are >= -(2^31 - 1))
@@ -95,6 +96,7 @@ struct PTParams {
   int max_depth;
   int aspect_corrected;
   int prune;            // closest-hit pruning (parity-safe margin)
+  int stack_need;       // deepest interior level of the binary BVH (selects the LDS stack size)
   float sobol_u[4], sobol_v[4];  // sobolVec2(frameCounter+1, b): uniform across pixels
   WFState wf;
 };
@@ -106,6 +108,7 @@ struct GBufParams {
   const float4* geom;   // 7 x float4 per raster triangle: (p1,idx)(e1,-)(e2,-)(Ng,-)(n1)(n2)(n3)
   const float4* bvh;
   int root_ref;
+  int stack_need;       // deepest interior level of the raster BVH
   float eye[3];
   float invR[9];        // row-major R^T (camera-to-world rotation)
   float P00, P11;       // projection diagonal (pixel ray scale)

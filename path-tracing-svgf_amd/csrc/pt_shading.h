@@ -169,7 +169,7 @@ __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
 // stream in a wave (they differ only in the pruning bound and the hit predicate).
 // Returns 1 occluded, 0 visible, -1 when the stack would overflow (the caller
 // re-traces that ray on the binary tree, whose depth the host bounds by kStack).
-template <int STRIDE>
+template <int STRIDE, int KS = kStack>
 __device__ int anyhit4(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, bool point, float maxd,
                        uint32_t* steps) {
   v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -198,7 +198,7 @@ __device__ int anyhit4(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, bo
           if (next == kNone) {
             next = ref[c];
           } else {
-            if (sp == kStack) return -1;
+            if (sp == KS) return -1;
             stk[sp++ * STRIDE] = ref[c];
           }
         }
