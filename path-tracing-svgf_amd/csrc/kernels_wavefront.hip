@@ -152,7 +152,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest(PTParams p
 }
 
 // Shadow rays from the compacted lists wf_shade queued: HDR rays, then point-light rays.
-template <int KS>
+template <int KS, bool WIDE>
 __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p, const int* __restrict__ list,
                                                                       const int* __restrict__ counts, int cap) {
   __shared__ int stk[KS * kTB];
@@ -166,14 +166,11 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p,
     return;
   }
   float4 o = p.wf.ray_o[pid];
-  float ts;
-  uint32_t steps;
+  uint32_t steps = 0;
   const float4 dir = point ? p.wf.sh_p[pid] : p.wf.sh_h[pid];  // point: (direction, distance)
-  int occ = p.scene.bvh4 ? anyhit4<kTB, KS>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps) : -1;
-  if (occ < 0) {  // no 4-wide tree, or its stack overflowed: binary walk
-    occ = (point ? traverse<2, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), dir.w, 0, &ts, &steps)
-                 : traverse<1, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), 0.0f, 0, &ts, &steps)) >= 0;
-  }
+  int occ = WIDE ? anyhit4<kTB, KS>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps) : -1;
+  if (occ < 0)  // binary walk (default), or the 4-wide stack overflowed
+    occ = anyhit2<kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps);
   (point ? p.wf.occ_p : p.wf.occ_h)[pid] = occ;
   add_row_cost(p, pid / p.W, steps);
 }
@@ -381,8 +378,12 @@ int launch_wavefront(const PTParams& p, hipStream_t s) {
     if (i > 0) hipLaunchKernelGGL(wf_trace_closest<KS>, dim3(gT), dim3(kTB), 0, s, p, lin, live_in, cap);
     hipLaunchKernelGGL(wf_shade, dim3(gN), dim3(256), 0, s, p, i, lin, live_in, lout, live, p.wf.shadow_list, shadow,
                        cap);
-    hipLaunchKernelGGL(wf_trace_shadow<KS>, dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
-                       (const int*)shadow, cap);
+    if (p.scene.bvh4)
+      hipLaunchKernelGGL((wf_trace_shadow<KS, true>), dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
+                         (const int*)shadow, cap);
+    else
+      hipLaunchKernelGGL((wf_trace_shadow<KS, false>), dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
+                         (const int*)shadow, cap);
     hipLaunchKernelGGL(wf_finish, dim3(gN), dim3(256), 0, s, p, (const int*)lout, (const int*)live, cap);
   }
   hipLaunchKernelGGL(wf_finalize, dim3(gN), dim3(256), 0, s, p);

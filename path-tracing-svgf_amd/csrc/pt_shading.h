@@ -167,6 +167,69 @@ __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
 // one per lane (while-while) so the wave intersects together.
 // `point` is a runtime flag so HDR and point-light rays share one instruction
 // stream in a wave (they differ only in the pruning bound and the hit predicate).
+// Any-hit walk of the binary tree for both shadow kinds: traverse<1> (HDR, any
+// hit) and traverse<2> (point light: boxes entered beyond the light pruned, hit
+// nearer than `maxd`) merged behind a runtime flag, so a wave runs one loop.
+template <int STRIDE>
+__device__ bool anyhit2(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, bool point, float maxd,
+                        uint32_t* steps) {
+  v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const float lim = point ? maxd * 1.0002f + 2.0e-4f : __builtin_inff();
+  int sp = 0;
+  int node = sc.root_ref;
+  int leaf = kNone;
+  uint32_t nvis = 0;
+  if (node < 0) { leaf = node; node = kNone; }
+  while (node != kNone || leaf != kNone) {
+    while (node >= 0) {
+      ++nvis;
+      const float4* nd = sc.bvh + 4 * node;
+      float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+      float t0l, t0r;
+      float dl = slab(S, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, &t0l);
+      float dr = slab(S, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, &t0r);
+      const bool hl = dl > 0.0f && !(t0l > lim), hr = dr > 0.0f && !(t0r > lim);
+      int cl = __float_as_int(q3.x), cr = __float_as_int(q3.y);
+      if (hl && hr) {
+        bool lnear = dl < dr;
+        stk[sp * STRIDE] = lnear ? cr : cl;
+        ++sp;
+        node = lnear ? cl : cr;
+      } else if (hl) {
+        node = cl;
+      } else if (hr) {
+        node = cr;
+      } else {
+        node = sp > 0 ? stk[--sp * STRIDE] : kNone;
+      }
+      if (node < 0 && node != kNone && leaf == kNone) {
+        leaf = node;
+        node = sp > 0 ? stk[--sp * STRIDE] : kNone;
+      }
+      if (!__any(leaf == kNone)) break;
+    }
+    while (leaf != kNone) {
+      int first = ref_leaf_first(leaf), cnt = ref_leaf_count(leaf);
+      nvis += (uint32_t)cnt;
+      for (int i = first; i < first + cnt; ++i) {
+        float t;
+        if (!tri_hit(sc.tri_geom, i, S, d, &t) || !(t < PT_INF)) continue;
+        if (!point || length(sub(add(S, muls(d, t)), S)) < maxd) {
+          if (steps) *steps = nvis;
+          return true;
+        }
+      }
+      leaf = kNone;
+      if (node < 0 && node != kNone) {
+        leaf = node;
+        node = sp > 0 ? stk[--sp * STRIDE] : kNone;
+      }
+    }
+  }
+  if (steps) *steps = nvis;
+  return false;
+}
+
 // Returns 1 occluded, 0 visible, -1 when the stack would overflow (the caller
 // re-traces that ray on the binary tree, whose depth the host bounds by kStack).
 template <int STRIDE, int KS = kStack>
