@@ -213,9 +213,12 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
   float best = 3.0e38f;
   int besti = -1, bests = -1;
   float bu = 0.f, bv = 0.f;
-  int sp = 0, node = p.root_ref;
-  while (true) {
-    if (node >= 0) {
+  // while-while walk with one postponed leaf per lane (as traverse<>): the result
+  // (closest t, ties to the lower original index) does not depend on visit order
+  int sp = 0, node = p.root_ref, leaf = kNone;
+  if (node < 0) { leaf = node; node = kNone; }
+  while (node != kNone || leaf != kNone) {
+    while (node >= 0) {
       const float4* nd = p.bvh + 4 * node;
       float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
       // conservative (widened) slab test: the box only culls, Moller-Trumbore decides
@@ -229,15 +232,21 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
         stk[sp * kBlock + threadIdx.x] = farc;
         ++sp;
         node = nearc;
-      } else if (hl) node = cl;
-      else if (hr) node = cr;
-      else {
-        if (sp == 0) break;
-        --sp;
-        node = stk[sp * kBlock + threadIdx.x];
+      } else if (hl) {
+        node = cl;
+      } else if (hr) {
+        node = cr;
+      } else {
+        node = sp > 0 ? stk[--sp * kBlock + threadIdx.x] : kNone;
       }
-    } else {
-      int first = ref_leaf_first(node), cnt = ref_leaf_count(node);
+      if (node < 0 && node != kNone && leaf == kNone) {
+        leaf = node;
+        node = sp > 0 ? stk[--sp * kBlock + threadIdx.x] : kNone;
+      }
+      if (!__any(leaf == kNone)) break;
+    }
+    while (leaf != kNone) {
+      int first = ref_leaf_first(leaf), cnt = ref_leaf_count(leaf);
       for (int i = first; i < first + cnt; ++i) {
         const float4* g = p.geom + 7 * i;
         float4 a = g[0], e1 = g[1], e2 = g[2], ng = g[3];
@@ -254,9 +263,11 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
           bv = h.v;
         }
       }
-      if (sp == 0) break;
-      --sp;
-      node = stk[sp * kBlock + threadIdx.x];
+      leaf = kNone;
+      if (node < 0 && node != kNone) {
+        leaf = node;
+        node = sp > 0 ? stk[--sp * kBlock + threadIdx.x] : kNone;
+      }
     }
   }
   if (bests < 0) {
