@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default="960x540", help="oracle sample frame size for cpu_baseline")
     ap.add_argument("--no-1080p", action="store_true", help="skip the secondary 1080p measurement")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for --gpus > 1 (nccl = RCCL)")
     ap.add_argument("--equal-bands", action="store_true", help="multi-GPU: equal band heights (no cost balancing)")
     ap.add_argument("--breakdown", action="store_true", help="print per-pass ms to stderr")
     ap.add_argument("--pt-kernel", type=int, default=0, help="0 wavefront (production), 1 megakernel (A/B)")
@@ -104,8 +105,13 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        # one GPU per rank; --backend gloo (host-staged halos) rehearses the multi-rank path on fewer GPUs
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     else:
         torch.cuda.set_device(0)
 
