@@ -28,7 +28,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 ATROUS_BYTES_PER_PX = 52  # illum 16 + normal/z 16 + depth-fwidth 4 + write 16
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8 TB/s spec
 METRIC = "frames/sec @1spp+SVGF, 1080p & 4K; \u00e0-trous HBM GB/s vs peak"  # BASELINE.json "metric"
-ATROUS_KERNEL = "atrous_step_kernel"
+ATROUS_KERNEL = "atrous_tile_kernel"
 # HBM bytes per a-trous launch measured with rocprofv3 PMC passes (tools/gpu_profile.sh), committed under profiles/
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "atrous_traffic.json")
 

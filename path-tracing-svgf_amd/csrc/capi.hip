@@ -652,8 +652,9 @@ int draw_svgf(Pass* p, int kind) {
     k.phi_color = uf(p, "gPhiColor", 0.0f);
     k.phi_normal = uf(p, "gPhiNormal", 0.0f);
     if (ui(p, "exact", 0)) rc = launch_atrous_exact(k, g.stream);          // bit-exact form (tests)
-    else if (ui(p, "atrous_variant", 0) == 1) rc = launch_atrous_simple(k, g.stream);  // A/B
-    else rc = launch_atrous_fast(k, g.stream);                             // step-specialised
+    else if (ui(p, "atrous_variant", 0) == 1) rc = launch_atrous_simple(k, g.stream);  // A/B: generic
+    else if (ui(p, "atrous_variant", 0) == 2) rc = launch_atrous_step(k, g.stream);    // A/B: step kernel
+    else rc = launch_atrous_fast(k, g.stream);                             // LDS-tiled (production)
   } else if (kind == PK_MODULATE) {
     ModulateParams k;
     memset(&k, 0, sizeof(k));

@@ -15,6 +15,8 @@
 // result would depend on which band or block it falls in.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "glsl_builtins.h"
 #include "pt_device.h"
 
@@ -44,7 +46,7 @@ __global__ void __launch_bounds__(256) atrous_fast_kernel(AtrousParams p) {
   const float LOG2E = 1.4426950408889634f;
   float lc = (0.2125f * ic.x + 0.7154f * ic.y) + 0.0721f * ic.z;
   float phiL = p.phi_color * __builtin_sqrtf(fmaxf(0.0f, 1e-10f + ic.w));  // variance: centre only (:36)
-  float fwz = p.fwidth.aux ? p.fwidth.aux[(size_t)arow(p.fwidth, y) * p.fwidth.W + x]
+  float fwz = p.fwidth.aux ? fabsf(p.fwidth.aux[(size_t)arow(p.fwidth, y) * p.fwidth.W + x])
                            : p.fwidth.p[(size_t)arow(p.fwidth, y) * p.fwidth.W + x].y;
   float phiD = fmaxf(fwz, 1e-8f) * (float)p.step;
   float kL = LOG2E / phiL;   // exp(-a) = exp2(-a*log2e)
@@ -167,7 +169,7 @@ __device__ __forceinline__ void atrous_pixel(const AtrousParams& p, int x, int y
   const float LOG2E = 1.4426950408889634f;
   c.lc = (0.2125f * c.ic.x + 0.7154f * c.ic.y) + 0.0721f * c.ic.z;
   const float phiL = p.phi_color * __builtin_sqrtf(fmaxf(0.0f, 1e-10f + c.ic.w));
-  const float fwz = p.fwidth.aux ? p.fwidth.aux[(size_t)ly * W + x] : p.fwidth.p[(size_t)ly * W + x].y;
+  const float fwz = p.fwidth.aux ? fabsf(p.fwidth.aux[(size_t)ly * W + x]) : p.fwidth.p[(size_t)ly * W + x].y;
   const float kL = LOG2E / phiL;
   // |lc - lp| * kL = |lp*kL - lc*kL|: luminance weights pre-scaled, centre folded into the first FMA
   c.wLr = 0.2125f * kL;
@@ -216,13 +218,163 @@ __global__ void __launch_bounds__(256) atrous_step_kernel(AtrousParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// LDS-tiled form (production). The step kernel above is bound by the texture
+// address path, not by HBM: 48 wave-wide 16-B loads per pixel keep the TA busy
+// ~85% of the launch (rocprofv3 TA_TA_BUSY, profiles/). Here a block of 8 waves
+// computes 64 columns x TJ = 8 rows taken from ONE residue class of rows mod S
+// (rows ybase + S*j), so the whole dilated 5x5 footprint of the block is a dense
+// (TJ+4) x (64+4S) texel tile of each plane: staged once into LDS with
+// coalesced loads, then all 24 taps of every pixel read LDS (ds_read_b128 at
+// immediate offsets). Blocks whose pixels are all background (zCenter == 1,
+// svgf_Atrous.frag:77) copy and exit without staging. Same arithmetic, same tap
+// order as atrous_taps: bit-identical to the step kernel.
+//
+// AUX: the G-buffer's compact depth-fwidth plane carries the zCenter == 1 flag in
+// its sign bit (its magnitude is .y, always >= 0 or a NaN with the sign clear), so
+// background pixels read 4 + 16 B and write 16 B.
+constexpr int kTileRows = 8;   // TJ
+constexpr int kTileWaves = 8;  // one pixel per thread
+
+__device__ __forceinline__ bool aux_flag(float a) { return (__float_as_uint(a) >> 31) != 0; }
+
+template <int S, bool AUX>
+__global__ void __launch_bounds__(64 * kTileWaves) atrous_tile_kernel(AtrousParams p) {
+  constexpr int TJ = kTileRows, NW = kTileWaves, R = TJ + 4, C = 64 + 4 * S, NT = 64 * NW;
+  __shared__ float4 LI[R * C];
+  __shared__ float4 LN[R * C];
+  const int W = p.illum.W, row0 = p.illum.row0;
+  const float4* __restrict__ I = p.illum.p;
+  const float4* __restrict__ ND = p.nd.p;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = blockIdx.y / S, b = blockIdx.y - g * S;
+  const int ybase = p.y0 + g * S * TJ + b;  // frame row of tile row j = 0
+  const int x0 = blockIdx.x * 64, x = x0 + lane, y = ybase + S * wv;
+  const bool own = x < p.W && y < p.y1;
+  const size_t ci = (size_t)(y - row0) * W + x;
+  bool bg = true;
+  float fwz = 0.0f;
+  if (own) {
+    if (AUX) {
+      const float a = p.fwidth.aux[ci];
+      bg = aux_flag(a);
+      fwz = fabsf(a);
+    } else {
+      bg = ND[ci].w == 1.0f;
+      fwz = p.fwidth.p[ci].y;
+    }
+  }
+  if (!__syncthreads_or(!bg)) {
+    if (own) p.out.p[ci] = I[ci];
+    return;
+  }
+  // stage: tile row r <-> frame row ybase + S*(r-2), column c <-> x0 - 2S + c; rows outside the frame and
+  // columns outside [0, W) are clamped (their taps are skipped below), rows outside the stored band clamp too
+  const int lo = max(0, row0), hi = min(p.H, row0 + p.illum.rows) - 1;
+  for (int e = tid; e < R * C; e += NT) {
+    const int r = e / C, c = e - r * C;
+    int gy = ybase + S * (r - 2), gx = x0 - 2 * S + c;
+    gy = gy < lo ? lo : (gy > hi ? hi : gy);
+    gx = gx < 0 ? 0 : (gx >= p.W ? p.W - 1 : gx);
+    const size_t gi = (size_t)(gy - row0) * W + gx;
+    LI[e] = I[gi];
+    LN[e] = ND[gi];
+  }
+  __syncthreads();
+  if (!own) return;
+  const float4* Li = LI + wv * C + lane;  // top-left tap of this pixel's window
+  const float4* Ln = LN + wv * C + lane;
+  const float4 ic = Li[2 * C + 2 * S];
+  float4* out = p.out.p + ci;
+  if (bg) {
+    *out = ic;
+    return;
+  }
+  const float4 nd = Ln[2 * C + 2 * S];
+  const bool edge = x0 - 2 * S < 0 || x0 + 63 + 2 * S >= p.W || ybase - 2 * S < 0 || ybase + S * (TJ + 1) >= p.H;
+  const float LOG2E = 1.4426950408889634f;
+  const float lc = (0.2125f * ic.x + 0.7154f * ic.y) + 0.0721f * ic.z;
+  const float phiL = p.phi_color * __builtin_sqrtf(fmaxf(0.0f, 1e-10f + ic.w));
+  const float kL = LOG2E / phiL;
+  const float kD = LOG2E / (fmaxf(fwz, 1e-8f) * (float)S);
+  const float kDr[5] = {kD, kD * 0.70710678f, kD * 0.5f, kD * 0.44721360f, kD * 0.35355339f};
+  float sumW = 1.0f;
+  f2v s01 = {ic.x, ic.y}, s23 = {ic.z, ic.w};
+  auto taps = [&](auto flat_tag) __attribute__((always_inline)) {
+    constexpr bool FLAT = decltype(flat_tag)::value;
+    const float wLr = 0.2125f * kL, wLg = 0.7154f * kL, wLb = 0.0721f * kL, cL = -(lc * kL);
+#pragma unroll
+    for (int yy = -2; yy <= 2; ++yy) {
+      if (edge && (y + yy * S < 0 || y + yy * S >= p.H)) continue;
+#pragma unroll
+      for (int xx = -2; xx <= 2; ++xx) {
+        if (xx == 0 && yy == 0) continue;
+        if (edge && (x + xx * S < 0 || x + xx * S >= p.W)) continue;
+        const int r2 = xx * xx + yy * yy;
+        const float kDl = r2 == 1 ? kDr[0] : r2 == 2 ? kDr[1] : r2 == 4 ? kDr[2] : r2 == 5 ? kDr[3] : kDr[4];
+        const int ax = xx < 0 ? -xx : xx, ay = yy < 0 ? -yy : yy;
+        const float kern = (ax == 0 ? 1.0f : ax == 1 ? 2.0f / 3.0f : 1.0f / 6.0f) *
+                           (ay == 0 ? 1.0f : ay == 1 ? 2.0f / 3.0f : 1.0f / 6.0f);
+        const int o = (yy + 2) * C + (xx + 2) * S;
+        const float4 ip = Li[o];
+        const float4 q = Ln[o];
+        const float dn =
+            fminf(fmaxf(__builtin_fmaf(nd.z, q.z, __builtin_fmaf(nd.y, q.y, nd.x * q.x)), 0.0f), 1.0f);
+        float a;
+        if (FLAT) {
+          const float lp = (0.2125f * ip.x + 0.7154f * ip.y) + 0.0721f * ip.z;
+          a = lp == lc ? fabsf(nd.w - q.w) * kDl : __builtin_inff();
+        } else {
+          const float tl = __builtin_fmaf(ip.z, wLb, __builtin_fmaf(ip.y, wLg, __builtin_fmaf(ip.x, wLr, cL)));
+          a = __builtin_fmaf(fabsf(nd.w - q.w), kDl, fabsf(tl));
+        }
+        const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(p.phi_normal, __builtin_amdgcn_logf(dn), -a)) * kern;
+        sumW += w;
+        s01 = __builtin_elementwise_fma(f2v{w, w}, f2v{ip.x, ip.y}, s01);
+        s23 = __builtin_elementwise_fma(f2v{w, w * w}, f2v{ip.z, ip.w}, s23);
+      }
+    }
+  };
+  if (__builtin_expect(phiL > 0.0f, 1)) taps(std::false_type{});
+  else taps(std::true_type{});
+  const float inv = 1.0f / sumW;
+  *out = float4{s01.x * inv, s01.y * inv, s23.x * inv, s23.y * (inv * inv)};
+}
+
+template <int S>
+static void launch_tile_s(const AtrousParams& p, bool aux, hipStream_t s) {
+  const int groups = (p.y1 - p.y0 + S * kTileRows - 1) / (S * kTileRows);
+  dim3 grid((p.W + 63) / 64, groups * S);
+  if (aux) hipLaunchKernelGGL((atrous_tile_kernel<S, true>), grid, dim3(64 * kTileWaves), 0, s, p);
+  else hipLaunchKernelGGL((atrous_tile_kernel<S, false>), grid, dim3(64 * kTileWaves), 0, s, p);
+}
+
+static bool same_geometry(const AtrousParams& p) {
+  const Plane* planes[3] = {&p.nd, &p.out, &p.fwidth};
+  for (const Plane* q : planes)
+    if (q->row0 != p.illum.row0 || q->rows != p.illum.rows || q->W != p.illum.W) return false;
+  return p.illum.W == p.W;
+}
+
 int launch_atrous_fast(const AtrousParams& p, hipStream_t s) {
   if (p.y1 <= p.y0) return 0;
-  const Plane* planes[3] = {&p.nd, &p.out, &p.fwidth};
-  int same = 1;
-  for (const Plane* q : planes)
-    if (q->row0 != p.illum.row0 || q->rows != p.illum.rows || q->W != p.illum.W) same = 0;
-  if (!same) return launch_atrous_simple(p, s);
+  if (!same_geometry(p)) return launch_atrous_simple(p, s);
+  const bool aux = p.fwidth.aux != nullptr;
+  switch (p.step) {
+    case 1: launch_tile_s<1>(p, aux, s); break;
+    case 2: launch_tile_s<2>(p, aux, s); break;
+    case 4: launch_tile_s<4>(p, aux, s); break;
+    case 8: launch_tile_s<8>(p, aux, s); break;
+    case 16: launch_tile_s<16>(p, aux, s); break;
+    default: return launch_atrous_step(p, s);
+  }
+  return (int)hipGetLastError();
+}
+
+int launch_atrous_step(const AtrousParams& p, hipStream_t s) {
+  if (p.y1 <= p.y0) return 0;
+  if (!same_geometry(p)) return launch_atrous_simple(p, s);
   dim3 grid((p.W + 63) / 64, (p.y1 - p.y0 + 3) / 4);
   switch (p.step) {
     case 1: hipLaunchKernelGGL(atrous_step_kernel<1>, grid, dim3(256), 0, s, p); break;

@@ -276,7 +276,7 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
     pst(p.normal_depth, x, y, bg);
     pst(p.motion, x, y, bg);
     pst(p.fwidth, x, y, bg);
-    if (p.fwidth_aux) p.fwidth_aux[(size_t)prow(p.fwidth, y) * p.W + x] = 0.3f;
+    if (p.fwidth_aux) p.fwidth_aux[(size_t)prow(p.fwidth, y) * p.W + x] = -0.3f;  // .y with the zCenter == 1 flag
     return;
   }
   const float4* g = p.geom + 7 * bests;
@@ -306,7 +306,9 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
   pst(p.normal_depth, x, y, f4(N.x, N.y, N.z, lz));
   pst(p.motion, x, y, f4(nowx - prex, nowy - prey, 0.0f, 1.0f));
   pst(p.fwidth, x, y, f4(length(fwN), fwz, lz, 1.0f));
-  if (p.fwidth_aux) p.fwidth_aux[(size_t)prow(p.fwidth, y) * p.W + x] = fwz;
+  if (p.fwidth_aux)  // .y, sign bit = (linearZ == 1.0): the a-trous background test (svgf_Atrous.frag:77)
+    p.fwidth_aux[(size_t)prow(p.fwidth, y) * p.W + x] =
+        __uint_as_float(__float_as_uint(fwz) | (lz == 1.0f ? 0x80000000u : 0u));
 }
 
 int launch_pathtrace(const PTParams& p, hipStream_t s) {

@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(256) atrous_exact_kernel(AtrousParams p) {
   }
   v3 nc = mk(nd.x, nd.y, nd.z);
   float phiL = p.phi_color * f_sqrt(f_max(0.0f, 1e-10f + var));
-  float fwz = p.fwidth.aux ? p.fwidth.aux[(size_t)row_of(p.fwidth, y) * p.fwidth.W + x] : ldp(p.fwidth, x, y).y;
+  float fwz = p.fwidth.aux ? fabsf(p.fwidth.aux[(size_t)row_of(p.fwidth, y) * p.fwidth.W + x]) : ldp(p.fwidth, x, y).y;
   float phiDepth = f_max(fwz, 1e-8f) * (float)p.step;
   const float kw[3] = {1.0f, 2.0f / 3.0f, 1.0f / 6.0f};
   float sumW = 1.0f;

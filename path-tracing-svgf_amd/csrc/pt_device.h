@@ -7,7 +7,10 @@
 //  * optional compact side plane `aux` (float, 4 B/px) next to a plane whose only
 //    consumer-visible channel is .y (the depth fwidth of gNormalDepthFwidth):
 //    written by the G-buffer kernel, read by the a-trous kernel instead of the
-//    16-B texel (52 B/px/iteration instead of 64);
+//    16-B texel (52 B/px/iteration instead of 64). Its magnitude is .y (always
+//    >= 0, or a NaN with the sign clear); its SIGN BIT flags zCenter == 1 (the
+//    pixel's gNormalAndLinearZ.w, background sentinel), so the a-trous skips
+//    reading the normal/depth texel of pixels it only copies;
 //  * scene: tri_geom  4 x float4 / triangle  (p1,N.p1)(p2,-)(p3,-)(N,-)  intersection
 //           tri_shade 9 x float4 / triangle  normals, material, uv, objIndex  closest hit only
 //           bvh       4 x float4 / interior node: both children's AABBs + child refs
@@ -164,7 +167,8 @@ int launch_gbuffer(const GBufParams& p, hipStream_t s);
 int launch_reproject(const ReprojParams& p, hipStream_t s);
 int launch_variance(const VarianceParams& p, hipStream_t s);
 int launch_atrous_exact(const AtrousParams& p, hipStream_t s);
-int launch_atrous_fast(const AtrousParams& p, hipStream_t s);
+int launch_atrous_fast(const AtrousParams& p, hipStream_t s);   // LDS-tiled (production)
+int launch_atrous_step(const AtrousParams& p, hipStream_t s);   // step-specialised, texture-path taps
 int launch_atrous_simple(const AtrousParams& p, hipStream_t s);
 int launch_modulate(const ModulateParams& p, hipStream_t s);
 int launch_output(const OutputParams& p, hipStream_t s);

@@ -62,7 +62,7 @@ def _run(gl, illum, nd, fw, step, variant):
     return out
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("step", [1, 2, 4, 8, 16])
 def test_atrous_kernel_vs_oracle(gpu, step, variant):
     illum, nd, fw = _planes()
@@ -74,3 +74,51 @@ def test_atrous_kernel_vs_oracle(gpu, step, variant):
     mx = float(np.nanmax(d))
     print(f"step {step} variant {variant}: max rel diff {mx:.3e}")
     assert mx <= 1e-3
+
+
+@pytest.mark.parametrize("step", [1, 2, 4, 8, 16])
+def test_tile_kernel_equals_step_kernel(gpu, step):
+    """The LDS-tiled kernel (variant 0) performs the step kernel's (variant 2) arithmetic in the same tap order:
+    identical bits, NaNs included."""
+    illum, nd, fw = _planes(seed=5)
+    a = _run(gpu, illum, nd, fw, step, 0)
+    b = _run(gpu, illum, nd, fw, step, 2)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_tile_kernel_aux_flag_on_rendered_planes(gpu, scene_small):
+    """On real G-buffer planes the tile kernel reads the compact depth-fwidth plane, whose sign bit carries the
+    zCenter == 1 flag: same bits as the step kernel reading the full texels, every step, 1080p-like aspect."""
+    from ptsvgf.gl import GL_TEXTURE_2D, RenderPass, getShaderProgram, getTextureRGB32F
+    from ptsvgf.camera import parameter_config
+    from ptsvgf.renderer import Renderer
+
+    Wr, Hr = 200, 120
+    r = Renderer(scene_small, Wr, Hr, parameter_config(), mode="fast", aspect_corrected=True, run_taa=False,
+                 run_output=False)
+    for _ in range(2):
+        r.frame()
+    pl = r.planes()
+    nd = gpu.readback(pl["normal_depth"])
+    assert 0.05 < float(np.mean(nd[..., 3] == 1.0)) < 0.95  # both background and surface pixels present
+    outs = {}
+    for variant in (0, 2):
+        for step in (1, 2, 4, 8, 16):
+            to = getTextureRGB32F(Wr, Hr)
+            p = RenderPass(getShaderProgram("shaders/svgf_Atrous.frag", "shaders/vert.vert"), Wr, Hr)
+            p.colorAttachments.append(to)
+            p.bindData(False)
+            p.set_uniform_float("gPhiColor", 4.0)
+            p.set_uniform_float("gPhiNormal", 128.0)
+            p.set_uniform_int("gStepSize", step)
+            p.set_uniform_int("atrous_variant", variant)
+            p.set_texture_uniform(GL_TEXTURE_2D, pl["variance"], "gIllumination")
+            p.set_texture_uniform(GL_TEXTURE_2D, pl["normal_depth"], "gNormalAndLinearZ")
+            p.set_texture_uniform(GL_TEXTURE_2D, pl["fwidth"], "gNormalDepthFwidth")
+            p.draw()
+            outs[variant, step] = gpu.readback(to)
+            p.destroy()
+            gpu.destroy_texture(to)
+    r.close()
+    for step in (1, 2, 4, 8, 16):
+        assert np.array_equal(outs[0, step].view(np.uint32), outs[2, step].view(np.uint32)), step

@@ -15,7 +15,7 @@ import shutil
 import sys
 from collections import defaultdict
 
-ATROUS = "atrous_step_kernel"
+ATROUS = "atrous_tile_kernel"
 
 
 def short(name: str) -> str:
