@@ -105,9 +105,18 @@ int wf_alloc(WFBuffers& b, size_t n) {
   return PT_OK;
 }
 
+// Cost-ordered tile dispatch state of one traversal pass (TileSched, pt_device.h).
+struct TileOrder {
+  uint32_t* cost = nullptr;  // per-tile cost recorded by the current launch
+  int* perm = nullptr;       // dispatch order computed from the previous launch
+  int n = 0;
+  bool ordered = false;      // perm holds a valid order for n tiles
+};
+
 struct Pass {
   uint32_t program = 0;
   WFBuffers wf;
+  TileOrder order;
   int W = 0, H = 0;
   std::vector<uint32_t> att;
   bool bound = false, final_pass = false;
@@ -490,6 +499,39 @@ int copy_plane(Texture* dst, Texture* src, Pass* p, int y0, int y1) {
   return PT_OK;
 }
 
+// Cost-ordered dispatch (TileSched): the launch records per-tile costs into o.cost and
+// runs in the order the previous launch's costs gave (once one exists for this tile
+// count); tile_order_finish then sorts the new costs for the next launch.
+int tile_order_begin(Pass* p, int ntiles, TileSched* out) {
+  TileOrder& o = p->order;
+  memset(out, 0, sizeof(*out));
+  if (ui(p, "tile_order", 1) == 0 || ntiles <= 0) return PT_OK;  // A/B switch: raster order
+  if (o.n != ntiles) {
+    if (o.cost) (void)hipFree(o.cost);
+    if (o.perm) (void)hipFree(o.perm);
+    o.cost = nullptr;
+    o.perm = nullptr;
+    o.n = 0;
+    o.ordered = false;
+    HIPCHK(hipMalloc((void**)&o.cost, (size_t)ntiles * 4));
+    HIPCHK(hipMalloc((void**)&o.perm, (size_t)ntiles * 4));
+    HIPCHK(hipMemsetAsync(o.cost, 0, (size_t)ntiles * 4, g.stream));
+    o.n = ntiles;
+  }
+  out->cost = o.cost;
+  out->perm = o.ordered ? o.perm : nullptr;
+  out->ntiles = ntiles;
+  return PT_OK;
+}
+
+int tile_order_finish(Pass* p, const TileSched& t) {
+  if (!t.cost) return PT_OK;
+  int rc = launch_tile_sort(p->order.cost, p->order.perm, p->order.n, g.stream);
+  if (rc) return hip_err((hipError_t)rc, "tile order sort");
+  p->order.ordered = true;
+  return PT_OK;
+}
+
 // ------------------------------------------------------------- draw calls ---
 int draw_pathtrace(Pass* p) {
   PTParams k;
@@ -556,7 +598,10 @@ int draw_pathtrace(Pass* p) {
     TRY(wf_alloc(p->wf, (size_t)k.W * (size_t)std::max(0, k.y1 - k.y0)));
     k.wf = p->wf.st;
     k.wf.row_cost = p->row_cost;
+    const int ntiles = ((k.W + 15) / 16) * ((std::max(0, k.y1 - k.y0) + 15) / 16);  // wf_primary's grid
+    TRY(tile_order_begin(p, ntiles, &k.tiles));
     rc = launch_pathtrace_wavefront(k, g.stream);
+    if (!rc) TRY(tile_order_finish(p, k.tiles));
   }
   return rc ? hip_err((hipError_t)rc, "pathtrace launch") : PT_OK;
 }
@@ -597,8 +642,11 @@ int draw_raster(Pass* p) {
                        P[3 * 4 + r] * V[c * 4 + 3];
   memcpy(k.PV, PV, 64);
   if (p->raster.ntris == 0) k.root_ref = -1;  // empty leaf
+  const int ntiles = ((k.W + 15) / 16) * ((std::max(0, k.y1 - k.y0) + 15) / 16);  // gbuffer_kernel's grid
+  TRY(tile_order_begin(p, ntiles, &k.tiles));
   int rc = launch_gbuffer(k, g.stream);
   if (rc) return hip_err((hipError_t)rc, "gbuffer launch");
+  TRY(tile_order_finish(p, k.tiles));
   fwt->aux_valid = true;
   return PT_OK;
 }
@@ -742,6 +790,8 @@ int pt_shutdown(void) {
     if (p->raster.geom) (void)hipFree(p->raster.geom);
     if (p->raster.bvh) (void)hipFree(p->raster.bvh);
     if (p->wf.base) (void)hipFree(p->wf.base);
+    if (p->order.cost) (void)hipFree(p->order.cost);
+    if (p->order.perm) (void)hipFree(p->order.perm);
     if (p->ev0) (void)hipEventDestroy(p->ev0);
     if (p->ev1) (void)hipEventDestroy(p->ev1);
   }
@@ -1203,6 +1253,8 @@ int pt_pass_destroy(uint32_t pass) {
   if (p->raster.geom) (void)hipFree(p->raster.geom);
   if (p->raster.bvh) (void)hipFree(p->raster.bvh);
   if (p->wf.base) (void)hipFree(p->wf.base);
+  if (p->order.cost) (void)hipFree(p->order.cost);
+  if (p->order.perm) (void)hipFree(p->order.perm);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
   g.passes.erase(it);

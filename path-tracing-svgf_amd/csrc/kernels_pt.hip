@@ -204,21 +204,25 @@ template <int KS>
 __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
   __shared__ int stk[KS * kBlock];
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-  const int x = blockIdx.x * 16 + (wv & 1) * 8 + (ln & 7);
-  const int y = p.y0 + blockIdx.y * 16 + (wv >> 1) * 8 + (ln >> 3);
-  if (x >= p.W || y >= p.y1) return;
+  const int tile = sched_tile(p.tiles, blockIdx.y * gridDim.x + blockIdx.x);  // cost-ordered dispatch
+  const int tx = tile % gridDim.x, ty = tile / gridDim.x;
+  const int x = tx * 16 + (wv & 1) * 8 + (ln & 7);
+  const int y = p.y0 + ty * 16 + (wv >> 1) * 8 + (ln >> 3);
+  const bool valid = x < p.W && y < p.y1;
   v3 o = mk(p.eye[0], p.eye[1], p.eye[2]);
   v3 d = gb_dir(p, x, y);
   v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   float best = 3.0e38f;
   int besti = -1, bests = -1;
   float bu = 0.f, bv = 0.f;
+  uint32_t steps = 0;
   // while-while walk with one postponed leaf per lane (as traverse<>): the result
   // (closest t, ties to the lower original index) does not depend on visit order
-  int sp = 0, node = p.root_ref, leaf = kNone;
+  int sp = 0, node = valid ? p.root_ref : kNone, leaf = kNone;
   if (node < 0) { leaf = node; node = kNone; }
   while (node != kNone || leaf != kNone) {
     while (node >= 0) {
+      ++steps;
       const float4* nd = p.bvh + 4 * node;
       float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
       // conservative (widened) slab test: the box only culls, Moller-Trumbore decides
@@ -247,6 +251,7 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
     }
     while (leaf != kNone) {
       int first = ref_leaf_first(leaf), cnt = ref_leaf_count(leaf);
+      steps += (uint32_t)cnt;
       for (int i = first; i < first + cnt; ++i) {
         const float4* g = p.geom + 7 * i;
         float4 a = g[0], e1 = g[1], e2 = g[2], ng = g[3];
@@ -270,6 +275,8 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
       }
     }
   }
+  sched_cost(p.tiles, tile, steps);
+  if (!valid) return;
   if (bests < 0) {
     float4 bg = f4(0.2f, 0.3f, 0.3f, 1.0f);  // glClearColor (main.cpp:62)
     pst(p.world, x, y, bg);

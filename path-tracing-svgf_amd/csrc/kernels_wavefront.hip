@@ -102,9 +102,15 @@ __device__ __forceinline__ void block_push3(bool p0, int v0, int* __restrict__ i
 }
 
 // load-balancing probe: accumulate traversal steps per band row (only when requested)
-__device__ __forceinline__ void add_row_cost(const PTParams& p, int local_row, uint32_t steps) {
+#ifndef PT_STEP_MAX
+__device__ __forceinline__ void add_row_cost(const PTParams& p, int local_row, int, uint32_t steps) {
   if (p.wf.row_cost) atomicAdd(p.wf.row_cost + local_row, steps);
 }
+#else  // investigation build (tools/exp_build.sh stepmax -DPT_STEP_MAX): per-pixel maximum of the steps
+__device__ __forceinline__ void add_row_cost(const PTParams& p, int, int pid, uint32_t steps) {
+  if (p.wf.row_cost) atomicMax(p.wf.row_cost + pid, steps);
+}
+#endif
 
 __device__ __forceinline__ v3 primary_dir(const PTParams& p, int x, int y) {
   float pixx = (float)(2 * x + 1) / (float)p.W - 1.0f;
@@ -122,17 +128,35 @@ template <int KS>
 __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
   __shared__ int stk[KS * 256];
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-  const int x = blockIdx.x * 16 + (wv & 1) * 8 + (ln & 7);
-  const int y = p.y0 + blockIdx.y * 16 + (wv >> 1) * 8 + (ln >> 3);
-  if (x >= p.W || y >= p.y1) return;
+  const int tile = sched_tile(p.tiles, blockIdx.y * gridDim.x + blockIdx.x);  // cost-ordered dispatch
+  const int tx = tile % gridDim.x, ty = tile / gridDim.x;
+  const int x = tx * 16 + (wv & 1) * 8 + (ln & 7);
+  const int y = p.y0 + ty * 16 + (wv >> 1) * 8 + (ln >> 3);
+  const bool valid = x < p.W && y < p.y1;
   const int pid = (y - p.y0) * p.W + x;
-  v3 S = mk(p.eye[0], p.eye[1], p.eye[2]);
-  v3 d = primary_dir(p, x, y);
-  float t;
-  uint32_t steps;
-  int tri = traverse<0, 256>(p.scene, stk + threadIdx.x, S, d, 0.0f, p.prune, &t, &steps);
-  p.wf.hit[pid] = make_int2(tri, __float_as_int(t));
-  add_row_cost(p, y - p.y0, steps);
+  uint32_t steps = 0;
+#ifdef PT_WAVE_TIMES
+  const uint32_t t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
+  if (valid) {
+    v3 S = mk(p.eye[0], p.eye[1], p.eye[2]);
+    v3 d = primary_dir(p, x, y);
+    float t;
+    int tri = traverse<0, 256>(p.scene, stk + threadIdx.x, S, d, 0.0f, p.prune, &t, &steps);
+    p.wf.hit[pid] = make_int2(tri, __float_as_int(t));
+  }
+#ifdef PT_WAVE_TIMES  // investigation build: per wave (start, end, max steps) in the row-cost buffer
+  uint32_t ms = steps;
+  for (int o = 32; o > 0; o >>= 1) ms = max(ms, (uint32_t)__shfl_xor((int)ms, o));
+  const uint32_t t_end = (uint32_t)__builtin_amdgcn_s_memrealtime();
+  if (p.wf.row_cost && ln == 0) {
+    uint32_t* q = p.wf.row_cost + 4 * (tile * 4 + wv);
+    q[0] = t_start; q[1] = t_end; q[2] = ms; q[3] = 1;
+  }
+#else
+  sched_cost(p.tiles, tile, steps);
+  if (valid) add_row_cost(p, y - p.y0, pid, steps);
+#endif
 }
 
 // ----------------------------------------------------------- bounce trace ---
@@ -148,7 +172,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest(PTParams p
   uint32_t steps;
   int tri = traverse<0, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dd), 0.0f, p.prune, &t, &steps);
   p.wf.hit[pid] = make_int2(tri, __float_as_int(t));
-  add_row_cost(p, pid / p.W, steps);
+  add_row_cost(p, pid / p.W, pid, steps);
 }
 
 // Shadow rays from the compacted lists wf_shade queued: HDR rays, then point-light rays.
@@ -172,7 +196,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p,
   if (occ < 0)  // binary walk (default), or the 4-wide stack overflowed
     occ = anyhit2<kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps);
   (point ? p.wf.occ_p : p.wf.occ_h)[pid] = occ;
-  add_row_cost(p, pid / p.W, steps);
+  add_row_cost(p, pid / p.W, pid, steps);
 }
 
 // shade()'s MIS combination (:950-966) for given shadow verdicts: hdriLight zeroes

@@ -51,6 +51,18 @@ struct Plane {          // banded RGBA32F plane
   int rows;             // allocated rows
 };
 
+// Cost-ordered dispatch of a tiled traversal launch (kernels_sched.hip). The
+// slowest waves of a traversal launch (rays through dense geometry: ~1000 node and
+// triangle visits at ~0.7 us each) set its tail; started last in raster order they
+// finish long after the bulk. Each launch records every tile's slowest wave and the
+// next launch dispatches tiles in descending order of that cost, so the long waves
+// start first and overlap the bulk. Dispatch order only: results are unchanged.
+struct TileSched {
+  const int* perm;      // launch slot -> tile index, may be null (raster order)
+  uint32_t* cost;       // per tile: max traversal steps of its waves in this launch, may be null
+  int ntiles;
+};
+
 struct Tex {            // non-banded float4 image (HDR map / cache)
   const float4* p;
   int W, H;
@@ -102,6 +114,7 @@ struct PTParams {
   int stack_need;       // deepest interior level of the binary BVH (selects the LDS stack size)
   float sobol_u[4], sobol_v[4];  // sobolVec2(frameCounter+1, b): uniform across pixels
   WFState wf;
+  TileSched tiles;      // primary-ray tiles (16 x 16 px)
 };
 
 struct GBufParams {
@@ -117,6 +130,7 @@ struct GBufParams {
   float P00, P11;       // projection diagonal (pixel ray scale)
   float M[16];          // projection * view (column-major)
   float PV[16];         // pre_viewproj
+  TileSched tiles;      // 16 x 16 px tiles
 };
 
 struct ReprojParams {
@@ -173,5 +187,17 @@ int launch_atrous_simple(const AtrousParams& p, hipStream_t s);
 int launch_modulate(const ModulateParams& p, hipStream_t s);
 int launch_output(const OutputParams& p, hipStream_t s);
 int launch_taa(const TAAParams& p, hipStream_t s);
+int launch_tile_sort(uint32_t* cost, int* perm, int ntiles, hipStream_t s);  // cost -> perm, clears cost
+}  // namespace ptk
+
+namespace ptk {
+__device__ __forceinline__ int sched_tile(const TileSched& t, int slot) { return t.perm ? t.perm[slot] : slot; }
+// Call with every lane of the wave active (steps = 0 for lanes without a ray).
+__device__ __forceinline__ void sched_cost(const TileSched& t, int tile, uint32_t steps) {
+  if (!t.cost) return;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) steps = max(steps, (uint32_t)__shfl_xor((int)steps, o));
+  if ((threadIdx.x & 63) == 0 && steps) atomicMax(t.cost + tile, steps);
+}
 }  // namespace ptk
 #endif

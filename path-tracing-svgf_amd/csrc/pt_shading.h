@@ -49,12 +49,17 @@ __device__ __forceinline__ float slab(v3 o, v3 inv, float ax, float ay, float az
 // hitTriangle (:215-272) hit test; N and dot(N,p1) precomputed on the host with
 // the same built-ins. Flipping N for back hits negates both dot products and
 // the denominator exactly, so t and the inside test are taken unflipped.
-__device__ __forceinline__ bool tri_hit(const float4* __restrict__ g, int i, v3 S, v3 d, float* t_out) {
-  float4 a = g[4 * i], b = g[4 * i + 1], c = g[4 * i + 2], n = g[4 * i + 3];
-  v3 p1 = xyz(a), p2 = xyz(b), p3 = xyz(c), N = xyz(n);
+struct TriGeom {
+  float4 a, b, c, n;  // (p1, N.p1) (p2, -) (p3, -) (N, -)
+};
+__device__ __forceinline__ TriGeom tri_load(const float4* __restrict__ g, int i) {
+  return TriGeom{g[4 * i], g[4 * i + 1], g[4 * i + 2], g[4 * i + 3]};
+}
+__device__ __forceinline__ bool tri_test(const TriGeom& tg, v3 S, v3 d, float* t_out) {
+  v3 p1 = xyz(tg.a), p2 = xyz(tg.b), p3 = xyz(tg.c), N = xyz(tg.n);
   float dn = dot(N, d);
   if (f_abs(dn) < 0.00001f) return false;
-  float t = (a.w - dot(S, N)) / dn;
+  float t = (tg.a.w - dot(S, N)) / dn;
   if (!(t >= 0.0005f)) return false;
   v3 P = add(S, muls(d, t));
   float e1 = dot(cross(sub(p2, p1), sub(P, p1)), N);
@@ -64,6 +69,36 @@ __device__ __forceinline__ bool tri_hit(const float4* __restrict__ g, int i, v3 
   bool r2 = e1 < 0.0f && e2 < 0.0f && e3 < 0.0f;
   *t_out = t;
   return r1 || r2;
+}
+__device__ __forceinline__ bool tri_hit(const float4* __restrict__ g, int i, v3 S, v3 d, float* t_out) {
+  return tri_test(tri_load(g, i), S, d, t_out);
+}
+
+// A leaf's triangles in index order (hitArray's strict '<' order, :298-369). The
+// geometry of up to PT_LEAF_CHUNK triangles is fetched together before they are
+// tested, so a leaf costs one memory round trip per chunk instead of one per
+// triangle (the latency chain of the longest rays sets a launch's tail).
+// on_hit(i, t) returns true to stop the scan (any-hit rays).
+#ifndef PT_LEAF_CHUNK
+#define PT_LEAF_CHUNK 1
+#endif
+template <class F>
+__device__ __forceinline__ bool leaf_scan(const float4* __restrict__ g, int first, int cnt, v3 S, v3 d,
+                                          F&& on_hit) {
+  const int end = first + cnt;
+  for (int i0 = first; i0 < end; i0 += PT_LEAF_CHUNK) {
+    TriGeom tg[PT_LEAF_CHUNK];
+#pragma unroll
+    for (int k = 0; k < PT_LEAF_CHUNK; ++k)
+      if (i0 + k < end) tg[k] = tri_load(g, i0 + k);
+#pragma unroll
+    for (int k = 0; k < PT_LEAF_CHUNK; ++k) {
+      if (i0 + k >= end) break;
+      float t;
+      if (tri_test(tg[k], S, d, &t) && on_hit(i0 + k, t)) return true;
+    }
+  }
+  return false;
 }
 
 __device__ __forceinline__ int ref_leaf_first(int ref) { return (-(ref + 1)) >> 4; }
@@ -132,19 +167,23 @@ __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
     while (leaf != kNone) {
       int first = ref_leaf_first(leaf), cnt = ref_leaf_count(leaf);
       nvis += (uint32_t)cnt;
-      for (int i = first; i < first + cnt; ++i) {
-        float t;
-        if (!tri_hit(sc.tri_geom, i, S, d, &t)) continue;
+      int anyi = -1;
+      float anyt = 0.0f;
+      const bool stop = leaf_scan(sc.tri_geom, first, cnt, S, d, [&](int i, float t) {
         if (MODE == 0) {
           if (t < tbest) { tbest = t; best = i; }
-        } else if (MODE == 1) {
-          if (t < PT_INF) { *t_best_out = t; if (steps) *steps = nvis; return i; }
-        } else {
-          if (t < PT_INF) {
-            float sd = length(sub(add(S, muls(d, t)), S));
-            if (sd < maxd) { *t_best_out = t; if (steps) *steps = nvis; return i; }
-          }
+          return false;
         }
+        if (!(t < PT_INF)) return false;
+        if (MODE == 2 && !(length(sub(add(S, muls(d, t)), S)) < maxd)) return false;
+        anyi = i;
+        anyt = t;
+        return true;
+      });
+      if (MODE != 0 && stop) {
+        *t_best_out = anyt;
+        if (steps) *steps = nvis;
+        return anyi;
       }
       leaf = kNone;
       if (node < 0 && node != kNone) {  // the walk stopped on a second leaf: it is next in order
@@ -211,13 +250,11 @@ __device__ bool anyhit2(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, b
     while (leaf != kNone) {
       int first = ref_leaf_first(leaf), cnt = ref_leaf_count(leaf);
       nvis += (uint32_t)cnt;
-      for (int i = first; i < first + cnt; ++i) {
-        float t;
-        if (!tri_hit(sc.tri_geom, i, S, d, &t) || !(t < PT_INF)) continue;
-        if (!point || length(sub(add(S, muls(d, t)), S)) < maxd) {
-          if (steps) *steps = nvis;
-          return true;
-        }
+      if (leaf_scan(sc.tri_geom, first, cnt, S, d, [&](int, float t) {
+            return t < PT_INF && (!point || length(sub(add(S, muls(d, t)), S)) < maxd);
+          })) {
+        if (steps) *steps = nvis;
+        return true;
       }
       leaf = kNone;
       if (node < 0 && node != kNone) {
@@ -276,13 +313,11 @@ __device__ int anyhit4(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, bo
     while (leaf != kNone) {
       int first = ref_leaf_first(leaf), cnt = ref_leaf_count(leaf);
       nvis += (uint32_t)cnt;
-      for (int i = first; i < first + cnt; ++i) {
-        float t;
-        if (!tri_hit(sc.tri_geom, i, S, d, &t) || !(t < PT_INF)) continue;
-        if (!point || length(sub(add(S, muls(d, t)), S)) < maxd) {  // :905-909 for point lights
-          if (steps) *steps = nvis;
-          return 1;
-        }
+      if (leaf_scan(sc.tri_geom, first, cnt, S, d, [&](int, float t) {  // :905-909 for point lights
+            return t < PT_INF && (!point || length(sub(add(S, muls(d, t)), S)) < maxd);
+          })) {
+        if (steps) *steps = nvis;
+        return 1;
       }
       leaf = kNone;
       if (node < 0 && node != kNone) {

@@ -1,0 +1,106 @@
+"""Single-GPU prediction of an N-GPU strong-scaling frame (ptsvgf.dist bands), ranks simulated one after another.
+
+For every rank r of N: build the BandRenderer of r with the halo exchanges replaced by a recorder, time its frame
+(GPU time of the band + host issue time) and probe its per-row BVH visit counts. Then fit the cost model of
+make_band_renderer (T = a*visits + b*rows over the ranks), derive the balanced bounds and simulate again.
+The predicted N-GPU frame time is the slowest rank plus the halo exchanges (not simulated: reported as bytes).
+usage: python tools/band_sim.py [N] [W] [H]"""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "path-tracing-svgf_amd"))
+import numpy as np
+import torch
+
+from ptsvgf import dist as D
+from ptsvgf import gl
+from ptsvgf.camera import parameter_config
+from ptsvgf.scene import build_scene
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+W = int(sys.argv[2]) if len(sys.argv) > 2 else 3840
+H = int(sys.argv[3]) if len(sys.argv) > 3 else 2160
+LOG = []
+
+
+class FakeDist:
+    def get_backend(self, group=None):
+        return "nccl"
+
+
+def fake_exchange(tensors, plan, n, dist, group=None):
+    if plan.world == 1 or n <= 0:
+        return
+    nb = (plan.up is not None) + (plan.down is not None)
+    LOG.append(sum(n * t.shape[1] * t.shape[2] * 4 for t in tensors) * nb)
+
+
+D.halo_exchange = fake_exchange
+torch.cuda.set_device(0)
+gl.init(0)
+from ptsvgf._lib import check, pt
+check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
+scene = build_scene("table_clock_plant")
+cfg = parameter_config()
+
+
+def sim_rank(rk, bounds, probe=False, K=10):
+    r = D.BandRenderer(scene, W, H, cfg, rk, N, FakeDist(), bounds=bounds)
+    r.pass_path_tracing.set_uniform_int("pt_kernel", int(os.environ.get("PTK", "0")))
+    for _ in range(3):
+        r.frame()
+    torch.cuda.synchronize()
+    LOG.clear()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        r.frame()
+    issue = (time.perf_counter() - t0) / K
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / K
+    xbytes = sum(LOG) / K
+    nex = len(LOG) / K
+    counts = None
+    if probe:
+        c = torch.zeros(r.plan.y1 - r.plan.y0, dtype=torch.int32, device="cuda")
+        r.pass_path_tracing.set_row_cost(c.data_ptr())
+        r.frame()
+        torch.cuda.synchronize()
+        r.pass_path_tracing.set_row_cost(0)
+        counts = c.cpu().numpy().astype(np.float64)
+    r.profile(True)
+    r.frame()
+    torch.cuda.synchronize()
+    pp = r.pass_times()
+    r.profile(False)
+    y0, y1 = r.plan.y0, r.plan.y1
+    r.close()
+    return dict(y0=y0, y1=y1, wall=wall * 1e3, issue=issue * 1e3, gpu=pp["frame_sum_ms"], pp=pp, counts=counts,
+                xbytes=xbytes, nex=nex)
+
+
+def report(tag, res):
+    print(f"--- {tag}: N={N} {W}x{H}")
+    for rk, s in enumerate(res):
+        print(f"rank {rk}: rows {s['y0']}..{s['y1']} ({s['y1'] - s['y0']}) wall {s['wall']:.3f} ms gpu {s['gpu']:.3f} "
+              f"issue {s['issue']:.3f}  gbuf {s['pp']['gbuffer']:.3f} pt {s['pp']['pathtrace']:.3f} "
+              f"svgf {s['gpu'] - s['pp']['gbuffer'] - s['pp']['pathtrace']:.3f}  halo {s['nex']:.0f}x "
+              f"{s['xbytes'] / 1e6:.2f} MB")
+    mx = max(s["wall"] for s in res)
+    print(f"predicted frame (slowest rank, no exchange time): {mx:.3f} ms = {1e3 / mx:.1f} fps; "
+          f"sum of rank GPU times {sum(s['gpu'] for s in res):.3f} ms")
+
+
+if __name__ == "__main__":
+    eq = [sim_rank(rk, None, probe=True) for rk in range(N)]
+    report("equal bands", eq)
+    if N > 1:
+        visits = np.concatenate([s["counts"] for s in eq])
+        a, b = D.fit_row_cost([s["counts"].sum() for s in eq], [s["y1"] - s["y0"] for s in eq],
+                              [s["gpu"] for s in eq])
+        bounds = D.balanced_bounds(a * visits + b, N)
+        print("fit a=%.3e b=%.3e bounds %s" % (a, b, bounds))
+        bal = [sim_rank(rk, bounds) for rk in range(N)]
+        report("balanced bands", bal)
+    gl.shutdown()
