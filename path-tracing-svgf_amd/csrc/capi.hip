@@ -80,11 +80,12 @@ struct WFBuffers {
   WFState st{};
 };
 
-int wf_alloc(WFBuffers& b, size_t n) {
+int wf_alloc(WFBuffers& b, int W, int rows) {
+  const size_t n = (size_t)W * (size_t)rows;
   if (b.base && b.n == n) return PT_OK;
   if (b.base) { (void)hipFree(b.base); b.base = nullptr; }
   const size_t f4 = n * 16, al = 256;
-  const size_t nl = (size_t)wf_list_capacity((int)n) * 8;  // 8 list segments
+  const size_t nl = (size_t)wf_list_capacity(W, rows) * 8;  // 8 list segments
   auto up = [&](size_t v) { return (v + al - 1) / al * al; };
   size_t total = up(f4) * 10 + up(n * 8) + up(n * 4) + up(n) * 2 + up(nl * 4) * 2 + up(nl * 8) +
                  up(kWfCounters * 4);
@@ -520,6 +521,7 @@ int tile_order_begin(Pass* p, int ntiles, TileSched* out) {
   }
   out->cost = o.cost;
   out->perm = o.ordered ? o.perm : nullptr;
+  out->perm_next = o.perm;
   out->ntiles = ntiles;
   return PT_OK;
 }
@@ -595,13 +597,13 @@ int draw_pathtrace(Pass* p) {
   if (ui(p, "pt_kernel", 0) == 1) {  // 1: single megakernel (kernels_pt.hip), kept for A/B
     rc = launch_pathtrace(k, g.stream);
   } else {                            // 0: wavefront (kernels_wavefront.hip), production
-    TRY(wf_alloc(p->wf, (size_t)k.W * (size_t)std::max(0, k.y1 - k.y0)));
+    TRY(wf_alloc(p->wf, k.W, std::max(0, k.y1 - k.y0)));
     k.wf = p->wf.st;
     k.wf.row_cost = p->row_cost;
     const int ntiles = ((k.W + 15) / 16) * ((std::max(0, k.y1 - k.y0) + 15) / 16);  // wf_primary's grid
     TRY(tile_order_begin(p, ntiles, &k.tiles));
-    rc = launch_pathtrace_wavefront(k, g.stream);
-    if (!rc) TRY(tile_order_finish(p, k.tiles));
+    rc = launch_pathtrace_wavefront(k, g.stream);  // sorts the tile order itself, after the primaries
+    if (!rc && k.tiles.cost) p->order.ordered = true;
   }
   return rc ? hip_err((hipError_t)rc, "pathtrace launch") : PT_OK;
 }

@@ -231,8 +231,14 @@ __global__ void __launch_bounds__(256) wf_shade(PTParams p, int bounce, const in
   int pid = 0;
   bool valid;
   if (bounce == 0) {
-    valid = k < p.W * (p.y1 - p.y0);
-    pid = k;
+    // one 16 x 16 primary tile per block, in descending order of this frame's primary-ray cost
+    // (tiles.perm_next, sorted right after wf_primary): the rays of expensive tiles are appended to
+    // the lists first, so every later list-driven trace launch starts its slowest rays first
+    const int ntx = (p.W + 15) / 16;
+    const int tile = p.tiles.cost ? p.tiles.perm_next[blockIdx.x] : (int)blockIdx.x;
+    const int x = (tile % ntx) * 16 + (threadIdx.x & 15), ly = (tile / ntx) * 16 + (threadIdx.x >> 4);
+    valid = x < p.W && ly < p.y1 - p.y0;
+    pid = ly * p.W + x;
   } else {
     valid = seg_get(list_in, counts_in, cap, k, &pid);
   }
@@ -379,19 +385,29 @@ __global__ void __launch_bounds__(256) wf_finalize(PTParams p) {
   pst(p.color, x, y, f4(color.x, color.y, color.z, 1.0f));
 }
 
-int wf_list_capacity(int npix) { return ((npix + 255) / 256 + kSeg - 1) / kSeg * 256; }
+// A producer block appends at most 256 items to the segment blockIdx % kSeg; the most blocks
+// an appending launch has is the larger of the per-pixel grid and the bounce-0 tile grid.
+int wf_list_capacity(int W, int rows) {
+  const int blocks = std::max((W * rows + 255) / 256, ((W + 15) / 16) * ((rows + 15) / 16));
+  return (blocks + kSeg - 1) / kSeg * 256;
+}
 
 template <int KS>
 int launch_wavefront(const PTParams& p, hipStream_t s) {
   const int rows = p.y1 - p.y0;
   if (rows <= 0) return 0;
   const int N = p.W * rows;
-  const int cap = wf_list_capacity(N);  // per segment; the host sized the lists with the same function
+  const int cap = wf_list_capacity(p.W, rows);  // per segment; the host sized the lists with the same function
   hipError_t e = hipMemsetAsync(p.wf.counters, 0, kWfCounters * sizeof(int), s);
   if (e != hipSuccess) return (int)e;
   dim3 tiles((p.W + 15) / 16, (rows + 15) / 16);
   hipLaunchKernelGGL(wf_primary<KS>, tiles, dim3(256), 0, s, p);
+  if (p.tiles.cost) {  // this frame's primary costs -> tile order of the bounce-0 shade and the next frame
+    const int rc = launch_tile_sort(p.tiles.cost, p.tiles.perm_next, p.tiles.ntiles, s);
+    if (rc) return rc;
+  }
   const int gN = (N + 255) / 256, gT = (N + kTB - 1) / kTB, gT2 = (2 * N + kTB - 1) / kTB;
+  const int gS0 = tiles.x * tiles.y;  // bounce-0 shade: one block per primary tile
   int* lists[2] = {p.wf.list0, p.wf.list1};
   for (int i = 0; i < p.max_depth; ++i) {
     const int* lin = lists[(i + 1) & 1];
@@ -400,8 +416,8 @@ int launch_wavefront(const PTParams& p, hipStream_t s) {
     int* shadow = p.wf.counters + 32 * i + 8;  // kSeg HDR + kSeg point-light shadow-list counts
     const int* live_in = p.wf.counters + 32 * (i > 0 ? i - 1 : 0);
     if (i > 0) hipLaunchKernelGGL(wf_trace_closest<KS>, dim3(gT), dim3(kTB), 0, s, p, lin, live_in, cap);
-    hipLaunchKernelGGL(wf_shade, dim3(gN), dim3(256), 0, s, p, i, lin, live_in, lout, live, p.wf.shadow_list, shadow,
-                       cap);
+    hipLaunchKernelGGL(wf_shade, dim3(i == 0 ? gS0 : gN), dim3(256), 0, s, p, i, lin, live_in, lout, live,
+                       p.wf.shadow_list, shadow, cap);
     if (p.scene.bvh4)
       hipLaunchKernelGGL((wf_trace_shadow<KS, true>), dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
                          (const int*)shadow, cap);

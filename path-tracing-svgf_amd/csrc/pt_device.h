@@ -59,6 +59,7 @@ struct Plane {          // banded RGBA32F plane
 // start first and overlap the bulk. Dispatch order only: results are unchanged.
 struct TileSched {
   const int* perm;      // launch slot -> tile index, may be null (raster order)
+  int* perm_next;       // where the order from this launch's costs is written (the same buffer as perm)
   uint32_t* cost;       // per tile: max traversal steps of its waves in this launch, may be null
   int ntiles;
 };
@@ -176,7 +177,7 @@ namespace ptk {
 // Launchers (kernels_*.hip). Return hipError_t as int.
 int launch_pathtrace(const PTParams& p, hipStream_t s);
 int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s);
-int wf_list_capacity(int npix);  // per-segment capacity of the compacted ray lists (8 segments)
+int wf_list_capacity(int W, int rows);  // per-segment capacity of the compacted ray lists (8 segments)
 int launch_gbuffer(const GBufParams& p, hipStream_t s);
 int launch_reproject(const ReprojParams& p, hipStream_t s);
 int launch_variance(const VarianceParams& p, hipStream_t s);
