@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--equal-bands", action="store_true", help="multi-GPU: equal band heights (no cost balancing)")
     ap.add_argument("--breakdown", action="store_true", help="print per-pass ms to stderr")
     ap.add_argument("--pt-kernel", type=int, default=0, help="0 wavefront (production), 1 megakernel (A/B)")
+    ap.add_argument("--frames-in-flight", type=int, default=1,
+                    help="K > 1: front ends (G-buffer + path tracer) of K frames overlap on K streams")
     ap.add_argument("--pt-uniform", action="append", default=[], metavar="NAME=INT",
                     help="extra int uniform on the path-tracing pass (A/B switches, e.g. shadow_bvh4=0)")
     return ap.parse_args()
@@ -131,10 +133,12 @@ def main():
         profiled frame for the per-pass HIP-event breakdown."""
         if world > 1:
             from ptsvgf.dist import make_band_renderer
-            r = make_band_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands)
+            r = make_band_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,
+                                   frames_in_flight=args.frames_in_flight)
         else:
             from ptsvgf.renderer import Renderer
-            r = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, run_taa=False, run_output=False)
+            r = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, run_taa=False, run_output=False,
+                         frames_in_flight=args.frames_in_flight)
         r.pass_path_tracing.set_uniform_int("pt_kernel", args.pt_kernel)
         for kv in args.pt_uniform:
             name, val = kv.split("=")

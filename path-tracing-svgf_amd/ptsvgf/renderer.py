@@ -30,15 +30,44 @@ def _prog(frag: str, vert: str = "vert.vert") -> int:
     return getShaderProgram(SHADERS + frag, SHADERS + vert)
 
 
+class PassGroup:
+    """Several passes of one program driven as one: a call applies to each (returns the first result)."""
+
+    def __init__(self, passes):
+        self.passes = list(passes)
+
+    def __getattr__(self, name):
+        fns = [getattr(p, name) for p in self.passes]
+
+        def call(*a, **k):
+            return [f(*a, **k) for f in fns][0]
+
+        return call
+
+
+def _set_stream(stream) -> None:
+    from ._lib import check, pt
+
+    check(pt().pt_set_stream(stream.cuda_stream))
+
+
 class Renderer:
     def __init__(self, scene: Scene, width: int, height: int, config: parameter_config | None = None,
                  mode: str = "fast", aspect_corrected: bool | None = None, band=None, prune: bool = True,
                  atrous_exact: bool = False, run_taa: bool = True, run_output: bool = True, tex_factory=None,
-                 halo=None, gbuffer_rows=None):
+                 halo=None, gbuffer_rows=None, frames_in_flight: int = 1):
         """band = (y0, y1, row0, rows) for screen-band sharding; tex_factory(w, h) -> handle allocates the
         frame-sized planes (ptsvgf.dist wraps torch tensors); halo(stage, handles) is called before the
         SVGF passes that read neighbour rows (dist.HALO_SCHEDULE); gbuffer_rows = (row0, row1) ghost rows
-        the G-buffer recomputes locally."""
+        the G-buffer recomputes locally.
+
+        frames_in_flight = K > 1 (fast driver): the G-buffer + path tracer of frame f (the front end, which
+        depends on nothing but the camera) run on stream f % K while the SVGF chain (sequential: each frame
+        reads the previous frame's history) runs on one back-end stream. Frame f's front end waits only for
+        the SVGF of frame f-K, whose buffers it reuses. The front end's launches end in long tails (a few
+        rays through dense geometry); with K frames in flight another frame's work fills them. Same
+        kernels, same inputs, same bits as K = 1 (tests/test_gpu_parity.py); throughput rises, latency
+        from camera to finished frame is up to K frames."""
         if mode not in ("fast", "reference"):
             raise ValueError(mode)
         if mode == "fast" and config is not None and config.accumulate_color:
@@ -82,7 +111,12 @@ class Renderer:
                         self.hdrCache]
         self.hdrResolution = hw
 
-        nbuf = 2 if mode == "fast" else 1
+        self.K = int(frames_in_flight)
+        if self.K < 1 or (self.K > 1 and mode != "fast"):
+            raise ValueError("frames_in_flight must be >= 1, and > 1 only with the fast driver")
+        # G-buffer sets: the reference has one; fast mode alternates two (this frame / previous frame);
+        # with K frames in flight, frame f writes set f % (K+1) once SVGF(f-K) has read it (as "previous")
+        nbuf = (self.K + 1 if self.K > 1 else 2) if mode == "fast" else 1
         # G-buffer (main.cpp:208-226); fast mode double-buffers it (prev normal/depth = other parity)
         self.init_pass = []
         self.gbuf = []
@@ -100,18 +134,30 @@ class Renderer:
             self.gbuf.append(g)
 
         # path tracer (main.cpp:229-248)
-        self.pass_path_tracing = RenderPass(_prog("path_tracing.frag"), W, H)
-        self.curColor, self.Emission, self.Albedo = tex(W, H), tex(W, H), tex(W, H)
-        self.pass_path_tracing.colorAttachments += [self.curColor, self.Emission, self.Albedo]
-        self.pass_path_tracing.bindData(False)
-        pt = self.pass_path_tracing
-        pt.set_uniform_int("nTriangles", scene.ntris)
-        pt.set_uniform_int("nNodes", scene.node_enc.shape[0])
-        pt.set_uniform_int("width", W)
-        pt.set_uniform_int("height", H)
-        pt.set_uniform_int("pointLightSize", scene.lights.shape[0])
-        pt.set_uniform_int("aspect_corrected", int(self.aspect_corrected))
-        pt.set_uniform_int("prune", int(prune))
+        # (one pass + output set per frame in flight: each owns its wavefront state)
+        self.pt_slots = []
+        for _ in range(self.K):
+            p = RenderPass(_prog("path_tracing.frag"), W, H)
+            outs = (tex(W, H), tex(W, H), tex(W, H))  # color, emission, albedo
+            p.colorAttachments += list(outs)
+            p.bindData(False)
+            p.set_uniform_int("nTriangles", scene.ntris)
+            p.set_uniform_int("nNodes", scene.node_enc.shape[0])
+            p.set_uniform_int("width", W)
+            p.set_uniform_int("height", H)
+            p.set_uniform_int("pointLightSize", scene.lights.shape[0])
+            p.set_uniform_int("aspect_corrected", int(self.aspect_corrected))
+            p.set_uniform_int("prune", int(prune))
+            self.pt_slots.append((p, outs))
+        self.pass_path_tracing = PassGroup([p for p, _ in self.pt_slots])  # settings apply to every slot
+        self._use_slot(0)
+        self._streams = None
+        if self.K > 1:
+            import torch  # streams and events are torch plumbing (the kernels are the library's)
+
+            self._streams = [torch.cuda.Stream() for _ in range(self.K)]
+            self._back = torch.cuda.Stream()
+            self._slot_free = [None] * self.K  # event: SVGF of the frame that last used the slot is done
 
         # SVGF targets
         if mode == "reference":
@@ -188,6 +234,10 @@ class Renderer:
             p.set_uniform_float("inv_screen_height", 1.0 / H)
 
     # ------------------------------------------------------------- frame ---
+    def _use_slot(self, s: int) -> None:
+        """Path-tracing pass and outputs of frame slot s (frame f uses slot f % K)."""
+        self.pt_pass, (self.curColor, self.Emission, self.Albedo) = self.pt_slots[s]
+
     def _gbuffer_and_pt(self, b: int):
         cam, cfg = self.camera, self.cfg
         view, proj = cam.cam_view_mat, cam.cam_proj_mat
@@ -198,7 +248,7 @@ class Renderer:
         ip.set_uniform_uint("frameCounter", cam.frameCounter)
         self._draw(ip, "gbuffer")
         self.cameraRotate = rigid_inverse(view)                # main.cpp:445
-        pt = self.pass_path_tracing                            # main.cpp:447-470
+        pt = self.pt_pass                                      # main.cpp:447-470
         pt.set_uniform_vec3("eye", cam.cam_position)
         pt.set_uniform_mat4("cameraRotate", self.cameraRotate)
         pt.set_uniform_uint("frameCounter", cam.frameCounter)
@@ -292,10 +342,27 @@ class Renderer:
 
     def _frame_fast(self):
         cfg = self.cfg
-        b = self.frame_index & 1
+        f = self.frame_index
+        b = f & 1                                              # history parity (back end, sequential)
         pb = 1 - b
-        g, gp = self.gbuf[b], self.gbuf[pb]
-        self._gbuffer_and_pt(b)
+        ng = len(self.gbuf)
+        g, gp = self.gbuf[f % ng], self.gbuf[(f - 1) % ng]
+        s = f % self.K
+        self._use_slot(s)
+        if self.K > 1:                                         # front end on stream s, after SVGF(f - K)
+            import torch
+
+            fe = self._streams[s]
+            if self._slot_free[s] is not None:
+                fe.wait_event(self._slot_free[s])
+            _set_stream(fe)
+            self._gbuffer_and_pt(f % ng)
+            done = torch.cuda.Event()
+            done.record(fe)
+            self._back.wait_event(done)
+            _set_stream(self._back)
+        else:
+            self._gbuffer_and_pt(f % ng)
         self._halo("reproject", [self.hist_illum[pb], self.moments[pb]])
         rp = self.reproject[b]
         rp.reset_texture_slot()
@@ -367,7 +434,14 @@ class Renderer:
         self.final = self.taa[b] if self.run_taa else self.modulate_color
 
     def _halo(self, stage: str, handles) -> None:
-        if self._halo_cb is not None:
+        if self._halo_cb is None:
+            return
+        if self.K > 1:  # the exchange belongs to the back-end stream (torch.distributed uses the current one)
+            import torch
+
+            with torch.cuda.stream(self._back):
+                self._halo_cb(stage, handles)
+        else:
             self._halo_cb(stage, handles)
 
     def _draw(self, p: RenderPass, name: str) -> None:
@@ -405,6 +479,12 @@ class Renderer:
             op.set_uniform_bool("accumulate", self.cfg.accumulate_color)
             op.set_texture_uniform(GL_TEXTURE_2D, self.final, "texPass0")
             self._draw(op, "output")
+        if self.K > 1:  # the slot's buffers are free again once this frame's back end has run
+            import torch
+
+            ev = torch.cuda.Event()
+            ev.record(self._back)
+            self._slot_free[self.frame_index % self.K] = ev
         # main.cpp:599-600: pre_viewproj = projection * inverse(cameraRotate) = projection * view
         self.pre_viewproj = mat_mul(self.camera.cam_proj_mat, self.camera.cam_view_mat)
         self.camera.frameCounter += 1
@@ -413,8 +493,16 @@ class Renderer:
     # --------------------------------------------------------- accessors ---
     def close(self) -> None:
         """Release every pass and texture this renderer created (the GL objects main.cpp never frees)."""
+        if self._streams is not None:
+            import torch
+
+            torch.cuda.synchronize()  # frames may still be in flight on the renderer's streams
         for v in list(vars(self).values()):
+            if isinstance(v, PassGroup):
+                continue  # its passes are the pt_slots' (destroyed below)
             for q in (v if isinstance(v, list) else list(v.values()) if isinstance(v, dict) else [v]):
+                if isinstance(q, tuple):
+                    q = q[0]  # pt_slots entries: (pass, outputs)
                 if isinstance(q, RenderPass):
                     q.destroy()
         for t in self._owned:
@@ -432,7 +520,7 @@ class Renderer:
                         history_illum=self.lastIllumination, modulate=self.modulate_color, final=self.final,
                         output=self.output_tex)
         b = (self.frame_index - 1) & 1
-        g = self.gbuf[b]
+        g = self.gbuf[(self.frame_index - 1) % len(self.gbuf)]
         return dict(world=g["world"], normal_depth=g["normal_depth"], velocity=g["velocity"], fwidth=g["fwidth"],
                     color=self.curColor, emission=self.Emission, albedo=self.Albedo, reproj_illum=self.illum,
                     reproj_moments=self.moments[b], variance=self.var_out, atrous=self.atrous_final,

@@ -162,6 +162,36 @@ def test_fast_driver_equals_reference_driver(gpu, scene_small):
             assert np.array_equal(pa[key], pb[key]), (f, key)
 
 
+@pytest.mark.parametrize("K", [2, 3])
+def test_frames_in_flight_equal_serial(gpu, scene_small, K):
+    """K frames in flight (front ends on K streams, SVGF chain on a back-end stream) give the serial fast
+    driver's bits: per frame (read back after each frame) and after K+3 frames issued without any host wait
+    (moving camera, so every frame's inputs differ)."""
+    gl = gpu
+    W, H = 96, 64
+    kw = dict(mode="fast", run_taa=True, run_output=True)
+    a = _renderer(scene_small, W, H, **kw)
+    b = _renderer(scene_small, W, H, frames_in_flight=K, **kw)
+    keys = ("normal_depth", "color", "albedo", "reproj_illum", "variance", "atrous", "modulate", "final", "output")
+    for f in range(K + 2):
+        for r in (a, b):
+            if f >= 2:
+                r.camera.orbit(1.0, 0.0)
+            r.frame()
+        pa, pb = _readback(gl, a), _readback(gl, b)
+        for key in keys:
+            assert np.array_equal(pa[key].view(np.uint32), pb[key].view(np.uint32)), (f, key)
+    for f in range(K + 3):  # no readback in between: the streams overlap frames
+        for r in (a, b):
+            r.camera.orbit(1.0, 0.0)
+            r.frame()
+    pa, pb = _readback(gl, a), _readback(gl, b)
+    for key in keys:
+        assert np.array_equal(pa[key].view(np.uint32), pb[key].view(np.uint32)), ("overlapped", key)
+    a.close()
+    b.close()
+
+
 def test_fast_atrous_within_tolerance(gpu, scene_small):
     """Production a-trous (hardware exp2/log2) vs the exact oracle on real frame data."""
     gl = gpu
