@@ -22,6 +22,9 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
+# frames in flight use K + 1 streams (K front ends + the SVGF back end); HIP's default of 4 hardware queues
+# per process would make streams share queues and serialise. Set before HIP initialises.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 sys.path.insert(0, os.path.join(REPO, "path-tracing-svgf_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
@@ -62,7 +65,7 @@ def parse():
     ap.add_argument("--equal-bands", action="store_true", help="multi-GPU: equal band heights (no cost balancing)")
     ap.add_argument("--breakdown", action="store_true", help="print per-pass ms to stderr")
     ap.add_argument("--pt-kernel", type=int, default=0, help="0 wavefront (production), 1 megakernel (A/B)")
-    ap.add_argument("--frames-in-flight", type=int, default=1,
+    ap.add_argument("--frames-in-flight", type=int, default=4,
                     help="K > 1: front ends (G-buffer + path tracer) of K frames overlap on K streams")
     ap.add_argument("--pt-uniform", action="append", default=[], metavar="NAME=INT",
                     help="extra int uniform on the path-tracing pass (A/B switches, e.g. shadow_bvh4=0)")
@@ -210,7 +213,7 @@ def main():
                                        + (" moving camera" if args.moving else ""),
                            "resolution": [W, H], "spp": 1, "max_tracing_depth": cfg.max_tracing_depth,
                            "atrous_iterations": cfg.num_atrous_iterations, "triangles": scene.ntris,
-                           "parallelism": f"bands{world}"},
+                           "parallelism": f"bands{world}", "frames_in_flight": args.frames_in_flight},
                 "roofline": roof, "cpu_baseline": cpu, **extra,
                 "passes_ms": {k: round(v, 4) for k, v in per_pass.items()}}
         print(json.dumps(line), flush=True)

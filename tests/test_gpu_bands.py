@@ -23,7 +23,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, outdir, moving, balance):
+def _worker(rank, world, port, outdir, moving, balance, fif=1):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(os.path.dirname(here), "path-tracing-svgf_amd"))
@@ -40,7 +40,8 @@ def _worker(rank, world, port, outdir, moving, balance):
     gl.init(0)
     check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
     scene = build_scene("table_clock_plant", hdr_size=(256, 128), plant_leaves=40)
-    r = make_band_renderer(scene, W, H, parameter_config(), rank, world, dist, balance=balance, run_taa=True)
+    r = make_band_renderer(scene, W, H, parameter_config(), rank, world, dist, balance=balance, run_taa=True,
+                           frames_in_flight=fif)
     for f in range(FRAMES):
         if moving and f:
             r.camera.orbit(1.5, 0.5)
@@ -53,8 +54,8 @@ def _worker(rank, world, port, outdir, moving, balance):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("moving,balance", [(False, False), (True, False), (True, True)])
-def test_two_bands_equal_full_frame(gpu, moving, balance):
+@pytest.mark.parametrize("moving,balance,fif", [(False, False, 1), (True, False, 1), (True, True, 1), (True, True, 3)])
+def test_two_bands_equal_full_frame(gpu, moving, balance, fif):
     import torch.multiprocessing as mp
 
     from ptsvgf.camera import parameter_config
@@ -63,7 +64,7 @@ def test_two_bands_equal_full_frame(gpu, moving, balance):
 
     gl = gpu
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(2, _port(), d, moving, balance), nprocs=2, join=True)
+        mp.spawn(_worker, args=(2, _port(), d, moving, balance, fif), nprocs=2, join=True)
         bands = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(2)]
     scene = build_scene("table_clock_plant", hdr_size=(256, 128), plant_leaves=40)
     full = Renderer(scene, W, H, parameter_config(), mode="fast", aspect_corrected=True, run_taa=True,

@@ -47,12 +47,14 @@ cfg = parameter_config()
 
 
 def sim_rank(rk, bounds, probe=False, K=10):
-    r = D.BandRenderer(scene, W, H, cfg, rk, N, FakeDist(), bounds=bounds)
+    r = D.BandRenderer(scene, W, H, cfg, rk, N, FakeDist(), bounds=bounds,
+                       frames_in_flight=int(os.environ.get("FIF", "1")))
     r.pass_path_tracing.set_uniform_int("pt_kernel", int(os.environ.get("PTK", "0")))
     for _ in range(3):
         r.frame()
     torch.cuda.synchronize()
     LOG.clear()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(K):
         r.frame()
