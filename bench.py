@@ -175,6 +175,9 @@ def main():
         torch.cuda.synchronize()
         per_pass = r.pass_times()
         r.profile(False)
+        # the roofline kernel alone: the last frame's 5 a-trous launches replayed back to back between two
+        # HIP events on the library's stream (per-draw events above include launch gaps)
+        per_pass["atrous_avg_ms"] = r.time_atrous(20)
         rows = r.rows_rendered() if hasattr(r, "rows_rendered") else H
         r.close() if hasattr(r, "close") else None
         return dt, per_pass, rows

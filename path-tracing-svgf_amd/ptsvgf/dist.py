@@ -163,6 +163,9 @@ class BandRenderer:
     def pass_times(self) -> dict:
         return self.r.pass_times()
 
+    def time_atrous(self, reps: int = 20) -> float:
+        return self.r.time_atrous(reps)
+
     def rows_rendered(self) -> int:
         return self.plan.y1 - self.plan.y0
 

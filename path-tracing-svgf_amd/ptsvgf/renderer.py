@@ -400,6 +400,7 @@ class Renderer:
             else:
                 prev_tex = None if not dests else self._atrous_tex(dests[-1])
                 dests.append("pong" if prev_tex == self.ping else "ping")
+        self._atrous_last = (g, [(dests[i], 1 << i) for i in range(n)], src)
         for i in range(n):
             self._halo(f"atrous{i}", [src])
             ap = self.atrous_to[dests[i]]
@@ -432,6 +433,35 @@ class Renderer:
             tp.set_uniform_uint("frameCounter", self.camera.frameCounter)
             self._draw(tp, "taa")
         self.final = self.taa[b] if self.run_taa else self.modulate_color
+
+    def time_atrous(self, reps: int = 20) -> float:
+        """Average duration (ms) of one a-trous launch: the last frame's iterations (same inputs, so the
+        replay rewrites the same bits) issued `reps` times back to back between two HIP events on the
+        library's stream, kernels alone on the GPU (everything in flight is drained first). Fast driver."""
+        import torch
+
+        g, iters, src0 = self._atrous_last
+        stream = self._back if self.K > 1 else torch.cuda.current_stream()
+        torch.cuda.synchronize()
+        _set_stream(stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+        def once():
+            src = src0
+            for key, step in iters:
+                ap = self.atrous_to[key]
+                ap.set_uniform_int("gStepSize", step)
+                ap.set_texture_uniform(GL_TEXTURE_2D, src, "gIllumination")
+                ap.draw()
+                src = self._atrous_tex(key)
+
+        once()  # warm
+        e0.record(stream)
+        for _ in range(reps):
+            once()
+        e1.record(stream)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / (reps * len(iters))
 
     def _halo(self, stage: str, handles) -> None:
         if self._halo_cb is None:

@@ -1,5 +1,6 @@
 #!/bin/bash
-# rocprofv3 passes for the 4K frame: kernel trace + stats, then separate PMC passes.
+# rocprofv3 passes for the 4K frame: kernel trace + stats, then separate PMC passes. One frame in flight, so
+# every kernel runs alone and its durations compare with the bench's serialised per-pass HIP-event timing.
 # usage: bash tools/gpu_profile.sh <tag>
 set -o pipefail
 TAG=${1:-r01}
@@ -7,7 +8,7 @@ R="$GRAFT_REPO_ROOT"
 OUT="$R/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-B="$R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-1080p"
+B="$R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-1080p --frames-in-flight 1"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $B > "$OUT/trace.log" 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $B > "$OUT/fetch.log" 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 $B > "$OUT/write.log" 2>&1 || exit $?
