@@ -37,6 +37,8 @@ typedef struct orc_scene orc_scene;
 orc_scene* orc_scene_create(const float* tri_enc, int ntris, const float* node_enc, int nnodes, const float* lights,
                             int nlights, const float* hdr_rgb, const float* cache_rgb, int hdr_w, int hdr_h);
 void orc_scene_destroy(orc_scene* s);
+/* material_array (main.cpp:184-205): RGBA8 texels, layer-major, rows of w texels; row 0 = GL t = 0. */
+int orc_scene_set_material_array(orc_scene* s, const uint8_t* rgba, int w, int h, int layers);
 
 typedef struct {
   uint32_t frameCounter;
@@ -48,6 +50,7 @@ typedef struct {
   int max_tracing_depth;
   int aspect_corrected; /* 0: reference (pix.x unscaled), 1: pix.x * width/height */
   int y_begin, y_end;   /* rows to compute */
+  int use_normal_map;   /* uniform use_normal_map (path_tracing.frag:338) */
 } orc_pt_params;
 
 /* path_tracing.frag main() (path_tracing.frag:1056-1128) for rows [y_begin, y_end).

@@ -60,6 +60,8 @@ const uint32_t SOBOL_V[8 * 32] = {
 struct orc_scene {
   std::vector<float> tri, node, light, hdr, cache;
   int ntris, nnodes, nlights, hdr_w, hdr_h;
+  std::vector<uint8_t> matarr;  // material_array: RGBA8, layers x mat_h x mat_w (main.cpp:184-205), may be empty
+  int mat_w = 0, mat_h = 0, mat_layers = 0;
 };
 
 namespace {
@@ -71,6 +73,7 @@ struct Shader {
   int width, height, hdrResolution, pointLightSize, max_tracing_depth;
   float clamp_threshold;
   bool accumulate;
+  bool use_normal_map;
   uint32_t seed;
   int px, py;  // uint((pix*0.5+0.5)*width): the integer pixel coordinate
 
@@ -182,23 +185,75 @@ struct Shader {
 
   static bool under_zero(v3 c) { return c.x < 0.0f || c.y < 0.0f || c.z < 0.0f; }
 
-  // :298-369 (the texture-array branch reads 0: no material array bound)
+  // texture2DArray(material_array, vec3(uv, layer)): RGBA8 UNORM (c/255), GL_LINEAR + GL_CLAMP_TO_EDGE with the
+  // shared bilinear addressing (glsl_builtins.h), one level, layer = clamp(floor(layer + 0.5)); the array
+  // unbound (no textures) reads 0.
+  void texArray(float u, float v, float layer, float out[4]) const {
+    if (s->matarr.empty()) { out[0] = out[1] = out[2] = out[3] = 0.0f; return; }
+    int l = clampi((int)f_floor(layer + 0.5f), 0, s->mat_layers - 1);
+    const int W = s->mat_w, H = s->mat_h;
+    const uint8_t* L = s->matarr.data() + (size_t)l * W * H * 4;
+    Bilin b = bilin_setup(u, v, W, H);
+    const uint8_t *p00 = L + ((size_t)b.y0 * W + b.x0) * 4, *p10 = L + ((size_t)b.y0 * W + b.x1) * 4;
+    const uint8_t *p01 = L + ((size_t)b.y1 * W + b.x0) * 4, *p11 = L + ((size_t)b.y1 * W + b.x1) * 4;
+    for (int c = 0; c < 4; ++c)
+      out[c] = bilin_mix(b, (float)p00[c] / 255.0f, (float)p10[c] / 255.0f, (float)p01[c] / 255.0f,
+                         (float)p11[c] / 255.0f);
+  }
+
+  // :298-369
   HitResult hitArray(const Ray& ray, int l, int r) const {
     HitResult res;
     res.isHit = false;
     res.distance = INF;
+    int nearest_tri_index = -1;
     for (int i = l; i <= r; ++i) {
       Triangle triangle = getTriangle(i);
       HitResult hr = hitTriangle(triangle, ray);
       if (hr.isHit && hr.distance < res.distance) {
         res = hr;
         res.material = getMaterial(i);
+        nearest_tri_index = i;
       }
     }
     if (res.isHit) {
-      if (under_zero(res.material.baseColor)) res.material.baseColor = splat(0.0f);
-      if (res.material.metallic < 0.0f) res.material.metallic = 0.0f;
-      if (res.material.roughness < 0.0f) res.material.roughness = 0.0f;
+      Triangle t = getTriangle(nearest_tri_index);
+      v3 p1 = t.p1, p2 = t.p2, p3 = t.p3, P = res.hitPoint;
+      float alpha = ((-(P.x - p2.x)) * (p3.y - p2.y) + (P.y - p2.y) * (p3.x - p2.x)) /
+                    ((-(p1.x - p2.x)) * (p3.y - p2.y) + (p1.y - p2.y) * (p3.x - p2.x) + 1e-7f);
+      float beta = ((-(P.x - p3.x)) * (p1.y - p3.y) + (P.y - p3.y) * (p1.x - p3.x)) /
+                   ((-(p2.x - p3.x)) * (p1.y - p3.y) + (p2.y - p3.y) * (p1.x - p3.x) + 1e-7f);
+      float gama = (1.0f - alpha) - beta;
+      float su = (alpha * t.uv1[0] + beta * t.uv2[0]) + gama * t.uv3[0];  // smooth_uv (:328)
+      float sv = (alpha * t.uv1[1] + beta * t.uv2[1]) + gama * t.uv3[1];
+      int mat_id = t.objIndex * 4;
+      float c[4];
+      if (under_zero(res.material.baseColor)) {
+        texArray(su, sv, (float)mat_id, c);
+        res.material.baseColor = mk(c[0], c[1], c[2]);
+      }
+      if (res.material.metallic < 0.0f) {
+        texArray(su, sv, (float)mat_id + 1.0f, c);
+        res.material.metallic = c[0];
+      }
+      if (use_normal_map) {  // :338-361
+        v3 edge1 = sub(p2, p1), edge2 = sub(p3, p1);
+        float dU1 = t.uv2[0] - t.uv1[0], dV1 = t.uv2[1] - t.uv1[1];
+        float dU2 = t.uv3[0] - t.uv1[0], dV2 = t.uv3[1] - t.uv1[1];
+        float f = 1.0f / (dU1 * dV2 - dU2 * dV1);
+        v3 tangent = mk(f * (dV2 * edge1.x - dV1 * edge2.x), f * (dV2 * edge1.y - dV1 * edge2.y),
+                        f * (dV2 * edge1.z - dV1 * edge2.z));
+        tangent = normalize(tangent);
+        v3 bitangent = cross(tangent, res.normal);
+        texArray(su, sv, (float)mat_id + 2.0f, c);
+        v3 tn = normalize(sub(muls(mk(c[0], c[1], c[2]), 2.0f), splat(1.0f)));
+        // mat3(tangent, bitangent, normal) * tn: columns weighted by tn's components
+        res.normal = normalize(add(add(muls(tangent, tn.x), muls(bitangent, tn.y)), muls(res.normal, tn.z)));
+      }
+      if (res.material.roughness < 0.0f) {
+        texArray(su, sv, (float)mat_id + 3.0f, c);
+        res.material.roughness = c[0];
+      }
     }
     return res;
   }
@@ -507,6 +562,15 @@ orc_scene* orc_scene_create(const float* tri, int ntris, const float* node, int 
 }
 void orc_scene_destroy(orc_scene* s) { delete s; }
 
+int orc_scene_set_material_array(orc_scene* s, const uint8_t* rgba, int w, int h, int layers) {
+  if (!s || w <= 0 || h <= 0 || layers <= 0 || !rgba) return -1;
+  s->matarr.assign(rgba, rgba + (size_t)w * h * layers * 4);
+  s->mat_w = w;
+  s->mat_h = h;
+  s->mat_layers = layers;
+  return 0;
+}
+
 int orc_path_trace(const orc_scene* s, const orc_pt_params* p, const float* last_frame, float* out_color,
                    float* out_emission, float* out_albedo, int threads) {
   const int W = p->width, H = p->height;
@@ -524,6 +588,7 @@ int orc_path_trace(const orc_scene* s, const orc_pt_params* p, const float* last
       sh.max_tracing_depth = p->max_tracing_depth;
       sh.clamp_threshold = p->clamp_threshold;
       sh.accumulate = p->accumulate != 0;
+      sh.use_normal_map = p->use_normal_map != 0;
       sh.px = x;
       sh.py = y;
       sh.seed = ((uint32_t)x * 1973u + (uint32_t)y * 9277u + p->frameCounter * 26699u) | 1u;  // :433-436

@@ -564,6 +564,15 @@ int draw_pathtrace(Pass* p) {
     k.scene.lights = (const float*)lt->dev;
     k.scene.nlights_buf = (int)(lt->bytes / (6 * sizeof(float)));
   }
+  // uniform sampler2DArray material_array (path_tracing.frag:331-364); unbound -> fetches read 0
+  Texture* ma = sampler(p, "material_array");
+  if (ma && ma->target == PT_TEXTURE_2D_ARRAY && ma->dev) {
+    k.scene.texarr = (const uint32_t*)ma->dev;
+    k.scene.tex_w = ma->W;
+    k.scene.tex_h = ma->H;
+    k.scene.tex_layers = ma->layers;
+  }
+  k.scene.use_normal_map = ui(p, "use_normal_map", 0);
   Texture* hm = sampler(p, "hdrMap");
   Texture* hc = sampler(p, "hdrCache");
   if (!hm || !hc || !hm->dev || !hc->dev) return err(PT_ERR_MISSING_TEXTURE, "path_tracing needs hdrMap and hdrCache");

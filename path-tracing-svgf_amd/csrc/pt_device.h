@@ -79,6 +79,10 @@ struct SceneDev {
   int ntris;
   const float* lights;  // 6 floats per light (PointLight: position, radiance)
   int nlights_buf;      // lights actually present in the buffer
+  // material_array (main.cpp:184-205): RGBA8 2-D array, layer-major rows of tex_w texels, may be null
+  const uint32_t* texarr;
+  int tex_w, tex_h, tex_layers;
+  int use_normal_map;   // uniform use_normal_map (path_tracing.frag:338)
 };
 
 // Wavefront path-tracer state (kernels_wavefront.hip): SoA per band pixel.

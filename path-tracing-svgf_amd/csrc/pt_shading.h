@@ -336,6 +336,23 @@ struct Hit {
   Mat m;
 };
 
+// texture2DArray(material_array, vec3(u, v, layer)) (:331-364): RGBA8 UNORM texels (c / 255), GL_LINEAR,
+// GL_CLAMP_TO_EDGE, one level (main.cpp:186-195), the layer rounded and clamped as GL does; the shared
+// bilinear addressing of glsl_builtins.h. With no array bound the fetch reads 0.
+__device__ __forceinline__ float unorm8(uint32_t t, int c) { return (float)((t >> (8 * c)) & 255u) / 255.0f; }
+__device__ __forceinline__ void tex_array(const SceneDev& sc, float u, float v, int layer, float* out) {
+  if (!sc.texarr) {
+    out[0] = out[1] = out[2] = out[3] = 0.0f;
+    return;
+  }
+  layer = clampi(layer, 0, sc.tex_layers - 1);
+  const Bilin b = bilin_setup(u, v, sc.tex_w, sc.tex_h);
+  const uint32_t* L = sc.texarr + (size_t)layer * sc.tex_w * sc.tex_h;
+  const uint32_t t00 = L[(size_t)b.y0 * sc.tex_w + b.x0], t10 = L[(size_t)b.y0 * sc.tex_w + b.x1];
+  const uint32_t t01 = L[(size_t)b.y1 * sc.tex_w + b.x0], t11 = L[(size_t)b.y1 * sc.tex_w + b.x1];
+  for (int c = 0; c < 4; ++c) out[c] = bilin_mix(b, unorm8(t00, c), unorm8(t10, c), unorm8(t01, c), unorm8(t11, c));
+}
+
 // Decode the closest hit (hitTriangle :243-268 normal; hitArray :315-366 material).
 __device__ Hit decode_hit(const SceneDev& sc, int i, float t, v3 S, v3 d) {
   Hit h;
@@ -367,10 +384,39 @@ __device__ Hit decode_hit(const SceneDev& sc, int i, float t, v3 S, v3 d) {
   h.m.sheenTint = r5.z;
   h.m.clearcoat = r5.w;
   h.m.clearcoatGloss = r6.x;
-  // texture-array branch (:331-364): no material array bound -> the fetch reads 0
-  if (h.m.baseColor.x < 0.0f || h.m.baseColor.y < 0.0f || h.m.baseColor.z < 0.0f) h.m.baseColor = splat(0.0f);
-  if (h.m.metallic < 0.0f) h.m.metallic = 0.0f;
-  if (h.m.roughness < 0.0f) h.m.roughness = 0.0f;
+  // texture-array branch (:315-364) of the closest hit (hitArray applies it per leaf to the leaf's closest
+  // triangle; hitBVH compares distances only, so applying it once to the global closest is the same)
+  const float4 r7 = r[7], r8 = r[8];
+  const float u = (alpha * r7.x + beta * r7.z) + gama * r8.x;  // smooth_uv (:328), uv1 uv2 uv3
+  const float v = (alpha * r7.y + beta * r7.w) + gama * r8.y;
+  const int mat_id = (int)r6.w * 4;                           // objIndex * 4 (:330)
+  if (h.m.baseColor.x < 0.0f || h.m.baseColor.y < 0.0f || h.m.baseColor.z < 0.0f) {
+    float c[4];
+    tex_array(sc, u, v, mat_id, c);
+    h.m.baseColor = mk(c[0], c[1], c[2]);
+  }
+  if (h.m.metallic < 0.0f) {
+    float c[4];
+    tex_array(sc, u, v, mat_id + 1, c);
+    h.m.metallic = c[0];
+  }
+  if (sc.use_normal_map) {  // :338-361, TBN from the triangle's edges and uv deltas
+    v3 edge1 = sub(p2, p1), edge2 = sub(p3, p1);
+    float du1 = r7.z - r7.x, dv1 = r7.w - r7.y, du2 = r8.x - r7.x, dv2 = r8.y - r7.y;
+    float f = 1.0f / (du1 * dv2 - du2 * dv1);
+    v3 tangent = normalize(mk(f * (dv2 * edge1.x - dv1 * edge2.x), f * (dv2 * edge1.y - dv1 * edge2.y),
+                              f * (dv2 * edge1.z - dv1 * edge2.z)));
+    v3 bitangent = cross(tangent, h.normal);
+    float c[4];
+    tex_array(sc, u, v, mat_id + 2, c);
+    v3 tn = normalize(sub(muls(mk(c[0], c[1], c[2]), 2.0f), splat(1.0f)));
+    h.normal = normalize(add(add(muls(tangent, tn.x), muls(bitangent, tn.y)), muls(h.normal, tn.z)));
+  }
+  if (h.m.roughness < 0.0f) {
+    float c[4];
+    tex_array(sc, u, v, mat_id + 3, c);
+    h.m.roughness = c[0];
+  }
   return h;
 }
 

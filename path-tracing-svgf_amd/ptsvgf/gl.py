@@ -90,6 +90,18 @@ def texture_buffer(data: np.ndarray) -> int:
     return h.value
 
 
+def texture_array(layers: np.ndarray) -> int:
+    """main.cpp:184-205: glTexStorage3D(GL_TEXTURE_2D_ARRAY, 1, GL_RGBA8, w, h, n) + one glTexSubImage3D per layer
+    (help_func.h:4-20). `layers` is (n, h, w, 3|4) uint8, rows already in GL order (stbi flipped on load)."""
+    a = np.ascontiguousarray(layers, dtype=np.uint8)
+    n, hh, ww, ch = a.shape
+    h = C.c_uint32()
+    check(pt().pt_texarray_create(ww, hh, n, C.byref(h)))
+    for i in range(n):
+        check(pt().pt_texarray_upload_layer(h.value, i, ww, hh, ch, a[i].ctypes.data_as(C.POINTER(C.c_uint8))))
+    return h.value
+
+
 def texture_info(tex: int):
     w, h, r0 = C.c_int(), C.c_int(), C.c_int()
     check(pt().pt_texture_info(tex, C.byref(w), C.byref(h), C.byref(r0)))

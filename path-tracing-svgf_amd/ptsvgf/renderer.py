@@ -20,7 +20,7 @@ import numpy as np
 
 from . import gl
 from .camera import Camera, mat_mul, parameter_config, rigid_inverse
-from .gl import GL_TEXTURE_2D, GL_TEXTURE_BUFFER, RenderPass, Rasterize_RenderPass, getShaderProgram, getTextureRGB32F
+from .gl import GL_TEXTURE_2D, GL_TEXTURE_2D_ARRAY, GL_TEXTURE_BUFFER, RenderPass, Rasterize_RenderPass, getShaderProgram, getTextureRGB32F
 from .scene import Scene
 
 SHADERS = "./shaders/"
@@ -109,6 +109,10 @@ class Renderer:
         gl.upload_rgb32f(self.hdrCache, scene.cache)
         self._owned += [self.trianglesTextureBuffer, self.nodesTextureBuffer, self.pointLightBuffer, self.hdrMap,
                         self.hdrCache]
+        self.materials_array = None                            # main.cpp:184-205
+        if getattr(scene, "textures", None) is not None:
+            self.materials_array = gl.texture_array(scene.textures)
+            self._owned.append(self.materials_array)
         self.hdrResolution = hw
 
         self.K = int(frames_in_flight)
@@ -263,6 +267,8 @@ class Renderer:
         if cfg.accumulate_color:
             last_acc = self.last_acc_color if self.mode == "reference" else self.acc[1 - b]
             pt.set_texture_uniform(GL_TEXTURE_2D, last_acc, "lastFrame")
+        if self.materials_array is not None:
+            pt.set_texture_uniform(GL_TEXTURE_2D_ARRAY, self.materials_array, "material_array")
         pt.set_texture_uniform(GL_TEXTURE_2D, self.hdrMap, "hdrMap")
         pt.set_texture_uniform(GL_TEXTURE_2D, self.hdrCache, "hdrCache")
         pt.set_texture_uniform(GL_TEXTURE_BUFFER, self.pointLightBuffer, "pointLights")

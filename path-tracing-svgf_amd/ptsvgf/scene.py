@@ -55,6 +55,7 @@ class Scene:
     hdr: np.ndarray            # (h, w, 3)
     cache: np.ndarray          # (h, w, 3)
     counts: dict = field(default_factory=dict)
+    textures: np.ndarray | None = None  # material_array (layers, h, w, 4) uint8, or None (no texture path)
 
     @property
     def ntris(self) -> int:
@@ -80,11 +81,13 @@ class SceneBuilder:
         check_host(pts().pts_scene_add_obj(self._s, path.encode(), fptr(mat), fptr(trans), int(smooth), obj_index))
 
     def add_mesh(self, positions: np.ndarray, indices: np.ndarray, mat: np.ndarray, trans: np.ndarray,
-                 smooth: bool = True, obj_index: int = 0):
+                 smooth: bool = True, obj_index: int = 0, uvs: np.ndarray | None = None):
         p = np.ascontiguousarray(positions, np.float32).reshape(-1)
         i = np.ascontiguousarray(indices, np.int32).reshape(-1)
-        check_host(pts().pts_scene_add_mesh(self._s, fptr(p), None, p.size // 3, i.ctypes.data_as(C.POINTER(C.c_int)),
-                                            i.size // 3, fptr(mat), fptr(trans), int(smooth), obj_index))
+        u = None if uvs is None else np.ascontiguousarray(uvs, np.float32).reshape(-1)
+        check_host(pts().pts_scene_add_mesh(self._s, fptr(p), None if u is None else fptr(u), p.size // 3,
+                                            i.ctypes.data_as(C.POINTER(C.c_int)), i.size // 3, fptr(mat), fptr(trans),
+                                            int(smooth), obj_index))
 
     def build(self, leaf_n: int = 8):
         check_host(pts().pts_scene_build_bvh(self._s, leaf_n))
@@ -143,12 +146,37 @@ def hdr_cache(hdr: np.ndarray) -> np.ndarray:
     return out
 
 
+def material_layers(size: int = 256, image: int = 192, objects: int = 3, seed: int = 0) -> np.ndarray:
+    """Synthetic stand-in for the reference's Textures/*.bmp (all absent): per object index o, layers 4o..4o+3 =
+    albedo, metallic, normal, roughness (main.cpp:196-205 order), each an `image`-texel square uploaded at the
+    origin of a `size`-texel layer — the reference's sub-rectangle upload into its 4096^2 array, so uv in [0, 1]
+    also samples the unwritten (zero) texels beyond the image (help_func.h:12). Seeded, deterministic."""
+    rng = np.random.default_rng(seed)
+    out = np.zeros((4 * objects, size, size, 4), np.uint8)
+    yy, xx = np.mgrid[0:image, 0:image].astype(np.float32) / image
+    for o in range(objects):
+        f = 4.0 + 3.0 * o
+        check = ((np.floor(xx * f) + np.floor(yy * f)) % 2).astype(np.float32)
+        base = rng.uniform(0.2, 0.9, 3).astype(np.float32)
+        alb = np.stack([base[c] * (0.55 + 0.45 * check) for c in range(3)], -1)
+        out[4 * o, :image, :image, :3] = np.round(alb * 255)
+        out[4 * o + 1, :image, :image, 0] = np.round((0.5 + 0.5 * np.sin(6.28 * xx * (o + 1))) * 255)
+        nx, ny = 0.35 * np.sin(6.28 * xx * f), 0.35 * np.cos(6.28 * yy * f)
+        nz = np.sqrt(np.maximum(0.0, 1.0 - nx * nx - ny * ny))
+        out[4 * o + 2, :image, :image, :3] = np.round((np.stack([nx, ny, nz], -1) * 0.5 + 0.5) * 255)
+        out[4 * o + 3, :image, :image, 0] = np.round((0.2 + 0.6 * yy) * 255)
+        out[4 * o:4 * o + 4, :image, :image, 3] = 255
+    return out
+
+
 def build_scene(name: str = "table_clock_plant", hdr_size=(2048, 1024), plant_leaves: int = 150) -> Scene:
     """Named scenes of BASELINE.json's configs.
 
     ``clock``               main.cpp:72-80 (textures absent -> constant brass material)
     ``table_clock_plant``   configs[1..4]: table + clock + synthetic plant (+ synthetic room.hdr)
     ``cornell_teapot``      configs[0]: Cornell-style box + synthetic teapot stand-in
+    ``textured``            table + clock with the texture path: negative baseColor / metallic / roughness
+                            select material_array layers objIndex*4 + {0, 1, 3} (path_tracing.frag:331-364)
     """
     b = SceneBuilder()
     clock = os.path.join(ASSETS, "clock.obj")
@@ -172,9 +200,15 @@ def build_scene(name: str = "table_clock_plant", hdr_size=(2048, 1024), plant_le
         b.add_mesh(cpos, cidx, white, transform(), False, 0)
         tpos, tidx = gen_teapot(48)
         b.add_mesh(tpos, tidx, china, transform(trans=(0.0, -1.0, 0.0), scale=(0.9, 0.9, 0.9)), True, 1)
+    elif name == "textured":
+        textured = material(baseColor=(-1.0, -1.0, -1.0), metallic=-1.0, roughness=-1.0, specular=0.5)
+        half = material(baseColor=(0.6, 0.6, 0.6), metallic=-1.0, roughness=0.4)  # texture on one param only
+        b.add_obj(table, half, transform(trans=(0.176, -0.73, -0.16), scale=(3.84, 3.84, 3.84)), True, 0)
+        b.add_obj(clock, textured, transform(trans=(-0.914, -0.155, -1.03), scale=(1.12, 1.12, 1.12)), True, 1)
     else:
         raise ValueError(f"unknown scene {name!r}")
     b.build(8)
     tri, node, raster = b.encode()
     hdr = env_map(*hdr_size)
-    return Scene(name, tri, node, raster, POINT_LIGHTS.copy(), hdr, hdr_cache(hdr), b.counts())
+    tex = material_layers() if name == "textured" else None
+    return Scene(name, tri, node, raster, POINT_LIGHTS.copy(), hdr, hdr_cache(hdr), b.counts(), tex)

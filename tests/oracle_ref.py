@@ -23,7 +23,7 @@ class PTParams(C.Structure):
     _fields_ = [("frameCounter", C.c_uint32), ("width", C.c_int), ("height", C.c_int), ("eye", C.c_float * 3),
                 ("cameraRotate", C.c_float * 16), ("accumulate", C.c_int), ("clamp_threshold", C.c_float),
                 ("max_tracing_depth", C.c_int), ("aspect_corrected", C.c_int), ("y_begin", C.c_int),
-                ("y_end", C.c_int)]
+                ("y_end", C.c_int), ("use_normal_map", C.c_int)]
 
 
 def lib() -> C.CDLL:
@@ -35,6 +35,7 @@ def lib() -> C.CDLL:
         L.orc_scene_create.restype = C.c_void_p
         L.orc_scene_create.argtypes = [_fp, C.c_int, _fp, C.c_int, _fp, C.c_int, _fp, _fp, C.c_int, C.c_int]
         L.orc_scene_destroy.argtypes = [C.c_void_p]
+        L.orc_scene_set_material_array.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
         L.orc_path_trace.argtypes = [C.c_void_p, C.POINTER(PTParams), _fp, _fp, _fp, _fp, C.c_int]
         L.orc_gbuffer.argtypes = [_fp, C.c_int, C.c_int, C.c_int, _fp, _fp, _fp, _fp, _fp, _fp, _fp, C.c_int]
         L.orc_reproject.argtypes = [C.c_int, C.c_int] + [_fp] * 9 + [C.c_float] * 4 + [_fp, _fp, C.c_int]
@@ -83,6 +84,12 @@ class OracleScene:
         t, n, l, h, c = self._keep
         self.h = lib().orc_scene_create(fp(t), t.shape[0], fp(n), n.shape[0], fp(l), l.shape[0], fp(h), fp(c),
                                         h.shape[1], h.shape[0])
+        tex = getattr(scene, "textures", None)
+        if tex is not None:  # (layers, h, w, 4) uint8 material_array
+            tex = np.ascontiguousarray(tex, np.uint8)
+            self._keep.append(tex)
+            assert lib().orc_scene_set_material_array(self.h, tex.ctypes.data, tex.shape[2], tex.shape[1],
+                                                      tex.shape[0]) == 0
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -90,7 +97,8 @@ class OracleScene:
             self.h = None
 
     def path_trace(self, W, H, frameCounter, eye, cameraRotate, clamp_threshold=10.0, max_depth=2,
-                   aspect_corrected=False, accumulate=False, last_frame=None, rows=None, threads=THREADS):
+                   aspect_corrected=False, accumulate=False, last_frame=None, rows=None, threads=THREADS,
+                   use_normal_map=False):
         p = PTParams()
         p.frameCounter = frameCounter & 0xFFFFFFFF
         p.width, p.height = W, H
@@ -101,6 +109,7 @@ class OracleScene:
         p.max_tracing_depth = max_depth
         p.aspect_corrected = int(aspect_corrected)
         p.y_begin, p.y_end = rows if rows else (0, H)
+        p.use_normal_map = int(use_normal_map)
         col, em, al = frame(H, W), frame(H, W), frame(H, W)
         lf = f32(last_frame) if last_frame is not None else None
         rc = lib().orc_path_trace(self.h, C.byref(p), fp(lf) if lf is not None else None, fp(col), fp(em), fp(al),
@@ -195,7 +204,7 @@ class OracleFrameLoop:
         g = gbuffer(self.scene.raster, W, H, view, proj, self.pre_viewproj, self.threads)
         col, em, al = self.os.path_trace(W, H, cam.frameCounter, cam.cam_position, rigid_inverse(view),
                                          cfg.clamp_threshold, cfg.max_tracing_depth, self.aspect_corrected,
-                                         threads=self.threads)
+                                         threads=self.threads, use_normal_map=cfg.use_normal_texture)
         ri, rm = reproject(g["velocity"], col, al, em, self.prev_illum, self.prev_moments, g["normal_depth"],
                            self.prev_nd, g["fwidth"], np.float32(1.0 / W), np.float32(1.0 / H),
                            cfg.reproj_depth_threshold, cfg.reproj_normal_threshold, self.threads)

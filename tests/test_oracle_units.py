@@ -179,3 +179,76 @@ def test_taa_oracle_properties():
     # blend factor 0.05 with zero velocity: the result sits between the clipped history and the current colour
     lo = np.minimum(cur, prev)[3:, :, :3] - 1e-3
     assert np.isfinite(out1).all() and (out1[3:, :, :3] >= lo.min()).all()
+
+
+def _quad_scene(mat, obj_index, textures):
+    """One camera-facing quad (z = 0, [-1, 1]^2, uv = xy in [0, 1]) with the given material and material_array."""
+    from ptsvgf.scene import POINT_LIGHTS, Scene, SceneBuilder, env_map, hdr_cache, transform
+
+    b = SceneBuilder()
+    pos = np.array([[-1, -1, 0], [1, -1, 0], [1, 1, 0], [-1, 1, 0]], np.float32)
+    uv = (pos[:, :2] + 1.0) * 0.5
+    b.add_mesh(pos, np.array([[0, 1, 2], [0, 2, 3]], np.int32), mat, transform(), False, obj_index, uvs=uv)
+    b.build(8)
+    tri, node, raster = b.encode()
+    hdr = env_map(64, 32)
+    return Scene("quad", tri, node, raster, POINT_LIGHTS.copy(), hdr, hdr_cache(hdr), b.counts(), textures)
+
+
+def _quad_albedo(scene, W=24, H=24):
+    from ptsvgf.camera import Camera, rigid_inverse
+
+    cam = Camera(W, H)
+    cam.update()
+    col, em, al = O.OracleScene(scene).path_trace(W, H, 0, cam.cam_position, rigid_inverse(cam.cam_view_mat),
+                                                  max_depth=1, threads=4)
+    return al
+
+
+def test_texture_array_branch_known_answers():
+    """hitArray's texture branch (path_tracing.frag:315-364): a negative baseColor reads layer objIndex*4 of the
+    RGBA8 material_array as c / 255; a constant layer gives that colour (to 2 ulp) wherever the quad is hit, the
+    layer index follows objIndex, and with no array bound the fetch reads 0."""
+    from ptsvgf.scene import material
+
+    tex = np.zeros((8, 16, 16, 4), np.uint8)
+    tex[4, :, :, :3] = (51, 102, 204)  # objIndex 1 -> layer 4 (albedo)
+    tex[0, :, :, :3] = (255, 0, 0)     # objIndex 0's albedo layer: must not be read
+    neg = material(baseColor=(-1.0, -1.0, -1.0))
+    al = _quad_albedo(_quad_scene(neg, 1, tex))
+    hit = al[..., 3] == 1.0
+    lit = np.any(al[..., :3] != 0.0, axis=-1)
+    assert lit.sum() > 100
+    want = np.array([51, 102, 204], np.float32) / np.float32(255.0)
+    # bilinear mixing of four equal texels, c*(1-a) + c*a, is exact up to float32 rounding (2 ulp)
+    assert np.allclose(al[lit][:, :3], want, rtol=3e-7, atol=0)
+    al0 = _quad_albedo(_quad_scene(neg, 1, None))  # no array bound: the fetch reads 0
+    assert not np.any(al0[..., :3] != 0.0) and hit.any()
+    pos = material(baseColor=(0.25, 0.5, 0.75))    # non-negative: the texture is never read
+    alp = _quad_albedo(_quad_scene(pos, 1, tex))
+    assert np.allclose(alp[lit][:, :3], [0.25, 0.5, 0.75])
+
+
+def test_texture_array_bilinear_and_subrect_quirk():
+    """GL_LINEAR + CLAMP_TO_EDGE on the RGBA8 layer, sampled at the quad's smooth uv (uv = (x+1)/2, (y+1)/2): a
+    red ramp image occupying only the left half of the layer (the reference uploads each image at the origin of
+    a larger layer, help_func.h:12). Left of the quad's centre line every hit reads the image (green = 1/255,
+    red non-decreasing along the row, within the ramp's range); right of it the fetch reads the unwritten zero
+    texels in every channel."""
+    from ptsvgf.scene import material
+
+    S, W = 32, 40
+    tex = np.zeros((4, S, S, 4), np.uint8)
+    tex[0, :, :S // 2, 0] = np.arange(S // 2, dtype=np.uint8)[None, :] * 16   # red ramp, left half only
+    tex[0, :, :S // 2, 1:3] = 1
+    al = _quad_albedo(_quad_scene(material(baseColor=(-1.0, -1.0, -1.0)), 0, tex), W=W, H=W)
+    quad = np.abs(al[..., 2] - 1.0 / 255.0) < 1e-7  # blue = 1/255 exactly only where the image is read
+    rows = [y for y in range(W) if quad[y].sum() > 4]
+    assert len(rows) > 10
+    for y in rows:
+        xs = np.nonzero(quad[y])[0]
+        assert xs.max() < W // 2 + 1                       # the image ends at the quad's centre line (uv.x = 0.5)
+        red = al[y, xs, 0]
+        assert np.all(np.diff(red) >= 0) and red.max() <= 240 / 255.0 + 1e-6 and red.min() >= 0.0
+        right = al[y, W // 2 + 2:, :3]
+        assert not np.any(right != 0.0)                    # beyond the image: zero texels (or sky misses)
