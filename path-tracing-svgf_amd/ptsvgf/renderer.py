@@ -70,8 +70,6 @@ class Renderer:
         from camera to finished frame is up to K frames."""
         if mode not in ("fast", "reference"):
             raise ValueError(mode)
-        if mode == "fast" and config is not None and config.accumulate_color:
-            raise NotImplementedError("accumulate mode runs through mode='reference' (SURVEY.md §8(f) item 3)")
         self.mode = mode
         self.W, self.H = int(width), int(height)
         self.cfg = config or parameter_config()
@@ -139,8 +137,13 @@ class Renderer:
 
         # path tracer (main.cpp:229-248)
         # (one pass + output set per frame in flight: each owns its wavefront state)
+        # accumulate mode (path_tracing.frag:1116-1119) reads the previous frame's colour: the fast driver keeps
+        # at least two slots so lastFrame is the other slot's colour output (the reference copies it,
+        # save_frame_data.frag), and with frames in flight each front end then waits for the previous one
+        self.accumulate = bool(self.cfg.accumulate_color)
+        nslots = max(self.K, 2) if (self.accumulate and mode == "fast") else self.K
         self.pt_slots = []
-        for _ in range(self.K):
+        for _ in range(nslots):
             p = RenderPass(_prog("path_tracing.frag"), W, H)
             outs = (tex(W, H), tex(W, H), tex(W, H))  # color, emission, albedo
             p.colorAttachments += list(outs)
@@ -162,6 +165,7 @@ class Renderer:
             self._streams = [torch.cuda.Stream() for _ in range(self.K)]
             self._back = torch.cuda.Stream()
             self._slot_free = [None] * self.K  # event: SVGF of the frame that last used the slot is done
+            self._fe_prev = None
 
         # SVGF targets
         if mode == "reference":
@@ -221,7 +225,6 @@ class Renderer:
         self.ping, self.pong = tex(W, H), tex(W, H)
         self.modulate_color = tex(W, H)
         self.taa = [tex(W, H), tex(W, H)]
-        self.acc = [tex(W, H), tex(W, H)] if self.cfg.accumulate_color else None
         self.reproject = [self._svgf_pass("svgf_reproject.frag", [self.illum, self.moments[b]]) for b in (0, 1)]
         self.variance_compute_pass = self._svgf_pass("svgf_variance.frag", [self.var_out])
         self.atrous_to = {"ping": self._svgf_pass("svgf_Atrous.frag", [self.ping]),
@@ -265,7 +268,8 @@ class Renderer:
         pt.set_texture_uniform(GL_TEXTURE_BUFFER, self.trianglesTextureBuffer, "triangles")
         pt.set_texture_uniform(GL_TEXTURE_BUFFER, self.nodesTextureBuffer, "nodes")
         if cfg.accumulate_color:
-            last_acc = self.last_acc_color if self.mode == "reference" else self.acc[1 - b]
+            last_acc = (self.last_acc_color if self.mode == "reference"
+                        else self.pt_slots[(self.frame_index - 1) % len(self.pt_slots)][1][0])
             pt.set_texture_uniform(GL_TEXTURE_2D, last_acc, "lastFrame")
         if self.materials_array is not None:
             pt.set_texture_uniform(GL_TEXTURE_2D_ARRAY, self.materials_array, "material_array")
@@ -353,18 +357,21 @@ class Renderer:
         pb = 1 - b
         ng = len(self.gbuf)
         g, gp = self.gbuf[f % ng], self.gbuf[(f - 1) % ng]
-        s = f % self.K
+        s = f % len(self.pt_slots)
         self._use_slot(s)
         if self.K > 1:                                         # front end on stream s, after SVGF(f - K)
             import torch
 
-            fe = self._streams[s]
-            if self._slot_free[s] is not None:
-                fe.wait_event(self._slot_free[s])
+            fe = self._streams[f % self.K]
+            if self._slot_free[f % self.K] is not None:
+                fe.wait_event(self._slot_free[f % self.K])
+            if self.accumulate and self._fe_prev is not None:  # lastFrame = the previous front end's colour
+                fe.wait_event(self._fe_prev)
             _set_stream(fe)
             self._gbuffer_and_pt(f % ng)
             done = torch.cuda.Event()
             done.record(fe)
+            self._fe_prev = done
             self._back.wait_event(done)
             _set_stream(self._back)
         else:

@@ -193,6 +193,31 @@ def test_fast_driver_equals_reference_driver(gpu, scene_small):
             assert np.array_equal(pa[key], pb[key]), (f, key)
 
 
+@pytest.mark.parametrize("K", [1, 2])
+def test_accumulate_fast_equals_reference(gpu, scene_small, K):
+    """Accumulate mode (path_tracing.frag:1116-1119, lastFrame = last frame's colour): the fast driver's slot
+    alternation (and, with frames in flight, front ends chained on the previous colour) gives the reference
+    driver's bits, through static frames (running mean) and a camera move (frameCounter reset, camera.h:71)."""
+    from ptsvgf.camera import parameter_config
+
+    gl = gpu
+    cfg = parameter_config()
+    cfg.accumulate_color = True
+    W, H = 64, 48
+    a = _renderer(scene_small, W, H, config=cfg, mode="reference", run_taa=True, run_output=True)
+    b = _renderer(scene_small, W, H, config=cfg, mode="fast", run_taa=True, run_output=True, frames_in_flight=K)
+    for f in range(5):
+        for r in (a, b):
+            if f == 3:
+                r.camera.orbit(1.0, 0.0)
+            r.frame()
+        pa, pb = _readback(gl, a), _readback(gl, b)
+        for key in ("color", "modulate", "final", "output"):
+            assert np.array_equal(pa[key].view(np.uint32), pb[key].view(np.uint32)), (f, key)
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("K", [2, 3])
 def test_frames_in_flight_equal_serial(gpu, scene_small, K):
     """K frames in flight (front ends on K streams, SVGF chain on a back-end stream) give the serial fast
