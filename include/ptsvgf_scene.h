@@ -81,6 +81,14 @@ void pts_transform_matrix(const float* rot3_deg, const float* trans3, const floa
  * R = sample x, G = sample y, B = pdf (hdr_compute.h:277-283). */
 int pts_hdr_cache(const float* hdr_rgb, int width, int height, float* cache_out);
 
+/* HDRLoader::load (lib/hdrloader.cpp:28-97): Radiance RGBE file -> RGB32F rows, file scanline order (the
+ * first scanline in the file is row 0, as the reference stores it), components (v / 256) * 2^(E - 128).
+ * Call with rgb_out == NULL to get the size, then with a w*h*3 buffer. Differences, all on malformed input
+ * only: the resolution is read into long and narrowed (the reference's "%ld" into int is undefined on LP64,
+ * hdrloader.cpp:68), run lengths are bounds-checked, and a truncated file is an error instead of a
+ * partially uninitialised image. */
+int pts_load_hdr(const char* path, int* width, int* height, float* rgb_out);
+
 /* ------------------------------------------------ synthetic stand-ins ---- */
 /* Seeded procedural potted plant (stand-in for models/plant.obj): writes
  * positions/indices into caller buffers when non-NULL; returns counts. */

@@ -705,6 +705,132 @@ int pts_gen_cornell(int* nv, int* nt, float* positions, int* indices) {
   return mesh_result(m, nv, nt, positions, indices);
 }
 
+// ------------------------------------------------------------- RGBE ---
+namespace {
+typedef unsigned char Rgbe[4];
+// decrunch / oldDecrunch (hdrloader.cpp:123-197) over a byte cursor; false = truncated or malformed
+struct Bytes {
+  const std::vector<unsigned char>& b;
+  size_t i;
+  int get() { return i < b.size() ? b[i++] : -1; }
+};
+bool old_decrunch(Rgbe* scan, int len, Bytes& f, Rgbe* first) {
+  int rshift = 0;
+  while (len > 0) {
+    int c[4];
+    for (int k = 0; k < 4; ++k) c[k] = f.get();
+    if (c[3] < 0) return false;  // feof
+    for (int k = 0; k < 4; ++k) scan[0][k] = (unsigned char)c[k];
+    if (scan[0][0] == 1 && scan[0][1] == 1 && scan[0][2] == 1) {  // repeat the previous pixel
+      if (scan == first) return false;                            // nothing before it
+      for (int i = scan[0][3] << rshift; i > 0; --i) {
+        if (len <= 0) return false;
+        memcpy(&scan[0][0], &scan[-1][0], 4);
+        ++scan;
+        --len;
+      }
+      rshift += 8;
+    } else {
+      ++scan;
+      --len;
+      rshift = 0;
+    }
+  }
+  return true;
+}
+bool decrunch(Rgbe* scan, int len, Bytes& f) {
+  if (len < 8 || len > 0x7fff) return old_decrunch(scan, len, f, scan);
+  size_t mark = f.i;
+  int i = f.get();
+  if (i != 2) {
+    f.i = mark;  // fseek(file, -1, SEEK_CUR)
+    return old_decrunch(scan, len, f, scan);
+  }
+  int g = f.get(), b = f.get();
+  i = f.get();
+  if (i < 0) return false;
+  scan[0][1] = (unsigned char)g;
+  scan[0][2] = (unsigned char)b;
+  if (scan[0][1] != 2 || (scan[0][2] & 128)) {
+    scan[0][0] = 2;
+    scan[0][3] = (unsigned char)i;
+    return old_decrunch(scan + 1, len - 1, f, scan);
+  }
+  for (int c = 0; c < 4; ++c) {
+    for (int j = 0; j < len;) {
+      int code = f.get();
+      if (code < 0) return false;
+      if (code > 128) {  // run
+        code &= 127;
+        int val = f.get();
+        if (val < 0 || j + code > len) return false;
+        while (code--) scan[j++][c] = (unsigned char)val;
+      } else {           // literal
+        if (j + code > len) return false;
+        while (code--) {
+          int v = f.get();
+          if (v < 0) return false;
+          scan[j++][c] = (unsigned char)v;
+        }
+      }
+    }
+  }
+  return true;
+}
+float rgbe_component(int expo, int val) {  // convertComponent (hdrloader.cpp:101-106)
+  float v = val / 256.0f;
+  float d = (float)pow(2.0, (double)expo);
+  return v * d;
+}
+}  // namespace
+
+int pts_load_hdr(const char* path, int* width, int* height, float* rgb_out) {
+  if (!path || !width || !height) return fail("pts_load_hdr: bad argument");
+  FILE* fp = fopen(path, "rb");
+  if (!fp) return fail(std::string("pts_load_hdr: cannot open ") + path);
+  std::vector<unsigned char> buf;
+  unsigned char chunk[65536];
+  size_t n;
+  while ((n = fread(chunk, 1, sizeof(chunk), fp)) > 0) buf.insert(buf.end(), chunk, chunk + n);
+  fclose(fp);
+  if (buf.size() < 11 || memcmp(buf.data(), "#?RADIANCE", 10)) return fail("pts_load_hdr: not a Radiance file");
+  Bytes f{buf, 11};  // magic + one skipped byte (fseek(file, 1, SEEK_CUR))
+  int c = 0, oldc;
+  for (;;) {  // header up to the empty line
+    oldc = c;
+    c = f.get();
+    if (c < 0) return fail("pts_load_hdr: truncated header");
+    if (c == 0xa && oldc == 0xa) break;
+  }
+  std::string reso;
+  for (;;) {
+    c = f.get();
+    if (c < 0) return fail("pts_load_hdr: truncated resolution line");
+    reso.push_back((char)c);
+    if (c == 0xa) break;
+  }
+  long lh = 0, lw = 0;
+  if (sscanf(reso.c_str(), "-Y %ld +X %ld", &lh, &lw) != 2 || lh <= 0 || lw <= 0 || lh > 65536 || lw > 65536)
+    return fail("pts_load_hdr: unsupported resolution line");
+  const int w = (int)lw, h = (int)lh;
+  *width = w;
+  *height = h;
+  if (!rgb_out) return 0;
+  std::vector<Rgbe> scan((size_t)w);
+  float* cols = rgb_out;
+  for (int y = h - 1; y >= 0; --y) {  // scanlines in file order; the reference ignores y for placement
+    if (!decrunch(scan.data(), w, f)) return fail("pts_load_hdr: truncated or malformed scanline data");
+    for (int x = 0; x < w; ++x) {
+      const int expo = scan[x][3] - 128;
+      cols[0] = rgbe_component(expo, scan[x][0]);
+      cols[1] = rgbe_component(expo, scan[x][1]);
+      cols[2] = rgbe_component(expo, scan[x][2]);
+      cols += 3;
+    }
+  }
+  return 0;
+}
+
 int pts_gen_env_map(int width, int height, float* out) {
   if (width <= 0 || height <= 0 || !out) return fail("pts_gen_env_map: bad argument");
   v3 sun = glsl::normalize(glsl::mk(0.4f, 0.6f, 0.3f));

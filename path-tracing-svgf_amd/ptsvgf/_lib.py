@@ -117,6 +117,7 @@ _PTS_SIGS = [
     ("pts_gen_teapot", C.c_int, [C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), _fp, C.POINTER(C.c_int)]),
     ("pts_gen_cornell", C.c_int, [C.POINTER(C.c_int), C.POINTER(C.c_int), _fp, C.POINTER(C.c_int)]),
     ("pts_gen_env_map", C.c_int, [C.c_int, C.c_int, _fp]),
+    ("pts_load_hdr", C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), _fp]),
     ("pts_last_error", C.c_char_p, []),
 ]
 

@@ -138,6 +138,15 @@ def env_map(width: int = 2048, height: int = 1024) -> np.ndarray:
     return out
 
 
+def load_hdr(path: str) -> np.ndarray:
+    """HDRLoader::load (lib/hdrloader.cpp): Radiance RGBE -> (h, w, 3) float32, file scanline order."""
+    w, h = C.c_int(), C.c_int()
+    check_host(pts().pts_load_hdr(path.encode(), C.byref(w), C.byref(h), None))
+    out = np.zeros((h.value, w.value, 3), np.float32)
+    check_host(pts().pts_load_hdr(path.encode(), C.byref(w), C.byref(h), fptr(out)))
+    return out
+
+
 def hdr_cache(hdr: np.ndarray) -> np.ndarray:
     h, w, _ = hdr.shape
     a = np.ascontiguousarray(hdr, np.float32)
