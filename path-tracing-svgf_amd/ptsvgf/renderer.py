@@ -143,20 +143,8 @@ class Renderer:
         self.accumulate = bool(self.cfg.accumulate_color)
         nslots = max(self.K, 2) if (self.accumulate and mode == "fast") else self.K
         self.pt_slots = []
-        for _ in range(nslots):
-            p = RenderPass(_prog("path_tracing.frag"), W, H)
-            outs = (tex(W, H), tex(W, H), tex(W, H))  # color, emission, albedo
-            p.colorAttachments += list(outs)
-            p.bindData(False)
-            p.set_uniform_int("nTriangles", scene.ntris)
-            p.set_uniform_int("nNodes", scene.node_enc.shape[0])
-            p.set_uniform_int("width", W)
-            p.set_uniform_int("height", H)
-            p.set_uniform_int("pointLightSize", scene.lights.shape[0])
-            p.set_uniform_int("aspect_corrected", int(self.aspect_corrected))
-            p.set_uniform_int("prune", int(prune))
-            self.pt_slots.append((p, outs))
-        self.pass_path_tracing = PassGroup([p for p, _ in self.pt_slots])  # settings apply to every slot
+        self._pt_prune = prune
+        self._ensure_slots(nslots)
         self._use_slot(0)
         self._streams = None
         if self.K > 1:
@@ -241,6 +229,48 @@ class Renderer:
             p.set_uniform_float("inv_screen_height", 1.0 / H)
 
     # ------------------------------------------------------------- frame ---
+    def _ensure_slots(self, n: int) -> None:
+        """Path-tracing passes + colour/emission/albedo outputs, one per frame slot (main.cpp:229-248)."""
+        W, H, scene = self.W, self.H, self.scene
+        while len(self.pt_slots) < n:
+            p = RenderPass(_prog("path_tracing.frag"), W, H)
+            outs = (self._tex(W, H), self._tex(W, H), self._tex(W, H))  # color, emission, albedo
+            p.colorAttachments += list(outs)
+            p.bindData(False)
+            p.set_uniform_int("nTriangles", scene.ntris)
+            p.set_uniform_int("nNodes", scene.node_enc.shape[0])
+            p.set_uniform_int("width", W)
+            p.set_uniform_int("height", H)
+            p.set_uniform_int("pointLightSize", scene.lights.shape[0])
+            p.set_uniform_int("aspect_corrected", int(self.aspect_corrected))
+            p.set_uniform_int("prune", int(self._pt_prune))
+            self.pt_slots.append((p, outs))
+        self.pass_path_tracing = PassGroup([p for p, _ in self.pt_slots])  # settings apply to every slot
+
+    VIEWS = ("path_tracing_pic_1spp", "svgf_reprojected_pic", "svgf_variance_pic", "svgf_atrous_pic",
+             "svgf_modulate_pic", "taa_pic", "final_pic", "accumulate_color")  # gui_config.h:7-17
+
+    def set_view(self, view: str) -> None:
+        """The debug-view switch (main.cpp:398-415 radio buttons + gui_config.h:37-45): selects the plane the
+        output pass shows (main.cpp:558-586); accumulate_color turns accumulation on, every other view off, and
+        any change restarts the frame counter."""
+        if view not in self.VIEWS:
+            raise ValueError(f"unknown view {view!r}; one of {self.VIEWS}")
+        self.view = view
+        self.cfg.accumulate_color = view == "accumulate_color"
+        self.accumulate = self.cfg.accumulate_color
+        if self.accumulate and self.mode == "fast":
+            self._ensure_slots(max(self.K, 2))
+        self.camera.frameCounter = 0
+
+    def _view_plane(self) -> int:
+        v = getattr(self, "view", "final_pic")
+        pl = self.planes()
+        return {"path_tracing_pic_1spp": pl["color"], "accumulate_color": pl["color"],
+                "svgf_reprojected_pic": pl["reproj_illum"], "svgf_variance_pic": pl["variance"],
+                "svgf_atrous_pic": pl["atrous"], "svgf_modulate_pic": pl["modulate"],
+                "taa_pic": pl["final"], "final_pic": pl["final"]}[v]
+
     def _use_slot(self, s: int) -> None:
         """Path-tracing pass and outputs of frame slot s (frame f uses slot f % K)."""
         self.pt_pass, (self.curColor, self.Emission, self.Albedo) = self.pt_slots[s]
@@ -520,7 +550,7 @@ class Renderer:
             op = self.output_pass
             op.reset_texture_slot()
             op.set_uniform_bool("accumulate", self.cfg.accumulate_color)
-            op.set_texture_uniform(GL_TEXTURE_2D, self.final, "texPass0")
+            op.set_texture_uniform(GL_TEXTURE_2D, self._view_plane(), "texPass0")
             self._draw(op, "output")
         if self.K > 1:  # the slot's buffers are free again once this frame's back end has run
             import torch

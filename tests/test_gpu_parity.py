@@ -193,6 +193,30 @@ def test_fast_driver_equals_reference_driver(gpu, scene_small):
             assert np.array_equal(pa[key], pb[key]), (f, key)
 
 
+def test_debug_views_feed_the_output_pass(gpu, scene_small):
+    """main.cpp:558-586: each debug view routes its plane through the output tonemap; switching views restarts
+    the frame counter and toggles accumulation (gui_config.h:37-45), in both drivers identically."""
+    gl = gpu
+    W, H = 48, 40
+    a = _renderer(scene_small, W, H, mode="reference", run_taa=True, run_output=True)
+    b = _renderer(scene_small, W, H, mode="fast", run_taa=True, run_output=True)
+    src = {"path_tracing_pic_1spp": "color", "svgf_reprojected_pic": "reproj_illum", "svgf_variance_pic": "variance",
+           "svgf_atrous_pic": "atrous", "svgf_modulate_pic": "modulate", "taa_pic": "final", "final_pic": "final",
+           "accumulate_color": "color"}
+    for view, key in src.items():
+        for r in (a, b):
+            r.camera.frameCounter = 7
+            r.set_view(view)
+            assert r.camera.frameCounter == 0 and r.cfg.accumulate_color == (view == "accumulate_color")
+            r.frame()
+        pa, pb = _readback(gl, a), _readback(gl, b)
+        want = O.output(pa[key])
+        _cmp(f"{view}/output", pa["output"], want, tol=1e-6)
+        assert np.array_equal(pa["output"].view(np.uint32), pb["output"].view(np.uint32)), view
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("K", [1, 2])
 def test_accumulate_fast_equals_reference(gpu, scene_small, K):
     """Accumulate mode (path_tracing.frag:1116-1119, lastFrame = last frame's colour): the fast driver's slot
