@@ -22,9 +22,10 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
-# frames in flight use K + 1 streams (K front ends + the SVGF back end); HIP's default of 4 hardware queues
-# per process would make streams share queues and serialise. Set before HIP initialises.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# frames in flight use K + 1 streams (K front ends + the SVGF back end; 3K + 1 with the optional G-buffer and
+# closest-hit side streams); HIP's default of 4 hardware queues per process would make streams share queues
+# and serialise. Set before HIP initialises.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 sys.path.insert(0, os.path.join(REPO, "path-tracing-svgf_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 

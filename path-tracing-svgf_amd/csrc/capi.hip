@@ -118,6 +118,8 @@ struct Pass {
   uint32_t program = 0;
   WFBuffers wf;
   TileOrder order;
+  hipStream_t aux = nullptr;                   // path tracer: stream for the concurrent closest-hit trace
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int W = 0, H = 0;
   std::vector<uint32_t> att;
   bool bound = false, final_pass = false;
@@ -611,7 +613,13 @@ int draw_pathtrace(Pass* p) {
     k.wf.row_cost = p->row_cost;
     const int ntiles = ((k.W + 15) / 16) * ((std::max(0, k.y1 - k.y0) + 15) / 16);  // wf_primary's grid
     TRY(tile_order_begin(p, ntiles, &k.tiles));
-    rc = launch_pathtrace_wavefront(k, g.stream);  // sorts the tile order itself, after the primaries
+    if (ui(p, "trace_fork", 0) && !p->aux) {  // A/B switch (off: measured slower with frames in flight)
+      HIPCHK(hipStreamCreateWithFlags(&p->aux, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
+    }
+    const bool fork = ui(p, "trace_fork", 0) && !g.profiling;  // profiling times each draw on one stream
+    rc = launch_pathtrace_wavefront(k, g.stream, fork ? p->aux : nullptr, p->ev_fork, p->ev_join);
     if (!rc && k.tiles.cost) p->order.ordered = true;
   }
   return rc ? hip_err((hipError_t)rc, "pathtrace launch") : PT_OK;
@@ -803,6 +811,9 @@ int pt_shutdown(void) {
     if (p->wf.base) (void)hipFree(p->wf.base);
     if (p->order.cost) (void)hipFree(p->order.cost);
     if (p->order.perm) (void)hipFree(p->order.perm);
+    if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
+    if (p->ev_join) (void)hipEventDestroy(p->ev_join);
+    if (p->aux) (void)hipStreamDestroy(p->aux);
     if (p->ev0) (void)hipEventDestroy(p->ev0);
     if (p->ev1) (void)hipEventDestroy(p->ev1);
   }
@@ -1266,6 +1277,9 @@ int pt_pass_destroy(uint32_t pass) {
   if (p->wf.base) (void)hipFree(p->wf.base);
   if (p->order.cost) (void)hipFree(p->order.cost);
   if (p->order.perm) (void)hipFree(p->order.perm);
+  if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
+  if (p->ev_join) (void)hipEventDestroy(p->ev_join);
+  if (p->aux) (void)hipStreamDestroy(p->aux);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
   g.passes.erase(it);

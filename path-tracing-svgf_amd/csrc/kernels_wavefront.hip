@@ -392,8 +392,12 @@ int wf_list_capacity(int W, int rows) {
   return (blocks + kSeg - 1) / kSeg * 256;
 }
 
+// Launch order of one frame. With an auxiliary stream the closest-hit trace of bounce i+1 (it needs only the
+// rays and live list shade(i) wrote) runs concurrently with the shadow trace and finish of bounce i; the join
+// comes before shade(i+1), which needs both. Two traversal launches then end together, so the frame's
+// dependency chain carries one tail fewer per bounce. Without `aux` the launches are serial.
 template <int KS>
-int launch_wavefront(const PTParams& p, hipStream_t s) {
+int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent_t ev_fork, hipEvent_t ev_join) {
   const int rows = p.y1 - p.y0;
   if (rows <= 0) return 0;
   const int N = p.W * rows;
@@ -408,16 +412,34 @@ int launch_wavefront(const PTParams& p, hipStream_t s) {
   }
   const int gN = (N + 255) / 256, gT = (N + kTB - 1) / kTB, gT2 = (2 * N + kTB - 1) / kTB;
   const int gS0 = tiles.x * tiles.y;  // bounce-0 shade: one block per primary tile
+  const bool fork = aux && ev_fork && ev_join;
   int* lists[2] = {p.wf.list0, p.wf.list1};
+  auto closest = [&](int i, hipStream_t st) {
+    const int* lin = lists[(i + 1) & 1];
+    const int* live_in = p.wf.counters + 32 * (i - 1);
+    hipLaunchKernelGGL(wf_trace_closest<KS>, dim3(gT), dim3(kTB), 0, st, p, lin, live_in, cap);
+  };
   for (int i = 0; i < p.max_depth; ++i) {
     const int* lin = lists[(i + 1) & 1];
     int* lout = lists[i & 1];
     int* live = p.wf.counters + 32 * i;        // kSeg live-list counts of bounce i
     int* shadow = p.wf.counters + 32 * i + 8;  // kSeg HDR + kSeg point-light shadow-list counts
     const int* live_in = p.wf.counters + 32 * (i > 0 ? i - 1 : 0);
-    if (i > 0) hipLaunchKernelGGL(wf_trace_closest<KS>, dim3(gT), dim3(kTB), 0, s, p, lin, live_in, cap);
+    if (i > 0) {
+      if (fork) {
+        if ((e = hipStreamWaitEvent(s, ev_join, 0)) != hipSuccess) return (int)e;  // closest(i) done
+      } else {
+        closest(i, s);
+      }
+    }
     hipLaunchKernelGGL(wf_shade, dim3(i == 0 ? gS0 : gN), dim3(256), 0, s, p, i, lin, live_in, lout, live,
                        p.wf.shadow_list, shadow, cap);
+    if (fork && i + 1 < p.max_depth) {  // closest(i+1) on aux, beside shadow(i) + finish(i)
+      if ((e = hipEventRecord(ev_fork, s)) != hipSuccess) return (int)e;
+      if ((e = hipStreamWaitEvent(aux, ev_fork, 0)) != hipSuccess) return (int)e;
+      closest(i + 1, aux);
+      if ((e = hipEventRecord(ev_join, aux)) != hipSuccess) return (int)e;
+    }
     if (p.scene.bvh4)
       hipLaunchKernelGGL((wf_trace_shadow<KS, true>), dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
                          (const int*)shadow, cap);
@@ -430,9 +452,11 @@ int launch_wavefront(const PTParams& p, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s) {
+int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent_t ev_fork,
+                               hipEvent_t ev_join) {
   // the LDS stack bounds resident waves: a tree that fits the small stack gets more of them
-  return p.stack_need <= kStackSmall ? launch_wavefront<kStackSmall>(p, s) : launch_wavefront<kStack>(p, s);
+  return p.stack_need <= kStackSmall ? launch_wavefront<kStackSmall>(p, s, aux, ev_fork, ev_join)
+                                     : launch_wavefront<kStack>(p, s, aux, ev_fork, ev_join);
 }
 
 }  // namespace ptk

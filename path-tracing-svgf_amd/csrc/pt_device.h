@@ -180,7 +180,8 @@ struct TAAParams {
 namespace ptk {
 // Launchers (kernels_*.hip). Return hipError_t as int.
 int launch_pathtrace(const PTParams& p, hipStream_t s);
-int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s);
+int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux = nullptr,
+                               hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr);
 int wf_list_capacity(int W, int rows);  // per-segment capacity of the compacted ray lists (8 segments)
 int launch_gbuffer(const GBufParams& p, hipStream_t s);
 int launch_reproject(const ReprojParams& p, hipStream_t s);

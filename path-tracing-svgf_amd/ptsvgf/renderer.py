@@ -16,6 +16,8 @@ TAA and the output tonemap run in both modes (main.cpp:537-590).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 from . import gl
@@ -151,6 +153,9 @@ class Renderer:
             import torch  # streams and events are torch plumbing (the kernels are the library's)
 
             self._streams = [torch.cuda.Stream() for _ in range(self.K)]
+            self._gstreams = [torch.cuda.Stream() for _ in range(self.K)]  # G-buffer beside the path tracer
+            # A/B switch, off by default: with K frames in flight the extra streams measured slower
+            self._gfork = os.environ.get("PTSVGF_GBUFFER_FORK", "0") != "0"
             self._back = torch.cuda.Stream()
             self._slot_free = [None] * self.K  # event: SVGF of the frame that last used the slot is done
             self._fe_prev = None
@@ -276,7 +281,11 @@ class Renderer:
         self.pt_pass, (self.curColor, self.Emission, self.Albedo) = self.pt_slots[s]
 
     def _gbuffer_and_pt(self, b: int):
-        cam, cfg = self.camera, self.cfg
+        self._gbuffer(b)
+        self._path_trace()
+
+    def _gbuffer(self, b: int):
+        cam = self.camera
         view, proj = cam.cam_view_mat, cam.cam_proj_mat
         ip = self.init_pass[b]
         ip.set_uniform_mat4("view", view)                      # main.cpp:436-443
@@ -284,6 +293,10 @@ class Renderer:
         ip.set_uniform_mat4("pre_viewproj", self.pre_viewproj)
         ip.set_uniform_uint("frameCounter", cam.frameCounter)
         self._draw(ip, "gbuffer")
+
+    def _path_trace(self):
+        cam, cfg = self.camera, self.cfg
+        view = cam.cam_view_mat
         self.cameraRotate = rigid_inverse(view)                # main.cpp:445
         pt = self.pt_pass                                      # main.cpp:447-470
         pt.set_uniform_vec3("eye", cam.cam_position)
@@ -397,8 +410,23 @@ class Renderer:
                 fe.wait_event(self._slot_free[f % self.K])
             if self.accumulate and self._fe_prev is not None:  # lastFrame = the previous front end's colour
                 fe.wait_event(self._fe_prev)
-            _set_stream(fe)
-            self._gbuffer_and_pt(f % ng)
+            # the G-buffer and the path tracer are independent (both need only the camera): the G-buffer runs on
+            # a side stream beside the path tracer, so the two launches' tails overlap
+            if self._gfork:
+                gs = self._gstreams[f % self.K]
+                start = torch.cuda.Event()
+                start.record(fe)
+                gs.wait_event(start)
+                _set_stream(gs)
+                self._gbuffer(f % ng)
+                gdone = torch.cuda.Event()
+                gdone.record(gs)
+                _set_stream(fe)
+                self._path_trace()
+                fe.wait_event(gdone)
+            else:
+                _set_stream(fe)
+                self._gbuffer_and_pt(f % ng)
             done = torch.cuda.Event()
             done.record(fe)
             self._fe_prev = done

@@ -50,6 +50,7 @@ def sim_rank(rk, bounds, probe=False, K=10):
     r = D.BandRenderer(scene, W, H, cfg, rk, N, FakeDist(), bounds=bounds,
                        frames_in_flight=int(os.environ.get("FIF", "1")))
     r.pass_path_tracing.set_uniform_int("pt_kernel", int(os.environ.get("PTK", "0")))
+    r.pass_path_tracing.set_uniform_int("trace_fork", int(os.environ.get("PTSVGF_TRACE_FORK", "0")))
     for _ in range(3):
         r.frame()
     torch.cuda.synchronize()
@@ -97,7 +98,7 @@ def report(tag, res):
 if __name__ == "__main__":
     eq = [sim_rank(rk, None, probe=True) for rk in range(N)]
     report("equal bands", eq)
-    if N > 1:
+    if N > 1 and os.environ.get("BALANCE", "1") != "0":
         visits = np.concatenate([s["counts"] for s in eq])
         a, b = D.fit_row_cost([s["counts"].sum() for s in eq], [s["y1"] - s["y0"] for s in eq],
                               [s["gpu"] for s in eq])

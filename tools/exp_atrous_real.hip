@@ -128,38 +128,33 @@ static void launch_exp(int S, dim3 g, const float4* I, const float4* N, const fl
 // Background (sign bit of the compact depth-fwidth plane) tiles copy and exit.
 __device__ __forceinline__ bool bgflag(float a) { return (__float_as_uint(a) >> 31) != 0; }
 
-// Block = NW waves; tile = 64 columns x TJ rows of one residue class mod S; wave wv computes tile rows
-// wv, wv + NW, ... (NH = TJ / NW pixels per thread, processed tap-interleaved for ILP).
-template <int S, int TJ, int NW>
-__global__ void __launch_bounds__(64 * NW) atrous_tile_kernel(const float4* __restrict__ I,
+// Block = TJ*NX waves, one pixel per thread; tile = 64*NX columns x TJ rows of one residue class mod S.
+template <int S, int TJ, int NX>
+__global__ void __launch_bounds__(64 * TJ * NX) atrous_tile_kernel(const float4* __restrict__ I,
                                                               const float4* __restrict__ ND,
                                                               const float* __restrict__ aux, float4* __restrict__ out,
                                                               int W, int H, int Y0, int Y1, float phi_color,
                                                               float phi_normal) {
-  constexpr int R = TJ + 4, C = 64 + 4 * S, NH = TJ / NW, NT = 64 * NW;
+  constexpr int R = TJ + 4, C = 64 * NX + 4 * S, NT = 64 * TJ * NX;
   __shared__ float4 LI[R * C];
   __shared__ float4 LN[R * C];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = wv / NX, xl = (wv % NX) * 64 + lane;
   const int g = blockIdx.y / S, b = blockIdx.y - g * S;
-  const int ybase = Y0 + g * S * TJ + b;  // row of tile row j = 0
-  const int x0 = blockIdx.x * 64, x = x0 + lane;
-  bool own[NH], fg[NH];
-  float fa[NH];
-  int yo[NH];
-  bool any = false;
-#pragma unroll
-  for (int k = 0; k < NH; ++k) {
-    yo[k] = ybase + S * (wv + NW * k);
-    own[k] = x < W && yo[k] < Y1;
-    fa[k] = own[k] ? aux[(size_t)yo[k] * W + x] : -1.0f;
-    fg[k] = own[k] && !bgflag(fa[k]);
-    any |= fg[k];
+  const int ybase = Y0 + g * S * TJ + b;
+  const int x0 = blockIdx.x * 64 * NX, x = x0 + xl, y = ybase + S * j;
+  const bool own = x < W && y < Y1;
+  const size_t ci = (size_t)y * W + x;
+  bool bg = true;
+  float fwz = 0.0f;
+  if (own) {
+    const float a = aux[ci];
+    bg = bgflag(a);
+    fwz = fabsf(a);
   }
-  if (!__syncthreads_or(any)) {
-#pragma unroll
-    for (int k = 0; k < NH; ++k)
-      if (own[k]) out[(size_t)yo[k] * W + x] = I[(size_t)yo[k] * W + x];
+  if (!__syncthreads_or(!bg)) {
+    if (own) out[ci] = I[ci];
     return;
   }
   for (int e = tid; e < R * C; e += NT) {
@@ -172,116 +167,69 @@ __global__ void __launch_bounds__(64 * NW) atrous_tile_kernel(const float4* __re
     LN[e] = ND[gi];
   }
   __syncthreads();
-  const bool edge = x0 - 2 * S < 0 || x0 + 63 + 2 * S >= W || ybase - 2 * S < 0 || ybase + S * (TJ + 1) >= H;
-  const float LOG2E = 1.4426950408889634f;
-  float4 ic[NH], nd[NH];
-  float lc[NH], wLr[NH], wLg[NH], wLb[NH], cL[NH], kD[NH], sumW[NH];
-  f2v s01[NH], s23[NH];
-  bool flat = false;
-#pragma unroll
-  for (int k = 0; k < NH; ++k) {
-    const int o = (wv + NW * k + 2) * C + lane + 2 * S;
-    ic[k] = LI[o];
-    nd[k] = LN[o];
-    lc[k] = (0.2125f * ic[k].x + 0.7154f * ic[k].y) + 0.0721f * ic[k].z;
-    const float phiL = phi_color * __builtin_sqrtf(fmaxf(0.0f, 1e-10f + ic[k].w));
-    flat |= fg[k] && !(phiL > 0.0f);
-    const float kL = LOG2E / phiL;
-    wLr[k] = 0.2125f * kL;
-    wLg[k] = 0.7154f * kL;
-    wLb[k] = 0.0721f * kL;
-    cL[k] = -(lc[k] * kL);
-    kD[k] = LOG2E / (fmaxf(fabsf(fa[k]), 1e-8f) * (float)S);
-    sumW[k] = 1.0f;
-    s01[k] = f2v{ic[k].x, ic[k].y};
-    s23[k] = f2v{ic[k].z, ic[k].w};
+  if (!own) return;
+  const float4* Li = LI + j * C + xl;
+  const float4* Ln = LN + j * C + xl;
+  const float4 ic = Li[2 * C + 2 * S];
+  if (bg) {
+    out[ci] = ic;
+    return;
   }
+  const float4 nd = Ln[2 * C + 2 * S];
+  const bool edge = x0 - 2 * S < 0 || x0 + 64 * NX - 1 + 2 * S >= W || ybase - 2 * S < 0 || ybase + S * (TJ + 1) >= H;
+  const float LOG2E = 1.4426950408889634f;
+  const float lc = (0.2125f * ic.x + 0.7154f * ic.y) + 0.0721f * ic.z;
+  const float phiL = phi_color * __builtin_sqrtf(fmaxf(0.0f, 1e-10f + ic.w));
+  const float kL = LOG2E / phiL;
+  const float kD = LOG2E / (fmaxf(fwz, 1e-8f) * (float)S);
+  const float kDr[5] = {kD, kD * 0.70710678f, kD * 0.5f, kD * 0.44721360f, kD * 0.35355339f};
+  float sumW = 1.0f;
+  f2v s01 = {ic.x, ic.y}, s23 = {ic.z, ic.w};
+  const float wLr = 0.2125f * kL, wLg = 0.7154f * kL, wLb = 0.0721f * kL, cL = -(lc * kL);
 #pragma unroll
   for (int yy = -2; yy <= 2; ++yy) {
+    if (edge && (y + yy * S < 0 || y + yy * S >= H)) continue;
 #pragma unroll
     for (int xx = -2; xx <= 2; ++xx) {
       if (xx == 0 && yy == 0) continue;
+      if (edge && (x + xx * S < 0 || x + xx * S >= W)) continue;
       const int r2 = xx * xx + yy * yy;
-      const float il = r2 == 1 ? 1.0f : r2 == 2 ? 0.70710678f : r2 == 4 ? 0.5f : r2 == 5 ? 0.44721360f : 0.35355339f;
+      const float kDl = r2 == 1 ? kDr[0] : r2 == 2 ? kDr[1] : r2 == 4 ? kDr[2] : r2 == 5 ? kDr[3] : kDr[4];
       const int ax = xx < 0 ? -xx : xx, ay = yy < 0 ? -yy : yy;
       const float kern = (ax == 0 ? 1.0f : ax == 1 ? 2.0f / 3.0f : 1.0f / 6.0f) *
                          (ay == 0 ? 1.0f : ay == 1 ? 2.0f / 3.0f : 1.0f / 6.0f);
-#pragma unroll
-      for (int k = 0; k < NH; ++k) {
-        if (edge && (yo[k] + yy * S < 0 || yo[k] + yy * S >= H || x + xx * S < 0 || x + xx * S >= W)) continue;
-        const int o = (wv + NW * k + 2 + yy) * C + lane + 2 * S + xx * S;
-        const float4 ip = LI[o];
-        const float4 q = LN[o];
-        const float dn =
-            fminf(fmaxf(__builtin_fmaf(nd[k].z, q.z, __builtin_fmaf(nd[k].y, q.y, nd[k].x * q.x)), 0.0f), 1.0f);
-        const float tl =
-            __builtin_fmaf(ip.z, wLb[k], __builtin_fmaf(ip.y, wLg[k], __builtin_fmaf(ip.x, wLr[k], cL[k])));
-        const float a = __builtin_fmaf(fabsf(nd[k].w - q.w), kD[k] * il, fabsf(tl));
-        const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(phi_normal, __builtin_amdgcn_logf(dn), -a)) * kern;
-        sumW[k] += w;
-        s01[k] = __builtin_elementwise_fma(f2v{w, w}, f2v{ip.x, ip.y}, s01[k]);
-        s23[k] = __builtin_elementwise_fma(f2v{w, w * w}, f2v{ip.z, ip.w}, s23[k]);
-      }
+      const int o = (yy + 2) * C + (xx + 2) * S;
+      const float4 ip = Li[o];
+      const float4 q = Ln[o];
+      const float dn = fminf(fmaxf(__builtin_fmaf(nd.z, q.z, __builtin_fmaf(nd.y, q.y, nd.x * q.x)), 0.0f), 1.0f);
+      const float tl = __builtin_fmaf(ip.z, wLb, __builtin_fmaf(ip.y, wLg, __builtin_fmaf(ip.x, wLr, cL)));
+      const float a = __builtin_fmaf(fabsf(nd.w - q.w), kDl, fabsf(tl));
+      const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(phi_normal, __builtin_amdgcn_logf(dn), -a)) * kern;
+      sumW += w;
+      s01 = __builtin_elementwise_fma(f2v{w, w}, f2v{ip.x, ip.y}, s01);
+      s23 = __builtin_elementwise_fma(f2v{w, w * w}, f2v{ip.z, ip.w}, s23);
     }
   }
-  if (__builtin_expect(flat, 0)) {
-    // phiIllumination == 0: |lc - lp| / 0 is +inf (weight 0) unless lp == lc (0/0 -> NaN -> max(., 0) = 0)
-#pragma unroll
-    for (int k = 0; k < NH; ++k) {
-      const float phiL = phi_color * __builtin_sqrtf(fmaxf(0.0f, 1e-10f + ic[k].w));
-      if (phiL > 0.0f) continue;
-      sumW[k] = 1.0f;
-      s01[k] = f2v{ic[k].x, ic[k].y};
-      s23[k] = f2v{ic[k].z, ic[k].w};
-      for (int yy = -2; yy <= 2; ++yy)
-        for (int xx = -2; xx <= 2; ++xx) {
-          if (xx == 0 && yy == 0) continue;
-          if (edge && (yo[k] + yy * S < 0 || yo[k] + yy * S >= H || x + xx * S < 0 || x + xx * S >= W)) continue;
-          const int r2 = xx * xx + yy * yy;
-          const float il = r2 == 1 ? 1.0f : r2 == 2 ? 0.70710678f : r2 == 4 ? 0.5f : r2 == 5 ? 0.44721360f : 0.35355339f;
-          const int ax = xx < 0 ? -xx : xx, ay = yy < 0 ? -yy : yy;
-          const float kern = (ax == 0 ? 1.0f : ax == 1 ? 2.0f / 3.0f : 1.0f / 6.0f) *
-                             (ay == 0 ? 1.0f : ay == 1 ? 2.0f / 3.0f : 1.0f / 6.0f);
-          const int o = (wv + NW * k + 2 + yy) * C + lane + 2 * S + xx * S;
-          const float4 ip = LI[o];
-          const float4 q = LN[o];
-          const float dn =
-              fminf(fmaxf(__builtin_fmaf(nd[k].z, q.z, __builtin_fmaf(nd[k].y, q.y, nd[k].x * q.x)), 0.0f), 1.0f);
-          const float lp = (0.2125f * ip.x + 0.7154f * ip.y) + 0.0721f * ip.z;
-          const float a = lp == lc[k] ? fabsf(nd[k].w - q.w) * (kD[k] * il) : __builtin_inff();
-          const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(phi_normal, __builtin_amdgcn_logf(dn), -a)) * kern;
-          sumW[k] += w;
-          s01[k] = __builtin_elementwise_fma(f2v{w, w}, f2v{ip.x, ip.y}, s01[k]);
-          s23[k] = __builtin_elementwise_fma(f2v{w, w * w}, f2v{ip.z, ip.w}, s23[k]);
-        }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < NH; ++k) {
-    if (!own[k]) continue;
-    float4 o4 = ic[k];
-    if (fg[k]) {
-      const float inv = 1.0f / sumW[k];
-      o4 = float4{s01[k].x * inv, s01[k].y * inv, s23[k].x * inv, s23[k].y * (inv * inv)};
-    }
-    out[(size_t)yo[k] * W + x] = o4;
-  }
+  const float inv = 1.0f / sumW;
+  out[ci] = float4{s01.x * inv, s01.y * inv, s23.x * inv, s23.y * (inv * inv)};
 }
 
-template <int S, int TJ, int NW>
+template <int S, int TJ, int NX>
 static void lt(const float4* I, const float4* N, const float* A, float4* O, int W, int H) {
-  dim3 grid((W + 63) / 64, ((H + S * TJ - 1) / (S * TJ)) * S);
-  hipLaunchKernelGGL((atrous_tile_kernel<S, TJ, NW>), grid, dim3(64 * NW), 0, 0, I, N, A, O, W, H, 0, H, 4.0f, 128.0f);
+  dim3 grid((W + 64 * NX - 1) / (64 * NX), ((H + S * TJ - 1) / (S * TJ)) * S);
+  hipLaunchKernelGGL((atrous_tile_kernel<S, TJ, NX>), grid, dim3(64 * TJ * NX), 0, 0, I, N, A, O, W, H, 0, H, 4.0f,
+                     128.0f);
 }
 static int g_cfg = 0;
-static const char* cfg_names[5] = {"TJ8 NW4", "TJ8 NW8", "TJ16 NW8", "TJ16 NW16", "TJ4 NW4"};
+static const char* cfg_names[6] = {"TJ8 NX1", "TJ4 NX2", "TJ8 NX2", "TJ4 NX4", "TJ2 NX4", "TJ16 NX1"};
 template <int S>
 static void lts(const float4* I, const float4* N, const float* A, float4* O, int W, int H) {
-  if (g_cfg == 0) lt<S, 8, 4>(I, N, A, O, W, H);
-  if (g_cfg == 1) lt<S, 8, 8>(I, N, A, O, W, H);
-  if (g_cfg == 2) lt<S, 16, 8>(I, N, A, O, W, H);
-  if (g_cfg == 3) lt<S, 16, 16>(I, N, A, O, W, H);
-  if (g_cfg == 4) lt<S, 4, 4>(I, N, A, O, W, H);
+  if (g_cfg == 0) lt<S, 8, 1>(I, N, A, O, W, H);
+  if (g_cfg == 1) lt<S, 4, 2>(I, N, A, O, W, H);
+  if (g_cfg == 2) lt<S, 8, 2>(I, N, A, O, W, H);
+  if (g_cfg == 3) lt<S, 4, 4>(I, N, A, O, W, H);
+  if (g_cfg == 4) lt<S, 2, 4>(I, N, A, O, W, H);
+  if (g_cfg == 5) lt<S, 16, 1>(I, N, A, O, W, H);
 }
 static void launch_tile(int S, const float4* I, const float4* N, const float* A, float4* O, int W, int H) {
   switch (S) {
@@ -325,7 +273,7 @@ int main(int argc, char** argv) {
   p.W = W; p.H = H; p.y0 = 0; p.y1 = H;
   p.illum = {dI, nullptr, W, 0, H};
   p.nd = {dN, nullptr, W, 0, H};
-  p.fwidth = {nullptr, dAp, W, 0, H};
+  p.fwidth = {nullptr, dA, W, 0, H};
   p.out = {dO, nullptr, W, 0, H};
   p.phi_color = 4.0f; p.phi_normal = 128.0f;
   hipEvent_t e0, e1;
@@ -347,8 +295,30 @@ int main(int argc, char** argv) {
     CK(hipDeviceSynchronize());
     return 0;
   }
+  for (int S : {1, 2, 4, 8, 16}) {  // tile statistics (TJ = 8, 64 columns)
+    long tiles = 0, fgt = 0, fgpx = 0, wavesfg = 0;
+    for (int y0 = 0; y0 < H; y0 += 8 * S)
+      for (int b = 0; b < S; ++b)
+        for (int x0 = 0; x0 < W; x0 += 64) {
+          bool any = false;
+          long n = 0;
+          int wf = 0;
+          for (int j = 0; j < 8; ++j) {
+            const int y = y0 + b + S * j;
+            if (y >= H) continue;
+            bool wany = false;
+            for (int x = x0; x < x0 + 64 && x < W; ++x)
+              if (!(__builtin_bit_cast(uint32_t, aux[(size_t)y * W + x]) >> 31)) { any = true; wany = true; ++n; }
+            wf += wany;
+          }
+          ++tiles;
+          if (any) { ++fgt; fgpx += n; wavesfg += wf; }
+        }
+    printf("S=%2d tiles %ld fg tiles %.1f%%  fg px %.1f%% of frame  fg waves in fg tiles %.1f%%\n", S, tiles,
+           100.0 * fgt / tiles, 100.0 * fgpx / N, 100.0 * wavesfg / (8.0 * fgt));
+  }
   const int R = 30;
-  for (int cfg = 0; cfg < 5; ++cfg) {
+  for (int cfg = 0; cfg < 1; ++cfg) {
   g_cfg = cfg;
   printf("tile cfg %s\n", cfg_names[cfg]);
   for (int S : {1, 2, 4, 8, 16}) {
