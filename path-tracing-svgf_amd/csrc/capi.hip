@@ -88,7 +88,7 @@ int wf_alloc(WFBuffers& b, int W, int rows) {
   const size_t nl = (size_t)wf_list_capacity(W, rows) * 8;  // 8 list segments
   auto up = [&](size_t v) { return (v + al - 1) / al * al; };
   size_t total = up(f4) * 10 + up(n * 8) + up(n * 4) + up(n) * 2 + up(nl * 4) * 2 + up(nl * 8) +
-                 up(kWfCounters * 4);
+                 up(n * 8) + up(kWfCounters * 4);
   if (hipMalloc(&b.base, total) != hipSuccess) { b.base = nullptr; return PT_ERR_HIP; }
   char* c = (char*)b.base;
   float4** f4p[10] = {&b.st.ray_o, &b.st.ray_d, &b.st.light, &b.st.red, &b.st.pend0,
@@ -101,6 +101,7 @@ int wf_alloc(WFBuffers& b, int W, int rows) {
   b.st.list0 = (int*)c; c += up(nl * 4);
   b.st.list1 = (int*)c; c += up(nl * 4);
   b.st.shadow_list = (int*)c; c += up(nl * 8);
+  b.st.straggler = (int*)c; c += up(n * 8);  // both shadow kinds of one bounce
   b.st.counters = (int*)c;
   b.n = n;
   return PT_OK;
@@ -611,6 +612,9 @@ int draw_pathtrace(Pass* p) {
     TRY(wf_alloc(p->wf, k.W, std::max(0, k.y1 - k.y0)));
     k.wf = p->wf.st;
     k.wf.row_cost = p->row_cost;
+    // > 0: shadow rays past this many visits finish in the wave-cooperative walk (A/B switch; off: with frames
+    // in flight it measured slower)
+    k.wf.shadow_budget = (uint32_t)ui(p, "shadow_budget", 0);
     const int ntiles = ((k.W + 15) / 16) * ((std::max(0, k.y1 - k.y0) + 15) / 16);  // wf_primary's grid
     TRY(tile_order_begin(p, ntiles, &k.tiles));
     if (ui(p, "trace_fork", 0) && !p->aux) {  // A/B switch (off: measured slower with frames in flight)

@@ -178,25 +178,60 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest(PTParams p
 // Shadow rays from the compacted lists wf_shade queued: HDR rays, then point-light rays.
 template <int KS, bool WIDE>
 __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p, const int* __restrict__ list,
-                                                                      const int* __restrict__ counts, int cap) {
+                                                                      const int* __restrict__ counts, int cap,
+                                                                      int* __restrict__ strag_count) {
   __shared__ int stk[KS * kTB];
   const int k = blockIdx.x * kTB + threadIdx.x;
   const int nh = seg_total(counts);  // HDR list first, then the point-light list
   const bool point = k >= nh;
-  int pid;
+  int pid = -1;
+  bool valid = true;
   if (!point) {
     seg_get(list, counts, cap, k, &pid);
   } else if (!seg_get(list + kSeg * cap, counts + kSeg, cap, k - nh, &pid)) {
-    return;
+    valid = false;
   }
-  float4 o = p.wf.ray_o[pid];
-  uint32_t steps = 0;
-  const float4 dir = point ? p.wf.sh_p[pid] : p.wf.sh_h[pid];  // point: (direction, distance)
-  int occ = WIDE ? anyhit4<kTB, KS>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps) : -1;
-  if (occ < 0)  // binary walk (default), or the 4-wide stack overflowed
-    occ = anyhit2<kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps);
-  (point ? p.wf.occ_p : p.wf.occ_h)[pid] = occ;
-  add_row_cost(p, pid / p.W, pid, steps);
+  bool deferred = false;
+  if (valid) {
+    float4 o = p.wf.ray_o[pid];
+    uint32_t steps = 0;
+    const float4 dir = point ? p.wf.sh_p[pid] : p.wf.sh_h[pid];  // point: (direction, distance)
+    int occ = WIDE ? anyhit4<kTB, KS>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps) : -1;
+    if (occ < 0)  // binary walk (default), or the 4-wide stack overflowed
+      occ = anyhit2<kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps, p.wf.shadow_budget,
+                         &deferred);
+    if (!deferred) (point ? p.wf.occ_p : p.wf.occ_h)[pid] = occ;
+    add_row_cost(p, pid / p.W, pid, steps);
+  }
+  // rays past the step budget go to the cooperative walk (one wave-aggregated append per wave)
+  const unsigned long long m = __ballot(deferred);
+  if (m) {
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(strag_count, __popcll(m));
+    base = __shfl(base, __ffsll((long long)m) - 1);
+    if (deferred) p.wf.straggler[base + __popcll(m & ((1ull << lane) - 1ull))] = pid | (point ? (int)0x80000000 : 0);
+  }
+}
+
+// The shadow rays wf_trace_shadow deferred: one wave per ray walks cooperatively (shadow_coop_walk). A fixed
+// grid strides over the straggler list (its length is known only on the device).
+constexpr int kCoopWaves = 4;          // waves per block
+constexpr int kCoopBlocks = 512;       // 2048 waves in flight
+constexpr int kCoopCap = 1024;         // LDS stack entries per wave
+__global__ void __launch_bounds__(64 * kCoopWaves) wf_shadow_coop(PTParams p, const int* __restrict__ strag_count) {
+  __shared__ int st[kCoopWaves][kCoopCap];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n = *strag_count;
+  for (int r = blockIdx.x * kCoopWaves + wv; r < n; r += gridDim.x * kCoopWaves) {
+    const int item = p.wf.straggler[r];
+    const bool point = item < 0;
+    const int pid = item & 0x7fffffff;
+    const float4 o = p.wf.ray_o[pid];
+    const float4 dir = point ? p.wf.sh_p[pid] : p.wf.sh_h[pid];
+    const bool occ = shadow_coop_walk(p.scene, st[wv], kCoopCap, xyz(o), xyz(dir), point, dir.w);
+    if ((threadIdx.x & 63) == 0) (point ? p.wf.occ_p : p.wf.occ_h)[pid] = occ;
+  }
 }
 
 // shade()'s MIS combination (:950-966) for given shadow verdicts: hdriLight zeroes
@@ -440,12 +475,15 @@ int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent
       closest(i + 1, aux);
       if ((e = hipEventRecord(ev_join, aux)) != hipSuccess) return (int)e;
     }
+    int* strag = p.wf.counters + 32 * i + 24;  // shadow rays handed to the cooperative walk
     if (p.scene.bvh4)
       hipLaunchKernelGGL((wf_trace_shadow<KS, true>), dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
-                         (const int*)shadow, cap);
+                         (const int*)shadow, cap, strag);
     else
       hipLaunchKernelGGL((wf_trace_shadow<KS, false>), dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
-                         (const int*)shadow, cap);
+                         (const int*)shadow, cap, strag);
+    if (p.wf.shadow_budget)
+      hipLaunchKernelGGL(wf_shadow_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, s, p, (const int*)strag);
     hipLaunchKernelGGL(wf_finish, dim3(gN), dim3(256), 0, s, p, (const int*)lout, (const int*)live, cap);
   }
   hipLaunchKernelGGL(wf_finalize, dim3(gN), dim3(256), 0, s, p);

@@ -99,6 +99,8 @@ struct WFState {
   int* counters;                // per bounce i: [32i, 32i+8) live-list, [32i+8, 32i+16) HDR and
                                 // [32i+16, 32i+24) point-light segment counts (kWfCounters ints)
   uint32_t* row_cost;           // optional: traversal steps per band row (load-balancing probe), may be null
+  int* straggler;               // shadow rays past the step budget: pid | (point << 31), count at counters[32i+24]
+  uint32_t shadow_budget;       // node + triangle visits before a shadow ray is handed to the cooperative walk (0: never)
 };
 
 struct PTParams {

@@ -209,9 +209,11 @@ __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
 // Any-hit walk of the binary tree for both shadow kinds: traverse<1> (HDR, any
 // hit) and traverse<2> (point light: boxes entered beyond the light pruned, hit
 // nearer than `maxd`) merged behind a runtime flag, so a wave runs one loop.
+// budget > 0: a ray whose walk exceeds `budget` node + triangle visits stops and reports *deferred (its
+// verdict is then decided by the wave-cooperative walk, shadow_coop_walk below).
 template <int STRIDE>
 __device__ bool anyhit2(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, bool point, float maxd,
-                        uint32_t* steps) {
+                        uint32_t* steps, uint32_t budget = 0, bool* deferred = nullptr) {
   v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   const float lim = point ? maxd * 1.0002f + 2.0e-4f : __builtin_inff();
   int sp = 0;
@@ -220,6 +222,11 @@ __device__ bool anyhit2(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, b
   uint32_t nvis = 0;
   if (node < 0) { leaf = node; node = kNone; }
   while (node != kNone || leaf != kNone) {
+    if (budget && nvis > budget) {
+      *deferred = true;
+      if (steps) *steps = nvis;
+      return false;
+    }
     while (node >= 0) {
       ++nvis;
       const float4* nd = sc.bvh + 4 * node;
@@ -265,6 +272,70 @@ __device__ bool anyhit2(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, b
   }
   if (steps) *steps = nvis;
   return false;
+}
+
+// Wave-cooperative any-hit walk of ONE shadow ray (the stragglers of anyhit2's budget): the 64 lanes pop the
+// top 64 entries of a shared LDS stack, each tests its node's two child boxes (hitAABB, the same pruning bound)
+// or its leaf's triangles, and the surviving children are pushed back (far before near, so the walk stays close
+// to depth-first and the stack small). A launch's tail is set by its longest chain of dependent fetches; this
+// expands up to 64 nodes per fetch instead of one. The verdict is order-free (any hit), so it equals the
+// serial walk's. `st` is this wave's LDS stack of `cap` entries; on overflow the wave falls back to the serial
+// walk on lane 0 (rare, correct, slow). Call with the whole wave (wave-uniform ray).
+__device__ bool shadow_coop_walk(const SceneDev& sc, int* __restrict__ st, int cap, v3 S, v3 d, bool point, float maxd) {
+  const int lane = threadIdx.x & 63;
+  const v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const float lim = point ? maxd * 1.0002f + 2.0e-4f : __builtin_inff();
+  int count = 1;
+  if (lane == 0) st[0] = sc.root_ref;
+  __builtin_amdgcn_wave_barrier();
+  bool overflow = false;
+  while (count > 0) {
+    const int k = count < 64 ? count : 64;
+    const int ref = lane < k ? st[count - 1 - lane] : kNone;
+    count -= k;
+    __builtin_amdgcn_wave_barrier();
+    bool hit = false;
+    int push0 = kNone, push1 = kNone;  // far, near
+    if (ref >= 0) {
+      const float4* nd = sc.bvh + 4 * ref;
+      float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+      float t0l, t0r;
+      float dl = slab(S, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, &t0l);
+      float dr = slab(S, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, &t0r);
+      const bool hl = dl > 0.0f && !(t0l > lim), hr = dr > 0.0f && !(t0r > lim);
+      const int cl = __float_as_int(q3.x), cr = __float_as_int(q3.y);
+      if (hl && hr) {
+        const bool lnear = dl < dr;
+        push0 = lnear ? cr : cl;
+        push1 = lnear ? cl : cr;
+      } else if (hl) {
+        push1 = cl;
+      } else if (hr) {
+        push1 = cr;
+      }
+    } else if (ref != kNone) {
+      hit = leaf_scan(sc.tri_geom, ref_leaf_first(ref), ref_leaf_count(ref), S, d, [&](int, float t) {
+        return t < PT_INF && (!point || length(sub(add(S, muls(d, t)), S)) < maxd);
+      });
+    }
+    if (__any(hit)) return true;
+    const unsigned long long m0 = __ballot(push0 != kNone), m1 = __ballot(push1 != kNone);
+    const int n0 = __popcll(m0), n1 = __popcll(m1);
+    if (count + n0 + n1 > cap) {
+      overflow = true;
+      break;
+    }
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    if (push0 != kNone) st[count + __popcll(m0 & lt)] = push0;           // all far children first,
+    if (push1 != kNone) st[count + n0 + __popcll(m1 & lt)] = push1;      // then the near ones on top
+    count += n0 + n1;
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (!overflow) return false;
+  // overflow: lane 0 walks the whole ray serially on the (now free) LDS region
+  bool occ = false;
+  if (lane == 0) occ = anyhit2<1>(sc, st, S, d, point, maxd, nullptr);
+  return __any(occ);
 }
 
 // Returns 1 occluded, 0 visible, -1 when the stack would overflow (the caller

@@ -161,6 +161,27 @@ def test_bvh4_shadows_are_result_preserving(gpu, scene_name, request):
         assert np.array_equal(outs[0][k], outs[1][k], equal_nan=True), k
 
 
+@pytest.mark.parametrize("scene_name", ["scene_small", "scene_nan"])
+def test_cooperative_shadow_walk_is_result_preserving(gpu, scene_name, request):
+    """Shadow rays past the step budget are finished by the wave-cooperative walk (kernels_wavefront.hip
+    wf_shadow_coop): budgets 4 (nearly every ray, including LDS-stack overflows), 16 and 128 (default) give the
+    serial walk's bits (budget 0)."""
+    gl = gpu
+    scene = request.getfixturevalue(scene_name)
+    W, H = 96, 64
+    outs = []
+    for budget in (0, 4, 16, 128):
+        r = _renderer(scene, W, H, mode="fast", run_taa=False, run_output=False)
+        r.pass_path_tracing.set_uniform_int("shadow_budget", budget)
+        for _ in range(2):
+            r.frame()
+        outs.append({k: gl.readback(r.planes()[k]) for k in ("color", "emission", "albedo")})
+        r.close()
+    for o in outs[1:]:
+        for k in o:
+            assert np.array_equal(outs[0][k], o[k], equal_nan=True), k
+
+
 def test_wavefront_equals_megakernel(gpu, scene_small):
     """The staged (wavefront) path tracer and the single-kernel form give identical bits."""
     gl = gpu

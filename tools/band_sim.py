@@ -51,6 +51,8 @@ def sim_rank(rk, bounds, probe=False, K=10):
                        frames_in_flight=int(os.environ.get("FIF", "1")))
     r.pass_path_tracing.set_uniform_int("pt_kernel", int(os.environ.get("PTK", "0")))
     r.pass_path_tracing.set_uniform_int("trace_fork", int(os.environ.get("PTSVGF_TRACE_FORK", "0")))
+    if "SHADOW_BUDGET" in os.environ:
+        r.pass_path_tracing.set_uniform_int("shadow_budget", int(os.environ["SHADOW_BUDGET"]))
     for _ in range(3):
         r.frame()
     torch.cuda.synchronize()
@@ -96,7 +98,8 @@ def report(tag, res):
 
 
 if __name__ == "__main__":
-    eq = [sim_rank(rk, None, probe=True) for rk in range(N)]
+    ranks = [int(v) for v in os.environ["RANKS"].split(",")] if "RANKS" in os.environ else range(N)
+    eq = [sim_rank(rk, None, probe=True) for rk in ranks]
     report("equal bands", eq)
     if N > 1 and os.environ.get("BALANCE", "1") != "0":
         visits = np.concatenate([s["counts"] for s in eq])
