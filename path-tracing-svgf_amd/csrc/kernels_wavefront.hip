@@ -65,40 +65,51 @@ __device__ __forceinline__ bool seg_get(const int* __restrict__ items, const int
   return false;
 }
 
-// Block-wide append of up to one item to each of three lists (live rays, HDR
-// shadow rays, point-light shadow rays). Every thread of the 256-thread block
-// must call it.
-__device__ __forceinline__ void block_push3(bool p0, int v0, int* __restrict__ items0, int* counts0, int cap0,
-                                            bool p1, int v1, int* __restrict__ items1, int* counts1, int cap1,
-                                            bool p2, int v2, int* __restrict__ items2, int* counts2, int cap2) {
-  __shared__ int wc[3][4];
-  __shared__ int base[3];
+// Block-wide append of up to one item to each of the shade lists: the live rays, the HDR shadow rays and the
+// point-light shadow rays, the latter into kPointBins lists by light index (rays toward one light from one
+// screen tile traverse alike, so a trace wave holding one light's rays diverges less). Every thread of the
+// 256-thread block must call it. One atomic per (list, bin) per block.
+constexpr int kLists = 2 + kPointBins;
+__device__ __forceinline__ void block_push_shade(bool p_live, bool p_h, bool p_p, int bin, int v, int* __restrict__ live,
+                                                 int* live_counts, int* __restrict__ shadow, int* shadow_counts,
+                                                 int cap) {
+  __shared__ int wc[kLists][4];
+  __shared__ int base[kLists];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const unsigned long long m0 = __ballot(p0), m1 = __ballot(p1), m2 = __ballot(p2);
-  if (lane == 0) {
-    wc[0][wv] = __popcll(m0);
-    wc[1][wv] = __popcll(m1);
-    wc[2][wv] = __popcll(m2);
-  }
+  unsigned long long m[kLists];
+  m[0] = __ballot(p_live);
+  m[1] = __ballot(p_h);
+#pragma unroll
+  for (int b = 0; b < kPointBins; ++b) m[2 + b] = __ballot(p_p && bin == b);
+  if (lane == 0)
+#pragma unroll
+    for (int l = 0; l < kLists; ++l) wc[l][wv] = __popcll(m[l]);
   __syncthreads();
   const int seg = blockIdx.x % kSeg;
-  if (threadIdx.x < 3) {
+  if (threadIdx.x < kLists) {
     const int l = threadIdx.x;
     const int t = (wc[l][0] + wc[l][1]) + (wc[l][2] + wc[l][3]);
-    int* c = l == 0 ? counts0 : (l == 1 ? counts1 : counts2);
+    int* c = l == 0 ? live_counts : shadow_counts + (l - 1) * kSeg;
     base[l] = t ? atomicAdd(c + seg, t) : 0;
   }
   __syncthreads();
-  int o0 = base[0], o1 = base[1], o2 = base[2];
-  for (int w = 0; w < wv; ++w) {
-    o0 += wc[0][w];
-    o1 += wc[1][w];
-    o2 += wc[2][w];
-  }
   const unsigned long long lt = (1ull << lane) - 1ull;
-  if (p0) items0[seg * cap0 + o0 + __popcll(m0 & lt)] = v0;
-  if (p1) items1[seg * cap1 + o1 + __popcll(m1 & lt)] = v1;
-  if (p2) items2[seg * cap2 + o2 + __popcll(m2 & lt)] = v2;
+  if (p_live) {
+    int o = base[0];
+    for (int w = 0; w < wv; ++w) o += wc[0][w];
+    live[seg * cap + o + __popcll(m[0] & lt)] = v;
+  }
+  if (p_h) {
+    int o = base[1];
+    for (int w = 0; w < wv; ++w) o += wc[1][w];
+    shadow[seg * cap + o + __popcll(m[1] & lt)] = v;
+  }
+  if (p_p) {
+    const int li = 2 + bin;
+    int o = base[li];
+    for (int w = 0; w < wv; ++w) o += wc[li][w];
+    shadow[(size_t)(1 + bin) * kSeg * cap + seg * cap + o + __popcll(m[li] & lt)] = v;
+  }
 }
 
 // load-balancing probe: accumulate traversal steps per band row (only when requested)
@@ -182,14 +193,25 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p,
                                                                       int* __restrict__ strag_count) {
   __shared__ int stk[KS * kTB];
   const int k = blockIdx.x * kTB + threadIdx.x;
-  const int nh = seg_total(counts);  // HDR list first, then the point-light list
+  const int nh = seg_total(counts);  // HDR list first, then the point-light lists bin by bin
   const bool point = k >= nh;
   int pid = -1;
   bool valid = true;
   if (!point) {
     seg_get(list, counts, cap, k, &pid);
-  } else if (!seg_get(list + kSeg * cap, counts + kSeg, cap, k - nh, &pid)) {
+  } else {
+    int r = k - nh;
     valid = false;
+#pragma unroll
+    for (int b = 0; b < kPointBins; ++b) {
+      const int nb = seg_total(counts + (1 + b) * kSeg);
+      if (r < nb) {
+        seg_get(list + (size_t)(1 + b) * kSeg * cap, counts + (1 + b) * kSeg, cap, r, &pid);
+        valid = true;
+        break;
+      }
+      r -= nb;
+    }
   }
   bool deferred = false;
   if (valid) {
@@ -278,6 +300,7 @@ __global__ void __launch_bounds__(256) wf_shade(PTParams p, int bounce, const in
     valid = seg_get(list_in, counts_in, cap, k, &pid);
   }
   bool push = false, need_h = false, need_p = false;
+  int pbin = 0;  // point-light list of this ray (light index mod kPointBins)
   if (valid) {
     int x, y;
     pix_xy(p, pid, &x, &y);
@@ -342,6 +365,7 @@ __global__ void __launch_bounds__(256) wf_shade(PTParams p, int bounce, const in
         if (p.pointLightSize != 0) {
           float ppdf = (2.0f * PT_PI) / (float)p.pointLightSize;
           int li = (int)(u32_to_unit(wang_hash(&seed)) * (float)p.pointLightSize);
+          pbin = li & (kPointBins - 1);
           v3 lpos = splat(0.0f), lrad = splat(0.0f);
           if (li >= 0 && li < p.scene.nlights_buf) {
             const float* lp = p.scene.lights + 6 * li;
@@ -380,8 +404,7 @@ __global__ void __launch_bounds__(256) wf_shade(PTParams p, int bounce, const in
     p.wf.light[pid] = f4(light.x, light.y, light.z, 0.0f);
   }
   // HDR and point-light shadow rays go to separate lists so trace waves stay homogeneous
-  block_push3(push, pid, list_out, counts_out, cap, need_h, pid, shadow_out, shadow_counts, cap, need_p, pid,
-              shadow_out + kSeg * cap, shadow_counts + kSeg, cap);
+  block_push_shade(push, need_h, need_p, pbin, pid, list_out, counts_out, shadow_out, shadow_counts, cap);
 }
 
 // ----------------------------------------------------------------- finish ---
@@ -451,15 +474,15 @@ int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent
   int* lists[2] = {p.wf.list0, p.wf.list1};
   auto closest = [&](int i, hipStream_t st) {
     const int* lin = lists[(i + 1) & 1];
-    const int* live_in = p.wf.counters + 32 * (i - 1);
+    const int* live_in = p.wf.counters + kWfCtr * (i - 1);
     hipLaunchKernelGGL(wf_trace_closest<KS>, dim3(gT), dim3(kTB), 0, st, p, lin, live_in, cap);
   };
   for (int i = 0; i < p.max_depth; ++i) {
     const int* lin = lists[(i + 1) & 1];
     int* lout = lists[i & 1];
-    int* live = p.wf.counters + 32 * i;        // kSeg live-list counts of bounce i
-    int* shadow = p.wf.counters + 32 * i + 8;  // kSeg HDR + kSeg point-light shadow-list counts
-    const int* live_in = p.wf.counters + 32 * (i > 0 ? i - 1 : 0);
+    int* live = p.wf.counters + kWfCtr * i;        // kSeg live-list counts of bounce i
+    int* shadow = p.wf.counters + kWfCtr * i + 8;  // kSeg HDR + kPointBins x kSeg point-light counts
+    const int* live_in = p.wf.counters + kWfCtr * (i > 0 ? i - 1 : 0);
     if (i > 0) {
       if (fork) {
         if ((e = hipStreamWaitEvent(s, ev_join, 0)) != hipSuccess) return (int)e;  // closest(i) done
@@ -475,7 +498,7 @@ int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent
       closest(i + 1, aux);
       if ((e = hipEventRecord(ev_join, aux)) != hipSuccess) return (int)e;
     }
-    int* strag = p.wf.counters + 32 * i + 24;  // shadow rays handed to the cooperative walk
+    int* strag = p.wf.counters + kWfCtr * i + 48;  // shadow rays handed to the cooperative walk
     if (p.scene.bvh4)
       hipLaunchKernelGGL((wf_trace_shadow<KS, true>), dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
                          (const int*)shadow, cap, strag);

@@ -41,7 +41,9 @@ constexpr int kStack = PT_KSTACK;  // traversal stack depth (host checks BVH dep
 constexpr int kStackSmall = 24;    // smaller LDS stack (more resident waves) for trees that fit it
 constexpr int kBlock = 256;      // threads per block for per-pixel kernels
 constexpr int kNoneRef = (int)0x80000000;
-constexpr int kWfCounters = 128;  // wavefront list counters (4 bounces x 32)  // "no node" (leaf refs are >= -(2^31 - 1))
+constexpr int kPointBins = 4;     // point-light shadow lists, one per light index mod 4 (coherent waves)
+constexpr int kWfCtr = 64;        // wavefront list counters per bounce (see WFState::counters)
+constexpr int kWfCounters = 4 * kWfCtr;  // 4 bounces  // "no node" (leaf refs are >= -(2^31 - 1))
 
 struct Plane {          // banded RGBA32F plane
   float4* p;
@@ -95,9 +97,10 @@ struct WFState {
   uint32_t* seed;               // RNG state (path_tracing.frag:433)
   uint8_t *occ_h, *occ_p;       // shadow verdicts
   int *list0, *list1;           // compacted live-ray lists (ping-pong)
-  int* shadow_list;             // compacted shadow rays of one bounce: HDR list, then point-light list
-  int* counters;                // per bounce i: [32i, 32i+8) live-list, [32i+8, 32i+16) HDR and
-                                // [32i+16, 32i+24) point-light segment counts (kWfCounters ints)
+  int* shadow_list;             // compacted shadow rays of one bounce: HDR list, then kPointBins point-light
+                                // lists (by light index), each kSeg segments of `cap`
+  int* counters;                // per bounce i, base 64i: [0, 8) live-list, [8, 16) HDR, [16, 16 + 8 kPointBins)
+                                // point-light segment counts, [48] cooperative-walk stragglers
   uint32_t* row_cost;           // optional: traversal steps per band row (load-balancing probe), may be null
   int* straggler;               // shadow rays past the step budget: pid | (point << 31), count at counters[32i+24]
   uint32_t shadow_budget;       // node + triangle visits before a shadow ray is handed to the cooperative walk (0: never)

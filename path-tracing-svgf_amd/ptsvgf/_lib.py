@@ -44,6 +44,14 @@ class PtError(RuntimeError):
 
 
 def _load(name: str) -> C.CDLL:
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7 and the dynamic loader
+    # binds every later request for that soname to whichever copy came first. Load torch's first, so the
+    # streams and buffers torch hands to the C ABI (renderer frames in flight, bench, dist) live in the
+    # same runtime as the kernels; loading /opt/rocm's first leaves torch without a device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     # PTSVGF_LIB_DIR: an alternative in-tree build (A/B experiments, tools/exp_*.sh)
     path = os.path.join(os.environ.get("PTSVGF_LIB_DIR", LIB_DIR), name)
     if not os.path.exists(path):
