@@ -605,8 +605,14 @@ int draw_pathtrace(Pass* p) {
     Texture* lf = sampler(p, "lastFrame");
     if (lf) TRY(plane_of(lf, p, &k.last, "lastFrame"));
   }
+  // tile subset (PTParams::tile_stride): this pass traces every tile_stride-th 16 x 16 tile of the band
+  k.tile_stride = ui(p, "tile_stride", 1);
+  k.tile_offset = ui(p, "tile_offset", 0);
+  if (wf_subset_tiles(k.W, std::max(0, k.y1 - k.y0), k.tile_stride, k.tile_offset) < 0)
+    return err(PT_ERR_ARG, "tile_offset must lie in [0, tile_stride)");
   int rc;
   if (ui(p, "pt_kernel", 0) == 1) {  // 1: single megakernel (kernels_pt.hip), kept for A/B
+    if (k.tile_stride != 1) return err(PT_ERR_ARG, "tile subsets need the wavefront path tracer");
     rc = launch_pathtrace(k, g.stream);
   } else {                            // 0: wavefront (kernels_wavefront.hip), production
     TRY(wf_alloc(p->wf, k.W, std::max(0, k.y1 - k.y0)));
@@ -615,7 +621,7 @@ int draw_pathtrace(Pass* p) {
     // > 0: shadow rays past this many visits finish in the wave-cooperative walk (A/B switch; off: with frames
     // in flight it measured slower)
     k.wf.shadow_budget = (uint32_t)ui(p, "shadow_budget", 0);
-    const int ntiles = ((k.W + 15) / 16) * ((std::max(0, k.y1 - k.y0) + 15) / 16);  // wf_primary's grid
+    const int ntiles = wf_subset_tiles(k.W, std::max(0, k.y1 - k.y0), k.tile_stride, k.tile_offset);  // wf_primary's grid
     TRY(tile_order_begin(p, ntiles, &k.tiles));
     if (ui(p, "trace_fork", 0) && !p->aux) {  // A/B switch (off: measured slower with frames in flight)
       HIPCHK(hipStreamCreateWithFlags(&p->aux, hipStreamNonBlocking));

@@ -139,8 +139,9 @@ template <int KS>
 __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
   __shared__ int stk[KS * 256];
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-  const int tile = sched_tile(p.tiles, blockIdx.y * gridDim.x + blockIdx.x);  // cost-ordered dispatch
-  const int tx = tile % gridDim.x, ty = tile / gridDim.x;
+  const int tile = sched_tile(p.tiles, blockIdx.x);  // cost-ordered dispatch (subset slot)
+  const int gt = tile * p.tile_stride + p.tile_offset, ntx = (p.W + 15) / 16;
+  const int tx = gt % ntx, ty = gt / ntx;
   const int x = tx * 16 + (wv & 1) * 8 + (ln & 7);
   const int y = p.y0 + ty * 16 + (wv >> 1) * 8 + (ln >> 3);
   const bool valid = x < p.W && y < p.y1;
@@ -292,7 +293,7 @@ __global__ void __launch_bounds__(256) wf_shade(PTParams p, int bounce, const in
     // (tiles.perm_next, sorted right after wf_primary): the rays of expensive tiles are appended to
     // the lists first, so every later list-driven trace launch starts its slowest rays first
     const int ntx = (p.W + 15) / 16;
-    const int tile = p.tiles.cost ? p.tiles.perm_next[blockIdx.x] : (int)blockIdx.x;
+    const int tile = (p.tiles.cost ? p.tiles.perm_next[blockIdx.x] : (int)blockIdx.x) * p.tile_stride + p.tile_offset;
     const int x = (tile % ntx) * 16 + (threadIdx.x & 15), ly = (tile / ntx) * 16 + (threadIdx.x >> 4);
     valid = x < p.W && ly < p.y1 - p.y0;
     pid = ly * p.W + x;
@@ -433,6 +434,10 @@ __global__ void __launch_bounds__(256) wf_finalize(PTParams p) {
   if (k >= p.W * (p.y1 - p.y0)) return;
   int x, y;
   pix_xy(p, k, &x, &y);
+  if (p.tile_stride > 1) {  // pixels of tiles outside the subset keep their contents
+    const int t = ((y - p.y0) >> 4) * ((p.W + 15) / 16) + (x >> 4);
+    if (t % p.tile_stride != p.tile_offset) return;
+  }
   v3 light = vclamp(xyz(p.wf.light[k]), 0.0f, p.clamp_threshold);  // :1110-1113
   v3 color = splat(0.0f);
   if (!f_isnan(light.x) && !f_isnan(light.y) && !f_isnan(light.z)) color = light;
@@ -450,6 +455,13 @@ int wf_list_capacity(int W, int rows) {
   return (blocks + kSeg - 1) / kSeg * 256;
 }
 
+// Tiles of the subset k * stride + offset among the band's 16 x 16 tiles (PTParams::tile_stride).
+int wf_subset_tiles(int W, int rows, int stride, int offset) {
+  const int n = ((W + 15) / 16) * ((rows + 15) / 16);
+  if (stride < 1 || offset < 0 || offset >= stride) return -1;
+  return offset < n ? (n - offset + stride - 1) / stride : 0;
+}
+
 // Launch order of one frame. With an auxiliary stream the closest-hit trace of bounce i+1 (it needs only the
 // rays and live list shade(i) wrote) runs concurrently with the shadow trace and finish of bounce i; the join
 // comes before shade(i+1), which needs both. Two traversal launches then end together, so the frame's
@@ -462,14 +474,15 @@ int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent
   const int cap = wf_list_capacity(p.W, rows);  // per segment; the host sized the lists with the same function
   hipError_t e = hipMemsetAsync(p.wf.counters, 0, kWfCounters * sizeof(int), s);
   if (e != hipSuccess) return (int)e;
-  dim3 tiles((p.W + 15) / 16, (rows + 15) / 16);
-  hipLaunchKernelGGL(wf_primary<KS>, tiles, dim3(256), 0, s, p);
+  const int ntiles = wf_subset_tiles(p.W, rows, p.tile_stride, p.tile_offset);
+  if (ntiles <= 0) return 0;
+  hipLaunchKernelGGL(wf_primary<KS>, dim3(ntiles), dim3(256), 0, s, p);
   if (p.tiles.cost) {  // this frame's primary costs -> tile order of the bounce-0 shade and the next frame
     const int rc = launch_tile_sort(p.tiles.cost, p.tiles.perm_next, p.tiles.ntiles, s);
     if (rc) return rc;
   }
   const int gN = (N + 255) / 256, gT = (N + kTB - 1) / kTB, gT2 = (2 * N + kTB - 1) / kTB;
-  const int gS0 = tiles.x * tiles.y;  // bounce-0 shade: one block per primary tile
+  const int gS0 = ntiles;  // bounce-0 shade: one block per primary tile
   const bool fork = aux && ev_fork && ev_join;
   int* lists[2] = {p.wf.list0, p.wf.list1};
   auto closest = [&](int i, hipStream_t st) {

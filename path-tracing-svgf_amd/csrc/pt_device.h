@@ -124,7 +124,12 @@ struct PTParams {
   int stack_need;       // deepest interior level of the binary BVH (selects the LDS stack size)
   float sobol_u[4], sobol_v[4];  // sobolVec2(frameCounter+1, b): uniform across pixels
   WFState wf;
-  TileSched tiles;      // primary-ray tiles (16 x 16 px)
+  TileSched tiles;      // primary-ray tiles (16 x 16 px), indexed by subset slot (below)
+  // Tile subset (wavefront path tracer only): trace the 16 x 16 tiles t = k * tile_stride + tile_offset of
+  // the band (raster tile order), k = 0 .. tiles.ntiles - 1; other pixels are left untouched. Stride 1,
+  // offset 0 = every tile. Interleaved subsets give every rank of a multi-GPU frame an equal share of the
+  // expensive tiles (ptsvgf.dist, DESIGN.md "Multi-GPU").
+  int tile_stride, tile_offset;
 };
 
 struct GBufParams {
@@ -188,6 +193,7 @@ int launch_pathtrace(const PTParams& p, hipStream_t s);
 int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux = nullptr,
                                hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr);
 int wf_list_capacity(int W, int rows);  // per-segment capacity of the compacted ray lists (8 segments)
+int wf_subset_tiles(int W, int rows, int stride, int offset);  // tiles of a PTParams tile subset (< 0: invalid)
 int launch_gbuffer(const GBufParams& p, hipStream_t s);
 int launch_reproject(const ReprojParams& p, hipStream_t s);
 int launch_variance(const VarianceParams& p, hipStream_t s);

@@ -49,6 +49,7 @@ class BandPlan:
         b = list(self.bounds) if self.bounds is not None else [(self.H * k) // self.world for k in range(self.world + 1)]
         if len(b) != self.world + 1 or b[0] != 0 or b[-1] != self.H or any(x >= y for x, y in zip(b, b[1:])):
             raise ValueError(f"bad band bounds {b}")
+        self.bounds = tuple(b)
         self.y0, self.y1 = b[self.rank], b[self.rank + 1]
         if self.y1 - self.y0 < max(ATROUS_HALO[4], self.reproj_halo):
             raise ValueError(f"band of {self.y1 - self.y0} rows is thinner than the largest halo")
@@ -131,6 +132,7 @@ class BandRenderer:
 
         self.plan = BandPlan(W, H, rank, world, reproj_halo=reproj_halo, bounds=bounds)
         self.dist = dist
+        self.exchange = True  # False only while calibrating (make_band_renderer): ranks time their bands alone
         self._tensors = {}
         gl.set_band(W, H, self.plan.y0, self.plan.y1, self.plan.row0, self.plan.rows)
         dev = torch.device("cuda", torch.cuda.current_device())
@@ -149,6 +151,8 @@ class BandRenderer:
         self.pass_path_tracing = self.r.pass_path_tracing
 
     def _halo(self, stage: str, handles) -> None:
+        if not self.exchange:
+            return
         for st, _, n in HALO_SCHEDULE:
             if st == stage:
                 halo_exchange([self._tensors[h] for h in handles], self.plan, self.plan.rows_for(n), self.dist)
@@ -176,35 +180,65 @@ class BandRenderer:
         self.r.close()
         self._tensors.clear()
 
-    def measure_row_cost(self):
-        """Estimated time (ms) of every frame row, identical on all ranks: one probed frame counts each row's
-        BVH visits (pt_pass_set_row_cost) and times every pass; the per-rank frame times are fitted as
-        T_k = a * visits_k + b * rows_k over the ranks (least squares, a, b >= 0) and spread back onto rows."""
+    def measure_row_cost(self, frames: int = 6):
+        """Estimated time (ms) of every frame row, identical on all ranks.
+
+        One probed frame counts each row's BVH visits (pt_pass_set_row_cost). Then every rank times `frames`
+        frames of its band ALONE (halo exchanges off, so a rank's time is its own work, not its wait for the
+        slowest neighbour) with the renderer's frames in flight: per-launch tails that overlap other frames'
+        work cost nothing, which a serial per-pass timing would count. The per-rank times are spread back onto
+        rows by band_row_cost. Calibration frames are discarded (the renderer is rebuilt afterwards)."""
+        import time
+
         import numpy as np
         import torch
 
-        p, W, H = self.plan, self.r.W, self.r.H
+        p, H = self.plan, self.r.H
         dev = torch.device("cuda", torch.cuda.current_device())
         counts = torch.zeros(p.y1 - p.y0, dtype=torch.int32, device=dev)
-        self.pass_path_tracing.set_row_cost(counts.data_ptr())
-        self.r.profile(True)
-        self.r.frame()
-        torch.cuda.synchronize()
-        times = self.r.pass_times()
-        self.r.profile(False)
-        self.pass_path_tracing.set_row_cost(0)
-        frame_ms = times["frame_sum_ms"]
+        self.exchange = False
+        try:
+            self.pass_path_tracing.set_row_cost(counts.data_ptr())
+            self.r.frame()
+            torch.cuda.synchronize()
+            self.pass_path_tracing.set_row_cost(0)
+            self.r.frame()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(frames):
+                self.r.frame()
+            torch.cuda.synchronize()
+            frame_ms = (time.perf_counter() - t0) * 1e3 / frames
+        finally:
+            self.exchange = True
         visits = torch.zeros(H, dtype=torch.float64, device=dev)
         visits[p.y0:p.y1] = counts.to(torch.float64)
-        per_rank = torch.zeros(3 * p.world, dtype=torch.float64, device=dev)
-        per_rank[3 * p.rank:3 * p.rank + 3] = torch.tensor([counts.sum().item(), p.y1 - p.y0, frame_ms],
-                                                           dtype=torch.float64)
+        per_rank = torch.zeros(p.world, dtype=torch.float64, device=dev)
+        per_rank[p.rank] = frame_ms
         self.dist.all_reduce(visits)
         self.dist.all_reduce(per_rank)
-        v = visits.cpu().numpy()
-        m = per_rank.cpu().numpy().reshape(p.world, 3)
-        a, b = fit_row_cost(m[:, 0], m[:, 1], m[:, 2])
-        return a * v + b
+        return band_row_cost(visits.cpu().numpy(), p.bounds, per_rank.cpu().numpy())
+
+
+def band_row_cost(visits, bounds, ms):
+    """Per-row cost (ms) from per-row BVH visits and the measured time of each band [bounds[k], bounds[k+1]).
+
+    A global model T = a*visits + b*rows (fit_row_cost over the bands) shapes the cost inside a band; each
+    band's rows are then scaled so that they sum to that band's measured time, so the model's misfit (tails,
+    sky rows) cannot move a boundary away from where the measurements put it."""
+    import numpy as np
+
+    v = np.asarray(visits, np.float64)
+    t = np.asarray(ms, np.float64)
+    segs = [(bounds[k], bounds[k + 1]) for k in range(len(bounds) - 1)]
+    a, b = fit_row_cost([v[y0:y1].sum() for y0, y1 in segs], [y1 - y0 for y0, y1 in segs], t)
+    model = a * v + b
+    out = np.empty_like(v)
+    for k, (y0, y1) in enumerate(segs):
+        m = model[y0:y1]
+        s = m.sum()
+        out[y0:y1] = m * (t[k] / s) if s > 0 else t[k] / max(y1 - y0, 1)
+    return out
 
 
 def fit_row_cost(visits, rows, ms):
@@ -225,15 +259,22 @@ def fit_row_cost(visits, rows, ms):
     return 0.0, float(t.sum() / max(A[:, 1].sum(), 1.0))
 
 
-def make_band_renderer(scene, W, H, cfg, rank, world, dist, balance: bool = True, **kw):
+def make_band_renderer(scene, W, H, cfg, rank, world, dist, balance: bool = True, rounds: int = 2, **kw):
     """BandRenderer whose band heights equalise the measured per-row cost (sky rows are cheap, the plant
-    and clock rows expensive). Calibration renders two frames on equal bands (warm-up + probe), then the
-    renderer is rebuilt on the balanced plan; every rank derives the same bounds from all-reduced data."""
+    and clock rows expensive). Each calibration round renders on the current bands, measures every rank's
+    band time and visits (measure_row_cost) and cuts new bands at equal quantiles of the mean of all rounds'
+    per-row cost estimates; the renderer is then rebuilt on the final plan. Every rank derives the same bounds
+    from all-reduced data."""
+    import numpy as np
+
     r = BandRenderer(scene, W, H, cfg, rank, world, dist, **kw)
     if not balance or world == 1:
         return r
-    r.frame()
-    cost = r.measure_row_cost()
-    bounds = balanced_bounds(cost, world)
-    r.close()
-    return BandRenderer(scene, W, H, cfg, rank, world, dist, bounds=bounds, **kw)
+    est = []
+    for _ in range(max(rounds, 1)):
+        r.frame()
+        est.append(r.measure_row_cost())
+        bounds = balanced_bounds(np.mean(est, axis=0), world)
+        r.close()
+        r = BandRenderer(scene, W, H, cfg, rank, world, dist, bounds=bounds, **kw)
+    return r

@@ -147,3 +147,21 @@ def test_balanced_bounds_properties():
     assert abs(a - 0.1) < 1e-9 and abs(c - 0.01) < 1e-9
     a, c = fit_row_cost([10.0, 30.0], [100, 100], [5.0, 1.0])   # negative slope -> single-term fallback
     assert a >= 0 and c >= 0
+
+
+def test_band_row_cost_matches_band_times():
+    """band_row_cost keeps every band's measured time (rows sum to it) and the model's shape inside a band;
+    cutting on it moves rows from a slow band to a fast one."""
+    from ptsvgf.dist import balanced_bounds, band_row_cost
+    rng = np.random.default_rng(5)
+    visits = rng.uniform(0.0, 100.0, 400)
+    visits[300:] = 0.0                                   # sky rows
+    bounds = (0, 100, 200, 300, 400)
+    ms = [3.0, 2.0, 2.0, 0.5]
+    c = band_row_cost(visits, bounds, ms)
+    for k in range(4):
+        assert abs(c[bounds[k]:bounds[k + 1]].sum() - ms[k]) < 1e-9
+    assert (c >= 0).all()
+    nb = balanced_bounds(c, 4)
+    assert nb[1] < 100 and nb[3] < 300                   # the slow first band shrinks, the cheap last one grows
+    assert abs(band_row_cost(np.zeros(400), bounds, ms)[350] - 0.5 / 100) < 1e-12

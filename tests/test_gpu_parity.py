@@ -197,6 +197,39 @@ def test_wavefront_equals_megakernel(gpu, scene_small):
         assert np.array_equal(outs[0][k], outs[1][k]), k
 
 
+@pytest.mark.parametrize("W,H,stride", [(96, 64, 3), (100, 70, 4)])
+def test_tile_subsets_compose_to_full_frame(gpu, scene_small, W, H, stride):
+    """tile_stride / tile_offset: each subset writes exactly its 16x16 tiles (others keep their contents) and
+    the subsets of one frame together give the full-frame bits (ragged edge tiles included)."""
+    gl = gpu
+    a = _renderer(scene_small, W, H, mode="fast", run_taa=False, run_output=False)
+    a.frame()
+    want = {k: gl.readback(a.planes()[k]) for k in ("color", "emission", "albedo")}
+    b = _renderer(scene_small, W, H, mode="fast", run_taa=False, run_output=False)
+    pt = b.pass_path_tracing
+    pt.set_uniform_int("tile_stride", stride)
+    pt.set_uniform_int("tile_offset", 0)
+    b.frame()
+    ntx = (W + 15) // 16
+    ty, tx = np.meshgrid(np.arange(H) // 16, np.arange(W) // 16, indexing="ij")
+    owner = (ty * ntx + tx) % stride
+    got = gl.readback(b.planes()["color"])
+    assert np.array_equal(got[owner == 0], want["color"][owner == 0])
+    assert not got[owner != 0].any()                     # zero-initialised planes, untouched
+    b.camera.frameCounter -= 1                           # the same frame again, the other subsets
+    for off in range(1, stride):
+        pt.set_uniform_int("tile_offset", off)
+        b._path_trace()
+    b.camera.frameCounter += 1
+    for k, v in want.items():
+        assert np.array_equal(gl.readback(b.planes()[k]), v), k
+    pt.set_uniform_int("tile_offset", stride)
+    with pytest.raises(Exception):
+        b._path_trace()
+    a.close()
+    b.close()
+
+
 def test_fast_driver_equals_reference_driver(gpu, scene_small):
     """Pointer-swapped fast driver == main.cpp call sequence with copies, bit for bit."""
     gl = gpu

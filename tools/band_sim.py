@@ -98,15 +98,18 @@ def report(tag, res):
 
 
 if __name__ == "__main__":
+    # calibration as in ptsvgf.dist.make_band_renderer: per-rank band time alone (frames in flight) + row visits,
+    # band_row_cost per round, bounds from the mean of the rounds' estimates
     ranks = [int(v) for v in os.environ["RANKS"].split(",")] if "RANKS" in os.environ else range(N)
-    eq = [sim_rank(rk, None, probe=True) for rk in ranks]
-    report("equal bands", eq)
-    if N > 1 and os.environ.get("BALANCE", "1") != "0":
-        visits = np.concatenate([s["counts"] for s in eq])
-        a, b = D.fit_row_cost([s["counts"].sum() for s in eq], [s["y1"] - s["y0"] for s in eq],
-                              [s["gpu"] for s in eq])
-        bounds = D.balanced_bounds(a * visits + b, N)
-        print("fit a=%.3e b=%.3e bounds %s" % (a, b, bounds))
-        bal = [sim_rank(rk, bounds) for rk in range(N)]
-        report("balanced bands", bal)
+    res = [sim_rank(rk, None, probe=True) for rk in ranks]
+    report("equal bands", res)
+    bounds = tuple(D.BandPlan(W, H, 0, N).bounds)
+    est = []
+    for rnd in range(int(os.environ.get("ROUNDS", "2")) if N > 1 and os.environ.get("BALANCE", "1") != "0" else 0):
+        visits = np.concatenate([s["counts"] for s in res])
+        est.append(D.band_row_cost(visits, bounds, [s["wall"] for s in res]))
+        bounds = D.balanced_bounds(np.mean(est, axis=0), N)
+        print("round %d bounds %s" % (rnd, bounds))
+        res = [sim_rank(rk, bounds, probe=True) for rk in range(N)]
+        report(f"balanced bands (round {rnd})", res)
     gl.shutdown()
