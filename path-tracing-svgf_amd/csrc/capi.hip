@@ -14,6 +14,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -139,6 +140,8 @@ struct SceneGPU {
   float4* shade = nullptr;
   float4* bvh = nullptr;
   float4* bvh4 = nullptr;
+  float4* bvh_any = nullptr;  // any-hit tree over the reference leaves (build_anyhit_tree)
+  int root_any = 0, need_any = 0;
   bool has4 = false;
   int root4 = 0;
   int stack_need = 0;
@@ -334,6 +337,187 @@ int pack_bvh4(const float* node_enc, int nnodes, int ntris, std::vector<float4>&
   return PT_OK;
 }
 
+// ------------------------------------------------------ binned SAH trees ---
+// Trees whose answer does not depend on their shape, built for speed instead of
+// reference compatibility (the reference's buildBVHwithSAH caps costs at INF =
+// 114514 and falls back to median-x splits near the root of a 30k-triangle
+// scene):
+//  * the G-buffer tree over the raster triangles: its walk keeps the closest t
+//    with ties to the lower original index and widened boxes only cull, so any
+//    tree gives the same pixel;
+//  * the any-hit (shadow) tree over the REFERENCE tree's leaves: its leaves are
+//    exactly the reference leaves (same triangle ranges, same boxes) and every
+//    interior box is an exact min/max union of them. A triangle is tested iff its
+//    leaf box passes the slab test in either tree (an enclosing box passes
+//    whenever an enclosed one does: slab rounding is monotone), so shadow
+//    verdicts are those of the reference tree.
+// A primitive is one triangle (G-buffer) or one reference leaf (any-hit).
+struct SahPrim {
+  float lo[3], hi[3];
+  int weight;  // triangles it holds (SAH intersection cost)
+  int ref;     // leaf ref it emits alone (any-hit tree), or its index (G-buffer)
+};
+struct SahNode {
+  float lo[3], hi[3];
+  int left = -1, right = -1;  // children (interior)
+  int first = 0, n = 0;       // primitive range (leaf)
+};
+
+static float sah_area(const float* lo, const float* hi) {
+  const float dx = std::max(hi[0] - lo[0], 0.0f), dy = std::max(hi[1] - lo[1], 0.0f), dz = std::max(hi[2] - lo[2], 0.0f);
+  return dx * dy + dy * dz + dz * dx;
+}
+
+// 16-bin SAH over primitive centroids (cost: 1 per node visit, `weight` per primitive test).
+// max_leaf: the most primitives a leaf may hold (leaves also stop at 15 triangles, the leaf ref's limit).
+static int sah_build(std::vector<SahPrim>& pr, int l, int r, int max_leaf, std::vector<SahNode>& nodes) {
+  const int id = (int)nodes.size();
+  nodes.emplace_back();
+  SahNode nd;
+  float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int a = 0; a < 3; ++a) { nd.lo[a] = INFINITY; nd.hi[a] = -INFINITY; }
+  int w = 0;
+  for (int i = l; i < r; ++i) {
+    for (int a = 0; a < 3; ++a) {
+      nd.lo[a] = std::min(nd.lo[a], pr[i].lo[a]);
+      nd.hi[a] = std::max(nd.hi[a], pr[i].hi[a]);
+      const float c = 0.5f * (pr[i].lo[a] + pr[i].hi[a]);
+      clo[a] = std::min(clo[a], c);
+      chi[a] = std::max(chi[a], c);
+    }
+    w += pr[i].weight;
+  }
+  const int n = r - l;
+  constexpr int kBins = 16;
+  float best = INFINITY;
+  int bax = -1, bsplit = 0;
+  if (n > 1) {
+    for (int a = 0; a < 3; ++a) {
+      const float ext = chi[a] - clo[a];
+      if (!(ext > 0.0f)) continue;
+      float blo[kBins][3], bhi[kBins][3];
+      int bw[kBins] = {0}, bn[kBins] = {0};
+      for (int b = 0; b < kBins; ++b)
+        for (int k = 0; k < 3; ++k) { blo[b][k] = INFINITY; bhi[b][k] = -INFINITY; }
+      for (int i = l; i < r; ++i) {
+        const float c = 0.5f * (pr[i].lo[a] + pr[i].hi[a]);
+        const int b = std::min(kBins - 1, (int)((c - clo[a]) / ext * kBins));
+        ++bn[b];
+        bw[b] += pr[i].weight;
+        for (int k = 0; k < 3; ++k) { blo[b][k] = std::min(blo[b][k], pr[i].lo[k]); bhi[b][k] = std::max(bhi[b][k], pr[i].hi[k]); }
+      }
+      float rlo[kBins][3], rhi[kBins][3];
+      int rw[kBins], rn[kBins];
+      for (int b = kBins - 1; b >= 0; --b) {
+        for (int k = 0; k < 3; ++k) {
+          rlo[b][k] = b + 1 < kBins ? std::min(rlo[b + 1][k], blo[b][k]) : blo[b][k];
+          rhi[b][k] = b + 1 < kBins ? std::max(rhi[b + 1][k], bhi[b][k]) : bhi[b][k];
+        }
+        rw[b] = (b + 1 < kBins ? rw[b + 1] : 0) + bw[b];
+        rn[b] = (b + 1 < kBins ? rn[b + 1] : 0) + bn[b];
+      }
+      float llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+      int lw = 0, ln = 0;
+      for (int b = 0; b + 1 < kBins; ++b) {
+        for (int k = 0; k < 3; ++k) { llo[k] = std::min(llo[k], blo[b][k]); lhi[k] = std::max(lhi[k], bhi[b][k]); }
+        lw += bw[b];
+        ln += bn[b];
+        if (ln == 0 || rn[b + 1] == 0) continue;
+        const float c = sah_area(llo, lhi) * lw + sah_area(rlo[b + 1], rhi[b + 1]) * rw[b + 1];
+        if (c < best) { best = c; bax = a; bsplit = b; }
+      }
+    }
+  }
+  const float area = sah_area(nd.lo, nd.hi);
+  const bool fits = n <= max_leaf && w <= 15;
+  if (n == 1 || (fits && (bax < 0 || !(area > 0.0f) || 1.0f + best / area >= (float)w))) {
+    nd.first = l;
+    nd.n = n;
+    nodes[id] = nd;
+    return id;
+  }
+  int m;
+  if (bax >= 0) {
+    const float ext = chi[bax] - clo[bax];
+    m = (int)(std::partition(pr.begin() + l, pr.begin() + r, [&](const SahPrim& q) {
+          const float c = 0.5f * (q.lo[bax] + q.hi[bax]);
+          return std::min(kBins - 1, (int)((c - clo[bax]) / ext * kBins)) <= bsplit;
+        }) - pr.begin());
+  } else {
+    m = l + n / 2;  // coincident centroids: halve the range
+  }
+  nd.left = sah_build(pr, l, m, max_leaf, nodes);
+  nd.right = sah_build(pr, m, r, max_leaf, nodes);
+  nodes[id] = nd;
+  return id;
+}
+
+// Pack a SahNode tree in pack_bvh's layout (DFS order, 4 x float4 per interior node).
+// leaf_ref(first, n) gives the ref of a leaf holding primitives [first, first + n).
+static int pack_sah(const std::vector<SahNode>& nodes, const std::function<int(int, int)>& leaf_ref,
+                    std::vector<float4>& out, int* root_ref, int* need) {
+  *need = 0;
+  out.clear();
+  if (nodes[0].n > 0) {
+    *root_ref = leaf_ref(nodes[0].first, nodes[0].n);
+    return PT_OK;
+  }
+  std::vector<int> idx(nodes.size(), -1), order;
+  struct Item { int id, depth; };
+  std::vector<Item> st{{0, 1}};
+  while (!st.empty()) {
+    const Item it = st.back();
+    st.pop_back();
+    if (it.depth >= kStack) return err(PT_ERR_FORMAT, "SAH tree deeper than the traversal stack");
+    *need = std::max(*need, it.depth);
+    idx[it.id] = (int)order.size();
+    order.push_back(it.id);
+    const SahNode& n = nodes[it.id];
+    if (nodes[n.right].n == 0) st.push_back({n.right, it.depth + 1});
+    if (nodes[n.left].n == 0) st.push_back({n.left, it.depth + 1});
+  }
+  out.assign(order.size() * 4, float4{0, 0, 0, 0});
+  for (size_t k = 0; k < order.size(); ++k) {
+    const SahNode& n = nodes[order[k]];
+    const SahNode& L = nodes[n.left];
+    const SahNode& R = nodes[n.right];
+    const int rl = L.n > 0 ? leaf_ref(L.first, L.n) : idx[n.left];
+    const int rr = R.n > 0 ? leaf_ref(R.first, R.n) : idx[n.right];
+    float4* q = &out[4 * k];
+    q[0] = float4{L.lo[0], L.lo[1], L.lo[2], L.hi[0]};
+    q[1] = float4{L.hi[1], L.hi[2], R.lo[0], R.lo[1]};
+    q[2] = float4{R.lo[2], R.hi[0], R.hi[1], R.hi[2]};
+    float a, b;
+    memcpy(&a, &rl, 4);
+    memcpy(&b, &rr, 4);
+    q[3] = float4{a, b, 0, 0};
+  }
+  *root_ref = 0;
+  return PT_OK;
+}
+
+// Any-hit tree over the leaves of the reference tree (see above).
+int build_anyhit_tree(const float* node_enc, int nnodes, int ntris, std::vector<float4>& out, int* root_ref,
+                      int* need) {
+  std::vector<SahPrim> pr;
+  for (int i = 1; i < nnodes; ++i) {
+    const float* f = node_enc + (size_t)i * 12;
+    const int n = (int)f[3], first = (int)f[4];
+    if (n <= 0) continue;
+    if (n > 15 || first < 0 || first + n > ntris) return err(PT_ERR_FORMAT, "BVH leaf out of range");
+    SahPrim q;
+    for (int a = 0; a < 3; ++a) { q.lo[a] = f[6 + a]; q.hi[a] = f[9 + a]; }
+    q.weight = n;
+    q.ref = -(first * 16 + n) - 1;
+    pr.push_back(q);
+  }
+  if (pr.empty()) return err(PT_ERR_FORMAT, "BVH without leaves");
+  std::vector<SahNode> nodes;
+  nodes.reserve(2 * pr.size());
+  sah_build(pr, 0, (int)pr.size(), 1, nodes);
+  return pack_sah(nodes, [&](int first, int) { return pr[first].ref; }, out, root_ref, need);
+}
+
 template <class T>
 int upload_vec(const std::vector<T>& v, T** dst) {
   if (*dst) { (void)hipFree(*dst); *dst = nullptr; }
@@ -382,6 +566,14 @@ int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU*
   if (sg.has4 && (rc = upload_vec(bvh4.empty() ? std::vector<float4>{float4{0, 0, 0, 0}} : bvh4, &sg.bvh4)) != PT_OK)
     return rc;
   sg.root4 = root4;
+  {
+    std::vector<float4> any;
+    if ((rc = build_anyhit_tree((const float*)nodes->host.data(), (int)nnodes, (int)ntris, any, &sg.root_any,
+                                &sg.need_any)) != PT_OK)
+      return rc;
+    if (any.empty()) any.push_back(float4{0, 0, 0, 0});
+    if ((rc = upload_vec(any, &sg.bvh_any)) != PT_OK) return rc;
+  }
   if ((rc = upload_vec(geom, &sg.geom)) != PT_OK) return rc;
   if ((rc = upload_vec(shade, &sg.shade)) != PT_OK) return rc;
   if (bvh.empty()) bvh.push_back(float4{0, 0, 0, 0});
@@ -560,6 +752,11 @@ int draw_pathtrace(Pass* p) {
   k.scene.bvh = sg->bvh;
   k.scene.root_ref = sg->root_ref;
   k.stack_need = sg->stack_need;
+  if (ui(p, "shadow_tree", 1)) {  // A/B switch: 0 = shadow rays walk the reference tree
+    k.scene.bvh_any = sg->bvh_any;
+    k.scene.root_any = sg->root_any;
+    k.stack_need = std::max(k.stack_need, sg->need_any);
+  }
   k.scene.bvh4 = (sg->has4 && ui(p, "shadow_bvh4", 0)) ? sg->bvh4 : nullptr;  // 1: 4-wide any-hit (A/B; slower here)
   k.scene.root4 = sg->root4;
   k.scene.ntris = sg->ntris;
@@ -832,6 +1029,7 @@ int pt_shutdown(void) {
     if (kv.second.shade) (void)hipFree(kv.second.shade);
     if (kv.second.bvh) (void)hipFree(kv.second.bvh);
     if (kv.second.bvh4) (void)hipFree(kv.second.bvh4);
+    if (kv.second.bvh_any) (void)hipFree(kv.second.bvh_any);
   }
   if (g.own) (void)hipStreamDestroy(g.own);
   g = Lib();
@@ -1119,40 +1317,42 @@ int pt_raster_pass_bind(uint32_t pass, const float* verts, size_t n_floats) {
   p->raster.ntris = ntris;
   p->bound = true;
   if (ntris == 0) return PT_OK;
-  // SAH BVH over the raster triangles (same builder as the scene), objIndex = original index
-  const float mat[PTS_MATERIAL_FLOATS] = {0};
-  pts_scene* s = pts_scene_create();
-  if (pts_scene_add_raw(s, verts, ntris, mat, -1) != 0 || pts_scene_build_bvh(s, 8) != 0) {
-    std::string m = pts_last_error();
-    pts_scene_destroy(s);
-    return err(PT_ERR_ARG, "raster BVH: " + m);
+  // binned SAH tree over the raster triangles (sah_build: the walk's answer does not depend on the tree);
+  // geom in leaf order, objIndex = original index (the depth-test tie rule)
+  std::vector<SahPrim> pr((size_t)ntris);
+  for (int i = 0; i < ntris; ++i) {
+    const float* q = verts + (size_t)i * 18;
+    for (int a = 0; a < 3; ++a) {
+      pr[i].lo[a] = std::min(q[a], std::min(q[6 + a], q[12 + a]));
+      pr[i].hi[a] = std::max(q[a], std::max(q[6 + a], q[12 + a]));
+    }
+    pr[i].weight = 1;
+    pr[i].ref = i;
   }
-  int64_t cnt[6];
-  pts_scene_counts(s, cnt);
-  std::vector<float> te((size_t)cnt[0] * 45), ne((size_t)cnt[1] * 12);
-  pts_scene_encode(s, te.data(), ne.data(), nullptr);
-  pts_scene_destroy(s);
+  std::vector<SahNode> tree;
+  tree.reserve(2 * (size_t)ntris);
+  sah_build(pr, 0, ntris, 8, tree);  // leaves of <= 8 (measured: 2 and 4 slower, tools/exp_tree_ab.sh)
   using namespace glsl;
   std::vector<float4> geom((size_t)ntris * 7);
-  for (int i = 0; i < ntris; ++i) {
-    const float* f = &te[(size_t)i * 45];
-    v3 p1 = mk(f[0], f[1], f[2]), p2 = mk(f[3], f[4], f[5]), p3 = mk(f[6], f[7], f[8]);
+  for (int k = 0; k < ntris; ++k) {
+    const int oi = pr[k].ref;
+    const float* f = verts + (size_t)oi * 18;
+    v3 p1 = mk(f[0], f[1], f[2]), p2 = mk(f[6], f[7], f[8]), p3 = mk(f[12], f[13], f[14]);
     v3 e1 = sub(p2, p1), e2 = sub(p3, p1), ng = cross(e1, e2);
-    int oi = (int)f[42];
     float oif;
     memcpy(&oif, &oi, 4);
-    float4* q = &geom[(size_t)i * 7];
+    float4* q = &geom[(size_t)k * 7];
     q[0] = float4{p1.x, p1.y, p1.z, oif};
     q[1] = float4{e1.x, e1.y, e1.z, 0};
     q[2] = float4{e2.x, e2.y, e2.z, 0};
     q[3] = float4{ng.x, ng.y, ng.z, 0};
-    q[4] = float4{f[9], f[10], f[11], 0};
-    q[5] = float4{f[12], f[13], f[14], 0};
+    q[4] = float4{f[3], f[4], f[5], 0};
+    q[5] = float4{f[9], f[10], f[11], 0};
     q[6] = float4{f[15], f[16], f[17], 0};
   }
   std::vector<float4> bvh;
   int root = 0;
-  TRY(pack_bvh(ne.data(), (int)cnt[1], bvh, &root, ntris, &p->raster.stack_need));
+  TRY(pack_sah(tree, [](int first, int n) { return -(first * 16 + n) - 1; }, bvh, &root, &p->raster.stack_need));
   if (bvh.empty()) bvh.push_back(float4{0, 0, 0, 0});
   TRY(upload_vec(geom, &p->raster.geom));
   TRY(upload_vec(bvh, &p->raster.bvh));

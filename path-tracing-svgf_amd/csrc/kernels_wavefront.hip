@@ -221,8 +221,8 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p,
     const float4 dir = point ? p.wf.sh_p[pid] : p.wf.sh_h[pid];  // point: (direction, distance)
     int occ = WIDE ? anyhit4<kTB, KS>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps) : -1;
     if (occ < 0)  // binary walk (default), or the 4-wide stack overflowed
-      occ = anyhit2<kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps, p.wf.shadow_budget,
-                         &deferred);
+      occ = anyhit2<kTB>(anyhit_scene(p.scene), stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps,
+                         p.wf.shadow_budget, &deferred);
     if (!deferred) (point ? p.wf.occ_p : p.wf.occ_h)[pid] = occ;
     add_row_cost(p, pid / p.W, pid, steps);
   }
@@ -252,7 +252,7 @@ __global__ void __launch_bounds__(64 * kCoopWaves) wf_shadow_coop(PTParams p, co
     const int pid = item & 0x7fffffff;
     const float4 o = p.wf.ray_o[pid];
     const float4 dir = point ? p.wf.sh_p[pid] : p.wf.sh_h[pid];
-    const bool occ = shadow_coop_walk(p.scene, st[wv], kCoopCap, xyz(o), xyz(dir), point, dir.w);
+    const bool occ = shadow_coop_walk(anyhit_scene(p.scene), st[wv], kCoopCap, xyz(o), xyz(dir), point, dir.w);
     if ((threadIdx.x & 63) == 0) (point ? p.wf.occ_p : p.wf.occ_h)[pid] = occ;
   }
 }

@@ -78,6 +78,8 @@ struct SceneDev {
   int root_ref;         // >= 0 interior node index, < 0 leaf ref
   const float4* bvh4;   // 4-wide collapse of bvh for any-hit rays (7 x float4 / node), may be null
   int root4;
+  const float4* bvh_any;  // binary any-hit tree over bvh's leaves (capi.hip build_anyhit_tree), may be null
+  int root_any;
   int ntris;
   const float* lights;  // 6 floats per light (PointLight: position, radiance)
   int nlights_buf;      // lights actually present in the buffer
@@ -208,6 +210,15 @@ int launch_tile_sort(uint32_t* cost, int* perm, int ntiles, hipStream_t s);  // 
 }  // namespace ptk
 
 namespace ptk {
+// The tree shadow (any-hit) rays walk: bvh_any when present (same verdicts), else the reference tree.
+__device__ __forceinline__ SceneDev anyhit_scene(const SceneDev& s) {
+  SceneDev r = s;
+  if (s.bvh_any) {
+    r.bvh = s.bvh_any;
+    r.root_ref = s.root_any;
+  }
+  return r;
+}
 __device__ __forceinline__ int sched_tile(const TileSched& t, int slot) { return t.perm ? t.perm[slot] : slot; }
 // Call with every lane of the wave active (steps = 0 for lanes without a ray).
 __device__ __forceinline__ void sched_cost(const TileSched& t, int tile, uint32_t steps) {
