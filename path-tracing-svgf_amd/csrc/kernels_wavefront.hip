@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
     v3 d = primary_dir(p, x, y);
     float t;
     int tri = traverse<0, 256>(p.scene, stk + threadIdx.x, S, d, 0.0f, p.prune, &t, &steps);
-    p.wf.hit[pid] = make_int2(tri, __float_as_int(t));
+    stnt(&p.wf.hit[pid], make_int2(tri, __float_as_int(t)));
   }
 #ifdef PT_WAVE_TIMES  // investigation build: per wave (start, end, max steps) in the row-cost buffer
   uint32_t ms = steps;
@@ -179,11 +179,11 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest(PTParams p
   const int k = blockIdx.x * kTB + threadIdx.x;
   int pid;
   if (!seg_get(list, counts, cap, k, &pid)) return;
-  float4 o = p.wf.ray_o[pid], dd = p.wf.ray_d[pid];
+  float4 o = ldnt(&p.wf.ray_o[pid]), dd = ldnt(&p.wf.ray_d[pid]);
   float t;
   uint32_t steps;
   int tri = traverse<0, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dd), 0.0f, p.prune, &t, &steps);
-  p.wf.hit[pid] = make_int2(tri, __float_as_int(t));
+  stnt(&p.wf.hit[pid], make_int2(tri, __float_as_int(t)));
   add_row_cost(p, pid / p.W, pid, steps);
 }
 
@@ -216,9 +216,9 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p,
   }
   bool deferred = false;
   if (valid) {
-    float4 o = p.wf.ray_o[pid];
+    float4 o = ldnt(&p.wf.ray_o[pid]);
     uint32_t steps = 0;
-    const float4 dir = point ? p.wf.sh_p[pid] : p.wf.sh_h[pid];  // point: (direction, distance)
+    const float4 dir = point ? ldnt(&p.wf.sh_p[pid]) : ldnt(&p.wf.sh_h[pid]);  // point: (direction, distance)
     int occ = WIDE ? anyhit4<kTB, KS>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps) : -1;
     if (occ < 0)  // binary walk (default), or the 4-wide stack overflowed
       occ = anyhit2<kTB>(anyhit_scene(p.scene), stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps,
@@ -250,8 +250,8 @@ __global__ void __launch_bounds__(64 * kCoopWaves) wf_shadow_coop(PTParams p, co
     const int item = p.wf.straggler[r];
     const bool point = item < 0;
     const int pid = item & 0x7fffffff;
-    const float4 o = p.wf.ray_o[pid];
-    const float4 dir = point ? p.wf.sh_p[pid] : p.wf.sh_h[pid];
+    const float4 o = ldnt(&p.wf.ray_o[pid]);
+    const float4 dir = point ? ldnt(&p.wf.sh_p[pid]) : ldnt(&p.wf.sh_h[pid]);
     const bool occ = shadow_coop_walk(anyhit_scene(p.scene), st[wv], kCoopCap, xyz(o), xyz(dir), point, dir.w);
     if ((threadIdx.x & 63) == 0) (point ? p.wf.occ_p : p.wf.occ_h)[pid] = occ;
   }
@@ -305,7 +305,7 @@ __global__ void __launch_bounds__(256) wf_shade(PTParams p, int bounce, const in
   if (valid) {
     int x, y;
     pix_xy(p, pid, &x, &y);
-    int2 hr = p.wf.hit[pid];
+    int2 hr = ldnt(&p.wf.hit[pid]);
     v3 S, d;
     uint32_t seed;
     v3 light, red;
@@ -318,11 +318,11 @@ __global__ void __launch_bounds__(256) wf_shade(PTParams p, int bounce, const in
       light = splat(0.0f);
       red = splat(1.0f);
     } else {
-      S = xyz(p.wf.ray_o[pid]);
-      d = xyz(p.wf.ray_d[pid]);
-      seed = p.wf.seed[pid];
-      light = xyz(p.wf.light[pid]);
-      red = xyz(p.wf.red[pid]);
+      S = xyz(ldnt(&p.wf.ray_o[pid]));
+      d = xyz(ldnt(&p.wf.ray_d[pid]));
+      seed = ldnt(&p.wf.seed[pid]);
+      light = xyz(ldnt(&p.wf.light[pid]));
+      red = xyz(ldnt(&p.wf.red[pid]));
     }
     if (hr.x < 0) {  // miss (:1084-1087)
       light = add(light, mul(hdr_color(p, d), red));
@@ -388,21 +388,21 @@ __global__ void __launch_bounds__(256) wf_shade(PTParams p, int bounce, const in
         const bool pz = zero_bits(pcalc);
         need_p = shp.w >= 0.0f && !pz;
         need_h = !(pz && zero_bits(hcalc) && zero_bits(bcalc) && __builtin_isfinite(hpdf) && __builtin_isfinite(bpdf));
-        p.wf.pend0[pid] = f4(hcalc.x, hcalc.y, hcalc.z, hpdf);
-        p.wf.pend1[pid] = f4(pcalc.x, pcalc.y, pcalc.z, bpdf);
-        p.wf.pend2[pid] = f4(bcalc.x, bcalc.y, bcalc.z, 0.0f);
-        p.wf.pend3[pid] = f4(cosb.x, cosb.y, cosb.z, 0.0f);
-        p.wf.sh_h[pid] = f4(hd.x, hd.y, hd.z, 0.0f);
-        p.wf.sh_p[pid] = shp;
-        p.wf.ray_o[pid] = f4(h.P.x, h.P.y, h.P.z, 0.0f);
-        p.wf.ray_d[pid] = f4(L.x, L.y, L.z, 0.0f);
-        p.wf.red[pid] = f4(red.x, red.y, red.z, 0.0f);
-        p.wf.occ_h[pid] = 0;
-        p.wf.occ_p[pid] = 0;
+        stnt(&p.wf.pend0[pid], f4(hcalc.x, hcalc.y, hcalc.z, hpdf));
+        stnt(&p.wf.pend1[pid], f4(pcalc.x, pcalc.y, pcalc.z, bpdf));
+        stnt(&p.wf.pend2[pid], f4(bcalc.x, bcalc.y, bcalc.z, 0.0f));
+        stnt(&p.wf.pend3[pid], f4(cosb.x, cosb.y, cosb.z, 0.0f));
+        stnt(&p.wf.sh_h[pid], f4(hd.x, hd.y, hd.z, 0.0f));
+        stnt(&p.wf.sh_p[pid], shp);
+        stnt(&p.wf.ray_o[pid], f4(h.P.x, h.P.y, h.P.z, 0.0f));
+        stnt(&p.wf.ray_d[pid], f4(L.x, L.y, L.z, 0.0f));
+        stnt(&p.wf.red[pid], f4(red.x, red.y, red.z, 0.0f));
+        stnt(&p.wf.occ_h[pid], (uint8_t)0);
+        stnt(&p.wf.occ_p[pid], (uint8_t)0);
       }
     }
-    p.wf.seed[pid] = seed;
-    p.wf.light[pid] = f4(light.x, light.y, light.z, 0.0f);
+    stnt(&p.wf.seed[pid], seed);
+    stnt(&p.wf.light[pid], f4(light.x, light.y, light.z, 0.0f));
   }
   // HDR and point-light shadow rays go to separate lists so trace waves stay homogeneous
   block_push_shade(push, need_h, need_p, pbin, pid, list_out, counts_out, shadow_out, shadow_counts, cap);
@@ -414,18 +414,18 @@ __global__ void __launch_bounds__(256) wf_finish(PTParams p, const int* __restri
   const int k = blockIdx.x * 256 + threadIdx.x;
   int pid;
   if (!seg_get(list, counts, cap, k, &pid)) return;
-  float4 q0 = p.wf.pend0[pid], q1 = p.wf.pend1[pid], q2 = p.wf.pend2[pid], q3 = p.wf.pend3[pid];
+  float4 q0 = ldnt(&p.wf.pend0[pid]), q1 = ldnt(&p.wf.pend1[pid]), q2 = ldnt(&p.wf.pend2[pid]), q3 = ldnt(&p.wf.pend3[pid]);
   NeeTerms nt;
   nt.hcalc = xyz(q0); nt.pcalc = xyz(q1); nt.bcalc = xyz(q2);
   nt.hpdf = q0.w; nt.bpdf = q1.w;
   nt.ppdf = p.pointLightSize != 0 ? (2.0f * PT_PI) / (float)p.pointLightSize : 0.0f;
   v3 cosb = xyz(q3);
-  v3 red = xyz(p.wf.red[pid]), light = xyz(p.wf.light[pid]);
+  v3 red = xyz(ldnt(&p.wf.red[pid])), light = xyz(ldnt(&p.wf.light[pid]));
   v3 hitLight = nee_hit_light(red, nt, p.wf.occ_h[pid] != 0, p.wf.occ_p[pid] != 0);
   red = mul(red, divs(cosb, nt.bpdf));
   light = add(light, hitLight);
-  p.wf.red[pid] = f4(red.x, red.y, red.z, 0.0f);
-  p.wf.light[pid] = f4(light.x, light.y, light.z, 0.0f);
+  stnt(&p.wf.red[pid], f4(red.x, red.y, red.z, 0.0f));
+  stnt(&p.wf.light[pid], f4(light.x, light.y, light.z, 0.0f));
 }
 
 // --------------------------------------------------------------- finalize ---
@@ -438,7 +438,7 @@ __global__ void __launch_bounds__(256) wf_finalize(PTParams p) {
     const int t = ((y - p.y0) >> 4) * ((p.W + 15) / 16) + (x >> 4);
     if (t % p.tile_stride != p.tile_offset) return;
   }
-  v3 light = vclamp(xyz(p.wf.light[k]), 0.0f, p.clamp_threshold);  // :1110-1113
+  v3 light = vclamp(xyz(ldnt(&p.wf.light[k])), 0.0f, p.clamp_threshold);  // :1110-1113
   v3 color = splat(0.0f);
   if (!f_isnan(light.x) && !f_isnan(light.y) && !f_isnan(light.z)) color = light;
   if (p.accumulate && p.last.p) {  // :1116-1119

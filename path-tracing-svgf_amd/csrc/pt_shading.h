@@ -21,7 +21,63 @@ __device__ __forceinline__ int prow(const Plane& P, int y) {
   return ly < 0 ? 0 : (ly >= P.rows ? P.rows - 1 : ly);
 }
 __device__ __forceinline__ float4 pld(const Plane& P, int x, int y) { return P.p[(size_t)prow(P, y) * P.W + x]; }
-__device__ __forceinline__ void pst(const Plane& P, int x, int y, float4 v) { P.p[(size_t)prow(P, y) * P.W + x] = v; }
+// Streaming (non-temporal) access to per-pixel state and output planes: each element is touched once per
+// launch, so it should not evict the scene (BVH nodes, triangles: ~7 MB) from the 4 MB per-XCD L2 that every
+// traversal step reads. Values are unchanged; only the cache policy differs.
+#ifndef PT_NT
+#define PT_NT 1
+#endif
+typedef float ptk_f4v __attribute__((ext_vector_type(4)));
+typedef int ptk_i2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 ldnt(const float4* p) {
+#if PT_NT
+  const ptk_f4v v = __builtin_nontemporal_load((const ptk_f4v*)p);
+  return make_float4(v.x, v.y, v.z, v.w);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ void stnt(float4* p, float4 a) {
+#if PT_NT
+  const ptk_f4v v = {a.x, a.y, a.z, a.w};
+  __builtin_nontemporal_store(v, (ptk_f4v*)p);
+#else
+  *p = a;
+#endif
+}
+__device__ __forceinline__ int2 ldnt(const int2* p) {
+#if PT_NT
+  const ptk_i2v v = __builtin_nontemporal_load((const ptk_i2v*)p);
+  return make_int2(v.x, v.y);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ void stnt(int2* p, int2 a) {
+#if PT_NT
+  const ptk_i2v v = {a.x, a.y};
+  __builtin_nontemporal_store(v, (ptk_i2v*)p);
+#else
+  *p = a;
+#endif
+}
+template <class T>
+__device__ __forceinline__ T ldnt(const T* p) {
+#if PT_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+template <class T>
+__device__ __forceinline__ void stnt(T* p, T a) {
+#if PT_NT
+  __builtin_nontemporal_store(a, p);
+#else
+  *p = a;
+#endif
+}
+__device__ __forceinline__ void pst(const Plane& P, int x, int y, float4 v) { stnt(P.p + (size_t)prow(P, y) * P.W + x, v); }
 __device__ __forceinline__ float4 f4(float x, float y, float z, float w) {
   float4 r;
   r.x = x; r.y = y; r.z = z; r.w = w;
