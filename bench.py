@@ -66,8 +66,9 @@ def parse():
     ap.add_argument("--equal-bands", action="store_true", help="multi-GPU: equal band heights (no cost balancing)")
     ap.add_argument("--breakdown", action="store_true", help="print per-pass ms to stderr")
     ap.add_argument("--pt-kernel", type=int, default=0, help="0 wavefront (production), 1 megakernel (A/B)")
-    ap.add_argument("--frames-in-flight", type=int, default=4,
-                    help="K > 1: front ends (G-buffer + path tracer) of K frames overlap on K streams")
+    ap.add_argument("--frames-in-flight", type=int, default=None,
+                    help="K > 1: front ends (G-buffer + path tracer) of K frames overlap on K streams "
+                         "(default 4 on one GPU, 8 on bands: thinner bands have relatively longer launch tails)")
     ap.add_argument("--pt-uniform", action="append", default=[], metavar="NAME=INT",
                     help="extra int uniform on the path-tracing pass (A/B switches, e.g. shadow_bvh4=0)")
     return ap.parse_args()
@@ -108,6 +109,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         world = args.gpus if world == 1 and args.gpus == 1 else world
+    if args.frames_in_flight is None:
+        args.frames_in_flight = 4 if world == 1 else 8
+    # every frame slot must have run once before the timed region (a slot's first frame allocates its
+    # wavefront state, and hipMalloc stalls the queues): at least K + 1 untimed frames
+    args.warmup = max(args.warmup, args.frames_in_flight + 1)
     dist = None
     if world > 1:
         import torch.distributed as dist

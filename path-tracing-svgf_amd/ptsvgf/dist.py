@@ -202,7 +202,8 @@ class BandRenderer:
             self.r.frame()
             torch.cuda.synchronize()
             self.pass_path_tracing.set_row_cost(0)
-            self.r.frame()
+            for _ in range(max(1, self.r.K)):  # every frame slot once: first use allocates (hipMalloc syncs)
+                self.r.frame()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(frames):

@@ -53,7 +53,7 @@ def sim_rank(rk, bounds, probe=False, K=10):
     r.pass_path_tracing.set_uniform_int("trace_fork", int(os.environ.get("PTSVGF_TRACE_FORK", "0")))
     if "SHADOW_BUDGET" in os.environ:
         r.pass_path_tracing.set_uniform_int("shadow_budget", int(os.environ["SHADOW_BUDGET"]))
-    for _ in range(3):
+    for _ in range(max(3, 2 * r.r.K)):  # every frame slot used before timing (first use allocates)
         r.frame()
     torch.cuda.synchronize()
     LOG.clear()
