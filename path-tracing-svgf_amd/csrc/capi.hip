@@ -69,6 +69,7 @@ struct Uniform {
 
 struct RasterScene {
   float4* geom = nullptr;
+  float4* nrm = nullptr;
   float4* bvh = nullptr;
   int root_ref = 0;
   int stack_need = 0;
@@ -847,6 +848,7 @@ int draw_raster(Pass* p) {
   if (!fwt->aux) HIPCHK(hipMalloc((void**)&fwt->aux, (size_t)fwt->W * fwt->rows * 4));
   k.fwidth_aux = fwt->aux;
   k.geom = p->raster.geom;
+  k.nrm = p->raster.nrm;
   k.bvh = p->raster.bvh;
   k.root_ref = p->raster.root_ref;
   k.stack_need = p->raster.stack_need;
@@ -1014,6 +1016,7 @@ int pt_shutdown(void) {
   for (auto& kv : g.passes) {
     Pass* p = kv.second.get();
     if (p->raster.geom) (void)hipFree(p->raster.geom);
+    if (p->raster.nrm) (void)hipFree(p->raster.nrm);
     if (p->raster.bvh) (void)hipFree(p->raster.bvh);
     if (p->wf.base) (void)hipFree(p->wf.base);
     if (p->order.cost) (void)hipFree(p->order.cost);
@@ -1333,7 +1336,7 @@ int pt_raster_pass_bind(uint32_t pass, const float* verts, size_t n_floats) {
   tree.reserve(2 * (size_t)ntris);
   sah_build(pr, 0, ntris, 8, tree);  // leaves of <= 8 (measured: 2 and 4 slower, tools/exp_tree_ab.sh)
   using namespace glsl;
-  std::vector<float4> geom((size_t)ntris * 7);
+  std::vector<float4> geom((size_t)ntris * 4), nrm((size_t)ntris * 3);
   for (int k = 0; k < ntris; ++k) {
     const int oi = pr[k].ref;
     const float* f = verts + (size_t)oi * 18;
@@ -1341,20 +1344,22 @@ int pt_raster_pass_bind(uint32_t pass, const float* verts, size_t n_floats) {
     v3 e1 = sub(p2, p1), e2 = sub(p3, p1), ng = cross(e1, e2);
     float oif;
     memcpy(&oif, &oi, 4);
-    float4* q = &geom[(size_t)k * 7];
+    float4* q = &geom[(size_t)k * 4];
     q[0] = float4{p1.x, p1.y, p1.z, oif};
     q[1] = float4{e1.x, e1.y, e1.z, 0};
     q[2] = float4{e2.x, e2.y, e2.z, 0};
     q[3] = float4{ng.x, ng.y, ng.z, 0};
-    q[4] = float4{f[3], f[4], f[5], 0};
-    q[5] = float4{f[9], f[10], f[11], 0};
-    q[6] = float4{f[15], f[16], f[17], 0};
+    float4* n = &nrm[(size_t)k * 3];
+    n[0] = float4{f[3], f[4], f[5], 0};
+    n[1] = float4{f[9], f[10], f[11], 0};
+    n[2] = float4{f[15], f[16], f[17], 0};
   }
   std::vector<float4> bvh;
   int root = 0;
   TRY(pack_sah(tree, [](int first, int n) { return -(first * 16 + n) - 1; }, bvh, &root, &p->raster.stack_need));
   if (bvh.empty()) bvh.push_back(float4{0, 0, 0, 0});
   TRY(upload_vec(geom, &p->raster.geom));
+  TRY(upload_vec(nrm, &p->raster.nrm));
   TRY(upload_vec(bvh, &p->raster.bvh));
   p->raster.root_ref = root;
   return PT_OK;
@@ -1483,6 +1488,7 @@ int pt_pass_destroy(uint32_t pass) {
   (void)hipStreamSynchronize(g.stream);
   Pass* p = it->second.get();
   if (p->raster.geom) (void)hipFree(p->raster.geom);
+  if (p->raster.nrm) (void)hipFree(p->raster.nrm);
   if (p->raster.bvh) (void)hipFree(p->raster.bvh);
   if (p->wf.base) (void)hipFree(p->wf.base);
   if (p->order.cost) (void)hipFree(p->order.cost);

@@ -253,7 +253,7 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
       int first = ref_leaf_first(leaf), cnt = ref_leaf_count(leaf);
       steps += (uint32_t)cnt;
       for (int i = first; i < first + cnt; ++i) {
-        const float4* g = p.geom + 7 * i;
+        const float4* g = p.geom + 4 * i;
         float4 a = g[0], e1 = g[1], e2 = g[2], ng = g[3];
         v3 p1 = xyz(a);
         if (!(dot(xyz(ng), sub(p1, o)) < 0.0f)) continue;  // back face culled (GL_BACK, CCW front)
@@ -286,9 +286,10 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
     if (p.fwidth_aux) p.fwidth_aux[(size_t)prow(p.fwidth, y) * p.W + x] = -0.3f;  // .y with the zCenter == 1 flag
     return;
   }
-  const float4* g = p.geom + 7 * bests;
+  const float4* g = p.geom + 4 * bests;
+  const float4* gn = p.nrm + 3 * bests;
   v3 p1 = xyz(g[0]), e1 = xyz(g[1]), e2 = xyz(g[2]);
-  v3 n1 = xyz(g[4]), n2 = xyz(g[5]), n3 = xyz(g[6]);
+  v3 n1 = xyz(gn[0]), n2 = xyz(gn[1]), n3 = xyz(gn[2]);
   auto interp = [&](float u, float v) {
     float w0 = (1.0f - u) - v;
     return add(add(muls(n1, w0), muls(n2, u)), muls(n3, v));

@@ -138,7 +138,8 @@ struct GBufParams {
   int W, H, y0, y1;
   Plane world, normal_depth, motion, fwidth;
   float* fwidth_aux;    // compact depth-fwidth plane (rows of fwidth), may be null
-  const float4* geom;   // 7 x float4 per raster triangle: (p1,idx)(e1,-)(e2,-)(Ng,-)(n1)(n2)(n3)
+  const float4* geom;   // 4 x float4 per raster triangle (walk): (p1,idx)(e1,-)(e2,-)(Ng,-)
+  const float4* nrm;    // 3 x float4 per raster triangle (closest hit only): n1, n2, n3
   const float4* bvh;
   int root_ref;
   int stack_need;       // deepest interior level of the raster BVH
