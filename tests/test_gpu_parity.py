@@ -36,7 +36,7 @@ def _readback(gl, r):
     return {k: gl.readback(v) for k, v in r.planes().items()}
 
 
-@pytest.mark.parametrize("W,H", [(64, 64), (96, 64)])
+@pytest.mark.parametrize("W,H", [(64, 64), (96, 64), (37, 23), (5, 3)])
 def test_frames_match_oracle(gpu, scene_small, W, H):
     """3 frames, static camera: every pass output vs the oracle frame loop."""
     gl = gpu
@@ -357,3 +357,40 @@ def test_taa_and_output_match_oracle(gpu, scene_small, mode):
         got = _readback(gl, r)
         for key in ("modulate", "final", "output"):
             _cmp(f"{mode}/f{f}/{key}", got[key], want[key], rel=True)
+
+
+@pytest.fixture(scope="module")
+def scene_bench():
+    from ptsvgf.scene import build_scene
+
+    return build_scene("table_clock_plant")
+
+
+def test_full_size_4k_properties(gpu, scene_bench):
+    """At the bench size (3840x2160, the bench scene) the oracle is too slow, so size-independent properties:
+    the wavefront path tracer (compacted ray lists at their largest, cost-ordered tiles, shadow trees) gives
+    the megakernel's bits, and 4 frames in flight give the serial driver's bits after a moving-camera run."""
+    gl = gpu
+    W, H = 3840, 2160
+    keys = ("color", "emission", "albedo")
+    outs = []
+    for kern in (0, 1):
+        r = _renderer(scene_bench, W, H, mode="fast", aspect_corrected=True, run_taa=False, run_output=False)
+        r.pass_path_tracing.set_uniform_int("pt_kernel", kern)
+        r.frame()
+        outs.append({k: gl.readback(r.planes()[k]) for k in keys})
+        r.close()
+    for k in keys:
+        assert np.array_equal(outs[0][k].view(np.uint32), outs[1][k].view(np.uint32)), k
+    del outs
+    planes = []
+    for K in (1, 4):
+        r = _renderer(scene_bench, W, H, mode="fast", aspect_corrected=True, run_taa=False, run_output=False,
+                      frames_in_flight=K)
+        for _ in range(6):
+            r.camera.orbit(1.0, 0.0)
+            r.frame()
+        planes.append({k: gl.readback(r.planes()[k]) for k in ("color", "atrous", "modulate")})
+        r.close()
+    for k in planes[0]:
+        assert np.array_equal(planes[0][k].view(np.uint32), planes[1][k].view(np.uint32)), k
