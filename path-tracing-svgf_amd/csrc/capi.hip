@@ -89,7 +89,8 @@ int wf_alloc(WFBuffers& b, int W, int rows) {
   const size_t f4 = n * 16, al = 256;
   const size_t nl = (size_t)wf_list_capacity(W, rows) * 8;  // 8 list segments
   auto up = [&](size_t v) { return (v + al - 1) / al * al; };
-  size_t total = up(f4) * 10 + up(n * 8) + up(n * 4) + up(n) * 2 + up(nl * 4) * 2 + up(nl * 4 * (1 + kPointBins)) +
+  size_t total = up(f4) * 10 + up(n * 8) + up(n * 4) + up(n) * 2 + up(nl * 4 * kLiveBins) * 2 +
+                 up(nl * 4 * (1 + kPointBins)) +
                  up(n * 8) + up(kWfCounters * 4);
   if (hipMalloc(&b.base, total) != hipSuccess) { b.base = nullptr; return PT_ERR_HIP; }
   char* c = (char*)b.base;
@@ -100,8 +101,8 @@ int wf_alloc(WFBuffers& b, int W, int rows) {
   b.st.seed = (uint32_t*)c; c += up(n * 4);
   b.st.occ_h = (uint8_t*)c; c += up(n);
   b.st.occ_p = (uint8_t*)c; c += up(n);
-  b.st.list0 = (int*)c; c += up(nl * 4);
-  b.st.list1 = (int*)c; c += up(nl * 4);
+  b.st.list0 = (int*)c; c += up(nl * 4 * kLiveBins);
+  b.st.list1 = (int*)c; c += up(nl * 4 * kLiveBins);
   b.st.shadow_list = (int*)c; c += up(nl * 4 * (1 + kPointBins));
   b.st.straggler = (int*)c; c += up(n * 8);  // both shadow kinds of one bounce
   b.st.counters = (int*)c;

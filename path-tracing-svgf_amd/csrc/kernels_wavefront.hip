@@ -50,6 +50,23 @@ __device__ __forceinline__ int seg_total(const int* __restrict__ counts) {
   for (int s = 0; s < kSeg; ++s) t += counts[s];
   return t;
 }
+// A list of `nbins` bins (bin b: items + b * kSeg * cap, counts + b * kSeg), read as one dense range.
+__device__ __forceinline__ bool bins_get(const int* __restrict__ items, const int* __restrict__ counts, int nbins,
+                                         int cap, int k, int* v) {
+  int base = 0;
+  for (int b = 0; b < nbins; ++b) {
+#pragma unroll
+    for (int s = 0; s < kSeg; ++s) {
+      const int c = counts[b * kSeg + s];
+      if (k < base + c) {
+        *v = items[((size_t)b * kSeg + s) * cap + (k - base)];
+        return true;
+      }
+      base += c;
+    }
+  }
+  return false;
+}
 __device__ __forceinline__ bool seg_get(const int* __restrict__ items, const int* __restrict__ counts, int cap, int k,
                                         int* v) {
   int base = 0;
@@ -65,22 +82,23 @@ __device__ __forceinline__ bool seg_get(const int* __restrict__ items, const int
   return false;
 }
 
-// Block-wide append of up to one item to each of the shade lists: the live rays, the HDR shadow rays and the
-// point-light shadow rays, the latter into kPointBins lists by light index (rays toward one light from one
-// screen tile traverse alike, so a trace wave holding one light's rays diverges less). Every thread of the
+// Block-wide append of up to one item to each of the shade lists: the live rays into kLiveBins lists by
+// direction octant, the HDR shadow rays, and the point-light shadow rays into kPointBins lists by light index
+// (rays of one bin traverse alike, so a trace wave holding one bin diverges less). Every thread of the
 // 256-thread block must call it. One atomic per (list, bin) per block.
-constexpr int kLists = 2 + kPointBins;
-__device__ __forceinline__ void block_push_shade(bool p_live, bool p_h, bool p_p, int bin, int v, int* __restrict__ live,
-                                                 int* live_counts, int* __restrict__ shadow, int* shadow_counts,
-                                                 int cap) {
+constexpr int kLists = kLiveBins + 1 + kPointBins;
+__device__ __forceinline__ void block_push_shade(bool p_live, int lbin, bool p_h, bool p_p, int bin, int v,
+                                                 int* __restrict__ live, int* live_counts, int* __restrict__ shadow,
+                                                 int* shadow_counts, int cap) {
   __shared__ int wc[kLists][4];
   __shared__ int base[kLists];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   unsigned long long m[kLists];
-  m[0] = __ballot(p_live);
-  m[1] = __ballot(p_h);
 #pragma unroll
-  for (int b = 0; b < kPointBins; ++b) m[2 + b] = __ballot(p_p && bin == b);
+  for (int b = 0; b < kLiveBins; ++b) m[b] = __ballot(p_live && lbin == b);
+  m[kLiveBins] = __ballot(p_h);
+#pragma unroll
+  for (int b = 0; b < kPointBins; ++b) m[kLiveBins + 1 + b] = __ballot(p_p && bin == b);
   if (lane == 0)
 #pragma unroll
     for (int l = 0; l < kLists; ++l) wc[l][wv] = __popcll(m[l]);
@@ -89,23 +107,23 @@ __device__ __forceinline__ void block_push_shade(bool p_live, bool p_h, bool p_p
   if (threadIdx.x < kLists) {
     const int l = threadIdx.x;
     const int t = (wc[l][0] + wc[l][1]) + (wc[l][2] + wc[l][3]);
-    int* c = l == 0 ? live_counts : shadow_counts + (l - 1) * kSeg;
+    int* c = l < kLiveBins ? live_counts + l * kSeg : shadow_counts + (l - kLiveBins) * kSeg;
     base[l] = t ? atomicAdd(c + seg, t) : 0;
   }
   __syncthreads();
   const unsigned long long lt = (1ull << lane) - 1ull;
   if (p_live) {
-    int o = base[0];
-    for (int w = 0; w < wv; ++w) o += wc[0][w];
-    live[seg * cap + o + __popcll(m[0] & lt)] = v;
+    int o = base[lbin];
+    for (int w = 0; w < wv; ++w) o += wc[lbin][w];
+    live[((size_t)lbin * kSeg + seg) * cap + o + __popcll(m[lbin] & lt)] = v;
   }
   if (p_h) {
-    int o = base[1];
-    for (int w = 0; w < wv; ++w) o += wc[1][w];
-    shadow[seg * cap + o + __popcll(m[1] & lt)] = v;
+    int o = base[kLiveBins];
+    for (int w = 0; w < wv; ++w) o += wc[kLiveBins][w];
+    shadow[seg * cap + o + __popcll(m[kLiveBins] & lt)] = v;
   }
   if (p_p) {
-    const int li = 2 + bin;
+    const int li = kLiveBins + 1 + bin;
     int o = base[li];
     for (int w = 0; w < wv; ++w) o += wc[li][w];
     shadow[(size_t)(1 + bin) * kSeg * cap + seg * cap + o + __popcll(m[li] & lt)] = v;
@@ -178,7 +196,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest(PTParams p
   __shared__ int stk[KS * kTB];
   const int k = blockIdx.x * kTB + threadIdx.x;
   int pid;
-  if (!seg_get(list, counts, cap, k, &pid)) return;
+  if (!bins_get(list, counts, kLiveBins, cap, k, &pid)) return;
   float4 o = ldnt(&p.wf.ray_o[pid]), dd = ldnt(&p.wf.ray_d[pid]);
   float t;
   uint32_t steps;
@@ -298,10 +316,11 @@ __global__ void __launch_bounds__(256) wf_shade(PTParams p, int bounce, const in
     valid = x < p.W && ly < p.y1 - p.y0;
     pid = ly * p.W + x;
   } else {
-    valid = seg_get(list_in, counts_in, cap, k, &pid);
+    valid = bins_get(list_in, counts_in, kLiveBins, cap, k, &pid);
   }
   bool push = false, need_h = false, need_p = false;
   int pbin = 0;  // point-light list of this ray (light index mod kPointBins)
+  int lbin = 0;  // live list of the continuing ray (direction octant)
   if (valid) {
     int x, y;
     pix_xy(p, pid, &x, &y);
@@ -350,6 +369,7 @@ __global__ void __launch_bounds__(256) wf_shade(PTParams p, int bounce, const in
       v3 L = sample_brdf(xi1, xi2, xi3, V, h.normal, h.m);
       if (dot(h.normal, L) > 0.0f) {
         push = true;
+        lbin = ((L.x < 0.0f) | ((L.y < 0.0f) << 1) | ((L.z < 0.0f) << 2)) & (kLiveBins - 1);
         v3 brdf = brdf_eval(V, h.normal, L, h.m);
         float bpdf = brdf_pdf(V, h.normal, L, h.m);
         // hdriLight, evaluated as if unoccluded (:922-946)
@@ -405,7 +425,7 @@ __global__ void __launch_bounds__(256) wf_shade(PTParams p, int bounce, const in
     stnt(&p.wf.light[pid], f4(light.x, light.y, light.z, 0.0f));
   }
   // HDR and point-light shadow rays go to separate lists so trace waves stay homogeneous
-  block_push_shade(push, need_h, need_p, pbin, pid, list_out, counts_out, shadow_out, shadow_counts, cap);
+  block_push_shade(push, lbin, need_h, need_p, pbin, pid, list_out, counts_out, shadow_out, shadow_counts, cap);
 }
 
 // ----------------------------------------------------------------- finish ---
@@ -413,7 +433,7 @@ __global__ void __launch_bounds__(256) wf_finish(PTParams p, const int* __restri
                                                  const int* __restrict__ counts, int cap) {
   const int k = blockIdx.x * 256 + threadIdx.x;
   int pid;
-  if (!seg_get(list, counts, cap, k, &pid)) return;
+  if (!bins_get(list, counts, kLiveBins, cap, k, &pid)) return;
   float4 q0 = ldnt(&p.wf.pend0[pid]), q1 = ldnt(&p.wf.pend1[pid]), q2 = ldnt(&p.wf.pend2[pid]), q3 = ldnt(&p.wf.pend3[pid]);
   NeeTerms nt;
   nt.hcalc = xyz(q0); nt.pcalc = xyz(q1); nt.bcalc = xyz(q2);
@@ -494,7 +514,7 @@ int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent
     const int* lin = lists[(i + 1) & 1];
     int* lout = lists[i & 1];
     int* live = p.wf.counters + kWfCtr * i;        // kSeg live-list counts of bounce i
-    int* shadow = p.wf.counters + kWfCtr * i + 8;  // kSeg HDR + kPointBins x kSeg point-light counts
+    int* shadow = p.wf.counters + kWfCtr * i + kCtrHdr;  // kSeg HDR + kPointBins x kSeg point-light counts
     const int* live_in = p.wf.counters + kWfCtr * (i > 0 ? i - 1 : 0);
     if (i > 0) {
       if (fork) {
@@ -511,7 +531,7 @@ int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent
       closest(i + 1, aux);
       if ((e = hipEventRecord(ev_join, aux)) != hipSuccess) return (int)e;
     }
-    int* strag = p.wf.counters + kWfCtr * i + 48;  // shadow rays handed to the cooperative walk
+    int* strag = p.wf.counters + kWfCtr * i + kCtrStrag;  // shadow rays handed to the cooperative walk
     if (p.scene.bvh4)
       hipLaunchKernelGGL((wf_trace_shadow<KS, true>), dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
                          (const int*)shadow, cap, strag);
