@@ -180,7 +180,7 @@ class BandRenderer:
         self.r.close()
         self._tensors.clear()
 
-    def measure_row_cost(self, frames: int = 12):
+    def measure_row_cost(self, frames: int = 24):
         """Estimated time (ms) of every frame row, identical on all ranks.
 
         One probed frame counts each row's BVH visits (pt_pass_set_row_cost). Then every rank times `frames`

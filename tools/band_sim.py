@@ -46,7 +46,7 @@ scene = build_scene("table_clock_plant")
 cfg = parameter_config()
 
 
-def sim_rank(rk, bounds, probe=False, K=10):
+def sim_rank(rk, bounds, probe=False, K=30):
     r = D.BandRenderer(scene, W, H, cfg, rk, N, FakeDist(), bounds=bounds,
                        frames_in_flight=int(os.environ.get("FIF", "1")))
     r.pass_path_tracing.set_uniform_int("pt_kernel", int(os.environ.get("PTK", "0")))
