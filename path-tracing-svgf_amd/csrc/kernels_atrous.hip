@@ -233,14 +233,19 @@ __global__ void __launch_bounds__(256) atrous_step_kernel(AtrousParams p) {
 // AUX: the G-buffer's compact depth-fwidth plane carries the zCenter == 1 flag in
 // its sign bit (its magnitude is .y, always >= 0 or a NaN with the sign clear), so
 // background pixels read 4 + 16 B and write 16 B.
+// NX: 64-column strips per tile (waves side by side). The halo costs 4S staged columns per tile, so the widest
+// step stages twice its output with NX = 1; S = 16 uses NX = 2 (128 columns, 1024 threads, 74 KB of LDS: measured
+// 100 -> 91.5 us on the 4K bench inputs, tools/exp_atrous_real.hip), the other steps are fastest with NX = 1.
 constexpr int kTileRows = 8;   // TJ
-constexpr int kTileWaves = 8;  // one pixel per thread
+constexpr int kTileWaves = 8;  // per 64-column strip; one pixel per thread
+template <int S> constexpr int tile_nx() { return S >= 16 ? 2 : 1; }
 
 __device__ __forceinline__ bool aux_flag(float a) { return (__float_as_uint(a) >> 31) != 0; }
 
 template <int S, bool AUX>
-__global__ void __launch_bounds__(64 * kTileWaves) atrous_tile_kernel(AtrousParams p) {
-  constexpr int TJ = kTileRows, NW = kTileWaves, R = TJ + 4, C = 64 + 4 * S, NT = 64 * NW;
+__global__ void __launch_bounds__(64 * kTileWaves * tile_nx<S>()) atrous_tile_kernel(AtrousParams p) {
+  constexpr int NX = tile_nx<S>();
+  constexpr int TJ = kTileRows, NW = kTileWaves * NX, R = TJ + 4, C = 64 * NX + 4 * S, NT = 64 * NW;
   __shared__ float4 LI[R * C];
   __shared__ float4 LN[R * C];
   const int W = p.illum.W, row0 = p.illum.row0;
@@ -250,7 +255,8 @@ __global__ void __launch_bounds__(64 * kTileWaves) atrous_tile_kernel(AtrousPara
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = blockIdx.y / S, b = blockIdx.y - g * S;
   const int ybase = p.y0 + g * S * TJ + b;  // frame row of tile row j = 0
-  const int x0 = blockIdx.x * 64, x = x0 + lane, y = ybase + S * wv;
+  const int j = wv / NX, xl = (wv - j * NX) * 64 + lane;  // tile row, tile column
+  const int x0 = blockIdx.x * 64 * NX, x = x0 + xl, y = ybase + S * j;
   const bool own = x < p.W && y < p.y1;
   const size_t ci = (size_t)(y - row0) * W + x;
   bool bg = true;
@@ -283,8 +289,8 @@ __global__ void __launch_bounds__(64 * kTileWaves) atrous_tile_kernel(AtrousPara
   }
   __syncthreads();
   if (!own) return;
-  const float4* Li = LI + wv * C + lane;  // top-left tap of this pixel's window
-  const float4* Ln = LN + wv * C + lane;
+  const float4* Li = LI + j * C + xl;  // top-left tap of this pixel's window
+  const float4* Ln = LN + j * C + xl;
   const float4 ic = Li[2 * C + 2 * S];
   float4* out = p.out.p + ci;
   if (bg) {
@@ -292,7 +298,8 @@ __global__ void __launch_bounds__(64 * kTileWaves) atrous_tile_kernel(AtrousPara
     return;
   }
   const float4 nd = Ln[2 * C + 2 * S];
-  const bool edge = x0 - 2 * S < 0 || x0 + 63 + 2 * S >= p.W || ybase - 2 * S < 0 || ybase + S * (TJ + 1) >= p.H;
+  const bool edge =
+      x0 - 2 * S < 0 || x0 + 64 * NX - 1 + 2 * S >= p.W || ybase - 2 * S < 0 || ybase + S * (TJ + 1) >= p.H;
   const float LOG2E = 1.4426950408889634f;
   const float lc = (0.2125f * ic.x + 0.7154f * ic.y) + 0.0721f * ic.z;
   const float phiL = p.phi_color * __builtin_sqrtf(fmaxf(0.0f, 1e-10f + ic.w));
@@ -344,10 +351,11 @@ __global__ void __launch_bounds__(64 * kTileWaves) atrous_tile_kernel(AtrousPara
 
 template <int S>
 static void launch_tile_s(const AtrousParams& p, bool aux, hipStream_t s) {
+  constexpr int NX = tile_nx<S>();
   const int groups = (p.y1 - p.y0 + S * kTileRows - 1) / (S * kTileRows);
-  dim3 grid((p.W + 63) / 64, groups * S);
-  if (aux) hipLaunchKernelGGL((atrous_tile_kernel<S, true>), grid, dim3(64 * kTileWaves), 0, s, p);
-  else hipLaunchKernelGGL((atrous_tile_kernel<S, false>), grid, dim3(64 * kTileWaves), 0, s, p);
+  dim3 grid((p.W + 64 * NX - 1) / (64 * NX), groups * S);
+  if (aux) hipLaunchKernelGGL((atrous_tile_kernel<S, true>), grid, dim3(64 * kTileWaves * NX), 0, s, p);
+  else hipLaunchKernelGGL((atrous_tile_kernel<S, false>), grid, dim3(64 * kTileWaves * NX), 0, s, p);
 }
 
 static bool same_geometry(const AtrousParams& p) {

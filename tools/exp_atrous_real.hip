@@ -318,7 +318,8 @@ int main(int argc, char** argv) {
            100.0 * fgt / tiles, 100.0 * fgpx / N, 100.0 * wavesfg / (8.0 * fgt));
   }
   const int R = 30;
-  for (int cfg = 0; cfg < 1; ++cfg) {
+  const int ncfg = getenv("NCFG") ? atoi(getenv("NCFG")) : 1;
+  for (int cfg = 0; cfg < ncfg; ++cfg) {
   g_cfg = cfg;
   printf("tile cfg %s\n", cfg_names[cfg]);
   for (int S : {1, 2, 4, 8, 16}) {
