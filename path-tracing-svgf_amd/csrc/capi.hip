@@ -613,6 +613,11 @@ uint32_t uu(Pass* p, const char* n, uint32_t def) {
   return def;
 }
 
+// A sampler the host bound by name (no texture-unit-0 fallback): optional inputs with no GL counterpart.
+Texture* bound_sampler(Pass* p, const char* name) {
+  auto it = p->tex.find(name);
+  return it != p->tex.end() ? tex_of(it->second) : nullptr;
+}
 Texture* sampler(Pass* p, const char* name, uint32_t* handle = nullptr) {
   auto it = p->tex.find(name);
   uint32_t h = it != p->tex.end() ? it->second : g.unit0;
@@ -803,6 +808,13 @@ int draw_pathtrace(Pass* p) {
   if (k.accumulate) {
     Texture* lf = sampler(p, "lastFrame");
     if (lf) TRY(plane_of(lf, p, &k.last, "lastFrame"));
+  }
+  // optional primary-ray bound from this frame's G-buffer (wf_primary), result-preserving
+  Texture* hp = bound_sampler(p, "gWorldPos");
+  Texture* hn = bound_sampler(p, "gNormalAndLinearZ");
+  if (hp && hn && ui(p, "primary_bound", 1)) {
+    TRY(plane_of(hp, p, &k.hint_pos, "gWorldPos"));
+    TRY(plane_of(hn, p, &k.hint_nd, "gNormalAndLinearZ"));
   }
   // tile subset (PTParams::tile_stride): this pass traces every tile_stride-th 16 x 16 tile of the band
   k.tile_stride = ui(p, "tile_stride", 1);

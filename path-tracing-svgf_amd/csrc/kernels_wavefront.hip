@@ -171,8 +171,26 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
   if (valid) {
     v3 S = mk(p.eye[0], p.eye[1], p.eye[2]);
     v3 d = primary_dir(p, x, y);
+    // Bound from the G-buffer: the surface this pixel rasterised lies at distance |P - eye|; the walk first seeks
+    // only hits nearer than that (plus a margin). The closest hit, if it is nearer, lies in boxes the pruned walk
+    // still visits in the reference's order (ties included), so the result is the unbounded walk's; when no hit
+    // is found below the bound (a different ray, a grazing or culled surface) the walk is repeated unbounded.
+    float bound = PT_INF;
+    if (p.hint_pos.p && p.prune) {
+      const float4 nd = pld(p.hint_nd, x, y);
+      if (nd.w != 1.0f) {  // not background (zCenter == 1)
+        const float4 P = pld(p.hint_pos, x, y);
+        const float dist = length(sub(xyz(P), S));
+        if (dist == dist) bound = dist * 1.001f + 1.0e-3f;
+      }
+    }
     float t;
-    int tri = traverse<0, 256>(p.scene, stk + threadIdx.x, S, d, 0.0f, p.prune, &t, &steps);
+    int tri = traverse<0, 256>(p.scene, stk + threadIdx.x, S, d, 0.0f, p.prune, &t, &steps, bound);
+    if (tri < 0 && bound < PT_INF) {
+      uint32_t more = 0;
+      tri = traverse<0, 256>(p.scene, stk + threadIdx.x, S, d, 0.0f, p.prune, &t, &more);
+      steps += more;
+    }
     stnt(&p.wf.hit[pid], make_int2(tri, __float_as_int(t)));
   }
 #ifdef PT_WAVE_TIMES  // investigation build: per wave (start, end, max steps) in the row-cost buffer

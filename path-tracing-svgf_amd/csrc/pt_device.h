@@ -132,6 +132,9 @@ struct PTParams {
   int stack_need;       // deepest interior level of the binary BVH (selects the LDS stack size)
   float sobol_u[4], sobol_v[4];  // sobolVec2(frameCounter+1, b): uniform across pixels
   WFState wf;
+  // optional bound for the primary rays from this frame's G-buffer (world position + normal/linearZ planes,
+  // drawn before on the same stream): see wf_primary. p == null: no bound
+  Plane hint_pos, hint_nd;
   TileSched tiles;      // primary-ray tiles (16 x 16 px), indexed by subset slot (below)
   // Tile subset (wavefront path tracer only): trace the 16 x 16 tiles t = k * tile_stride + tile_offset of
   // the band (raster tile order), k = 0 .. tiles.ntiles - 1; other pixels are left untouched. Stride 1,

@@ -174,9 +174,9 @@ constexpr int kNone = kNoneRef;
 // `steps` (optional) receives the node + triangle visits (load-balancing probe).
 template <int MODE, int STRIDE>
 __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, float maxd, int prune,
-                        float* t_best_out, uint32_t* steps = nullptr) {
+                        float* t_best_out, uint32_t* steps = nullptr, float t_init = PT_INF) {
   v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-  float tbest = PT_INF;
+  float tbest = t_init;  // MODE 0 with t_init < inf: only hits nearer than t_init are sought (caller falls back)
   int best = -1;
   int sp = 0;
   int node = sc.root_ref;

@@ -282,7 +282,7 @@ class Renderer:
 
     def _gbuffer_and_pt(self, b: int):
         self._gbuffer(b)
-        self._path_trace()
+        self._path_trace(self.gbuf[b] if self.mode == "fast" else None)
 
     def _gbuffer(self, b: int):
         cam = self.camera
@@ -294,7 +294,10 @@ class Renderer:
         ip.set_uniform_uint("frameCounter", cam.frameCounter)
         self._draw(ip, "gbuffer")
 
-    def _path_trace(self):
+    def _path_trace(self, hint=None):
+        """hint: this frame's G-buffer set (drawn before on the same stream); its world position and normal/depth
+        planes bound the primary rays' walk (a result-preserving hint with no GL counterpart, kernels_wavefront.hip
+        wf_primary). The reference driver binds none, as main.cpp."""
         cam, cfg = self.camera, self.cfg
         view = cam.cam_view_mat
         self.cameraRotate = rigid_inverse(view)                # main.cpp:445
@@ -319,6 +322,9 @@ class Renderer:
         pt.set_texture_uniform(GL_TEXTURE_2D, self.hdrMap, "hdrMap")
         pt.set_texture_uniform(GL_TEXTURE_2D, self.hdrCache, "hdrCache")
         pt.set_texture_uniform(GL_TEXTURE_BUFFER, self.pointLightBuffer, "pointLights")
+        if hint is not None:
+            pt.set_texture_uniform(GL_TEXTURE_2D, hint["world"], "gWorldPos")
+            pt.set_texture_uniform(GL_TEXTURE_2D, hint["normal_depth"], "gNormalAndLinearZ")
         self._draw(pt, "pathtrace")
 
     def _frame_reference(self):
