@@ -799,6 +799,8 @@ int draw_pathtrace(Pass* p) {
   if (k.max_depth > 4) return err(PT_ERR_ARG, "max_tracing_depth > 4 indexes past the 8 Sobol dimensions (:463)");
   k.aspect_corrected = ui(p, "aspect_corrected", 0);
   k.prune = ui(p, "prune", 1);
+  // A/B switch: 1 = wavefront closest-hit rays walk bvh_any (ties re-walked on the reference tree)
+  k.closest_tree = (k.prune && k.scene.bvh_any) ? ui(p, "closest_tree", 1) : 0;
   for (int b = 0; b < 4; ++b) {
     uint32_t i = k.frameCounter + 1u;
     uint32_t gc = i ^ (i >> 1);

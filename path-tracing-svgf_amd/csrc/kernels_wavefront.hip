@@ -185,10 +185,10 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
       }
     }
     float t;
-    int tri = traverse<0, 256>(p.scene, stk + threadIdx.x, S, d, 0.0f, p.prune, &t, &steps, bound);
+    int tri = closest_hit<256>(p.scene, p.closest_tree, stk + threadIdx.x, S, d, p.prune, &t, &steps, bound);
     if (tri < 0 && bound < PT_INF) {
       uint32_t more = 0;
-      tri = traverse<0, 256>(p.scene, stk + threadIdx.x, S, d, 0.0f, p.prune, &t, &more);
+      tri = closest_hit<256>(p.scene, p.closest_tree, stk + threadIdx.x, S, d, p.prune, &t, &more);
       steps += more;
     }
     stnt(&p.wf.hit[pid], make_int2(tri, __float_as_int(t)));
@@ -218,7 +218,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest(PTParams p
   float4 o = ldnt(&p.wf.ray_o[pid]), dd = ldnt(&p.wf.ray_d[pid]);
   float t;
   uint32_t steps;
-  int tri = traverse<0, kTB>(p.scene, stk + threadIdx.x, xyz(o), xyz(dd), 0.0f, p.prune, &t, &steps);
+  int tri = closest_hit<kTB>(p.scene, p.closest_tree, stk + threadIdx.x, xyz(o), xyz(dd), p.prune, &t, &steps);
   stnt(&p.wf.hit[pid], make_int2(tri, __float_as_int(t)));
   add_row_cost(p, pid / p.W, pid, steps);
 }

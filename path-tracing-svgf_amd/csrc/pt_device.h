@@ -129,6 +129,7 @@ struct PTParams {
   int max_depth;
   int aspect_corrected;
   int prune;            // closest-hit pruning (parity-safe margin)
+  int closest_tree;     // closest-hit rays walk the SAH tree over the reference leaves (closest_hit, pt_shading.h)
   int stack_need;       // deepest interior level of the binary BVH (selects the LDS stack size)
   float sobol_u[4], sobol_v[4];  // sobolVec2(frameCounter+1, b): uniform across pixels
   WFState wf;

@@ -174,10 +174,11 @@ constexpr int kNone = kNoneRef;
 // `steps` (optional) receives the node + triangle visits (load-balancing probe).
 template <int MODE, int STRIDE>
 __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, float maxd, int prune,
-                        float* t_best_out, uint32_t* steps = nullptr, float t_init = PT_INF) {
+                        float* t_best_out, uint32_t* steps = nullptr, float t_init = PT_INF, bool* tie = nullptr) {
   v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   float tbest = t_init;  // MODE 0 with t_init < inf: only hits nearer than t_init are sought (caller falls back)
   int best = -1;
+  bool tied = false;  // another triangle met the current best t exactly (the visit order would decide)
   int sp = 0;
   int node = sc.root_ref;
   int leaf = kNone;
@@ -227,7 +228,8 @@ __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
       float anyt = 0.0f;
       const bool stop = leaf_scan(sc.tri_geom, first, cnt, S, d, [&](int i, float t) {
         if (MODE == 0) {
-          if (t < tbest) { tbest = t; best = i; }
+          if (t < tbest) { tbest = t; best = i; tied = false; }
+          else if (t == tbest) tied = true;
           return false;
         }
         if (!(t < PT_INF)) return false;
@@ -250,7 +252,28 @@ __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
   }
   *t_best_out = tbest;
   if (steps) *steps = nvis;
+  if (tie) *tie = tied;
   return best;
+}
+
+// Closest hit (hitBVH :372-424) for the wavefront kernels. With `sah` (PTParams::closest_tree) the walk runs on
+// the SAH tree over the reference's leaves (bvh_any): the candidate set is the reference walk's (the same leaves,
+// tested on the same leaf boxes, which lie inside every reference ancestor box, so a leaf box the ray passes is
+// one hitBVH reaches), so the minimum t and, when one triangle alone attains it, the triangle are the reference's.
+// When two triangles attain the same t exactly, the reference keeps the one its depth-first order meets first:
+// that ray is walked again on the reference tree in the reference's order. Same bits either way.
+template <int STRIDE>
+__device__ __forceinline__ int closest_hit(const SceneDev& sc, bool sah, int* __restrict__ stk, v3 S, v3 d, int prune,
+                                           float* t, uint32_t* steps, float t_init = PT_INF) {
+  if (!sah) return traverse<0, STRIDE>(sc, stk, S, d, 0.0f, prune, t, steps, t_init);
+  bool tie = false;
+  int tri = traverse<0, STRIDE>(anyhit_scene(sc), stk, S, d, 0.0f, 1, t, steps, t_init, &tie);
+  if (tie) {
+    uint32_t more = 0;
+    tri = traverse<0, STRIDE>(sc, stk, S, d, 0.0f, 1, t, &more, t_init);
+    if (steps) *steps += more;
+  }
+  return tri;
 }
 
 // Any-hit traversal of the 4-wide BVH (shadow rays): HDR rays take any hit,
