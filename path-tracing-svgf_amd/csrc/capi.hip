@@ -370,7 +370,58 @@ static float sah_area(const float* lo, const float* hi) {
   return dx * dy + dy * dz + dz * dx;
 }
 
-// 16-bin SAH over primitive centroids (cost: 1 per node visit, `weight` per primitive test).
+// Exact (full-sweep) SAH split of pr[l, r): per axis the primitives sorted by centroid, every cut priced; pr is
+// left sorted along the best axis and *m is the cut. Returns the best cost (INFINITY: no split).
+static float sah_sweep(std::vector<SahPrim>& pr, int l, int r, int* m) {
+  const int n = r - l;
+  std::vector<float> rarea((size_t)n);
+  std::vector<int> rw((size_t)n);
+  float best = INFINITY;
+  int bax = -1, bcut = 0;
+  auto by_axis = [&](int a) {
+    std::sort(pr.begin() + l, pr.begin() + r, [a](const SahPrim& x, const SahPrim& y) {
+      const float cx = x.lo[a] + x.hi[a], cy = y.lo[a] + y.hi[a];
+      return cx < cy || (cx == cy && x.ref < y.ref);
+    });
+  };
+  for (int a = 0; a < 3; ++a) {
+    by_axis(a);
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    int w = 0;
+    for (int i = n - 1; i >= 1; --i) {
+      const SahPrim& q = pr[l + i];
+      for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], q.lo[k]); hi[k] = std::max(hi[k], q.hi[k]); }
+      w += q.weight;
+      rarea[i] = sah_area(lo, hi);
+      rw[i] = w;
+    }
+    for (int k = 0; k < 3; ++k) { lo[k] = INFINITY; hi[k] = -INFINITY; }
+    w = 0;
+    for (int i = 0; i + 1 < n; ++i) {
+      const SahPrim& q = pr[l + i];
+      for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], q.lo[k]); hi[k] = std::max(hi[k], q.hi[k]); }
+      w += q.weight;
+      const float c = sah_area(lo, hi) * w + rarea[i + 1] * rw[i + 1];
+      if (c < best) { best = c; bax = a; bcut = i + 1; }
+    }
+  }
+  if (bax < 0) return INFINITY;
+  if (bax != 2) by_axis(bax);
+  *m = l + bcut;
+  return best;
+}
+
+// Build-quality switch (PTSVGF_SAH_SWEEP, read once): 1 (default) = exact sweep SAH, 0 = 16-bin SAH
+// (measured 4K 6.885 -> 6.79 ms, 1080p 2.72 -> 2.64 ms with the sweep, tools/exp_env_ab.sh).
+static bool sah_use_sweep() {
+  static const bool on = [] {
+    const char* e = getenv("PTSVGF_SAH_SWEEP");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
+// 16-bin SAH over primitive centroids (cost: 1 per node visit, `weight` per primitive test), or the exact sweep.
 // max_leaf: the most primitives a leaf may hold (leaves also stop at 15 triangles, the leaf ref's limit).
 static int sah_build(std::vector<SahPrim>& pr, int l, int r, int max_leaf, std::vector<SahNode>& nodes) {
   const int id = (int)nodes.size();
@@ -392,8 +443,13 @@ static int sah_build(std::vector<SahPrim>& pr, int l, int r, int max_leaf, std::
   const int n = r - l;
   constexpr int kBins = 16;
   float best = INFINITY;
-  int bax = -1, bsplit = 0;
-  if (n > 1) {
+  int bax = -1, bsplit = 0, msweep = -1;
+  const bool sweep = sah_use_sweep();
+  if (sweep && n > 1) {
+    best = sah_sweep(pr, l, r, &msweep);
+    if (best < INFINITY) bax = 0;
+  }
+  if (!sweep && n > 1) {
     for (int a = 0; a < 3; ++a) {
       const float ext = chi[a] - clo[a];
       if (!(ext > 0.0f)) continue;
@@ -439,7 +495,9 @@ static int sah_build(std::vector<SahPrim>& pr, int l, int r, int max_leaf, std::
     return id;
   }
   int m;
-  if (bax >= 0) {
+  if (sweep && msweep > l) {
+    m = msweep;
+  } else if (!sweep && bax >= 0) {
     const float ext = chi[bax] - clo[bax];
     m = (int)(std::partition(pr.begin() + l, pr.begin() + r, [&](const SahPrim& q) {
           const float c = 0.5f * (q.lo[bax] + q.hi[bax]);
@@ -1335,7 +1393,7 @@ int pt_raster_pass_bind(uint32_t pass, const float* verts, size_t n_floats) {
   p->raster.ntris = ntris;
   p->bound = true;
   if (ntris == 0) return PT_OK;
-  // binned SAH tree over the raster triangles (sah_build: the walk's answer does not depend on the tree);
+  // SAH tree over the raster triangles (sah_build: the walk's answer does not depend on the tree);
   // geom in leaf order, objIndex = original index (the depth-test tie rule)
   std::vector<SahPrim> pr((size_t)ntris);
   for (int i = 0; i < ntris; ++i) {

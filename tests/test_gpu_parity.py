@@ -161,6 +161,26 @@ def test_bvh4_shadows_are_result_preserving(gpu, scene_name, request):
         assert np.array_equal(outs[0][k], outs[1][k], equal_nan=True), k
 
 
+@pytest.mark.parametrize("scene_name", ["scene_small", "scene_cornell", "scene_nan"])
+def test_closest_tree_is_result_preserving(gpu, scene_name, request):
+    """Closest-hit rays on the SAH tree over the reference leaves (closest_tree=1, exact-t ties re-walked on the
+    reference tree) give the reference-order walk's bits (closest_tree=0). The Cornell box's axis-aligned quads
+    put many rays on shared diagonal edges, where two triangles meet the same t."""
+    gl = gpu
+    scene = request.getfixturevalue(scene_name)
+    W, H = 96, 64
+    outs = []
+    for tree in (1, 0):
+        r = _renderer(scene, W, H, mode="fast", run_taa=False, run_output=False)
+        r.pass_path_tracing.set_uniform_int("closest_tree", tree)
+        for _ in range(2):
+            r.frame()
+        outs.append({k: gl.readback(r.planes()[k]) for k in ("color", "emission", "albedo")})
+        r.close()
+    for k in outs[0]:
+        assert np.array_equal(outs[0][k].view(np.uint32), outs[1][k].view(np.uint32)), k
+
+
 @pytest.mark.parametrize("scene_name", ["scene_small", "scene_nan"])
 def test_cooperative_shadow_walk_is_result_preserving(gpu, scene_name, request):
     """Shadow rays past the step budget are finished by the wave-cooperative walk (kernels_wavefront.hip
