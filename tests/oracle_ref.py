@@ -178,7 +178,10 @@ def output(color, threads=THREADS):
 
 class OracleFrameLoop:
     """main.cpp:436-553 on the oracle: G-buffer -> PT -> reproject -> variance -> a-trous x N -> modulate,
-    with the reference's history plumbing (iteration-1 a-trous output becomes next frame's gPrevIllum)."""
+    with the reference's history plumbing (iteration-1 a-trous output becomes next frame's gPrevIllum).
+
+    Accumulate mode (cfg.accumulate_color, path_tracing.frag:1116-1119): lastFrame is last_acc_color, which
+    save_frame_data (main.cpp:546-553, save_frame_data.frag accColor) refreshes from this frame's curColor."""
 
     def __init__(self, scene, W, H, cfg=None, aspect_corrected=None, threads=THREADS, run_taa=True,
                  run_output=False):
@@ -194,6 +197,7 @@ class OracleFrameLoop:
         self.pre_viewproj = mat_mul(self.camera.cam_proj_mat, self.camera.cam_view_mat)
         z = lambda: frame(H, W)  # noqa: E731
         self.prev_illum, self.prev_moments, self.prev_nd, self.prev_taa = z(), z(), z(), z()
+        self.prev_acc = z()  # last_acc_color (zero-filled like every build texture)
         self._mat_mul = mat_mul
 
     def frame(self):
@@ -204,6 +208,8 @@ class OracleFrameLoop:
         g = gbuffer(self.scene.raster, W, H, view, proj, self.pre_viewproj, self.threads)
         col, em, al = self.os.path_trace(W, H, cam.frameCounter, cam.cam_position, rigid_inverse(view),
                                          cfg.clamp_threshold, cfg.max_tracing_depth, self.aspect_corrected,
+                                         accumulate=cfg.accumulate_color,
+                                         last_frame=self.prev_acc if cfg.accumulate_color else None,
                                          threads=self.threads, use_normal_map=cfg.use_normal_texture)
         ri, rm = reproject(g["velocity"], col, al, em, self.prev_illum, self.prev_moments, g["normal_depth"],
                            self.prev_nd, g["fwidth"], np.float32(1.0 / W), np.float32(1.0 / H),
@@ -224,6 +230,7 @@ class OracleFrameLoop:
             if self.run_output:                                           # main.cpp:555-591
                 out["output"] = output(out["final"], self.threads)
         self.prev_illum, self.prev_moments, self.prev_nd = hist, rm, g["normal_depth"]
+        self.prev_acc = col
         self.pre_viewproj = self._mat_mul(proj, view)
         cam.frameCounter += 1
         return out

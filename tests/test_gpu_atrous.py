@@ -1,9 +1,16 @@
 """Production a-trous kernels (kernels_atrous.hip) against the exact oracle on
-synthetic planes large enough that every step (1..16) runs both the interior
-(unchecked) and the border (checked) code paths, with the special cases the
-shader's arithmetic has: background pixels (z == 1), phiIllumination == 0
-(variance <= -1e-10) next to neighbours of exactly equal luminance, zero depth
-fwidth, NaN normals. Bar: north_star's 1e-3 per channel (relative above 1)."""
+synthetic planes with the special cases the shader's arithmetic has: background
+pixels (z == 1), phiIllumination == 0 (variance <= -1e-10) next to neighbours of
+exactly equal luminance, zero depth fwidth, NaN normals. Bar: north_star's 1e-3
+per channel (relative above 1).
+
+Interior vs border: a tile of the LDS kernel takes its unchecked (interior) path
+only when its whole dilated footprint lies inside the frame, i.e. columns
+[x0 - 2S, x0 + 64*NX + 2S) and rows [ybase - 2S, ybase + S*(TJ+1)] with TJ = 8.
+At 320x200 every S = 16 tile is a border tile (ybase >= 32 and ybase + 144 < 200
+cannot both hold), so the S = 16 interior path is exercised by the 416x320
+planes (tiles with x0 = 128, ybase in [128, 175]); `_interior_tiles` counts the
+interior tiles of each case and the test requires at least one for every step."""
 import numpy as np
 import pytest
 
@@ -11,10 +18,23 @@ import oracle_ref as O
 
 pytestmark = pytest.mark.gpu
 
-W, H = 320, 200
+SIZES = [(320, 200), (416, 320)]
 
 
-def _planes(seed=11):
+def _interior_tiles(W, H, S):
+    """Tiles of atrous_tile_kernel<S> (kernels_atrous.hip) that take the unchecked path at W x H."""
+    nx = 2 if S >= 16 else 1
+    n = 0
+    for x0 in range(0, W, 64 * nx):
+        for g in range((H + S * 8 - 1) // (S * 8)):
+            for b in range(S):
+                yb = g * S * 8 + b
+                if x0 - 2 * S >= 0 and x0 + 64 * nx - 1 + 2 * S < W and yb - 2 * S >= 0 and yb + S * 9 < H:
+                    n += 1
+    return n
+
+
+def _planes(seed=11, W=320, H=200):
     rng = np.random.default_rng(seed)
     yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
     illum = np.empty((H, W, 4), np.float32)
@@ -40,6 +60,7 @@ def _planes(seed=11):
 
 def _run(gl, illum, nd, fw, step, variant):
     from ptsvgf.gl import GL_TEXTURE_2D, RenderPass, getShaderProgram, getTextureRGB32F
+    H, W, _ = illum.shape
     ti, tn, tf, to = (getTextureRGB32F(W, H) for _ in range(4))
     gl.upload_rgba(ti, illum)
     gl.upload_rgba(tn, nd)
@@ -62,25 +83,36 @@ def _run(gl, illum, nd, fw, step, variant):
     return out
 
 
+@pytest.mark.parametrize("size", SIZES)
 @pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("step", [1, 2, 4, 8, 16])
-def test_atrous_kernel_vs_oracle(gpu, step, variant):
-    illum, nd, fw = _planes()
+def test_atrous_kernel_vs_oracle(gpu, step, variant, size):
+    W, H = size
+    illum, nd, fw = _planes(W=W, H=H)
     want = O.atrous(illum, nd, fw, step)
     got = _run(gpu, illum, nd, fw, step, variant)
     assert np.array_equal(np.isnan(got), np.isnan(want)), \
         f"NaN pattern differs: gpu {int(np.isnan(got).sum())} oracle {int(np.isnan(want).sum())}"
     d = np.abs(got.astype(np.float64) - want) / np.maximum(1.0, np.abs(want))
     mx = float(np.nanmax(d))
-    print(f"step {step} variant {variant}: max rel diff {mx:.3e}")
+    print(f"{W}x{H} step {step} variant {variant}: max rel diff {mx:.3e} "
+          f"(interior tiles of the tile kernel: {_interior_tiles(W, H, step)})")
     assert mx <= 1e-3
 
 
+def test_interior_tiles_cover_every_step():
+    """The SIZES above reach the unchecked path of every step (CPU-side geometry check)."""
+    for step in (1, 2, 4, 8, 16):
+        assert max(_interior_tiles(W, H, step) for W, H in SIZES) > 0, step
+    assert _interior_tiles(320, 200, 16) == 0 and _interior_tiles(416, 320, 16) > 0
+
+
+@pytest.mark.parametrize("size", SIZES)
 @pytest.mark.parametrize("step", [1, 2, 4, 8, 16])
-def test_tile_kernel_equals_step_kernel(gpu, step):
+def test_tile_kernel_equals_step_kernel(gpu, step, size):
     """The LDS-tiled kernel (variant 0) performs the step kernel's (variant 2) arithmetic in the same tap order:
     identical bits, NaNs included."""
-    illum, nd, fw = _planes(seed=5)
+    illum, nd, fw = _planes(seed=5, W=size[0], H=size[1])
     a = _run(gpu, illum, nd, fw, step, 0)
     b = _run(gpu, illum, nd, fw, step, 2)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))

@@ -414,3 +414,39 @@ def test_full_size_4k_properties(gpu, scene_bench):
         r.close()
     for k in planes[0]:
         assert np.array_equal(planes[0][k].view(np.uint32), planes[1][k].view(np.uint32)), k
+
+
+@pytest.mark.parametrize("mode,K", [("reference", 1), ("fast", 1), ("fast", 3)])
+def test_accumulate_matches_oracle(gpu, scene_small, mode, K):
+    """Accumulate mode against the oracle (path_tracing.frag:1116-1119: color = mix(lastFrame, color,
+    1/(frameCounter+1)), lastFrame = last_acc_color refreshed by save_frame_data, main.cpp:546-553): a running mean
+    over static frames, then a camera move (frameCounter reset to 0, camera.h:71, so the mean restarts), then more
+    static frames. The accumulated colour is bit-exact; the SVGF chain that consumes it within the tolerance."""
+    from ptsvgf.camera import parameter_config
+
+    gl = gpu
+    cfg = parameter_config()
+    cfg.accumulate_color = True
+    W, H = 64, 48
+    r = _renderer(scene_small, W, H, config=cfg, mode=mode, atrous_exact=True, run_taa=False, run_output=False,
+                  frames_in_flight=K)
+    ref = O.OracleFrameLoop(scene_small, W, H, cfg, run_taa=False)
+    for f in range(6):
+        if f == 3:
+            r.camera.orbit(1.0, 0.5)
+            ref.camera.orbit(1.0, 0.5)
+        r.frame()
+        want = ref.frame()
+        got = _readback(gl, r)
+        if f == 2:
+            acc2 = want["color"]
+        ex = _cmp(f"{mode}/K{K}/f{f}/color", got["color"], want["color"])
+        assert ex == 1.0, f"accumulated colour is not bit-exact ({ex})"
+        for key in ("reproj_illum", "variance", "atrous", "modulate"):
+            _cmp(f"{mode}/K{K}/f{f}/{key}", got[key], want[key], rel=True)
+    # the mean really accumulates: frame 2's accumulated colour is not frame 2's own 1-spp colour
+    single = O.OracleFrameLoop(scene_small, W, H, run_taa=False)
+    for _ in range(3):
+        one = single.frame()
+    assert not np.array_equal(one["color"], acc2)
+    r.close()
