@@ -131,6 +131,13 @@ int pt_pass_set_rows(uint32_t pass, int y_begin, int y_end);
  * device_counts[row - y_begin] (uint32 per computed row; caller zeroes it).
  * NULL disables. No reference counterpart (multi-GPU band planning). */
 int pt_pass_set_row_cost(uint32_t pass, void* device_counts);
+/* Motion bound (G-buffer pass): while set, every draw first zeroes *device_u32 and
+ * then stores there the largest |motion.y| (UV units, the bits of a non-negative
+ * float; +inf for a non-finite motion) over the surface pixels it computes. The
+ * multi-GPU band renderer sizes its reprojection / TAA history exchange from it
+ * (svgf_reproject.frag:45-156 reads the history at uv - motion). NULL disables.
+ * No reference counterpart (the single-GPU reference reads the whole frame). */
+int pt_pass_set_motion_bound(uint32_t pass, void* device_u32);
 int pt_pass_draw(uint32_t pass);
 /* Time the last draw of this pass (ms, HIP events on the library stream; syncs). */
 int pt_pass_last_ms(uint32_t pass, float* ms);

@@ -135,6 +135,7 @@ struct Pass {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   uint32_t* row_cost = nullptr;  // pt_pass_set_row_cost (not owned)
+  uint32_t* motion_max = nullptr;  // pt_pass_set_motion_bound (not owned)
 };
 
 struct SceneGPU {
@@ -943,6 +944,10 @@ int draw_raster(Pass* p) {
                        P[3 * 4 + r] * V[c * 4 + 3];
   memcpy(k.PV, PV, 64);
   if (p->raster.ntris == 0) k.root_ref = -1;  // empty leaf
+  if (p->motion_max) {
+    HIPCHK(hipMemsetAsync(p->motion_max, 0, sizeof(uint32_t), g.stream));
+    k.motion_max = p->motion_max;
+  }
   const int ntiles = ((k.W + 15) / 16) * ((std::max(0, k.y1 - k.y0) + 15) / 16);  // gbuffer_kernel's grid
   TRY(tile_order_begin(p, ntiles, &k.tiles));
   int rc = launch_gbuffer(k, g.stream);
@@ -1519,6 +1524,15 @@ int pt_pass_set_row_cost(uint32_t pass, void* device_counts) {
   Pass* p = pass_of(pass);
   if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
   p->row_cost = (uint32_t*)device_counts;
+  return PT_OK;
+}
+
+int pt_pass_set_motion_bound(uint32_t pass, void* device_u32) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  Pass* p = pass_of(pass);
+  if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
+  if (device_u32 && g.programs[p->program] != PK_RASTER) return err(PT_ERR_ARG, "motion bound needs a rasterize pass");
+  p->motion_max = (uint32_t*)device_u32;
   return PT_OK;
 }
 

@@ -276,6 +276,21 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
     }
   }
   sched_cost(p.tiles, tile, steps);
+  if (p.motion_max) {  // band planning (pt_pass_set_motion_bound): wave max of |motion.y|, one atomic per wave
+    float mv = 0.0f;
+    if (valid && bests >= 0) {  // the motion written below, recomputed for this lane
+      const v3 P = add(o, muls(d, best));
+      float c[4], pc[4];
+      mat_vec4(p.M, P, c);
+      mat_vec4(p.PV, P, pc);
+      mv = f_abs(((c[1] / c[3]) * 0.5f + 0.5f) - ((pc[1] / pc[3]) * 0.5f + 0.5f));
+      if (!(mv <= 3.0e38f)) mv = __builtin_inff();  // NaN / inf: unbounded
+    }
+    uint32_t mb = __float_as_uint(mv);  // non-negative floats order as their bits
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) mb = max(mb, (uint32_t)__shfl_xor((int)mb, s));
+    if (ln == 0 && mb) atomicMax(p.motion_max, mb);
+  }
   if (!valid) return;
   if (bests < 0) {
     float4 bg = f4(0.2f, 0.3f, 0.3f, 1.0f);  // glClearColor (main.cpp:62)

@@ -159,6 +159,7 @@ struct GBufParams {
   float M[16];          // projection * view (column-major)
   float PV[16];         // pre_viewproj
   TileSched tiles;      // 16 x 16 px tiles
+  uint32_t* motion_max; // optional: max |motion.y| (float bits) over the launch's surface pixels, zeroed by the host
 };
 
 struct ReprojParams {

@@ -2,37 +2,75 @@
 
 One process per GPU; rank r renders the horizontal band of global rows
 [y0, y1). The path tracer is embarrassingly parallel (RNG seeds use global pixel
-coordinates, path_tracing.frag:433-436), so it runs on owned rows only. The SVGF
-passes are bounded stencils; before each one the ranks swap halo rows with
-their up/down neighbours (torch.distributed P2P: RCCL over xGMI on the GPU,
-gloo on the CPU tests). The G-buffer ghost rows are recomputed locally (a
-primary-ray cast is cheaper than shipping 2 planes).
+coordinates, path_tracing.frag:433-436), and so is the G-buffer: both compute the
+owned rows only. The SVGF passes are bounded stencils; before each one the ranks
+exchange the rows it reads outside their bands (torch.distributed P2P: RCCL over
+xGMI on the GPU, gloo on the CPU tests).
 
-Every frame-sized plane is stored with GHOST rows either side of the band:
-rows [row0, row1) = [y0 - GHOST, y1 + GHOST) clipped to the frame.
+Every frame-sized plane is stored with `ghost` rows either side of the band:
+rows [row0, row1) = [y0 - ghost, y1 + ghost) clipped to the frame. Ghost rows are
+storage only: nothing computes them, an exchange fills the ones a pass reads.
 
-HALO_SCHEDULE is the single source of truth for which planes are exchanged
-before which pass and how many rows; BandRenderer (GPU) and
-tests/test_dist_gloo.py (CPU, oracle) both execute it.
+How many rows each pass reads beyond the band (HALO_SCHEDULE):
+  * reprojection (svgf_reproject.frag:45-156): the history is fetched at uv - motion,
+    bilinearly, with +1-texel taps and a 3x3 fallback: at most ceil(M*H) + 3 rows,
+    M = the largest |motion.y| (UV units) over the frame's surface pixels THIS
+    frame. The G-buffer kernel reduces M on the device (pt_pass_set_motion_bound);
+    the ranks all-reduce MAX on the host (a gloo group), so every pair of ranks
+    agrees on the count. History planes: previous a-trous iteration-1 output and
+    moments; the previous normal/depth plane only where M reaches past the rows
+    the previous frame already exchanged;
+  * variance (svgf_variance.frag:39-117): 3 rows of illumination + moments; the
+    G-buffer normal/depth plane once per frame, as many rows as the widest a-trous
+    iteration reads (2 * 2^(n-1), svgf_Atrous.frag:92-97), for variance and every
+    a-trous iteration;
+  * a-trous iteration i: 2 * 2^i rows of its input;
+  * TAA (taa.frag:19-39, 88-98, 137-139): 2 rows of the modulated colour and the
+    velocity (3x3 neighbourhood and closest-depth tap, each a LINEAR fetch whose
+    zero-weight neighbour row the sampler still reads), ceil(M*H) + 3 rows of the
+    TAA history (fetched at the pixel's own uv - velocity).
+A row is exchanged between ANY two ranks whose intervals meet (a halo may span
+several thin bands). A motion beyond the ghost rows raises instead of reading
+stale or clamped rows.
+
+HALO_SCHEDULE is the single source of truth; BandRenderer (GPU) and
+tests/test_dist_gloo.py (CPU, oracle) both execute it through run_stage().
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass
 
-# a-trous radius 2*step (svgf_Atrous.frag:92-97) up to step 16; variance radius 3
-# (svgf_variance.frag:273); reprojection taps within |motion|+2 rows (svgf_reproject.frag:63,116)
+# a-trous radius 2*step (svgf_Atrous.frag:92-97) for step 1 << i; the reference allows up to 8 iterations
+# (main.cpp:383); variance radius 3 (svgf_variance.frag:68)
 ATROUS_HALO = [2 * (1 << i) for i in range(8)]
 VARIANCE_HALO = 3
-GHOST = 34
+REPROJ_REACH = 3  # rows beyond |motion| the history taps reach: bilinear + 1-texel tap / 3x3 fallback + rounding
+TAA_NEIGHBOURS = 2  # rows of the TAA 3x3 neighbourhood: +-1 texel, plus the LINEAR sampler's zero-weight row
+GHOST = 96        # default stored rows either side of a band (storage only); motion up to GHOST - 3 rows per frame
+MIN_BAND_ROWS = 16
 
-# (stage, planes, rows): executed before `stage`
+# stage -> ((plane, rows), ...) exchanged before that stage; rows: int, or "reproj" / "reproj_nd" (set from this
+# frame's motion bound) / "nd" (the widest a-trous halo of the configured iterations)
 HALO_SCHEDULE = (
-    ("reproject", ("prev_illum", "prev_moments"), "reproj"),
-    ("variance", ("illum", "moments"), VARIANCE_HALO),
-    *((f"atrous{i}", ("atrous_in",), ATROUS_HALO[i]) for i in range(8)),
-    # taa.frag: 3x3 neighbourhood of the current colour, history fetched at uv - velocity (:88-98, :137-139)
-    ("taa", ("modulate", "prev_taa"), "reproj"),
+    ("reproject", (("prev_illum", "reproj"), ("prev_moments", "reproj"), ("prev_nd", "reproj_nd"))),
+    ("variance", (("illum", VARIANCE_HALO), ("moments", VARIANCE_HALO), ("nd", "nd"))),
+    *((f"atrous{i}", (("atrous_in", ATROUS_HALO[i]),)) for i in range(8)),
+    ("taa", (("modulate", TAA_NEIGHBOURS), ("velocity", TAA_NEIGHBOURS), ("prev_taa", "reproj"))),
 )
+STAGES = {st: planes for st, planes in HALO_SCHEDULE}
+
+
+def nd_halo(iterations: int) -> int:
+    """Rows of the G-buffer normal/depth plane the SVGF passes read beyond the band."""
+    return max([VARIANCE_HALO] + ATROUS_HALO[:max(0, int(iterations))])
+
+
+def motion_rows(m: float, H: int) -> int:
+    """Rows the history taps reach beyond a band for a largest |motion.y| of m (UV units) in an H-row frame."""
+    if not math.isfinite(m):
+        raise RuntimeError(f"non-finite G-buffer motion ({m}): the history rows a band needs are unbounded")
+    return int(math.ceil(m * H)) + REPROJ_REACH
 
 
 @dataclass
@@ -42,8 +80,8 @@ class BandPlan:
     rank: int
     world: int
     ghost: int = GHOST
-    reproj_halo: int = 8
     bounds: tuple | None = None  # world+1 row boundaries (balanced_bounds); None = equal bands
+    iterations: int = 5          # a-trous iterations the bands serve (sizes the normal/depth halo)
 
     def __post_init__(self):
         b = list(self.bounds) if self.bounds is not None else [(self.H * k) // self.world for k in range(self.world + 1)]
@@ -51,21 +89,42 @@ class BandPlan:
             raise ValueError(f"bad band bounds {b}")
         self.bounds = tuple(b)
         self.y0, self.y1 = b[self.rank], b[self.rank + 1]
-        if self.y1 - self.y0 < max(ATROUS_HALO[4], self.reproj_halo):
-            raise ValueError(f"band of {self.y1 - self.y0} rows is thinner than the largest halo")
-        if self.reproj_halo + 1 > self.ghost:
-            raise ValueError("reprojection halo exceeds the ghost rows")
+        self.nd_rows = nd_halo(self.iterations)
+        if self.nd_rows > self.ghost:
+            raise ValueError(f"{self.iterations} a-trous iterations read {self.nd_rows} rows beyond a band, more than "
+                             f"its {self.ghost} ghost rows (BandPlan(ghost=...))")
         self.row0 = max(0, self.y0 - self.ghost)
         self.row1 = min(self.H, self.y1 + self.ghost)
         self.rows = self.row1 - self.row0
         self.up = self.rank - 1 if self.rank > 0 else None
         self.down = self.rank + 1 if self.rank < self.world - 1 else None
+        self.motion = 0  # history rows of the current frame (set_motion)
 
-    def rows_for(self, n) -> int:
-        return self.reproj_halo if n == "reproj" else int(n)
+    def set_motion(self, m: float) -> int:
+        """This frame's all-reduced largest |motion.y| (UV) -> rows the history exchanges carry."""
+        n = motion_rows(m, self.H)
+        if n > self.ghost:
+            raise RuntimeError(f"the camera moved {n - REPROJ_REACH} rows in one frame; a band holds {self.ghost} "
+                               f"ghost rows (history reach {n}): build the band renderer with a larger ghost")
+        self.motion = n
+        return n
 
+    def rows_for(self, spec) -> int:
+        if spec == "reproj":
+            return self.motion
+        if spec == "reproj_nd":  # the previous frame's normal/depth already holds nd_rows exchanged ghost rows
+            return self.motion if self.motion > self.nd_rows else 0
+        if spec == "nd":
+            return self.nd_rows
+        return int(spec)
 
-MIN_BAND_ROWS = max(ATROUS_HALO[4], 8) + 4  # a band must hold the widest halo it ships (5-iteration a-trous)
+    def owned(self, k: int) -> tuple:
+        return self.bounds[k], self.bounds[k + 1]
+
+    def need(self, k: int, n: int) -> tuple:
+        """Rows rank k reads outside its band for a halo of n rows: ((above), (below)), clipped to the frame."""
+        a, b = self.owned(k)
+        return (max(0, a - n), a), (b, min(self.H, b + n))
 
 
 def balanced_bounds(row_cost, world: int, min_rows: int = MIN_BAND_ROWS, align: int = 2) -> tuple:
@@ -93,46 +152,89 @@ def balanced_bounds(row_cost, world: int, min_rows: int = MIN_BAND_ROWS, align: 
     return tuple(b)
 
 
-def halo_exchange(tensors, plan: BandPlan, n: int, dist, group=None) -> None:
-    """Swap n halo rows with both neighbours for each (rows, W, C) tensor holding rows [row0, row1)."""
-    if plan.world == 1 or n <= 0:
+def _meet(a: tuple, b: tuple) -> tuple:
+    return max(a[0], b[0]), min(a[1], b[1])
+
+
+def halo_exchange(items, plan: BandPlan, dist, group=None) -> None:
+    """Fill the ghost rows each (tensor, n) item reads: every rank sends the rows of its band that another rank's
+    n-row halo covers. Tensors are (rows, W, C) holding global rows [row0, row1) of this rank."""
+    items = [(t, int(n)) for t, n in items if int(n) > 0]
+    if plan.world == 1 or not items:
         return
-    if tensors and tensors[0].is_cuda and dist.get_backend(group) == "gloo":
-        # gloo has no device P2P: stage through host memory (tests run 2 ranks on one GPU this way)
-        host = [t.cpu() for t in tensors]
-        halo_exchange(host, plan, n, dist, group)
-        for t, h in zip(tensors, host):
+    if max(n for _, n in items) > plan.ghost:
+        raise RuntimeError(f"halo of {max(n for _, n in items)} rows exceeds the {plan.ghost} ghost rows")
+    if items[0][0].is_cuda and dist.get_backend(group) == "gloo":
+        # gloo has no device P2P: stage through host memory (tests run several ranks on one GPU this way)
+        host = [(t.cpu(), n) for t, n in items]
+        halo_exchange(host, plan, dist, group)
+        for (t, _), (h, _) in zip(items, host):
             t.copy_(h)
         return
+    me = plan.rank
+    mine = plan.owned(me)
     ops = []
-    lo = plan.y0 - plan.row0  # local index of the first owned row
-    hi = plan.y1 - plan.row0  # one past the last owned row
-    for t in tensors:
-        if plan.up is not None:
-            k = min(n, lo)
-            ops.append(dist.P2POp(dist.isend, t[lo:lo + k], plan.up, group))  # row slices are contiguous
-            ops.append(dist.P2POp(dist.irecv, t[lo - k:lo], plan.up, group))
-        if plan.down is not None:
-            k = min(n, plan.rows - hi)
-            ops.append(dist.P2POp(dist.isend, t[hi - k:hi], plan.down, group))
-            ops.append(dist.P2POp(dist.irecv, t[hi:hi + k], plan.down, group))
+    for t, n in items:
+        for k in range(plan.world):  # same (tensor, peer) order on every rank: sends and receives pair up in order
+            if k == me:
+                continue
+            for part in plan.need(k, n):       # rows of my band that rank k reads
+                a, b = _meet(mine, part)
+                if b > a:
+                    ops.append(dist.P2POp(dist.isend, t[a - plan.row0:b - plan.row0], k, group))
+            for part in plan.need(me, n):      # rows of rank k's band that I read
+                a, b = _meet(plan.owned(k), part)
+                if b > a:
+                    ops.append(dist.P2POp(dist.irecv, t[a - plan.row0:b - plan.row0], k, group))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
 
 
+def run_stage(stage: str, planes: dict, plan: BandPlan, dist, group=None) -> None:
+    """Execute HALO_SCHEDULE's exchanges before `stage`; planes maps plane names to (rows, W, C) tensors."""
+    items = [(planes[name], plan.rows_for(spec)) for name, spec in STAGES.get(stage, ()) if name in planes]
+    halo_exchange(items, plan, dist, group)
+
+
+_HOST_GROUP = {}
+
+
+def host_group(dist):
+    """A gloo group for the per-frame motion all-reduce (host values: no device stream is involved, so it cannot
+    interleave with the RCCL halo traffic). Collective: every rank creates it at the same point."""
+    if dist.get_backend() == "gloo":
+        return None
+    key = id(dist.group.WORLD)
+    if key not in _HOST_GROUP:
+        _HOST_GROUP[key] = dist.new_group(backend="gloo")
+    return _HOST_GROUP[key]
+
+
+def allreduce_motion(m: float, dist, group=None) -> float:
+    """MAX over ranks of the per-rank largest |motion.y| (host float)."""
+    import torch
+
+    t = torch.tensor([m], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
 class BandRenderer:
     """One rank's share of a frame: the fast Renderer on band storage + HALO_SCHEDULE exchanges."""
 
-    def __init__(self, scene, W, H, cfg, rank, world, dist, reproj_halo: int = 8, bounds=None, **kw):
+    def __init__(self, scene, W, H, cfg, rank, world, dist, bounds=None, ghost=None, **kw):
         import torch
 
         from . import gl
         from .renderer import Renderer
 
-        self.plan = BandPlan(W, H, rank, world, reproj_halo=reproj_halo, bounds=bounds)
+        iters = cfg.num_atrous_iterations
+        ghost = max(GHOST, nd_halo(iters)) if ghost is None else int(ghost)
+        self.plan = BandPlan(W, H, rank, world, ghost=ghost, bounds=bounds, iterations=iters)
         self.dist = dist
         self.exchange = True  # False only while calibrating (make_band_renderer): ranks time their bands alone
+        self._group = host_group(dist) if world > 1 else None
         self._tensors = {}
         gl.set_band(W, H, self.plan.y0, self.plan.y1, self.plan.row0, self.plan.rows)
         dev = torch.device("cuda", torch.cuda.current_device())
@@ -145,18 +247,50 @@ class BandRenderer:
 
         kw.setdefault("run_taa", False)
         kw.setdefault("run_output", False)
+        if kw.get("frames_in_flight", 1) == 1:  # exchanges run on torch's stream: the draws must too
+            from ._lib import check, pt
+            check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
         self.r = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, tex_factory=factory,
-                          halo=self._halo, gbuffer_rows=(self.plan.row0, self.plan.row1), **kw)
+                          halo=self._halo, after_gbuffer=self._after_gbuffer, **kw)
+        # per G-buffer set: the device motion bound the G-buffer kernel writes, its pinned host copy, an event
+        ng = len(self.r.gbuf)
+        self._mb_dev = torch.zeros(ng, dtype=torch.int32, device=dev)
+        self._mb_host = torch.zeros(ng, dtype=torch.int32).pin_memory()
+        self._mb_event = [torch.cuda.Event() for _ in range(ng)]
+        for b, p in enumerate(self.r.init_pass):
+            p.set_motion_bound(self._mb_dev[b:b + 1].data_ptr())
+        self._mb_set = None
+        self.motion_log = []  # per frame: (all-reduced |motion.y| in rows, history rows exchanged)
         self.camera = self.r.camera
         self.pass_path_tracing = self.r.pass_path_tracing
 
-    def _halo(self, stage: str, handles) -> None:
+    def _after_gbuffer(self, b: int, stream) -> None:
+        """The G-buffer of set b was issued on `stream`: fetch its motion bound behind it (no wait here)."""
+        import torch
+
+        with torch.cuda.stream(stream):
+            self._mb_host[b:b + 1].copy_(self._mb_dev[b:b + 1], non_blocking=True)
+            self._mb_event[b].record(stream)
+        self._mb_set = b
+
+    def _motion(self) -> None:
+        """This frame's history reach: wait for the G-buffer's bound (the path tracer is already queued), MAX over
+        ranks on the host."""
+        import numpy as np
+
+        b = self._mb_set
+        self._mb_event[b].synchronize()
+        m = float(self._mb_host[b:b + 1].numpy().view(np.float32)[0])
+        m = allreduce_motion(m, self.dist, self._group)
+        n = self.plan.set_motion(m)
+        self.motion_log.append((m * self.plan.H, n))
+
+    def _halo(self, stage: str, handles: dict) -> None:
         if not self.exchange:
             return
-        for st, _, n in HALO_SCHEDULE:
-            if st == stage:
-                halo_exchange([self._tensors[h] for h in handles], self.plan, self.plan.rows_for(n), self.dist)
-                return
+        if stage == "reproject":
+            self._motion()
+        run_stage(stage, {k: self._tensors[h] for k, h in handles.items()}, self.plan, self.dist)
 
     def frame(self) -> None:
         self.r.frame()

@@ -197,6 +197,10 @@ class RenderPass:
         """Accumulate per-row BVH visits into a device uint32 array (path tracer; 0 disables)."""
         check(pt().pt_pass_set_row_cost(self._handle(), C.c_void_p(device_ptr or None)))
 
+    def set_motion_bound(self, device_ptr: int) -> None:
+        """G-buffer pass: store the largest |motion.y| of every draw into a device uint32 (float bits; 0 disables)."""
+        check(pt().pt_pass_set_motion_bound(self._handle(), C.c_void_p(device_ptr or None)))
+
     def destroy(self) -> None:
         if self._h is not None:
             check(pt().pt_pass_destroy(self._h))

@@ -57,11 +57,12 @@ class Renderer:
     def __init__(self, scene: Scene, width: int, height: int, config: parameter_config | None = None,
                  mode: str = "fast", aspect_corrected: bool | None = None, band=None, prune: bool = True,
                  atrous_exact: bool = False, run_taa: bool = True, run_output: bool = True, tex_factory=None,
-                 halo=None, gbuffer_rows=None, frames_in_flight: int = 1):
+                 halo=None, gbuffer_rows=None, frames_in_flight: int = 1, after_gbuffer=None):
         """band = (y0, y1, row0, rows) for screen-band sharding; tex_factory(w, h) -> handle allocates the
-        frame-sized planes (ptsvgf.dist wraps torch tensors); halo(stage, handles) is called before the
-        SVGF passes that read neighbour rows (dist.HALO_SCHEDULE); gbuffer_rows = (row0, row1) ghost rows
-        the G-buffer recomputes locally.
+        frame-sized planes (ptsvgf.dist wraps torch tensors); halo(stage, {plane name: handle}) is called before
+        the SVGF passes that read rows beyond the band (dist.HALO_SCHEDULE names the planes); after_gbuffer(set,
+        torch stream) right after a G-buffer draw is issued; gbuffer_rows = (y0, y1) rows the G-buffer computes
+        (default: the band).
 
         frames_in_flight = K > 1 (fast driver): the G-buffer + path tracer of frame f (the front end, which
         depends on nothing but the camera) run on stream f % K while the SVGF chain (sequential: each frame
@@ -82,6 +83,8 @@ class Renderer:
         self.run_taa = run_taa
         self.run_output = run_output
         self.scene = scene
+        self._after_gbuffer = after_gbuffer
+        self._lib_stream = None  # torch stream the library draws on (None: torch's current stream)
         if band is not None:
             y0, y1, row0, rows = band
             gl.set_band(self.W, self.H, y0, y1, row0, rows)
@@ -293,6 +296,10 @@ class Renderer:
         ip.set_uniform_mat4("pre_viewproj", self.pre_viewproj)
         ip.set_uniform_uint("frameCounter", cam.frameCounter)
         self._draw(ip, "gbuffer")
+        if self._after_gbuffer is not None:
+            import torch
+
+            self._after_gbuffer(b, self._lib_stream or torch.cuda.current_stream())
 
     def _path_trace(self, hint=None):
         """hint: this frame's G-buffer set (drawn before on the same stream); its world position and normal/depth
@@ -423,24 +430,25 @@ class Renderer:
                 start = torch.cuda.Event()
                 start.record(fe)
                 gs.wait_event(start)
-                _set_stream(gs)
+                self._stream_to(gs)
                 self._gbuffer(f % ng)
                 gdone = torch.cuda.Event()
                 gdone.record(gs)
-                _set_stream(fe)
+                self._stream_to(fe)
                 self._path_trace()
                 fe.wait_event(gdone)
             else:
-                _set_stream(fe)
+                self._stream_to(fe)
                 self._gbuffer_and_pt(f % ng)
             done = torch.cuda.Event()
             done.record(fe)
             self._fe_prev = done
             self._back.wait_event(done)
-            _set_stream(self._back)
+            self._stream_to(self._back)
         else:
             self._gbuffer_and_pt(f % ng)
-        self._halo("reproject", [self.hist_illum[pb], self.moments[pb]])
+        self._halo("reproject", {"prev_illum": self.hist_illum[pb], "prev_moments": self.moments[pb],
+                                 "prev_nd": gp["normal_depth"]})
         rp = self.reproject[b]
         rp.reset_texture_slot()
         rp.set_uniform_float("depth_threshold", cfg.reproj_depth_threshold)
@@ -455,7 +463,7 @@ class Renderer:
         rp.set_texture_uniform(GL_TEXTURE_2D, gp["normal_depth"], "gPrevNormalAndLinearZ")
         rp.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
         self._draw(rp, "reproject")
-        self._halo("variance", [self.illum, self.moments[b]])
+        self._halo("variance", {"illum": self.illum, "moments": self.moments[b], "nd": g["normal_depth"]})
         vp = self.variance_compute_pass
         vp.reset_texture_slot()
         vp.set_uniform_float("gPhiColor", cfg.sigma_l)
@@ -479,7 +487,7 @@ class Renderer:
                 dests.append("pong" if prev_tex == self.ping else "ping")
         self._atrous_last = (g, [(dests[i], 1 << i) for i in range(n)], src)
         for i in range(n):
-            self._halo(f"atrous{i}", [src])
+            self._halo(f"atrous{i}", {"atrous_in": src})
             ap = self.atrous_to[dests[i]]
             ap.reset_texture_slot()
             ap.set_uniform_float("gPhiColor", cfg.sigma_l)
@@ -500,7 +508,7 @@ class Renderer:
         mp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
         self._draw(mp, "modulate")
         if self.run_taa:
-            self._halo("taa", [self.modulate_color, self.taa[pb]])
+            self._halo("taa", {"modulate": self.modulate_color, "velocity": g["velocity"], "prev_taa": self.taa[pb]})
             tp = self.pass_taa[b]
             tp.reset_texture_slot()
             tp.set_texture_uniform(GL_TEXTURE_2D, self.modulate_color, "currentColor")
@@ -520,7 +528,7 @@ class Renderer:
         g, iters, src0 = self._atrous_last
         stream = self._back if self.K > 1 else torch.cuda.current_stream()
         torch.cuda.synchronize()
-        _set_stream(stream)
+        self._stream_to(stream)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
         def once():
@@ -540,7 +548,12 @@ class Renderer:
         e1.synchronize()
         return e0.elapsed_time(e1) / (reps * len(iters))
 
-    def _halo(self, stage: str, handles) -> None:
+    def _stream_to(self, stream) -> None:
+        """Issue the following draws on this torch stream."""
+        _set_stream(stream)
+        self._lib_stream = stream
+
+    def _halo(self, stage: str, handles: dict) -> None:
         if self._halo_cb is None:
             return
         if self.K > 1:  # the exchange belongs to the back-end stream (torch.distributed uses the current one)

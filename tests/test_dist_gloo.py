@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, W, H, frames, moving, bounds=None):
+def _worker(rank, world, port, W, H, frames, moves, bounds=None, ghost=None):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, here)
@@ -35,14 +35,14 @@ def _worker(rank, world, port, W, H, frames, moving, bounds=None):
     try:
         import oracle_ref as O
         from ptsvgf.camera import rigid_inverse
-        from ptsvgf.dist import HALO_SCHEDULE, BandPlan, halo_exchange
+        from ptsvgf.dist import GHOST, BandPlan, allreduce_motion, run_stage
         from ptsvgf.scene import build_scene
 
         scene = build_scene("table_clock_plant", hdr_size=(128, 64), plant_leaves=20)
-        plan = BandPlan(W, H, rank, world, ghost=34, reproj_halo=8, bounds=bounds)
+        plan = BandPlan(W, H, rank, world, ghost=ghost or GHOST, bounds=bounds)
         full = O.OracleFrameLoop(scene, W, H, threads=2)
         band = O.OracleFrameLoop(scene, W, H, threads=2)  # same camera path, band-restricted execution
-        sched = {st: n for st, _, n in HALO_SCHEDULE}
+        log = []
 
         def poison(a, lo, hi):
             a[:lo] = np.nan
@@ -50,64 +50,125 @@ def _worker(rank, world, port, W, H, frames, moving, bounds=None):
             return a
 
         def halo(stage, arrays):
-            ts = [torch.from_numpy(a)[plan.row0:plan.row1] for a in arrays]
-            halo_exchange(ts, plan, plan.rows_for(sched[stage]), dist)
+            run_stage(stage, {k: torch.from_numpy(a)[plan.row0:plan.row1] for k, a in arrays.items()}, plan, dist)
 
         nan = lambda: np.full((H, W, 4), np.nan, np.float32)  # noqa: E731
         prev_illum, prev_moments, prev_nd, prev_taa = nan(), nan(), nan(), nan()
         for q in (prev_illum, prev_moments, prev_nd, prev_taa):  # history starts as zeros (the build zero-fills)
             q[plan.row0:plan.row1] = 0.0
         for f in range(frames):
-            if moving and f:
-                full.camera.orbit(1.5, 0.5)
-                band.camera.orbit(1.5, 0.5)
+            mv = moves[f] if f < len(moves) else None
+            if mv:
+                full.camera.orbit(*mv)
+                band.camera.orbit(*mv)
             want = full.frame()
             cam, cfg = band.camera, band.cfg
             cam.update()
             view, proj = cam.cam_view_mat, cam.cam_proj_mat
             g = O.gbuffer(scene.raster, W, H, view, proj, band.pre_viewproj, 2)
-            for k in g:
-                poison(g[k], plan.row0, plan.row1)
+            for k in g:                      # the G-buffer computes the owned rows only
+                poison(g[k], plan.y0, plan.y1)
             col, em, al = band.os.path_trace(W, H, cam.frameCounter, cam.cam_position, rigid_inverse(view),
                                              cfg.clamp_threshold, cfg.max_tracing_depth, band.aspect_corrected,
                                              rows=(plan.y0, plan.y1), threads=2)
             for a in (col, em, al):
                 poison(a, plan.y0, plan.y1)
-            halo("reproject", [prev_illum, prev_moments])
+            # the motion bound the G-buffer kernel reduces (owned surface pixels), MAX over ranks
+            own = g["velocity"][plan.y0:plan.y1]
+            surf = g["normal_depth"][plan.y0:plan.y1, :, 3] != 1.0
+            m = float(np.abs(own[..., 1][surf]).max()) if surf.any() else 0.0
+            n = plan.set_motion(allreduce_motion(m, dist))
+            log.append(n)
+            halo("reproject", dict(prev_illum=prev_illum, prev_moments=prev_moments, prev_nd=prev_nd))
             ri, rm = O.reproject(g["velocity"], col, al, em, prev_illum, prev_moments, g["normal_depth"], prev_nd,
                                  g["fwidth"], np.float32(1.0 / W), np.float32(1.0 / H), 10.0, 16.0, 2)
             poison(ri, plan.y0, plan.y1)
             poison(rm, plan.y0, plan.y1)
-            halo("variance", [ri, rm])
+            halo("variance", dict(illum=ri, moments=rm, nd=g["normal_depth"]))
             a = poison(O.variance(ri, rm, g["normal_depth"], g["fwidth"], 4.0, 128.0, 2), plan.y0, plan.y1)
-            hist = None
             for i in range(cfg.num_atrous_iterations):
-                halo(f"atrous{i}", [a])
+                halo(f"atrous{i}", dict(atrous_in=a))
                 a = poison(O.atrous(a, g["normal_depth"], g["fwidth"], 1 << i, 4.0, 128.0, 2), plan.y0, plan.y1)
                 if i == 1:
                     hist = a
             m = poison(O.modulate(al, em, a, g["normal_depth"], 2), plan.y0, plan.y1)
-            halo("taa", [m, prev_taa])
+            halo("taa", dict(modulate=m, velocity=g["velocity"], prev_taa=prev_taa))
             t = poison(O.taa(m, prev_taa, g["velocity"], g["normal_depth"], cam.frameCounter, 2), plan.y0, plan.y1)
             prev_taa = t
             band.pre_viewproj = band._mat_mul(proj, view)
             cam.frameCounter += 1
             prev_illum, prev_moments, prev_nd = hist, rm, g["normal_depth"]
-            got = dict(color=col, reproj_illum=ri, reproj_moments=rm, variance=None, atrous=a, modulate=m, final=t)
+            got = dict(color=col, reproj_illum=ri, reproj_moments=rm, atrous=a, modulate=m, final=t)
             for k, v in got.items():
-                if v is None:
-                    continue
                 o, w = v[plan.y0:plan.y1], want[k][plan.y0:plan.y1]
                 assert np.array_equal(np.isnan(o), np.isnan(w)), (rank, f, k, "NaN leaked into the band")
                 assert np.array_equal(np.nan_to_num(o), np.nan_to_num(w)), (rank, f, k)
+        if rank == 0:
+            print("history rows per frame:", log)
+        return log
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,moving,bounds", [(2, False, None), (3, True, None), (2, True, (0, 38, 108))])
-def test_band_halo_schedule_gloo(world, moving, bounds):
-    W, H = 48, 108  # bands of 54 / 36 rows (>= the 32-row a-trous halo); uneven (balanced) split 38 / 70
-    mp.spawn(_worker, args=(world, _free_port(), W, H, 3, moving, bounds), nprocs=world, join=True)
+SMALL = [(1.5, 0.5)] * 3
+
+
+@pytest.mark.parametrize("world,moves,bounds", [(2, [], None), (3, SMALL, None), (2, SMALL, (0, 38, 108))])
+def test_band_halo_schedule_gloo(world, moves, bounds):
+    W, H = 48, 108  # bands of 54 / 36 rows; uneven (balanced) split 38 / 70
+    mp.spawn(_worker, args=(world, _free_port(), W, H, 3, moves, bounds), nprocs=world, join=True)
+
+
+# 5-6 degrees of pitch per frame at 64 x 256 move the surface pixels of rows 0-21 by 11-16 rows (the orbit turns
+# about the frame centre, so motion is largest near the frame edges): band boundaries there read history rows far
+# beyond round 1's fixed 8-row halo (forcing a fixed 8 rows makes this case fail). The 16-row bands make
+# the halos span several ranks (rows from rank r +- 2).
+BIG = [(0.0, 5.0), (2.0, -5.0), (-3.0, 6.0)]
+
+
+@pytest.mark.parametrize("world,bounds", [(2, (0, 20, 256)), (4, (0, 16, 32, 140, 256))])
+def test_band_halo_large_motion_gloo(world, bounds):
+    W, H = 64, 256
+    mp.spawn(_worker, args=(world, _free_port(), W, H, 4, [None] + BIG, bounds), nprocs=world, join=True)
+
+
+def test_band_motion_beyond_ghost_raises():
+    from ptsvgf.dist import REPROJ_REACH, BandPlan, motion_rows
+    p = BandPlan(64, 400, 0, 2, ghost=40)
+    assert p.set_motion(10.0 / 400) == 10 + REPROJ_REACH
+    assert p.rows_for("reproj") == 13 and p.rows_for("reproj_nd") == 0
+    assert p.rows_for("nd") == 32
+    p.set_motion(37.0 / 400)
+    assert p.rows_for("reproj_nd") == 40
+    with pytest.raises(RuntimeError):
+        p.set_motion(37.5 / 400)   # 38 + 3 rows of reach > 40 ghost rows
+    with pytest.raises(RuntimeError):
+        p.set_motion(float("inf"))
+    with pytest.raises(RuntimeError):
+        motion_rows(float("nan"), 100)
+    with pytest.raises(ValueError):
+        BandPlan(64, 400, 0, 2, ghost=40, iterations=6)   # step 32 reads 64 rows
+    assert BandPlan(64, 600, 0, 2, ghost=128, iterations=6).nd_rows == 64
+
+
+def test_halo_intervals_cover_exactly_what_is_read():
+    """need()/owned() bookkeeping: for every rank pair the rows sent equal the rows received, and the union of what
+    a rank receives is exactly its n-row halo (minus frame edges)."""
+    from ptsvgf.dist import BandPlan, _meet
+    for bounds in [(0, 90, 106, 122, 256), (0, 64, 128, 192, 256), (0, 16, 240, 256)]:
+        world = len(bounds) - 1
+        plans = [BandPlan(40, 256, r, world, ghost=128, bounds=bounds) for r in range(world)]
+        for n in (1, 3, 20, 40, 100):
+            for me in plans:
+                got = set()
+                for k in plans:
+                    if k.rank == me.rank:
+                        continue
+                    for part in me.need(me.rank, n):
+                        a, b = _meet(k.owned(k.rank), part)
+                        got.update(range(a, b))
+                want = set(range(max(0, me.y0 - n), me.y0)) | set(range(me.y1, min(256, me.y1 + n)))
+                assert got == want, (bounds, n, me.rank)
 
 
 def test_band_plan_properties():
@@ -120,7 +181,7 @@ def test_band_plan_properties():
         for p in plans:
             assert p.row0 == max(0, p.y0 - GHOST) and p.row1 == min(2160, p.y1 + GHOST)
     with pytest.raises(ValueError):
-        BandPlan(64, 40, 0, 4)  # bands thinner than the a-trous halo
+        BandPlan(64, 40, 0, 4, bounds=(0, 10, 10, 30, 40))  # empty band
 
 
 def test_balanced_bounds_properties():
@@ -142,7 +203,7 @@ def test_balanced_bounds_properties():
     b = balanced_bounds(spike, 4)
     assert (np.diff(b) >= MIN_BAND_ROWS).all()
     with pytest.raises(ValueError):
-        balanced_bounds(np.ones(100), 4)
+        balanced_bounds(np.ones(40), 4)   # 4 bands of >= MIN_BAND_ROWS do not fit
     a, c = fit_row_cost([10.0, 30.0], [100, 100], [2.0, 4.0])
     assert abs(a - 0.1) < 1e-9 and abs(c - 0.01) < 1e-9
     a, c = fit_row_cost([10.0, 30.0], [100, 100], [5.0, 1.0])   # negative slope -> single-term fallback

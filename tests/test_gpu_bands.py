@@ -1,7 +1,13 @@
-"""GPU band rendering: two ranks on the one visible GPU (gloo with host staging —
-RCCL needs one device per rank, which the driver's 8-GPU scaling run provides)
-render one frame as two bands with ptsvgf.dist.BandRenderer; the owned rows
-must equal the single-GPU full-frame render bit for bit."""
+"""GPU band rendering: several ranks on the one visible GPU (gloo with host
+staging — RCCL needs one device per rank, which the driver's 8-GPU scaling run
+provides) render frames as bands with ptsvgf.dist.BandRenderer; the owned rows
+must equal the single-GPU full-frame render bit for bit.
+
+The 8-rank case is BASELINE configs[3]/[4] on one GPU: the bench scene at 4K,
+equal 270-row bands, 8 frames in flight, TAA on, and a camera that moves up to
+~35 rows per frame near the frame edges (where the band boundaries at rows 270
+and 1890 sit), so the history exchanges are sized by the per-frame motion bound
+(ptsvgf.dist.BandPlan.set_motion) far beyond round 1's fixed 8 rows."""
 import os
 import socket
 import tempfile
@@ -23,7 +29,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, outdir, moving, balance, fif=1):
+def _worker(rank, world, port, outdir, moving, balance, fif=1, size=(W, H), bench_scene=False, moves=None):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(os.path.dirname(here), "path-tracing-svgf_amd"))
@@ -39,19 +45,40 @@ def _worker(rank, world, port, outdir, moving, balance, fif=1):
     torch.cuda.set_device(0)
     gl.init(0)
     check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
-    scene = build_scene("table_clock_plant", hdr_size=(256, 128), plant_leaves=40)
-    r = make_band_renderer(scene, W, H, parameter_config(), rank, world, dist, balance=balance, run_taa=True,
+    scene = _scene(bench_scene)
+    Wf, Hf = size
+    r = make_band_renderer(scene, Wf, Hf, parameter_config(), rank, world, dist, balance=balance, run_taa=True,
                            frames_in_flight=fif)
-    for f in range(FRAMES):
-        if moving and f:
-            r.camera.orbit(1.5, 0.5)
+    for f in range(len(moves) if moves else FRAMES):
+        mv = moves[f] if moves else ((1.5, 0.5) if moving and f else None)
+        if mv:
+            r.camera.orbit(*mv)
         r.frame()
     torch.cuda.synchronize()
     p = r.plan
     out = {k: gl.readback(r.planes()[k])[p.y0 - p.row0:p.y1 - p.row0] for k in KEYS}
-    np.savez(os.path.join(outdir, f"rank{rank}.npz"), y0=p.y0, y1=p.y1, **out)
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"), y0=p.y0, y1=p.y1, motion=np.array(r.motion_log), **out)
     gl.shutdown()
     dist.destroy_process_group()
+
+
+def _scene(bench):
+    from ptsvgf.scene import build_scene
+    if bench:
+        return build_scene("table_clock_plant")  # the bench scene, full size
+    return build_scene("table_clock_plant", hdr_size=(256, 128), plant_leaves=40)
+
+
+def _compare(bands, want):
+    for b in bands:
+        y0, y1 = int(b["y0"]), int(b["y1"])
+        for k in KEYS:
+            bad = np.argwhere(np.any(b[k].view(np.uint32) != want[k][y0:y1].view(np.uint32), axis=-1))
+            if len(bad):
+                rows = sorted(set(int(r) + y0 for r in bad[:, 0]))
+                print(k, "band", (y0, y1), "differing rows", rows[:20], "count", len(bad),
+                      "sample", b[k][tuple(bad[0])], want[k][y0:y1][tuple(bad[0])])
+            assert len(bad) == 0, (k, y0, y1)
 
 
 @pytest.mark.parametrize("moving,balance,fif", [(False, False, 1), (True, False, 1), (True, True, 1), (True, True, 3)])
@@ -74,12 +101,35 @@ def test_two_bands_equal_full_frame(gpu, moving, balance, fif):
             full.camera.orbit(1.5, 0.5)
         full.frame()
     want = {k: gl.readback(full.planes()[k]) for k in KEYS}
-    for b in bands:
-        y0, y1 = int(b["y0"]), int(b["y1"])
-        for k in KEYS:
-            bad = np.argwhere(np.any(b[k] != want[k][y0:y1], axis=-1))
-            if len(bad):
-                rows = sorted(set(int(r) + y0 for r in bad[:, 0]))
-                print(k, "band", (y0, y1), "differing rows", rows[:20], "count", len(bad),
-                      "sample", b[k][tuple(bad[0])], want[k][y0:y1][tuple(bad[0])])
-            assert len(bad) == 0, (k, y0, y1)
+    full.close()
+    _compare(bands, want)
+
+
+MOVES_4K = [None, (1.0, 0.75), (-1.5, -1.0), (0.5, 1.5)]
+
+
+def test_eight_bands_4k_moving_equal_full_frame(gpu):
+    """8 ranks x 270 rows of the 4K bench frame, frames in flight, TAA, moving camera: bit-equal to one GPU."""
+    import torch.multiprocessing as mp
+
+    from ptsvgf.camera import parameter_config
+    from ptsvgf.renderer import Renderer
+
+    gl = gpu
+    Wf, Hf, world = 3840, 2160, 8
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _port(), d, True, False, 8, (Wf, Hf), True, MOVES_4K), nprocs=world,
+                 join=True)
+        bands = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(world)]
+    motion = bands[0]["motion"]
+    print("all-reduced max |motion.y| (rows) and history rows exchanged per frame:", motion.tolist())
+    assert motion[:, 1].max() > 30  # the history exchange really grew past round 1's 8 rows
+    full = Renderer(_scene(True), Wf, Hf, parameter_config(), mode="fast", aspect_corrected=True, run_taa=True,
+                    run_output=False)
+    for mv in MOVES_4K:
+        if mv:
+            full.camera.orbit(*mv)
+        full.frame()
+    want = {k: gl.readback(full.planes()[k]) for k in KEYS}
+    full.close()
+    _compare(bands, want)

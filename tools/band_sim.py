@@ -26,15 +26,25 @@ LOG = []
 
 
 class FakeDist:
+    """Stands in for torch.distributed: this rank's own motion bound is the all-reduced one."""
+    class ReduceOp:
+        MAX = "max"
+
     def get_backend(self, group=None):
-        return "nccl"
+        return "gloo"
+
+    def all_reduce(self, t, op=None, group=None):
+        return None
 
 
-def fake_exchange(tensors, plan, n, dist, group=None):
-    if plan.world == 1 or n <= 0:
-        return
-    nb = (plan.up is not None) + (plan.down is not None)
-    LOG.append(sum(n * t.shape[1] * t.shape[2] * 4 for t in tensors) * nb)
+def fake_exchange(items, plan, dist, group=None):
+    """Record the bytes the real exchange would send (rows this rank sends to the others, ghost-bounded)."""
+    for t, n in items:
+        if plan.world == 1 or n <= 0:
+            continue
+        sent = sum(max(0, min(b, plan.y1) - max(a, plan.y0)) for k in range(plan.world) if k != plan.rank
+                   for a, b in plan.need(k, n))
+        LOG.append(sent * t.shape[1] * t.shape[2] * 4)
 
 
 D.halo_exchange = fake_exchange
