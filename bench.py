@@ -9,6 +9,14 @@ the output tonemap are excluded there and excluded here). Inputs (scene, BVH,
 environment) are resident in HBM before timing starts; the camera orbits by a
 fixed step each frame only with --moving.
 
+`value` is the pipelined rate (frames_in_flight front ends overlap, DESIGN.md);
+the line also carries the serial rate (one frame at a time: camera-to-display
+latency of one frame), 1080p (configs[1]), the path tracer's rays/s and BVH
+visits/s, a surface-dominated view, the a-trous roofline three ways (SURVEY.md's
+52 B/px convention, PMC traffic, background-weighted bytes), the CPU oracle on
+16 threads and on 1 core, and configs[0] (Cornell box + teapot 512x512, SVGF off,
+CPU reference traversal).
+
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
 each rank renders one horizontal band of the SAME 4K frame and exchanges SVGF
 halo rows with its neighbours over RCCL (ptsvgf.dist) — strong scaling.
@@ -29,12 +37,16 @@ os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 sys.path.insert(0, os.path.join(REPO, "path-tracing-svgf_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
-ATROUS_BYTES_PER_PX = 52  # illum 16 + normal/z 16 + depth-fwidth 4 + write 16
-HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8 TB/s spec
-METRIC = "frames/sec @1spp+SVGF, 1080p & 4K; \u00e0-trous HBM GB/s vs peak"  # BASELINE.json "metric"
+ATROUS_BYTES_PER_PX = 52     # illum 16 + normal/z 16 + depth-fwidth 4 + write 16
+ATROUS_BYTES_BG_PX = 36      # a background pixel: depth-fwidth/flag 4 + illum 16 + write 16 (copied)
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8 TB/s spec
+METRIC = "frames/sec @1spp+SVGF, 1080p & 4K; à-trous HBM GB/s vs peak"  # BASELINE.json "metric"
 ATROUS_KERNEL = "atrous_tile_kernel"
 # HBM bytes per a-trous launch measured with rocprofv3 PMC passes (tools/gpu_profile.sh), committed under profiles/
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "atrous_traffic.json")
+# configs[2] on a surface-dominated camera (94 % geometry pixels: the plant, a corner of the clock; ~24 % on the
+# default view): orbit radius, elevation, azimuth and look-at point (Utils/camera.h:14-38 parameters)
+VIEWS = {"default": None, "surface": dict(r_dis=0.8, upAngle=70.0, rotatAngle=180.0, move_vec=(0.4, -0.25, 0.0))}
 
 
 def atrous_traffic(W, rows):
@@ -58,10 +70,13 @@ def parse():
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--scene", default="table_clock_plant")
+    ap.add_argument("--view", default="default", choices=sorted(VIEWS), help="camera of the headline run")
     ap.add_argument("--moving", action="store_true", help="orbit the camera 1 deg/frame (configs[4])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", default="960x540", help="oracle sample frame size for cpu_baseline")
+    ap.add_argument("--cpu-sample", default="960x540", help="oracle sample frame size for cpu_baseline (16 threads)")
+    ap.add_argument("--cpu-sample-1core", default="480x270", help="oracle sample frame size on 1 core")
     ap.add_argument("--no-1080p", action="store_true", help="skip the secondary 1080p measurement")
+    ap.add_argument("--no-extras", action="store_true", help="skip the serial, surface-view and configs[0] runs")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for --gpus > 1 (nccl = RCCL)")
     ap.add_argument("--equal-bands", action="store_true", help="multi-GPU: equal band heights (no cost balancing)")
     ap.add_argument("--breakdown", action="store_true", help="print per-pass ms to stderr")
@@ -74,29 +89,86 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(scene, W, H, sample: str):
-    """Time the CPU oracle (the reference algorithm restated, OpenMP over rows) on a bounded sample
-    frame and scale to the full frame by pixel count."""
-    import oracle_ref as O
-    from ptsvgf.camera import parameter_config
+def log(msg: str) -> None:
+    """Progress on stderr (the JSON line is the only stdout)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
-    sw, sh = (int(v) for v in sample.split("x"))
-    threads = min(16, os.cpu_count() or 1)
-    loop = O.OracleFrameLoop(scene, sw, sh, parameter_config(), aspect_corrected=True, threads=threads,
-                              run_taa=False)
-    loop.frame()  # warm (first frame: young history, full 7x7 variance)
+
+def oracle_fps(scene, W, H, threads, seconds, svgf=True):
+    """Frames/s of the CPU oracle (the reference algorithm restated, OpenMP over rows) on a W x H frame: the whole
+    frame loop (G-buffer + PT + SVGF), or the path tracer alone (svgf=False)."""
+    import oracle_ref as O
+    from ptsvgf.camera import parameter_config, rigid_inverse
+
+    loop = O.OracleFrameLoop(scene, W, H, parameter_config(), aspect_corrected=W != H, threads=threads, run_taa=False)
+
+    def frame():
+        if svgf:
+            loop.frame()
+            return
+        cam = loop.camera
+        cam.update()
+        loop.os.path_trace(W, H, cam.frameCounter, cam.cam_position, rigid_inverse(cam.cam_view_mat),
+                           aspect_corrected=loop.aspect_corrected, threads=threads)
+        cam.frameCounter += 1
+
+    frame()  # warm (first frame: young history, full 7x7 variance)
     t0 = time.perf_counter()
     n = 0
     while True:
-        loop.frame()
+        frame()
         n += 1
-        if time.perf_counter() - t0 > 10.0 and n >= 3:  # ~10 s of CPU work
+        if time.perf_counter() - t0 > seconds and n >= 3:
             break
-    dt = (time.perf_counter() - t0) / n
-    scale = (W * H) / (sw * sh)
-    return {"value": 1.0 / (dt * scale), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"oracle frame loop (G-buffer+PT+SVGF) at {sw}x{sh}, {n} frames, {dt * 1e3:.1f} ms/frame, "
-                      f"scaled by pixel count to {W}x{H}"}
+    return n / (time.perf_counter() - t0), n
+
+
+def cpu_baseline(scene, W, H, sample: str, sample1: str):
+    """The CPU oracle on a bounded sample frame (16 threads, and 1 core), scaled to W x H by pixel count."""
+    out = {}
+    for key, smp, threads in (("all", sample, min(16, os.cpu_count() or 1)), ("one", sample1, 1)):
+        sw, sh = (int(v) for v in smp.split("x"))
+        fps, n = oracle_fps(scene, sw, sh, threads, 10.0)
+        scale = (W * H) / (sw * sh)
+        out[key] = {"value": fps / scale, "unit": "frames/s", "cores": threads, "kind": "port",
+                    "sample": f"oracle frame loop (G-buffer+PT+SVGF) at {sw}x{sh} on {threads} thread(s), {n} frames, "
+                              f"{1e3 / fps:.1f} ms/frame, scaled by pixel count to {W}x{H}"}
+    line = dict(out["all"])
+    line["single_core"] = out["one"]
+    return line
+
+
+def config0(gl):
+    """configs[0]: Cornell box + teapot stand-in, 512x512, 1 spp, SVGF off — the CPU reference traversal (oracle
+    path tracer, 16 threads and 1 core), with the GPU path tracer's rate on the same frame beside it."""
+    import torch
+
+    from ptsvgf.camera import parameter_config
+    from ptsvgf.renderer import Renderer
+    from ptsvgf.scene import build_scene
+
+    from ptsvgf._lib import check, pt
+
+    check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
+    scene = build_scene("cornell_teapot")
+    res = {"workload": "cornell_teapot 512x512 1spp depth2, SVGF off", "triangles": scene.ntris}
+    for key, threads in (("cpu_fps_16t", min(16, os.cpu_count() or 1)), ("cpu_fps_1t", 1)):
+        fps, n = oracle_fps(scene, 512, 512, threads, 4.0, svgf=False)
+        res[key] = round(fps, 3)
+    r = Renderer(scene, 512, 512, parameter_config(), mode="fast", run_taa=False, run_output=False)
+    for _ in range(3):
+        r._path_trace()
+        r.camera.frameCounter += 1
+    torch.cuda.synchronize()
+    n = 200
+    t0 = time.perf_counter()
+    for _ in range(n):
+        r._path_trace()
+        r.camera.frameCounter += 1
+    torch.cuda.synchronize()
+    res["gpu_pt_fps"] = round(n / (time.perf_counter() - t0), 1)
+    r.close()
+    return res
 
 
 def main():
@@ -138,28 +210,43 @@ def main():
     from ptsvgf._lib import check, pt
     check(pt().pt_set_stream(stream.cuda_stream))
 
-    def run(W, H):
-        """Warm up, time exactly args.steps frames (barrier + sync on both sides, max over ranks), then one
-        profiled frame for the per-pass HIP-event breakdown."""
+    def allsum(vals):
+        if not dist:
+            return vals
+        t = torch.tensor(vals, dtype=torch.float64, device="cuda")
+        dist.all_reduce(t)
+        return t.tolist()
+
+    def run(W, H, K, view="default", probes=True):
+        """Warm up, time exactly args.steps frames (barrier + sync on both sides, max over ranks); then, untimed:
+        one frame with the traversal counters on, one profiled frame (per-pass HIP events), the a-trous launches
+        replayed between HIP events, and the surface fraction of the frame."""
+        check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))  # a previous renderer's streams are gone
+        log(f"run {W}x{H} K={K} view={view}")
         if world > 1:
             from ptsvgf.dist import make_band_renderer
             r = make_band_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,
-                                   frames_in_flight=args.frames_in_flight)
+                                   frames_in_flight=K)
         else:
             from ptsvgf.renderer import Renderer
             r = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, run_taa=False, run_output=False,
-                         frames_in_flight=args.frames_in_flight)
+                         frames_in_flight=K)
         r.pass_path_tracing.set_uniform_int("pt_kernel", args.pt_kernel)
         for kv in args.pt_uniform:
             name, val = kv.split("=")
             r.pass_path_tracing.set_uniform_int(name, int(val))
+        if VIEWS[view]:
+            cam = r.camera
+            for k, v in VIEWS[view].items():
+                setattr(cam, k, np.array(v, np.float32) if isinstance(v, tuple) else np.float32(v))
+            cam.dirty = True
 
         def step():
             if args.moving:
                 r.camera.orbit(1.0, 0.0)
             r.frame()
 
-        for _ in range(args.warmup):
+        for _ in range(max(args.warmup, K + 1)):
             step()
         torch.cuda.synchronize()
         if dist:
@@ -177,42 +264,105 @@ def main():
             t = torch.tensor([dt], device="cuda")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
-        r.profile(True)
-        step()
-        torch.cuda.synchronize()
-        per_pass = r.pass_times()
-        r.profile(False)
-        # the roofline kernel alone: the last frame's 5 a-trous launches replayed back to back between two
-        # HIP events on the library's stream (per-draw events above include launch gaps)
-        per_pass["atrous_avg_ms"] = r.time_atrous(20)
-        rows = r.rows_rendered() if hasattr(r, "rows_rendered") else H
+        out = {"dt": dt, "rows": r.rows_rendered() if hasattr(r, "rows_rendered") else H}
+        log(f"  {args.steps} frames in {dt:.3f} s = {args.steps / dt:.2f} frames/s")
+        if probes:
+            st = r.trace_stats()
+            out["stats"] = dict(zip(st, allsum([float(v) for v in st.values()])))
+            r.profile(True)
+            step()
+            torch.cuda.synchronize()
+            out["per_pass"] = r.pass_times()
+            r.profile(False)
+            # the roofline kernel alone: the last frame's 5 a-trous launches replayed back to back between two
+            # HIP events on the library's stream (per-draw events above include launch gaps)
+            out["per_pass"]["atrous_avg_ms"] = r.time_atrous(20)
+            nd = gl.readback(r.planes()["normal_depth"])
+            if world > 1:
+                p = r.plan
+                nd = nd[p.y0 - p.row0:p.y1 - p.row0]
+            bg, px = allsum([float(np.count_nonzero(nd[..., 3] == 1.0)), float(nd.shape[0] * nd.shape[1])])
+            out["background_fraction"] = bg / px
+            if hasattr(r, "motion_log") and r.motion_log:
+                out["max_history_rows"] = int(max(n for _, n in r.motion_log))
         r.close() if hasattr(r, "close") else None
-        return dt, per_pass, rows
+        return out
+
+    def atrous_roofline(res, W, rows):
+        atrous_ms = res["per_pass"].get("atrous_avg_ms")
+        if not atrous_ms:
+            return None
+        t = atrous_ms * 1e-3
+        alg = ATROUS_BYTES_PER_PX * W * rows
+        achieved = alg / t / 1e9
+        bgf = res["background_fraction"]
+        weighted = W * rows * (bgf * ATROUS_BYTES_BG_PX + (1.0 - bgf) * ATROUS_BYTES_PER_PX)
+        traffic = atrous_traffic(W, rows)
+        return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": ATROUS_KERNEL, "avg_launch_ms": round(atrous_ms, 4), "algorithmic_bytes_per_launch": alg,
+                "frac_pmc_traffic": round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+                "frac_background_weighted": round(weighted / t / 1e9 / HBM_PEAK_GBS, 4),
+                "background_fraction": round(bgf, 4)}
+
+    def pt_rates(res, fps):
+        """Rays and BVH node + triangle visits per frame (traversal counters), as rates at the measured frame rate
+        and over the path tracer's own (profiled, serial) time."""
+        st = res["stats"]
+        rays = st["primary_rays"] + st["bounce_rays"] + st["shadow_rays"]
+        visits = st["primary_visits"] + st["bounce_visits"] + st["shadow_visits"]
+        pt_ms = res["per_pass"].get("pathtrace")
+        return {"rays_per_frame": {k: int(st[k]) for k in ("primary_rays", "bounce_rays", "shadow_rays")},
+                "visits_per_frame": {k: int(st[k]) for k in ("primary_visits", "bounce_visits", "shadow_visits")},
+                "tie_rewalks": int(st["tie_rewalks"]), "primary_retries": int(st["primary_retries"]),
+                "traversals_per_pixel": round(rays / st["primary_rays"], 3) if st["primary_rays"] else None,
+                "visits_per_ray": round(visits / rays, 2) if rays else None,
+                "rays_per_s": round(rays * fps, 0), "visits_per_s": round(visits * fps, 0),
+                "pt_ms_profiled": round(pt_ms, 4) if pt_ms else None,
+                "rays_per_s_pt_only": round(rays / (pt_ms * 1e-3), 0) if pt_ms else None,
+                "visits_per_s_pt_only": round(visits / (pt_ms * 1e-3), 0) if pt_ms else None}
 
     W, H = args.width, args.height
-    dt, per_pass, rows = run(W, H)
-    ms = dt / args.steps * 1e3
-    fps = args.steps / dt  # whole frames per second (all ranks together render one frame)
+    K = args.frames_in_flight
+    res = run(W, H, K, args.view)
+    ms = res["dt"] / args.steps * 1e3
+    fps = args.steps / res["dt"]  # whole frames per second (all ranks together render one frame)
     extra = {}
+    if not args.no_extras and world == 1 and K > 1:
+        ser = run(W, H, 1, args.view, probes=False)
+        extra["fps_serial"] = round(args.steps / ser["dt"], 3)
+        extra["ms_per_step_serial"] = round(ser["dt"] / args.steps * 1e3, 3)
     if not args.no_1080p and (W, H) == (3840, 2160):
-        dt2, _, _ = run(1920, 1080)
-        extra = {"fps_1080p": round(args.steps / dt2, 3), "ms_per_step_1080p": round(dt2 / args.steps * 1e3, 3)}
-
-    atrous_ms = per_pass.get("atrous_avg_ms")
-    roof = None
-    if atrous_ms:
-        achieved = ATROUS_BYTES_PER_PX * W * rows / (atrous_ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": atrous_traffic(W, rows),
-                "kernel": ATROUS_KERNEL, "avg_launch_ms": round(atrous_ms, 4),
-                "algorithmic_bytes_per_launch": ATROUS_BYTES_PER_PX * W * rows}
+        r2 = run(1920, 1080, K, args.view)
+        fps2 = args.steps / r2["dt"]
+        extra.update({"fps_1080p": round(fps2, 3), "ms_per_step_1080p": round(r2["dt"] / args.steps * 1e3, 3),
+                      "roofline_1080p": atrous_roofline(r2, 1920, r2["rows"])})
+        if not args.no_extras and world == 1 and K > 1:
+            s2 = run(1920, 1080, 1, args.view, probes=False)
+            extra["fps_1080p_serial"] = round(args.steps / s2["dt"], 3)
+    if not args.no_extras and world == 1 and args.view == "default":
+        sv = run(W, H, K, "surface")
+        sfps = args.steps / sv["dt"]
+        extra["surface_view"] = {"camera": VIEWS["surface"], "fps": round(sfps, 3),
+                                 "ms_per_step": round(sv["dt"] / args.steps * 1e3, 3),
+                                 "surface_fraction": round(1.0 - sv["background_fraction"], 4),
+                                 "roofline": atrous_roofline(sv, W, sv["rows"]),
+                                 "path_tracer": pt_rates(sv, sfps),
+                                 "passes_ms": {k: round(v, 4) for k, v in sv["per_pass"].items()}}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(scene, W, H, args.cpu_sample)
+            log("cpu baseline (oracle, 16 threads and 1 core)")
+            cpu = cpu_baseline(scene, W, H, args.cpu_sample, args.cpu_sample_1core)
         except Exception as e:  # the baseline is reported, never the target
             cpu = {"value": None, "error": str(e)}
+        if not args.no_extras:
+            try:
+                log("configs[0]: cornell_teapot 512x512, SVGF off")
+                extra["config0"] = config0(gl)
+            except Exception as e:
+                extra["config0"] = {"error": str(e)}
 
     if rank == 0:
         line = {"metric": METRIC, "value": round(fps, 3),
@@ -220,12 +370,16 @@ def main():
                 "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
                 "dtype": "f32", "data": "synthetic",
                 "config": {"workload": f"{args.scene} {W}x{H} 1spp depth2 + 5-iter SVGF"
-                                       + (" moving camera" if args.moving else ""),
+                                       + (" moving camera" if args.moving else "")
+                                       + (f" {args.view} view" if args.view != "default" else ""),
                            "resolution": [W, H], "spp": 1, "max_tracing_depth": cfg.max_tracing_depth,
                            "atrous_iterations": cfg.num_atrous_iterations, "triangles": scene.ntris,
-                           "parallelism": f"bands{world}", "frames_in_flight": args.frames_in_flight},
-                "roofline": roof, "cpu_baseline": cpu, **extra,
-                "passes_ms": {k: round(v, 4) for k, v in per_pass.items()}}
+                           "parallelism": f"bands{world}", "frames_in_flight": K},
+                "roofline": atrous_roofline(res, W, res["rows"]), "cpu_baseline": cpu,
+                "path_tracer": pt_rates(res, fps), **extra,
+                "passes_ms": {k: round(v, 4) for k, v in res["per_pass"].items()}}
+        if "max_history_rows" in res:
+            line["max_history_rows"] = res["max_history_rows"]
         print(json.dumps(line), flush=True)
     gl.shutdown()
     if dist:

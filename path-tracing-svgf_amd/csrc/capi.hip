@@ -136,6 +136,7 @@ struct Pass {
   bool timed = false;
   uint32_t* row_cost = nullptr;  // pt_pass_set_row_cost (not owned)
   uint32_t* motion_max = nullptr;  // pt_pass_set_motion_bound (not owned)
+  unsigned long long* stats = nullptr;  // pt_pass_set_trace_stats (not owned)
 };
 
 struct SceneGPU {
@@ -890,6 +891,7 @@ int draw_pathtrace(Pass* p) {
     TRY(wf_alloc(p->wf, k.W, std::max(0, k.y1 - k.y0)));
     k.wf = p->wf.st;
     k.wf.row_cost = p->row_cost;
+    k.wf.stats = p->stats;
     // > 0: shadow rays past this many visits finish in the wave-cooperative walk (A/B switch; off: with frames
     // in flight it measured slower)
     k.wf.shadow_budget = (uint32_t)ui(p, "shadow_budget", 0);
@@ -1524,6 +1526,15 @@ int pt_pass_set_row_cost(uint32_t pass, void* device_counts) {
   Pass* p = pass_of(pass);
   if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
   p->row_cost = (uint32_t*)device_counts;
+  return PT_OK;
+}
+
+int pt_pass_set_trace_stats(uint32_t pass, void* device_u64) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  Pass* p = pass_of(pass);
+  if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
+  if (device_u64 && g.programs[p->program] != PK_PATHTRACE) return err(PT_ERR_ARG, "trace stats need a path-tracing pass");
+  p->stats = (unsigned long long*)device_u64;
   return PT_OK;
 }
 

@@ -130,6 +130,15 @@ __device__ __forceinline__ void block_push_shade(bool p_live, int lbin, bool p_h
   }
 }
 
+// traversal counters (PTParams::wf.stats, pt_pass_set_trace_stats): a wave sum, one 64-bit atomic per wave.
+// Call with every lane of the wave active.
+__device__ __forceinline__ void stat_add(const PTParams& p, int k, uint32_t v) {
+  if (!p.wf.stats) return;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(p.wf.stats + k, (unsigned long long)v);
+}
+
 // load-balancing probe: accumulate traversal steps per band row (only when requested)
 #ifndef PT_STEP_MAX
 __device__ __forceinline__ void add_row_cost(const PTParams& p, int local_row, int, uint32_t steps) {
@@ -165,6 +174,7 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
   const bool valid = x < p.W && y < p.y1;
   const int pid = (y - p.y0) * p.W + x;
   uint32_t steps = 0;
+  bool rewalk = false, retry = false;
 #ifdef PT_WAVE_TIMES
   const uint32_t t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -185,14 +195,21 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
       }
     }
     float t;
-    int tri = closest_hit<256>(p.scene, p.closest_tree, stk + threadIdx.x, S, d, p.prune, &t, &steps, bound);
+    int tri = closest_hit<256>(p.scene, p.closest_tree, stk + threadIdx.x, S, d, p.prune, &t, &steps, bound, &rewalk);
     if (tri < 0 && bound < PT_INF) {
       uint32_t more = 0;
-      tri = closest_hit<256>(p.scene, p.closest_tree, stk + threadIdx.x, S, d, p.prune, &t, &more);
+      bool rw2 = false;
+      tri = closest_hit<256>(p.scene, p.closest_tree, stk + threadIdx.x, S, d, p.prune, &t, &more, PT_INF, &rw2);
       steps += more;
+      retry = true;
+      rewalk = rewalk || rw2;
     }
     stnt(&p.wf.hit[pid], make_int2(tri, __float_as_int(t)));
   }
+  stat_add(p, kStatPrimRays, valid ? 1u : 0u);
+  stat_add(p, kStatPrimVisits, steps);
+  stat_add(p, kStatTieRewalks, rewalk ? 1u : 0u);
+  stat_add(p, kStatPrimRetries, retry ? 1u : 0u);
 #ifdef PT_WAVE_TIMES  // investigation build: per wave (start, end, max steps) in the row-cost buffer
   uint32_t ms = steps;
   for (int o = 32; o > 0; o >>= 1) ms = max(ms, (uint32_t)__shfl_xor((int)ms, o));
@@ -214,13 +231,21 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest(PTParams p
   __shared__ int stk[KS * kTB];
   const int k = blockIdx.x * kTB + threadIdx.x;
   int pid;
-  if (!bins_get(list, counts, kLiveBins, cap, k, &pid)) return;
-  float4 o = ldnt(&p.wf.ray_o[pid]), dd = ldnt(&p.wf.ray_d[pid]);
-  float t;
-  uint32_t steps;
-  int tri = closest_hit<kTB>(p.scene, p.closest_tree, stk + threadIdx.x, xyz(o), xyz(dd), p.prune, &t, &steps);
-  stnt(&p.wf.hit[pid], make_int2(tri, __float_as_int(t)));
-  add_row_cost(p, pid / p.W, pid, steps);
+  const bool valid = bins_get(list, counts, kLiveBins, cap, k, &pid);
+  if (!p.wf.stats && !valid) return;  // (with counters on, every lane stays for the wave sums)
+  uint32_t steps = 0;
+  bool rewalk = false;
+  if (valid) {
+    float4 o = ldnt(&p.wf.ray_o[pid]), dd = ldnt(&p.wf.ray_d[pid]);
+    float t;
+    int tri = closest_hit<kTB>(p.scene, p.closest_tree, stk + threadIdx.x, xyz(o), xyz(dd), p.prune, &t, &steps,
+                               PT_INF, &rewalk);
+    stnt(&p.wf.hit[pid], make_int2(tri, __float_as_int(t)));
+    add_row_cost(p, pid / p.W, pid, steps);
+  }
+  stat_add(p, kStatBounceRays, valid ? 1u : 0u);
+  stat_add(p, kStatBounceVisits, steps);
+  stat_add(p, kStatTieRewalks, rewalk ? 1u : 0u);
 }
 
 // Shadow rays from the compacted lists wf_shade queued: HDR rays, then point-light rays.
@@ -251,9 +276,9 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p,
     }
   }
   bool deferred = false;
+  uint32_t steps = 0;
   if (valid) {
     float4 o = ldnt(&p.wf.ray_o[pid]);
-    uint32_t steps = 0;
     const float4 dir = point ? ldnt(&p.wf.sh_p[pid]) : ldnt(&p.wf.sh_h[pid]);  // point: (direction, distance)
     int occ = WIDE ? anyhit4<kTB, KS>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps) : -1;
     if (occ < 0)  // binary walk (default), or the 4-wide stack overflowed
@@ -262,6 +287,8 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p,
     if (!deferred) (point ? p.wf.occ_p : p.wf.occ_h)[pid] = occ;
     add_row_cost(p, pid / p.W, pid, steps);
   }
+  stat_add(p, kStatShadowRays, valid && pid >= 0 ? 1u : 0u);
+  stat_add(p, kStatShadowVisits, steps);
   // rays past the step budget go to the cooperative walk (one wave-aggregated append per wave)
   const unsigned long long m = __ballot(deferred);
   if (m) {

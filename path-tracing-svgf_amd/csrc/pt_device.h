@@ -112,7 +112,12 @@ struct WFState {
   uint32_t* row_cost;           // optional: traversal steps per band row (load-balancing probe), may be null
   int* straggler;               // shadow rays past the step budget: pid | (point << 31), count at kCtrStrag
   uint32_t shadow_budget;       // node + triangle visits before a shadow ray is handed to the cooperative walk (0: never)
+  unsigned long long* stats;    // optional traversal counters (kStat*), wave-aggregated atomics; may be null
 };
+// Traversal counters of one path-tracing draw (pt_pass_set_trace_stats): rays traced and node + triangle visits
+// per traversal kind, tie re-walks on the reference tree, primary rays retried unbounded after the G-buffer bound.
+enum { kStatPrimRays, kStatPrimVisits, kStatBounceRays, kStatBounceVisits, kStatShadowRays, kStatShadowVisits,
+       kStatTieRewalks, kStatPrimRetries, kStatCount };
 
 struct PTParams {
   int W, H, y0, y1;     // frame size (global) and rows to compute

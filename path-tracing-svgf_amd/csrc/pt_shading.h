@@ -264,10 +264,11 @@ __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
 // that ray is walked again on the reference tree in the reference's order. Same bits either way.
 template <int STRIDE>
 __device__ __forceinline__ int closest_hit(const SceneDev& sc, bool sah, int* __restrict__ stk, v3 S, v3 d, int prune,
-                                           float* t, uint32_t* steps, float t_init = PT_INF) {
+                                           float* t, uint32_t* steps, float t_init = PT_INF, bool* rewalk = nullptr) {
   if (!sah) return traverse<0, STRIDE>(sc, stk, S, d, 0.0f, prune, t, steps, t_init);
   bool tie = false;
   int tri = traverse<0, STRIDE>(anyhit_scene(sc), stk, S, d, 0.0f, 1, t, steps, t_init, &tie);
+  if (rewalk) *rewalk = tie;
   if (tie) {
     uint32_t more = 0;
     tri = traverse<0, STRIDE>(sc, stk, S, d, 0.0f, 1, t, &more, t_init);

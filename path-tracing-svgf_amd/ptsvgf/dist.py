@@ -304,6 +304,9 @@ class BandRenderer:
     def time_atrous(self, reps: int = 20) -> float:
         return self.r.time_atrous(reps)
 
+    def trace_stats(self) -> dict:
+        return self.r.trace_stats()
+
     def rows_rendered(self) -> int:
         return self.plan.y1 - self.plan.y0
 

@@ -548,6 +548,26 @@ class Renderer:
         e1.synchronize()
         return e0.elapsed_time(e1) / (reps * len(iters))
 
+    STAT_KEYS = ("primary_rays", "primary_visits", "bounce_rays", "bounce_visits", "shadow_rays", "shadow_visits",
+                 "tie_rewalks", "primary_retries")  # pt_pass_set_trace_stats order
+
+    def trace_stats(self) -> dict:
+        """Render one frame with the path tracer's traversal counters on (pt_pass_set_trace_stats): rays traced and
+        node + triangle visits per traversal kind. Synchronises; diagnostics, not for timed frames."""
+        import torch
+
+        buf = torch.zeros(len(self.STAT_KEYS), dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        for p, _ in self.pt_slots:
+            p.set_trace_stats(buf.data_ptr())
+        try:
+            self.frame()
+            torch.cuda.synchronize()
+        finally:
+            for p, _ in self.pt_slots:
+                p.set_trace_stats(0)
+        return dict(zip(self.STAT_KEYS, (int(v) for v in buf.cpu().tolist())))
+
     def _stream_to(self, stream) -> None:
         """Issue the following draws on this torch stream."""
         _set_stream(stream)

@@ -29,7 +29,7 @@ def main(src: str, dst: str, pixels: int) -> None:
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
     acc = defaultdict(lambda: defaultdict(list))
-    for sub in ("fetch", "write", "sq"):
+    for sub in ("fetch", "write", "sq", "l2", "sq2"):
         path = os.path.join(src, sub, "run_counter_collection.csv")
         if not os.path.exists(path):
             continue
