@@ -78,7 +78,7 @@ int pts_scene_encode(const pts_scene* s, float* tri_out, float* node_out, float*
 void pts_transform_matrix(const float* rot3_deg, const float* trans3, const float* scale3, float* out16);
 
 /* calculateHdrCache(HDR, width, height): hdr RGB32F rows (w*h*3) -> cache RGB32F (w*h*3):
- * R = sample x, G = sample y, B = pdf (hdr_compute.h:277-283). */
+ * R = sample x, G = sample y, B = pdf (hdr_compute.h:88-99). */
 int pts_hdr_cache(const float* hdr_rgb, int width, int height, float* cache_out);
 
 /* HDRLoader::load (lib/hdrloader.cpp:28-97): Radiance RGBE file -> RGB32F rows, file scanline order (the

@@ -25,7 +25,7 @@ inline float uv_of(int x, int W) {  // vert.vert: pix = NDC; uv = pix*0.5+0.5
   return pix * 0.5f + 0.5f;
 }
 
-// svgf_reproject.frag:158-160 / svgf_variance.frag:223-225 / svgf_Atrous.frag:57-59
+// svgf_reproject.frag:158-160 / svgf_variance.frag:18-20 / svgf_Atrous.frag:57-59
 inline float luminance(float r, float g, float b) { return (0.2125f * r + 0.7154f * g) + 0.0721f * b; }
 
 // svgf_reproject.frag:31-43
@@ -37,7 +37,7 @@ bool isReprjValid(float cx, float cy, float Z, float Zprev, float fwidthZ, v3 no
   return true;
 }
 
-// svgf_variance.frag:228-240 == svgf_Atrous.frag:43-55
+// svgf_variance.frag:23-35 == svgf_Atrous.frag:43-55
 float computeWeight(float depthCenter, float depthP, float phiDepth, v3 normalCenter, v3 normalP, float phiNormal,
                     float lC, float lP, float phiIllum) {
   float weightNormal = g_pow(f_clamp(dot(normalCenter, normalP), 0.0f, 1.0f), phiNormal);
@@ -186,7 +186,7 @@ extern "C" int orc_variance(int W, int H, const float* illum_p, const float* mom
       float* o = out + ((size_t)y * W + x) * 4;
       float h = gM.at(x, y)[2];
       const float* ic = gI.at(x, y);
-      if (h < 4.0f) {  // svgf_variance.frag:249-316
+      if (h < 4.0f) {  // svgf_variance.frag:44-111
         float sumW = 0.0f;
         float sI[3] = {0, 0, 0}, sM[2] = {0, 0};
         float lC = luminance(ic[0], ic[1], ic[2]);
@@ -294,7 +294,7 @@ extern "C" int orc_modulate(int W, int H, const float* albedo_p, const float* em
       size_t i = ((size_t)y * W + x) * 4;
       float depth = nd_p[i + 3];
       float* o = out + i;
-      if (depth == 1.0f) {  // svgf_modulate.frag:150-154
+      if (depth == 1.0f) {  // svgf_modulate.frag:24-28
         o[0] = illum_p[i]; o[1] = illum_p[i + 1]; o[2] = illum_p[i + 2];
       } else {
         for (int q = 0; q < 3; ++q) o[q] = illum_p[i + q] * albedo_p[i + q] + emission_p[i + q];

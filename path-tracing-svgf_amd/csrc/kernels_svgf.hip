@@ -4,9 +4,9 @@
 //
 // Reference shaders (behaviour restated, GLSL file:line):
 //   reproject  shaders/svgf_reproject.frag:26-204
-//   variance   shaders/svgf_variance.frag:223-322
+//   variance   shaders/svgf_variance.frag:18-117
 //   a-trous    shaders/svgf_Atrous.frag:20-126
-//   modulate   shaders/svgf_modulate.frag:144-156
+//   modulate   shaders/svgf_modulate.frag:18-29
 //   output     shaders/output_pass.frag:12-24
 //
 // Exactness: built with -ffp-contract=off and the GLSL built-ins of
@@ -57,7 +57,7 @@ __device__ __forceinline__ bool reprj_valid(float cx, float cy, float Z, float Z
   return true;
 }
 
-// computeWeight (svgf_variance.frag:228-240, svgf_Atrous.frag:43-55)
+// computeWeight (svgf_variance.frag:23-35, svgf_Atrous.frag:43-55)
 __device__ __forceinline__ float edge_weight(float zc, float zp, float phiDepth, v3 nc, v3 np, float phiNormal,
                                              float lc, float lp, float phiIllum) {
   float wN = g_pow(f_clamp(dot(nc, np), 0.0f, 1.0f), phiNormal);

@@ -506,7 +506,7 @@ int pts_hdr_cache(const float* HDR, int width, int height, float* cache) {
   if (!HDR || !cache || width <= 0 || height <= 0) return fail("pts_hdr_cache: bad argument");
   const size_t W = width, H = height;
   float lumSum = 0.0f;
-  std::vector<float> pdf(W * H);  // pdf[i][j] at i*W+j (hdr_compute.h:194-205)
+  std::vector<float> pdf(W * H);  // pdf[i][j] at i*W+j (hdr_compute.h:7-21)
   for (size_t i = 0; i < H; ++i)
     for (size_t j = 0; j < W; ++j) {
       float R = HDR[3 * (i * W + j)], G = HDR[3 * (i * W + j) + 1], B = HDR[3 * (i * W + j) + 2];
@@ -520,7 +520,7 @@ int pts_hdr_cache(const float* HDR, int width, int height, float* cache) {
     for (size_t i = 0; i < H; ++i) pdf_x_margin[j] += pdf[i * W + j];
   std::vector<float> cdf_x_margin = pdf_x_margin;
   for (size_t i = 1; i < W; ++i) cdf_x_margin[i] += cdf_x_margin[i - 1];
-  // conditional cdf, stored column-major: cdf_y[j][i] at j*H+i (hdr_compute.h:225-243)
+  // conditional cdf, stored column-major: cdf_y[j][i] at j*H+i (hdr_compute.h:40-59)
   std::vector<float> cdf_y(W * H);
   for (size_t j = 0; j < W; ++j) {
     for (size_t i = 0; i < H; ++i) cdf_y[j * H + i] = pdf[i * W + j] / pdf_x_margin[j];
@@ -708,7 +708,7 @@ int pts_gen_cornell(int* nv, int* nt, float* positions, int* indices) {
 // ------------------------------------------------------------- RGBE ---
 namespace {
 typedef unsigned char Rgbe[4];
-// decrunch / oldDecrunch (hdrloader.cpp:123-197) over a byte cursor; false = truncated or malformed
+// decrunch / oldDecrunch (hdrloader.cpp:118-192) over a byte cursor; false = truncated or malformed
 struct Bytes {
   const std::vector<unsigned char>& b;
   size_t i;

@@ -113,7 +113,7 @@ def test_hdr_cache_properties():
 
 
 def test_hdr_cache_single_bright_texel():
-    """A one-hot environment makes every cache entry sample that texel (hdr_compute.h:255-270)."""
+    """A one-hot environment makes every cache entry sample that texel (hdr_compute.h:71-86)."""
     hdr = np.full((16, 32, 3), 1e-6, np.float32)
     hdr[5, 9] = 1000.0
     cache = hdr_cache(hdr)
