@@ -708,7 +708,7 @@ int pts_gen_cornell(int* nv, int* nt, float* positions, int* indices) {
 // ------------------------------------------------------------- RGBE ---
 namespace {
 typedef unsigned char Rgbe[4];
-// decrunch / oldDecrunch (hdrloader.cpp:118-192) over a byte cursor; false = truncated or malformed
+// decrunch / oldDecrunch (hdrloader.cpp:118-191) over a byte cursor; false = truncated or malformed
 struct Bytes {
   const std::vector<unsigned char>& b;
   size_t i;
