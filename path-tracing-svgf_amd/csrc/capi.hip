@@ -80,7 +80,29 @@ struct WFBuffers {
   void* base = nullptr;  // one allocation carved into the WFState arrays
   size_t n = 0;          // pixels covered
   WFState st{};
+  int* spill = nullptr;  // deep reference trees: stack entries past the LDS stack (WFState::spill)
+  int spill_levels = 0;
 };
+
+// Spill columns for a reference tree needing `need` stack entries (> the LDS stack): (need - kStack + 1) entries per
+// pixel of the band, allocated on first use and kept while the depth fits.
+int wf_spill(WFBuffers& b, int need) {
+  const int levels = need - kStack + 1;
+  if (levels <= 0) {
+    b.st.spill = nullptr;
+    b.st.spill_stride = 0;
+    return PT_OK;
+  }
+  if (!b.spill || b.spill_levels < levels) {
+    if (b.spill) (void)hipFree(b.spill);
+    b.spill = nullptr;
+    if (hipMalloc((void**)&b.spill, (size_t)levels * b.n * sizeof(int)) != hipSuccess) return PT_ERR_HIP;
+    b.spill_levels = levels;
+  }
+  b.st.spill = b.spill;
+  b.st.spill_stride = b.n;
+  return PT_OK;
+}
 
 int wf_alloc(WFBuffers& b, int W, int rows) {
   const size_t n = (size_t)W * (size_t)rows;
@@ -211,6 +233,8 @@ struct NodeRaw {
   float AA[3], BB[3];
 };
 
+constexpr int kRefStack = 256;  // path_tracing.frag:378
+
 // *need: deepest interior level (root = 1) = the most stack entries a walk holds
 int pack_bvh(const float* node_enc, int nnodes, std::vector<float4>& out, int* root_ref, int ntris, int* need) {
   if (nnodes < 2) return err(PT_ERR_FORMAT, "BVH needs the dummy node 0 and a root node 1");
@@ -247,7 +271,8 @@ int pack_bvh(const float* node_enc, int nnodes, std::vector<float4>& out, int* r
   while (!st.empty()) {
     Item it = st.back();
     st.pop_back();
-    if (it.depth >= kStack) return err(PT_ERR_FORMAT, "BVH deeper than the traversal stack");
+    // the reference walks with int stack[256] (path_tracing.frag:378); deeper trees are undefined there
+    if (it.depth >= kRefStack) return err(PT_ERR_FORMAT, "BVH deeper than the reference's stack[256]");
     *need = std::max(*need, it.depth);
     idx[it.id] = (int)order.size();
     order.push_back(it.id);
@@ -425,7 +450,16 @@ static bool sah_use_sweep() {
 
 // 16-bin SAH over primitive centroids (cost: 1 per node visit, `weight` per primitive test), or the exact sweep.
 // max_leaf: the most primitives a leaf may hold (leaves also stop at 15 triangles, the leaf ref's limit).
-static int sah_build(std::vector<SahPrim>& pr, int l, int r, int max_leaf, std::vector<SahNode>& nodes) {
+static int ceil_log2(int n) {
+  int k = 0;
+  while ((1 << k) < n) ++k;
+  return k;
+}
+
+// depth: this node's level (root = 1). Once the SAH splits could take the tree past the LDS stack, the rest of the
+// range is halved by index (sorted along the widest centroid axis), so every tree fits the stack: interior levels
+// stay below kStack - 1 whatever the geometry (coincident centroids make SAH peel one primitive per level).
+static int sah_build(std::vector<SahPrim>& pr, int l, int r, int max_leaf, std::vector<SahNode>& nodes, int depth = 1) {
   const int id = (int)nodes.size();
   nodes.emplace_back();
   SahNode nd;
@@ -497,7 +531,16 @@ static int sah_build(std::vector<SahPrim>& pr, int l, int r, int max_leaf, std::
     return id;
   }
   int m;
-  if (sweep && msweep > l) {
+  if (depth + ceil_log2(n) >= kStack - 2) {  // depth cap: balanced halves from here on
+    int ax = 0;
+    for (int a = 1; a < 3; ++a)
+      if (chi[a] - clo[a] > chi[ax] - clo[ax]) ax = a;
+    std::sort(pr.begin() + l, pr.begin() + r, [ax](const SahPrim& x, const SahPrim& y) {
+      const float cx = x.lo[ax] + x.hi[ax], cy = y.lo[ax] + y.hi[ax];
+      return cx < cy || (cx == cy && x.ref < y.ref);
+    });
+    m = l + n / 2;
+  } else if (sweep && msweep > l) {
     m = msweep;
   } else if (!sweep && bax >= 0) {
     const float ext = chi[bax] - clo[bax];
@@ -508,8 +551,8 @@ static int sah_build(std::vector<SahPrim>& pr, int l, int r, int max_leaf, std::
   } else {
     m = l + n / 2;  // coincident centroids: halve the range
   }
-  nd.left = sah_build(pr, l, m, max_leaf, nodes);
-  nd.right = sah_build(pr, m, r, max_leaf, nodes);
+  nd.left = sah_build(pr, l, m, max_leaf, nodes, depth + 1);
+  nd.right = sah_build(pr, m, r, max_leaf, nodes, depth + 1);
   nodes[id] = nd;
   return id;
 }
@@ -580,6 +623,14 @@ int build_anyhit_tree(const float* node_enc, int nnodes, int ntris, std::vector<
   return pack_sah(nodes, [&](int first, int) { return pr[first].ref; }, out, root_ref, need);
 }
 
+void free_scene(SceneGPU& sg) {
+  float4** bufs[5] = {&sg.geom, &sg.shade, &sg.bvh, &sg.bvh4, &sg.bvh_any};
+  for (auto b : bufs) {
+    if (*b) (void)hipFree(*b);
+    *b = nullptr;
+  }
+}
+
 template <class T>
 int upload_vec(const std::vector<T>& v, T** dst) {
   if (*dst) { (void)hipFree(*dst); *dst = nullptr; }
@@ -628,13 +679,16 @@ int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU*
   if (sg.has4 && (rc = upload_vec(bvh4.empty() ? std::vector<float4>{float4{0, 0, 0, 0}} : bvh4, &sg.bvh4)) != PT_OK)
     return rc;
   sg.root4 = root4;
-  {
+  {  // optional, like the 4-wide tree: without it shadow and closest-hit rays walk the reference tree
     std::vector<float4> any;
-    if ((rc = build_anyhit_tree((const float*)nodes->host.data(), (int)nnodes, (int)ntris, any, &sg.root_any,
-                                &sg.need_any)) != PT_OK)
-      return rc;
-    if (any.empty()) any.push_back(float4{0, 0, 0, 0});
-    if ((rc = upload_vec(any, &sg.bvh_any)) != PT_OK) return rc;
+    if (build_anyhit_tree((const float*)nodes->host.data(), (int)nnodes, (int)ntris, any, &sg.root_any,
+                          &sg.need_any) == PT_OK) {
+      if (any.empty()) any.push_back(float4{0, 0, 0, 0});
+      if ((rc = upload_vec(any, &sg.bvh_any)) != PT_OK) return rc;
+    } else if (sg.bvh_any) {
+      (void)hipFree(sg.bvh_any);
+      sg.bvh_any = nullptr;
+    }
   }
   if ((rc = upload_vec(geom, &sg.geom)) != PT_OK) return rc;
   if ((rc = upload_vec(shade, &sg.shade)) != PT_OK) return rc;
@@ -886,9 +940,13 @@ int draw_pathtrace(Pass* p) {
   int rc;
   if (ui(p, "pt_kernel", 0) == 1) {  // 1: single megakernel (kernels_pt.hip), kept for A/B
     if (k.tile_stride != 1) return err(PT_ERR_ARG, "tile subsets need the wavefront path tracer");
+    if (k.stack_need >= kStack)
+      return err(PT_ERR_ARG, "the megakernel (pt_kernel=1) walks a 32-entry LDS stack; this BVH is deeper: use the "
+                             "wavefront path tracer (pt_kernel=0, the default)");
     rc = launch_pathtrace(k, g.stream);
   } else {                            // 0: wavefront (kernels_wavefront.hip), production
     TRY(wf_alloc(p->wf, k.W, std::max(0, k.y1 - k.y0)));
+    if (wf_spill(p->wf, k.stack_need) != PT_OK) return err(PT_ERR_HIP, "spill stack allocation failed");
     k.wf = p->wf.st;
     k.wf.row_cost = p->row_cost;
     k.wf.stats = p->stats;
@@ -1099,6 +1157,7 @@ int pt_shutdown(void) {
     if (p->raster.nrm) (void)hipFree(p->raster.nrm);
     if (p->raster.bvh) (void)hipFree(p->raster.bvh);
     if (p->wf.base) (void)hipFree(p->wf.base);
+    if (p->wf.spill) (void)hipFree(p->wf.spill);
     if (p->order.cost) (void)hipFree(p->order.cost);
     if (p->order.perm) (void)hipFree(p->order.perm);
     if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
@@ -1107,13 +1166,7 @@ int pt_shutdown(void) {
     if (p->ev0) (void)hipEventDestroy(p->ev0);
     if (p->ev1) (void)hipEventDestroy(p->ev1);
   }
-  for (auto& kv : g.scenes) {
-    if (kv.second.geom) (void)hipFree(kv.second.geom);
-    if (kv.second.shade) (void)hipFree(kv.second.shade);
-    if (kv.second.bvh) (void)hipFree(kv.second.bvh);
-    if (kv.second.bvh4) (void)hipFree(kv.second.bvh4);
-    if (kv.second.bvh_any) (void)hipFree(kv.second.bvh_any);
-  }
+  for (auto& kv : g.scenes) free_scene(kv.second);
   if (g.own) (void)hipStreamDestroy(g.own);
   g = Lib();
   return PT_OK;
@@ -1354,6 +1407,15 @@ int pt_texture_destroy(uint32_t tex) {
   if (it->second->owned && it->second->dev) (void)hipFree(it->second->dev);
   if (it->second->aux) (void)hipFree(it->second->aux);
   g.textures.erase(it);
+  // the device scenes decoded from this buffer (keyed by (triangles, nodes) handles) go with it
+  for (auto sc = g.scenes.begin(); sc != g.scenes.end();) {
+    if (sc->first.first == tex || sc->first.second == tex) {
+      free_scene(sc->second);
+      sc = g.scenes.erase(sc);
+    } else {
+      ++sc;
+    }
+  }
   return PT_OK;
 }
 
@@ -1589,6 +1651,7 @@ int pt_pass_destroy(uint32_t pass) {
   if (p->raster.nrm) (void)hipFree(p->raster.nrm);
   if (p->raster.bvh) (void)hipFree(p->raster.bvh);
   if (p->wf.base) (void)hipFree(p->wf.base);
+  if (p->wf.spill) (void)hipFree(p->wf.spill);
   if (p->order.cost) (void)hipFree(p->order.cost);
   if (p->order.perm) (void)hipFree(p->order.perm);
   if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);

@@ -31,7 +31,7 @@ namespace ptk {
 // ------------------------------------------------------------ path tracer ---
 __global__ void __launch_bounds__(kBlock) pathtrace_kernel(PTParams p) {
   __shared__ int stk[kStack * kBlock];
-  int* s = stk + threadIdx.x;
+  LdsStack<kBlock> s{stk + threadIdx.x};
   // 16x16 pixel tile per block; each wave owns an 8x8 sub-tile (ray coherence).
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   const int x = blockIdx.x * 16 + (wv & 1) * 8 + (ln & 7);
@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(kBlock) pathtrace_kernel(PTParams p) {
 
   for (int i = 0; i < p.max_depth; ++i) {
     float t;
-    int tri = traverse<0, kBlock>(p.scene, s, S, d, 0.0f, p.prune, &t);
+    int tri = traverse<0>(p.scene, s, S, d, 0.0f, p.prune, &t);
     if (tri < 0) {
       light = add(light, mul(hdr_color(p, d), red));
       break;
@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(kBlock) pathtrace_kernel(PTParams p) {
     v3 hcalc = splat(0.0f);
     {
       float ts;
-      if (traverse<1, kBlock>(p.scene, s, h.P, hd, 0.0f, 0, &ts) < 0) {
+      if (traverse<1>(p.scene, s, h.P, hd, 0.0f, 0, &ts) < 0) {
         v3 hv = hdr_color(p, hd);
         v3 hb = brdf_eval(V, h.normal, hd, h.m);
         hpdf = hdr_pdf(p, hd);
@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(kBlock) pathtrace_kernel(PTParams p) {
       v3 ld = normalize(sub(lpos, h.P));
       float dist = length(sub(lpos, h.P));
       float ts;
-      if (traverse<2, kBlock>(p.scene, s, h.P, ld, dist, 0, &ts) < 0) {
+      if (traverse<2>(p.scene, s, h.P, ld, dist, 0, &ts) < 0) {
         v3 plv = divs(lrad, dist * dist);
         v3 pb = brdf_eval(V, h.normal, ld, h.m);
         pcalc = divs(muls(mul(plv, pb), f_abs(dot(ld, h.normal))), ppdf);

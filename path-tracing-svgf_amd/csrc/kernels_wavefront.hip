@@ -150,6 +150,15 @@ __device__ __forceinline__ void add_row_cost(const PTParams& p, int, int pid, ui
 }
 #endif
 
+// This lane's traversal stack: its LDS column, and with DEEP (a reference tree deeper than the LDS stack, launched
+// only for such trees) the pixel's spill column for the entries beyond it.
+template <int STRIDE, int KS, bool DEEP>
+__device__ __forceinline__ auto ray_stack(int* lds_column, const PTParams& p, int pid) {
+  if constexpr (DEEP) return SpillStack<STRIDE, KS>{lds_column, p.wf.spill + pid, p.wf.spill_stride};
+  else return LdsStack<STRIDE>{lds_column};
+}
+
+
 __device__ __forceinline__ v3 primary_dir(const PTParams& p, int x, int y) {
   float pixx = (float)(2 * x + 1) / (float)p.W - 1.0f;
   float pixy = (float)(2 * y + 1) / (float)p.H - 1.0f;
@@ -162,7 +171,7 @@ __device__ __forceinline__ v3 primary_dir(const PTParams& p, int x, int y) {
 
 // ------------------------------------------------------------ primaries ---
 // 16x16 screen tiles, each wave an 8x8 sub-tile: coherent camera rays.
-template <int KS>
+template <int KS, bool DEEP>
 __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
   __shared__ int stk[KS * 256];
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
@@ -174,7 +183,7 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
   const bool valid = x < p.W && y < p.y1;
   const int pid = (y - p.y0) * p.W + x;
   uint32_t steps = 0;
-  bool rewalk = false, retry = false;
+  bool rewalk = false, retry = false, spill = false;
 #ifdef PT_WAVE_TIMES
   const uint32_t t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -195,21 +204,24 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
       }
     }
     float t;
-    int tri = closest_hit<256>(p.scene, p.closest_tree, stk + threadIdx.x, S, d, p.prune, &t, &steps, bound, &rewalk);
+    auto st = ray_stack<256, KS, DEEP>(stk + threadIdx.x, p, pid);
+    int tri = closest_hit(p.scene, p.closest_tree, st, S, d, p.prune, &t, &steps, bound, &rewalk);
     if (tri < 0 && bound < PT_INF) {
       uint32_t more = 0;
       bool rw2 = false;
-      tri = closest_hit<256>(p.scene, p.closest_tree, stk + threadIdx.x, S, d, p.prune, &t, &more, PT_INF, &rw2);
+      tri = closest_hit(p.scene, p.closest_tree, st, S, d, p.prune, &t, &more, PT_INF, &rw2);
       steps += more;
       retry = true;
       rewalk = rewalk || rw2;
     }
     stnt(&p.wf.hit[pid], make_int2(tri, __float_as_int(t)));
+    spill = st.spilled;
   }
   stat_add(p, kStatPrimRays, valid ? 1u : 0u);
   stat_add(p, kStatPrimVisits, steps);
   stat_add(p, kStatTieRewalks, rewalk ? 1u : 0u);
   stat_add(p, kStatPrimRetries, retry ? 1u : 0u);
+  stat_add(p, kStatSpills, spill ? 1u : 0u);
 #ifdef PT_WAVE_TIMES  // investigation build: per wave (start, end, max steps) in the row-cost buffer
   uint32_t ms = steps;
   for (int o = 32; o > 0; o >>= 1) ms = max(ms, (uint32_t)__shfl_xor((int)ms, o));
@@ -225,7 +237,7 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
 }
 
 // ----------------------------------------------------------- bounce trace ---
-template <int KS>
+template <int KS, bool DEEP>
 __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest(PTParams p, const int* __restrict__ list,
                                                                        const int* __restrict__ counts, int cap) {
   __shared__ int stk[KS * kTB];
@@ -234,22 +246,24 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest(PTParams p
   const bool valid = bins_get(list, counts, kLiveBins, cap, k, &pid);
   if (!p.wf.stats && !valid) return;  // (with counters on, every lane stays for the wave sums)
   uint32_t steps = 0;
-  bool rewalk = false;
+  bool rewalk = false, spill = false;
   if (valid) {
     float4 o = ldnt(&p.wf.ray_o[pid]), dd = ldnt(&p.wf.ray_d[pid]);
     float t;
-    int tri = closest_hit<kTB>(p.scene, p.closest_tree, stk + threadIdx.x, xyz(o), xyz(dd), p.prune, &t, &steps,
-                               PT_INF, &rewalk);
+    auto st = ray_stack<kTB, KS, DEEP>(stk + threadIdx.x, p, pid);
+    int tri = closest_hit(p.scene, p.closest_tree, st, xyz(o), xyz(dd), p.prune, &t, &steps, PT_INF, &rewalk);
     stnt(&p.wf.hit[pid], make_int2(tri, __float_as_int(t)));
     add_row_cost(p, pid / p.W, pid, steps);
+    spill = st.spilled;
   }
+  stat_add(p, kStatSpills, spill ? 1u : 0u);
   stat_add(p, kStatBounceRays, valid ? 1u : 0u);
   stat_add(p, kStatBounceVisits, steps);
   stat_add(p, kStatTieRewalks, rewalk ? 1u : 0u);
 }
 
 // Shadow rays from the compacted lists wf_shade queued: HDR rays, then point-light rays.
-template <int KS, bool WIDE>
+template <int KS, bool WIDE, bool DEEP>
 __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p, const int* __restrict__ list,
                                                                       const int* __restrict__ counts, int cap,
                                                                       int* __restrict__ strag_count) {
@@ -275,19 +289,22 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p,
       r -= nb;
     }
   }
-  bool deferred = false;
+  bool deferred = false, spill = false;
   uint32_t steps = 0;
   if (valid) {
     float4 o = ldnt(&p.wf.ray_o[pid]);
     const float4 dir = point ? ldnt(&p.wf.sh_p[pid]) : ldnt(&p.wf.sh_h[pid]);  // point: (direction, distance)
     int occ = WIDE ? anyhit4<kTB, KS>(p.scene, stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps) : -1;
-    if (occ < 0)  // binary walk (default), or the 4-wide stack overflowed
-      occ = anyhit2<kTB>(anyhit_scene(p.scene), stk + threadIdx.x, xyz(o), xyz(dir), point, dir.w, &steps,
-                         p.wf.shadow_budget, &deferred);
+    if (occ < 0) {  // binary walk (default), or the 4-wide stack overflowed
+      auto st = ray_stack<kTB, KS, DEEP>(stk + threadIdx.x, p, pid);
+      occ = anyhit2(anyhit_scene(p.scene), st, xyz(o), xyz(dir), point, dir.w, &steps, p.wf.shadow_budget, &deferred);
+      spill = st.spilled;
+    }
     if (!deferred) (point ? p.wf.occ_p : p.wf.occ_h)[pid] = occ;
     add_row_cost(p, pid / p.W, pid, steps);
   }
   stat_add(p, kStatShadowRays, valid && pid >= 0 ? 1u : 0u);
+  stat_add(p, kStatSpills, spill ? 1u : 0u);
   stat_add(p, kStatShadowVisits, steps);
   // rays past the step budget go to the cooperative walk (one wave-aggregated append per wave)
   const unsigned long long m = __ballot(deferred);
@@ -531,7 +548,7 @@ int wf_subset_tiles(int W, int rows, int stride, int offset) {
 // rays and live list shade(i) wrote) runs concurrently with the shadow trace and finish of bounce i; the join
 // comes before shade(i+1), which needs both. Two traversal launches then end together, so the frame's
 // dependency chain carries one tail fewer per bounce. Without `aux` the launches are serial.
-template <int KS>
+template <int KS, bool DEEP>
 int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent_t ev_fork, hipEvent_t ev_join) {
   const int rows = p.y1 - p.y0;
   if (rows <= 0) return 0;
@@ -541,7 +558,7 @@ int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent
   if (e != hipSuccess) return (int)e;
   const int ntiles = wf_subset_tiles(p.W, rows, p.tile_stride, p.tile_offset);
   if (ntiles <= 0) return 0;
-  hipLaunchKernelGGL(wf_primary<KS>, dim3(ntiles), dim3(256), 0, s, p);
+  hipLaunchKernelGGL((wf_primary<KS, DEEP>), dim3(ntiles), dim3(256), 0, s, p);
   if (p.tiles.cost) {  // this frame's primary costs -> tile order of the bounce-0 shade and the next frame
     const int rc = launch_tile_sort(p.tiles.cost, p.tiles.perm_next, p.tiles.ntiles, s);
     if (rc) return rc;
@@ -553,7 +570,7 @@ int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent
   auto closest = [&](int i, hipStream_t st) {
     const int* lin = lists[(i + 1) & 1];
     const int* live_in = p.wf.counters + kWfCtr * (i - 1);
-    hipLaunchKernelGGL(wf_trace_closest<KS>, dim3(gT), dim3(kTB), 0, st, p, lin, live_in, cap);
+    hipLaunchKernelGGL((wf_trace_closest<KS, DEEP>), dim3(gT), dim3(kTB), 0, st, p, lin, live_in, cap);
   };
   for (int i = 0; i < p.max_depth; ++i) {
     const int* lin = lists[(i + 1) & 1];
@@ -578,10 +595,10 @@ int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent
     }
     int* strag = p.wf.counters + kWfCtr * i + kCtrStrag;  // shadow rays handed to the cooperative walk
     if (p.scene.bvh4)
-      hipLaunchKernelGGL((wf_trace_shadow<KS, true>), dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
+      hipLaunchKernelGGL((wf_trace_shadow<KS, true, DEEP>), dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
                          (const int*)shadow, cap, strag);
     else
-      hipLaunchKernelGGL((wf_trace_shadow<KS, false>), dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
+      hipLaunchKernelGGL((wf_trace_shadow<KS, false, DEEP>), dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
                          (const int*)shadow, cap, strag);
     if (p.wf.shadow_budget)
       hipLaunchKernelGGL(wf_shadow_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, s, p, (const int*)strag);
@@ -594,8 +611,9 @@ int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent
 int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent_t ev_fork,
                                hipEvent_t ev_join) {
   // the LDS stack bounds resident waves: a tree that fits the small stack gets more of them
-  return p.stack_need <= kStackSmall ? launch_wavefront<kStackSmall>(p, s, aux, ev_fork, ev_join)
-                                     : launch_wavefront<kStack>(p, s, aux, ev_fork, ev_join);
+  if (p.wf.spill) return launch_wavefront<kStack, true>(p, s, nullptr, nullptr, nullptr);  // deep tree, no fork
+  return p.stack_need <= kStackSmall ? launch_wavefront<kStackSmall, false>(p, s, aux, ev_fork, ev_join)
+                                     : launch_wavefront<kStack, false>(p, s, aux, ev_fork, ev_join);
 }
 
 }  // namespace ptk

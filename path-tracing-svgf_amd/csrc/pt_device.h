@@ -113,11 +113,14 @@ struct WFState {
   int* straggler;               // shadow rays past the step budget: pid | (point << 31), count at kCtrStrag
   uint32_t shadow_budget;       // node + triangle visits before a shadow ray is handed to the cooperative walk (0: never)
   unsigned long long* stats;    // optional traversal counters (kStat*), wave-aggregated atomics; may be null
+  int* spill;                   // deep trees only: stack entries past the LDS stack, entry kStack + j of pixel pid at
+  size_t spill_stride;          // spill[j * spill_stride + pid] (spill_stride = band pixels); null otherwise
 };
 // Traversal counters of one path-tracing draw (pt_pass_set_trace_stats): rays traced and node + triangle visits
-// per traversal kind, tie re-walks on the reference tree, primary rays retried unbounded after the G-buffer bound.
+// per traversal kind, tie re-walks on the reference tree, primary rays retried unbounded after the G-buffer bound, rays
+// whose stack went past the LDS stack into the spill columns (deep reference trees).
 enum { kStatPrimRays, kStatPrimVisits, kStatBounceRays, kStatBounceVisits, kStatShadowRays, kStatShadowVisits,
-       kStatTieRewalks, kStatPrimRetries, kStatCount };
+       kStatTieRewalks, kStatPrimRetries, kStatSpills, kStatCount };
 
 struct PTParams {
   int W, H, y0, y1;     // frame size (global) and rows to compute

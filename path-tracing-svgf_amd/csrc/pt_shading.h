@@ -160,6 +160,34 @@ __device__ __forceinline__ bool leaf_scan(const float4* __restrict__ g, int firs
 __device__ __forceinline__ int ref_leaf_first(int ref) { return (-(ref + 1)) >> 4; }
 __device__ __forceinline__ int ref_leaf_count(int ref) { return (-(ref + 1)) & 15; }
 
+// Traversal stacks. LdsStack: a column of the block's LDS array (slots STRIDE ints apart); the host guarantees the
+// walked tree fits it. SpillStack: the first KS entries in LDS, deeper ones in this ray's column of global memory
+// (entry KS + j at g[j * gs]) — for reference trees deeper than the LDS stack, which the reference walks with its
+// stack[256] (path_tracing.frag:378). Only kernels launched for such trees use it.
+template <int STRIDE>
+struct LdsStack {
+  static constexpr bool spilled = false;
+  int* __restrict__ p;
+  __device__ __forceinline__ void put(int sp, int v) const { p[sp * STRIDE] = v; }
+  __device__ __forceinline__ int get(int sp) const { return p[sp * STRIDE]; }
+};
+template <int STRIDE, int KS>
+struct SpillStack {
+  int* __restrict__ p;
+  int* __restrict__ g;
+  size_t gs;
+  bool spilled = false;  // some entry went past the LDS stack (traversal counter kStatSpills)
+  __device__ __forceinline__ void put(int sp, int v) {
+    if (sp < KS) {
+      p[sp * STRIDE] = v;
+    } else {
+      g[(size_t)(sp - KS) * gs] = v;
+      spilled = true;
+    }
+  }
+  __device__ __forceinline__ int get(int sp) const { return sp < KS ? p[sp * STRIDE] : g[(size_t)(sp - KS) * gs]; }
+};
+
 // mode 0: closest hit (hitBVH :372-424); mode 1: any hit (HDR shadow);
 // mode 2: any hit nearer than `maxd` by length(P - S) (point-light shadow).
 //
@@ -168,12 +196,12 @@ __device__ __forceinline__ int ref_leaf_count(int ref) { return (-(ref + 1)) & 1
 // all intersect together, which keeps wave64 lanes converged. Leaves are still
 // intersected in the order the depth-first walk reaches them, so the strict '<'
 // tie rule of hitArray/hitBVH picks the same triangle.
-// `stk` points at this lane's first slot; slots are STRIDE ints apart (LDS column).
+// `stk` is this lane's stack (LdsStack / SpillStack above).
 constexpr int kNone = kNoneRef;
 
 // `steps` (optional) receives the node + triangle visits (load-balancing probe).
-template <int MODE, int STRIDE>
-__device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, float maxd, int prune,
+template <int MODE, class Stk>
+__device__ int traverse(const SceneDev& sc, Stk& stk, v3 S, v3 d, float maxd, int prune,
                         float* t_best_out, uint32_t* steps = nullptr, float t_init = PT_INF, bool* tie = nullptr) {
   v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   float tbest = t_init;  // MODE 0 with t_init < inf: only hits nearer than t_init are sought (caller falls back)
@@ -205,19 +233,18 @@ __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
       int cl = __float_as_int(q3.x), cr = __float_as_int(q3.y);
       if (hl && hr) {
         bool lnear = dl < dr;
-        stk[sp * STRIDE] = lnear ? cr : cl;
-        ++sp;
+        stk.put(sp++, lnear ? cr : cl);
         node = lnear ? cl : cr;
       } else if (hl) {
         node = cl;
       } else if (hr) {
         node = cr;
       } else {
-        node = sp > 0 ? stk[--sp * STRIDE] : kNone;
+        node = sp > 0 ? stk.get(--sp) : kNone;
       }
       if (node < 0 && node != kNone && leaf == kNone) {  // postpone this leaf, keep walking
         leaf = node;
-        node = sp > 0 ? stk[--sp * STRIDE] : kNone;
+        node = sp > 0 ? stk.get(--sp) : kNone;
       }
       if (!__any(leaf == kNone)) break;  // every lane holds a leaf: intersect together
     }
@@ -229,7 +256,7 @@ __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
       const bool stop = leaf_scan(sc.tri_geom, first, cnt, S, d, [&](int i, float t) {
         if (MODE == 0) {
           if (t < tbest) { tbest = t; best = i; tied = false; }
-          else if (t == tbest) tied = true;
+          else if (t == tbest && best >= 0) tied = true;  // (a hit exactly at the bound t_init is no tie)
           return false;
         }
         if (!(t < PT_INF)) return false;
@@ -246,7 +273,7 @@ __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
       leaf = kNone;
       if (node < 0 && node != kNone) {  // the walk stopped on a second leaf: it is next in order
         leaf = node;
-        node = sp > 0 ? stk[--sp * STRIDE] : kNone;
+        node = sp > 0 ? stk.get(--sp) : kNone;
       }
     }
   }
@@ -262,16 +289,16 @@ __device__ int traverse(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, f
 // one hitBVH reaches), so the minimum t and, when one triangle alone attains it, the triangle are the reference's.
 // When two triangles attain the same t exactly, the reference keeps the one its depth-first order meets first:
 // that ray is walked again on the reference tree in the reference's order. Same bits either way.
-template <int STRIDE>
-__device__ __forceinline__ int closest_hit(const SceneDev& sc, bool sah, int* __restrict__ stk, v3 S, v3 d, int prune,
+template <class Stk>
+__device__ __forceinline__ int closest_hit(const SceneDev& sc, bool sah, Stk& stk, v3 S, v3 d, int prune,
                                            float* t, uint32_t* steps, float t_init = PT_INF, bool* rewalk = nullptr) {
-  if (!sah) return traverse<0, STRIDE>(sc, stk, S, d, 0.0f, prune, t, steps, t_init);
+  if (!sah) return traverse<0>(sc, stk, S, d, 0.0f, prune, t, steps, t_init);
   bool tie = false;
-  int tri = traverse<0, STRIDE>(anyhit_scene(sc), stk, S, d, 0.0f, 1, t, steps, t_init, &tie);
+  int tri = traverse<0>(anyhit_scene(sc), stk, S, d, 0.0f, 1, t, steps, t_init, &tie);
   if (rewalk) *rewalk = tie;
   if (tie) {
     uint32_t more = 0;
-    tri = traverse<0, STRIDE>(sc, stk, S, d, 0.0f, 1, t, &more, t_init);
+    tri = traverse<0>(sc, stk, S, d, 0.0f, 1, t, &more, t_init);
     if (steps) *steps += more;
   }
   return tri;
@@ -291,8 +318,8 @@ __device__ __forceinline__ int closest_hit(const SceneDev& sc, bool sah, int* __
 // nearer than `maxd`) merged behind a runtime flag, so a wave runs one loop.
 // budget > 0: a ray whose walk exceeds `budget` node + triangle visits stops and reports *deferred (its
 // verdict is then decided by the wave-cooperative walk, shadow_coop_walk below).
-template <int STRIDE>
-__device__ bool anyhit2(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, bool point, float maxd,
+template <class Stk>
+__device__ bool anyhit2(const SceneDev& sc, Stk& stk, v3 S, v3 d, bool point, float maxd,
                         uint32_t* steps, uint32_t budget = 0, bool* deferred = nullptr) {
   v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   const float lim = point ? maxd * 1.0002f + 2.0e-4f : __builtin_inff();
@@ -318,19 +345,18 @@ __device__ bool anyhit2(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, b
       int cl = __float_as_int(q3.x), cr = __float_as_int(q3.y);
       if (hl && hr) {
         bool lnear = dl < dr;
-        stk[sp * STRIDE] = lnear ? cr : cl;
-        ++sp;
+        stk.put(sp++, lnear ? cr : cl);
         node = lnear ? cl : cr;
       } else if (hl) {
         node = cl;
       } else if (hr) {
         node = cr;
       } else {
-        node = sp > 0 ? stk[--sp * STRIDE] : kNone;
+        node = sp > 0 ? stk.get(--sp) : kNone;
       }
       if (node < 0 && node != kNone && leaf == kNone) {
         leaf = node;
-        node = sp > 0 ? stk[--sp * STRIDE] : kNone;
+        node = sp > 0 ? stk.get(--sp) : kNone;
       }
       if (!__any(leaf == kNone)) break;
     }
@@ -346,7 +372,7 @@ __device__ bool anyhit2(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, b
       leaf = kNone;
       if (node < 0 && node != kNone) {
         leaf = node;
-        node = sp > 0 ? stk[--sp * STRIDE] : kNone;
+        node = sp > 0 ? stk.get(--sp) : kNone;
       }
     }
   }
@@ -414,7 +440,8 @@ __device__ bool shadow_coop_walk(const SceneDev& sc, int* __restrict__ st, int c
   if (!overflow) return false;
   // overflow: lane 0 walks the whole ray serially on the (now free) LDS region
   bool occ = false;
-  if (lane == 0) occ = anyhit2<1>(sc, st, S, d, point, maxd, nullptr);
+  LdsStack<1> ls{st};
+  if (lane == 0) occ = anyhit2(sc, ls, S, d, point, maxd, nullptr);
   return __any(occ);
 }
 

@@ -549,7 +549,7 @@ class Renderer:
         return e0.elapsed_time(e1) / (reps * len(iters))
 
     STAT_KEYS = ("primary_rays", "primary_visits", "bounce_rays", "bounce_visits", "shadow_rays", "shadow_visits",
-                 "tie_rewalks", "primary_retries")  # pt_pass_set_trace_stats order
+                 "tie_rewalks", "primary_retries", "spills")  # pt_pass_set_trace_stats order
 
     def trace_stats(self) -> dict:
         """Render one frame with the path tracer's traversal counters on (pt_pass_set_trace_stats): rays traced and
