@@ -1068,6 +1068,7 @@ int draw_svgf(Pass* p, int kind) {
     if (ui(p, "exact", 0)) rc = launch_atrous_exact(k, g.stream);          // bit-exact form (tests)
     else if (ui(p, "atrous_variant", 0) == 1) rc = launch_atrous_simple(k, g.stream);  // A/B: generic
     else if (ui(p, "atrous_variant", 0) == 2) rc = launch_atrous_step(k, g.stream);    // A/B: step kernel
+    else if (ui(p, "atrous_variant", 0) == 3) rc = launch_atrous_pair(k, g.stream);    // A/B: packed pairs
     else rc = launch_atrous_fast(k, g.stream);                             // LDS-tiled (production)
   } else if (kind == PK_MODULATE) {
     ModulateParams k;

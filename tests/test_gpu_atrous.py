@@ -84,7 +84,7 @@ def _run(gl, illum, nd, fw, step, variant):
 
 
 @pytest.mark.parametrize("size", SIZES)
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("step", [1, 2, 4, 8, 16])
 def test_atrous_kernel_vs_oracle(gpu, step, variant, size):
     W, H = size
@@ -110,12 +110,13 @@ def test_interior_tiles_cover_every_step():
 @pytest.mark.parametrize("size", SIZES)
 @pytest.mark.parametrize("step", [1, 2, 4, 8, 16])
 def test_tile_kernel_equals_step_kernel(gpu, step, size):
-    """The LDS-tiled kernel (variant 0) performs the step kernel's (variant 2) arithmetic in the same tap order:
-    identical bits, NaNs included."""
+    """The LDS-tiled kernels (variant 0, and variant 3: channel-planar tile, packed pixel pairs) perform the step
+    kernel's (variant 2) arithmetic in the same tap order: identical bits, NaNs included."""
     illum, nd, fw = _planes(seed=5, W=size[0], H=size[1])
-    a = _run(gpu, illum, nd, fw, step, 0)
     b = _run(gpu, illum, nd, fw, step, 2)
-    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    for v in (0, 3):
+        a = _run(gpu, illum, nd, fw, step, v)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), v
 
 
 def test_tile_kernel_aux_flag_on_rendered_planes(gpu, scene_small):
@@ -134,7 +135,7 @@ def test_tile_kernel_aux_flag_on_rendered_planes(gpu, scene_small):
     nd = gpu.readback(pl["normal_depth"])
     assert 0.05 < float(np.mean(nd[..., 3] == 1.0)) < 0.95  # both background and surface pixels present
     outs = {}
-    for variant in (0, 2):
+    for variant in (0, 2, 3):
         for step in (1, 2, 4, 8, 16):
             to = getTextureRGB32F(Wr, Hr)
             p = RenderPass(getShaderProgram("shaders/svgf_Atrous.frag", "shaders/vert.vert"), Wr, Hr)
@@ -154,3 +155,4 @@ def test_tile_kernel_aux_flag_on_rendered_planes(gpu, scene_small):
     r.close()
     for step in (1, 2, 4, 8, 16):
         assert np.array_equal(outs[0, step].view(np.uint32), outs[2, step].view(np.uint32)), step
+        assert np.array_equal(outs[3, step].view(np.uint32), outs[2, step].view(np.uint32)), step

@@ -1,56 +1,86 @@
-"""A/B timing of the a-trous variants on real 4K frame data (interleaved rounds, one process)."""
-import os, sys, time, json
+"""A/B timing of the a-trous variants on real 4K frame data, default and surface-dominated views.
+
+For each view: render 3 frames, then time every variant x step as 20 back-to-back launches between two HIP
+events on the library stream (no per-launch sync), interleaved over ROUNDS rounds; report the median per-launch
+time and the algorithmic (52 B/px) fraction of 8 TB/s. The variants' outputs are compared bit for bit.
+usage: python tools/bench_atrous.py [variant ...]   (variants: 0 tile, 2 step, 3 pair; default 0 3)"""
+import json
+import os
+import sys
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "path-tracing-svgf_amd"))
+sys.path.insert(0, REPO)
 import numpy as np
+import torch
+
+from bench import VIEWS
 from ptsvgf import gl
-from ptsvgf.gl import GL_TEXTURE_2D, RenderPass
+from ptsvgf._lib import check, pt
 from ptsvgf.camera import parameter_config
+from ptsvgf.gl import GL_TEXTURE_2D, RenderPass
 from ptsvgf.renderer import Renderer, _prog
 from ptsvgf.scene import build_scene
 
 W, H = int(os.environ.get("W", 3840)), int(os.environ.get("H", 2160))
+VARIANTS = [int(v) for v in sys.argv[1:]] or [0, 3]
+torch.cuda.set_device(0)
 gl.init(0)
+check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
 scene = build_scene("table_clock_plant")
-r = Renderer(scene, W, H, parameter_config(), mode="fast", aspect_corrected=True, run_taa=False, run_output=False)
-for _ in range(3):
-    r.frame()
-gl.sync()
-pl = r.planes()
-out = gl.getTextureRGB32F(W, H)
-ap = RenderPass(_prog("svgf_Atrous.frag"), W, H)
-ap.colorAttachments.append(out)
-ap.bindData(False)
-ap.set_uniform_float("gPhiColor", 4.0); ap.set_uniform_float("gPhiNormal", 128.0)
-ap.set_texture_uniform(GL_TEXTURE_2D, pl["normal_depth"], "gNormalAndLinearZ")
-ap.set_texture_uniform(GL_TEXTURE_2D, pl["fwidth"], "gNormalDepthFwidth")
-ap.set_texture_uniform(GL_TEXTURE_2D, pl["variance"], "gIllumination")
-gl.set_profiling(True)
-res = {}
-variants = {"step": 0, "simple": 1}
-for rnd in range(int(os.environ.get("ROUNDS", 5))):
-    for name, v in variants.items():
-        ap.set_uniform_int("atrous_variant", v)
-        for step in (1, 2, 4, 8, 16):
-            ap.set_uniform_int("gStepSize", step)
-            ts = []
-            for _ in range(10):
+for view in ("default", "surface"):
+    r = Renderer(scene, W, H, parameter_config(), mode="fast", aspect_corrected=True, run_taa=False, run_output=False)
+    if VIEWS[view]:
+        for k, v in VIEWS[view].items():
+            setattr(r.camera, k, np.array(v, np.float32) if isinstance(v, tuple) else np.float32(v))
+        r.camera.dirty = True
+    for _ in range(3):
+        r.frame()
+    torch.cuda.synchronize()
+    pl = r.planes()
+    out = gl.getTextureRGB32F(W, H)
+    ap = RenderPass(_prog("svgf_Atrous.frag"), W, H)
+    ap.colorAttachments.append(out)
+    ap.bindData(False)
+    ap.set_uniform_float("gPhiColor", 4.0)
+    ap.set_uniform_float("gPhiNormal", 128.0)
+    ap.set_texture_uniform(GL_TEXTURE_2D, pl["normal_depth"], "gNormalAndLinearZ")
+    ap.set_texture_uniform(GL_TEXTURE_2D, pl["fwidth"], "gNormalDepthFwidth")
+    ap.set_texture_uniform(GL_TEXTURE_2D, pl["variance"], "gIllumination")
+    surf = float(np.mean(gl.readback(pl["normal_depth"])[..., 3] != 1.0))
+    res = {}
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for rnd in range(int(os.environ.get("ROUNDS", 5))):
+        for v in VARIANTS:
+            ap.set_uniform_int("atrous_variant", v)
+            for step in (1, 2, 4, 8, 16):
+                ap.set_uniform_int("gStepSize", step)
                 ap.draw()
-                ts.append(ap.last_ms())
-            res.setdefault((name, step), []).extend(ts)
-bytes_ = 52 * W * H
-rows = []
-for (name, step), ts in sorted(res.items()):
-    med = float(np.median(ts))
-    rows.append(dict(variant=name, step=step, median_us=round(med * 1e3, 1), min_us=round(min(ts) * 1e3, 1),
-                     algo_GBs=round(bytes_ / (med * 1e-3) / 1e9, 1)))
-for row in rows:
-    print(json.dumps(row))
-# equivalence of the two variants on this data
-outs = {}
-for name, v in variants.items():
-    ap.set_uniform_int("atrous_variant", v); ap.set_uniform_int("gStepSize", 4); ap.draw()
-    outs[name] = gl.readback(out)
-d = np.abs(outs["step"] - outs["simple"]) / np.maximum(1, np.abs(outs["simple"]))
-print("max rel diff step vs simple:", float(np.nanmax(d)))
+                e0.record()
+                for _ in range(20):
+                    ap.draw()
+                e1.record()
+                e1.synchronize()
+                res.setdefault((v, step), []).append(e0.elapsed_time(e1) / 20)
+    for (v, step), ts in sorted(res.items()):
+        med = float(np.median(ts))
+        print(json.dumps(dict(view=view, surface=round(surf, 3), variant=v, step=step, us=round(med * 1e3, 1),
+                              frac=round(52 * W * H / (med * 1e-3) / 8e12, 3))), flush=True)
+    for v in VARIANTS:
+        print(json.dumps(dict(view=view, variant=v, mean_us=round(float(np.mean(
+            [np.median(res[(v, s)]) for s in (1, 2, 4, 8, 16)])) * 1e3, 1))), flush=True)
+    outs = {}
+    for v in VARIANTS:
+        for step in (1, 2, 4, 8, 16):
+            ap.set_uniform_int("atrous_variant", v)
+            ap.set_uniform_int("gStepSize", step)
+            ap.draw()
+            outs[(v, step)] = gl.readback(out)
+    for v in VARIANTS[1:]:
+        same = all(np.array_equal(outs[(v, s)].view(np.uint32), outs[(VARIANTS[0], s)].view(np.uint32))
+                   for s in (1, 2, 4, 8, 16))
+        print(f"{view}: variant {v} bit-identical to variant {VARIANTS[0]}: {same}", flush=True)
+    ap.destroy()
+    gl.destroy_texture(out)
+    r.close()
 gl.shutdown()
