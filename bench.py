@@ -317,6 +317,9 @@ def main():
                 "tie_rewalks": int(st["tie_rewalks"]), "primary_retries": int(st["primary_retries"]),
                 "traversals_per_pixel": round(rays / st["primary_rays"], 3) if st["primary_rays"] else None,
                 "visits_per_ray": round(visits / rays, 2) if rays else None,
+                # share of SIMD lanes doing traversal work: a wave runs as long as its longest ray
+                "lane_efficiency": {k: round(st[f"{k}_visits"] / st[f"{k}_slots"], 3) if st.get(f"{k}_slots") else None
+                                    for k in ("primary", "bounce", "shadow")},
                 "rays_per_s": round(rays * fps, 0), "visits_per_s": round(visits * fps, 0),
                 "pt_ms_profiled": round(pt_ms, 4) if pt_ms else None,
                 "rays_per_s_pt_only": round(rays / (pt_ms * 1e-3), 0) if pt_ms else None,

@@ -953,6 +953,9 @@ int draw_pathtrace(Pass* p) {
     // > 0: shadow rays past this many visits finish in the wave-cooperative walk (A/B switch; off: with frames
     // in flight it measured slower)
     k.wf.shadow_budget = (uint32_t)ui(p, "shadow_budget", 0);
+    // percent of the bounce / shadow lists traced by lane-refill waves: 75 pays with frames in flight (the renderer
+    // sets it then), 0 (default) keeps the shortest single-frame latency
+    k.refill = std::min(100, std::max(0, ui(p, "trace_refill", 0)));
     const int ntiles = wf_subset_tiles(k.W, std::max(0, k.y1 - k.y0), k.tile_stride, k.tile_offset);  // wf_primary's grid
     TRY(tile_order_begin(p, ntiles, &k.tiles));
     if (ui(p, "trace_fork", 0) && !p->aux) {  // A/B switch (off: measured slower with frames in flight)

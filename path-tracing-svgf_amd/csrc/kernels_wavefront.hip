@@ -139,6 +139,13 @@ __device__ __forceinline__ void stat_add(const PTParams& p, int k, uint32_t v) {
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(p.wf.stats + k, (unsigned long long)v);
 }
 
+__device__ __forceinline__ void stat_slots(const PTParams& p, int k, uint32_t v) {  // 64 x the wave maximum
+  if (!p.wf.stats) return;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(p.wf.stats + k, 64ull * v);
+}
+
 // load-balancing probe: accumulate traversal steps per band row (only when requested)
 #ifndef PT_STEP_MAX
 __device__ __forceinline__ void add_row_cost(const PTParams& p, int local_row, int, uint32_t steps) {
@@ -219,6 +226,7 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
   }
   stat_add(p, kStatPrimRays, valid ? 1u : 0u);
   stat_add(p, kStatPrimVisits, steps);
+  stat_slots(p, kStatPrimSlots, steps);
   stat_add(p, kStatTieRewalks, rewalk ? 1u : 0u);
   stat_add(p, kStatPrimRetries, retry ? 1u : 0u);
   stat_add(p, kStatSpills, spill ? 1u : 0u);
@@ -259,6 +267,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest(PTParams p
   stat_add(p, kStatSpills, spill ? 1u : 0u);
   stat_add(p, kStatBounceRays, valid ? 1u : 0u);
   stat_add(p, kStatBounceVisits, steps);
+  stat_slots(p, kStatBounceSlots, steps);
   stat_add(p, kStatTieRewalks, rewalk ? 1u : 0u);
 }
 
@@ -306,6 +315,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p,
   stat_add(p, kStatShadowRays, valid && pid >= 0 ? 1u : 0u);
   stat_add(p, kStatSpills, spill ? 1u : 0u);
   stat_add(p, kStatShadowVisits, steps);
+  stat_slots(p, kStatShadowSlots, steps);
   // rays past the step budget go to the cooperative walk (one wave-aggregated append per wave)
   const unsigned long long m = __ballot(deferred);
   if (m) {
@@ -315,6 +325,337 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow(PTParams p,
     base = __shfl(base, __ffsll((long long)m) - 1);
     if (deferred) p.wf.straggler[base + __popcll(m & ((1ull << lane) - 1ull))] = pid | (point ? (int)0x80000000 : 0);
   }
+}
+
+// Dense index k of the shadow lists (HDR list, then the point-light lists bin by bin) -> pixel, kind.
+__device__ __forceinline__ bool shadow_item(const int* __restrict__ list, const int* __restrict__ counts, int cap,
+                                            int nh, int k, int* pid, bool* point) {
+  if (k < nh) {
+    *point = false;
+    return seg_get(list, counts, cap, k, pid);
+  }
+  *point = true;
+  int r = k - nh;
+#pragma unroll
+  for (int b = 0; b < kPointBins; ++b) {
+    const int nb = seg_total(counts + (1 + b) * kSeg);
+    if (r < nb) return seg_get(list + (size_t)(1 + b) * kSeg * cap, counts + (1 + b) * kSeg, cap, r, pid);
+    r -= nb;
+  }
+  return false;
+}
+
+// Work queue of the refill traversal kernels: the list's dense index range is cut into 8 regions, one per XCD,
+// each with its own head word (one returning atomic per grab of kGrab items; a per-XCD head keeps the grabs of
+// 256 CUs off one word, MI355X_MICROARCH.md "dequeue"). A wave drains its XCD's region first, then the others;
+// regions seen exhausted (a relaxed load of the head) are skipped without an atomic. Wave-uniform.
+constexpr int kGrab = 64;
+struct WaveQueue {
+  int* heads;
+  int total, xcd;
+  unsigned done;  // regions known exhausted
+  int next, end;  // current grab [next, end)
+  __device__ __forceinline__ bool grab() {
+    for (int t = 0; t < 8; ++t) {
+      const int r = (xcd + t) & 7;
+      if ((done >> r) & 1u) continue;
+      const int rs = (int)(((long long)total * r) >> 3), re = (int)(((long long)total * (r + 1)) >> 3);
+      if (rs + __hip_atomic_load(heads + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= re) {
+        done |= 1u << r;
+        continue;
+      }
+      int base = 0;
+      if ((threadIdx.x & 63) == 0) base = atomicAdd(heads + r, kGrab);
+      base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
+      if (rs + base < re) {
+        next = rs + base;
+        end = min(next + kGrab, re);
+        return true;
+      }
+      done |= 1u << r;
+    }
+    return false;
+  }
+};
+// Resident blocks the refill kernels launch with the queue: enough to fill the chip at their occupancy (5 waves/SIMD
+// at 86 VGPRs, 2-wave blocks); waves beyond the work exit at their first grab.
+constexpr int kRefillBlocks = 256 * 10;
+// Static chunks (default), guided: the first PTParams::refill percent of the list goes out in chunks of 64 * R items
+// (R = kRefillRounds) to the first waves, the rest in chunks of 64 (one item per lane) to the waves after them, so
+// the launch does not end on long refill waves; idle lanes take new items only once at least kRefillMin lanes of
+// the wave are idle (a refill stalls the whole wave for the new rays' loads). PT_REFILL_QUEUE=1: the per-XCD work
+// queue above instead (measured slower: 109 fps against 148 without refill at 4K).
+// Measured at 4K (tools/lib_ab.sh, R = 4, kRefillMin = 16): refill 0 / 50 / 75 / 85 % -> 147.7 / 156.0 / 159.3 /
+// 158.7 fps with 4 frames in flight, 117.1 / 116.0 / 110.0 / 108.1 fps serial: the refill waves raise the share of
+// busy lanes (shadow 0.42 -> 0.65) but lengthen the launch's tail, which other frames in flight fill.
+#ifndef PT_REFILL_ROUNDS
+#define PT_REFILL_ROUNDS 4
+#endif
+#ifndef PT_REFILL_MIN
+#define PT_REFILL_MIN 16
+#endif
+#ifndef PT_REFILL_QUEUE
+#define PT_REFILL_QUEUE 0
+#endif
+constexpr int kRefillRounds = PT_REFILL_ROUNDS, kRefillMin = PT_REFILL_MIN;
+// Chunk rounds per big wave, from the list length: a big wave lasts about R one-ray waves, which pays only when the
+// launch spans several rounds of resident waves anyway (at 1080p the lists are too short: refill there measured
+// 367 -> 312 fps with R = 4 everywhere; with R from the length 380 fps at 1080p, 156.6 at 4K). kResidentWaves: 256 CUs
+// x 20 waves (86 VGPRs: 5 waves per SIMD).
+constexpr int kResidentWaves = 256 * 20;
+#ifndef PT_REFILL_DIV
+#define PT_REFILL_DIV 1
+#endif
+__device__ __forceinline__ int refill_rounds(int total) {
+  const int r = total / (64 * kResidentWaves * PT_REFILL_DIV);
+  return r < 1 ? 1 : (r > kRefillRounds ? kRefillRounds : r);
+}
+__device__ __forceinline__ WaveQueue refill_queue(int* heads, int total, int big_pct) {
+  WaveQueue q{heads, total, (int)(blockIdx.x & 7), 0u, 0, 0};
+  if (PT_REFILL_QUEUE) {
+    q.grab();
+  } else {
+    const int wave = blockIdx.x * (kTB / 64) + (threadIdx.x >> 6);
+    const int R = refill_rounds(total);
+    const int big = R > 1 ? (int)((long long)total * big_pct / 100) / (64 * R) : 0;  // waves with big chunks
+    if (wave < big) {
+      q.next = wave * 64 * R;
+      q.end = q.next + 64 * R;
+    } else {
+      q.next = min(big * 64 * R + (wave - big) * 64, total);
+      q.end = min(q.next + 64, total);
+    }
+    q.done = 0xffu;  // no grabs beyond the chunk
+  }
+  return q;
+}
+__host__ __device__ constexpr int refill_blocks(int items_max) {
+  return PT_REFILL_QUEUE ? (items_max + kTB - 1) / kTB < kRefillBlocks ? (items_max + kTB - 1) / kTB : kRefillBlocks
+                         : (items_max + kTB - 1) / kTB;  // enough 64-item waves for every item (spare waves exit)
+}
+
+// Shadow rays with lane refill. In wf_trace_shadow a wave lives as long as its longest ray while lanes whose rays
+// ended idle: only ~42 % of the lane slots of shadow waves do traversal work on the 4K bench frame (35 % on the
+// surface view; trace counters, bench.py "lane_efficiency"). Here waves stay resident and, between two leaf phases
+// of their while-while walks, hand list items from the work queue to their idle lanes, so lanes stay busy until the
+// queue runs dry. Per ray the walk is anyhit2's (same boxes, same pruning bound, same triangle tests, visit order
+// per ray unchanged); any-hit verdicts do not depend on which lane or when.
+template <int KS, bool DEEP>
+__global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTParams p, const int* __restrict__ list,
+                                                                             const int* __restrict__ counts, int cap,
+                                                                             int* __restrict__ heads) {
+  __shared__ int stk[KS * kTB];
+  const int lane = threadIdx.x & 63;
+  const int nh = seg_total(counts);
+  int total = nh;
+#pragma unroll
+  for (int b = 0; b < kPointBins; ++b) total += seg_total(counts + (1 + b) * kSeg);
+  WaveQueue q = refill_queue(heads, total, p.refill);
+  if (q.next >= q.end) return;
+  const SceneDev sc = anyhit_scene(p.scene);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  auto st = ray_stack<kTB, KS, DEEP>(stk + threadIdx.x, p, 0);
+  bool have = false, point = false, spill = false;
+  int pid = 0, sp = 0, node = kNone, leaf = kNone;
+  v3 S = splat(0.0f), d = splat(0.0f), inv = splat(0.0f);
+  float lim = 0.0f, maxd = 0.0f;
+  uint32_t nvis = 0, nray = 0;
+  while (true) {
+    const unsigned long long idle = __ballot(!have);
+    if (__popcll(idle) >= (__ballot(have) ? kRefillMin : 1) && (q.next < q.end || q.grab())) {
+      // refill: the next items go to the idle lanes in lane order
+      const int k = q.next + __popcll(idle & below);
+      if (!have && k < q.end && shadow_item(list, counts, cap, nh, k, &pid, &point)) {
+        const float4 o = ldnt(&p.wf.ray_o[pid]);
+        const float4 dir = point ? ldnt(&p.wf.sh_p[pid]) : ldnt(&p.wf.sh_h[pid]);  // point: (direction, distance)
+        S = xyz(o);
+        d = xyz(dir);
+        inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        maxd = dir.w;
+        lim = point ? maxd * 1.0002f + 2.0e-4f : __builtin_inff();
+        sp = 0;
+        node = sc.root_ref;
+        leaf = kNone;
+        if (node < 0) { leaf = node; node = kNone; }
+        if constexpr (DEEP) st = ray_stack<kTB, KS, DEEP>(stk + threadIdx.x, p, pid);
+        have = true;
+        ++nray;
+      }
+      q.next = min(q.next + __popcll(idle), q.end);
+    }
+    if (!__any(have)) break;
+    while (node >= 0) {  // anyhit2's descent (only lanes holding a ray have node >= 0)
+      ++nvis;
+      const float4* nd = sc.bvh + 4 * node;
+      const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+      float t0l, t0r;
+      const float dl = slab(S, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, &t0l);
+      const float dr = slab(S, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, &t0r);
+      const bool hl = dl > 0.0f && !(t0l > lim), hr = dr > 0.0f && !(t0r > lim);
+      const int cl = __float_as_int(q3.x), cr = __float_as_int(q3.y);
+      if (hl && hr) {
+        const bool lnear = dl < dr;
+        st.put(sp++, lnear ? cr : cl);
+        node = lnear ? cl : cr;
+      } else if (hl) {
+        node = cl;
+      } else if (hr) {
+        node = cr;
+      } else {
+        node = sp > 0 ? st.get(--sp) : kNone;
+      }
+      if (node < 0 && node != kNone && leaf == kNone) {
+        leaf = node;
+        node = sp > 0 ? st.get(--sp) : kNone;
+      }
+      if (!__any(leaf == kNone)) break;
+    }
+    bool hit = false;
+    while (leaf != kNone) {  // anyhit2's leaf phase
+      const int first = ref_leaf_first(leaf), cnt = ref_leaf_count(leaf);
+      nvis += (uint32_t)cnt;
+      if (leaf_scan(sc.tri_geom, first, cnt, S, d, [&](int, float t) {
+            return t < PT_INF && (!point || length(sub(add(S, muls(d, t)), S)) < maxd);
+          })) {
+        hit = true;
+        break;
+      }
+      leaf = kNone;
+      if (node < 0 && node != kNone) {
+        leaf = node;
+        node = sp > 0 ? st.get(--sp) : kNone;
+      }
+    }
+    if (have && (hit || (node == kNone && leaf == kNone))) {  // this lane's ray is decided
+      (point ? p.wf.occ_p : p.wf.occ_h)[pid] = hit;
+      have = false;
+      node = leaf = kNone;
+      spill = spill || st.spilled;
+    }
+  }
+  stat_add(p, kStatShadowRays, nray);
+  stat_add(p, kStatSpills, spill ? 1u : 0u);
+  stat_add(p, kStatShadowVisits, nvis);
+  stat_slots(p, kStatShadowSlots, nvis);
+}
+
+// Bounce rays (closest hit) with lane refill, as wf_trace_shadow_refill: per ray closest_hit's walk on the SAH tree
+// over the reference leaves (pruned), and for a ray whose best t was met exactly by a second triangle the walk again
+// on the reference tree in the reference's order (traverse<0>; the same lane restarts it before taking a new ray).
+// Production switches only (closest_tree = prune = 1); the host keeps wf_trace_closest otherwise.
+template <int KS, bool DEEP>
+__global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTParams p, const int* __restrict__ list,
+                                                                              const int* __restrict__ counts, int cap,
+                                                                              int* __restrict__ heads) {
+  __shared__ int stk[KS * kTB];
+  const int lane = threadIdx.x & 63;
+  int total = 0;
+#pragma unroll
+  for (int b = 0; b < kLiveBins * kSeg; ++b) total += counts[b];
+  WaveQueue q = refill_queue(heads, total, p.refill);
+  if (q.next >= q.end) return;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  auto st = ray_stack<kTB, KS, DEEP>(stk + threadIdx.x, p, 0);
+  bool have = false, rewalk = false, tied = false, spill = false;
+  int pid = 0, sp = 0, node = kNone, leaf = kNone, best = -1;
+  const float4* tree = p.scene.bvh_any;  // this lane's tree: the SAH tree, or the reference tree for a re-walk
+  v3 S = splat(0.0f), d = splat(0.0f), inv = splat(0.0f);
+  float tbest = PT_INF;
+  uint32_t nvis = 0, nray = 0, nrewalk = 0;
+  while (true) {
+    const unsigned long long idle = __ballot(!have);
+    if (__popcll(idle) >= (__ballot(have) ? kRefillMin : 1) && (q.next < q.end || q.grab())) {
+      const int k = q.next + __popcll(idle & below);
+      if (!have && k < q.end && bins_get(list, counts, kLiveBins, cap, k, &pid)) {
+        const float4 o = ldnt(&p.wf.ray_o[pid]), dd = ldnt(&p.wf.ray_d[pid]);
+        S = xyz(o);
+        d = xyz(dd);
+        inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        tree = p.scene.bvh_any;
+        node = p.scene.root_any;
+        rewalk = false;
+        tbest = PT_INF;
+        best = -1;
+        tied = false;
+        sp = 0;
+        leaf = kNone;
+        if (node < 0) { leaf = node; node = kNone; }
+        if constexpr (DEEP) st = ray_stack<kTB, KS, DEEP>(stk + threadIdx.x, p, pid);
+        have = true;
+        ++nray;
+      }
+      q.next = min(q.next + __popcll(idle), q.end);
+    }
+    if (!__any(have)) break;
+    while (node >= 0) {  // traverse<0>'s descent, pruned by the current best t
+      ++nvis;
+      const float4* nd = tree + 4 * node;
+      const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+      float t0l, t0r;
+      const float dl = slab(S, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, &t0l);
+      const float dr = slab(S, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, &t0r);
+      const float lim = tbest * 1.0002f + 2.0e-4f;
+      const bool hl = dl > 0.0f && !(t0l > lim), hr = dr > 0.0f && !(t0r > lim);
+      const int cl = __float_as_int(q3.x), cr = __float_as_int(q3.y);
+      if (hl && hr) {
+        const bool lnear = dl < dr;
+        st.put(sp++, lnear ? cr : cl);
+        node = lnear ? cl : cr;
+      } else if (hl) {
+        node = cl;
+      } else if (hr) {
+        node = cr;
+      } else {
+        node = sp > 0 ? st.get(--sp) : kNone;
+      }
+      if (node < 0 && node != kNone && leaf == kNone) {
+        leaf = node;
+        node = sp > 0 ? st.get(--sp) : kNone;
+      }
+      if (!__any(leaf == kNone)) break;
+    }
+    while (leaf != kNone) {  // traverse<0>'s leaf phase: strict '<' keeps the first triangle at a given t
+      const int first = ref_leaf_first(leaf), cnt = ref_leaf_count(leaf);
+      nvis += (uint32_t)cnt;
+      leaf_scan(p.scene.tri_geom, first, cnt, S, d, [&](int i, float t) {
+        if (t < tbest) {
+          tbest = t;
+          best = i;
+          tied = false;
+        } else if (t == tbest && best >= 0) {
+          tied = true;
+        }
+        return false;
+      });
+      leaf = kNone;
+      if (node < 0 && node != kNone) {
+        leaf = node;
+        node = sp > 0 ? st.get(--sp) : kNone;
+      }
+    }
+    if (have && node == kNone && leaf == kNone) {  // this lane's walk is complete
+      if (!rewalk && tied) {  // exact tie: walk the ray again on the reference tree, in the reference's order
+        rewalk = true;
+        ++nrewalk;
+        tree = p.scene.bvh;
+        node = p.scene.root_ref;
+        tbest = PT_INF;
+        best = -1;
+        tied = false;
+        sp = 0;
+        if (node < 0) { leaf = node; node = kNone; }
+      } else {
+        stnt(&p.wf.hit[pid], make_int2(best, __float_as_int(tbest)));
+        have = false;
+        spill = spill || st.spilled;
+      }
+    }
+  }
+  stat_add(p, kStatBounceRays, nray);
+  stat_add(p, kStatSpills, spill ? 1u : 0u);
+  stat_add(p, kStatBounceVisits, nvis);
+  stat_slots(p, kStatBounceSlots, nvis);
+  stat_add(p, kStatTieRewalks, nrewalk);
 }
 
 // The shadow rays wf_trace_shadow deferred: one wave per ray walks cooperatively (shadow_coop_walk). A fixed
@@ -567,10 +908,15 @@ int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent
   const int gS0 = ntiles;  // bounce-0 shade: one block per primary tile
   const bool fork = aux && ev_fork && ev_join;
   int* lists[2] = {p.wf.list0, p.wf.list1};
+  const bool refill_closest = p.refill && p.closest_tree && p.prune && p.scene.bvh_any;
   auto closest = [&](int i, hipStream_t st) {
     const int* lin = lists[(i + 1) & 1];
     const int* live_in = p.wf.counters + kWfCtr * (i - 1);
-    hipLaunchKernelGGL((wf_trace_closest<KS, DEEP>), dim3(gT), dim3(kTB), 0, st, p, lin, live_in, cap);
+    if (refill_closest)
+      hipLaunchKernelGGL((wf_trace_closest_refill<KS, DEEP>), dim3(refill_blocks(N)), dim3(kTB), 0, st, p,
+                         lin, live_in, cap, p.wf.counters + kWfCtr * i + kCtrQClosest);
+    else
+      hipLaunchKernelGGL((wf_trace_closest<KS, DEEP>), dim3(gT), dim3(kTB), 0, st, p, lin, live_in, cap);
   };
   for (int i = 0; i < p.max_depth; ++i) {
     const int* lin = lists[(i + 1) & 1];
@@ -594,7 +940,10 @@ int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent
       if ((e = hipEventRecord(ev_join, aux)) != hipSuccess) return (int)e;
     }
     int* strag = p.wf.counters + kWfCtr * i + kCtrStrag;  // shadow rays handed to the cooperative walk
-    if (p.scene.bvh4)
+    if (p.refill && !p.scene.bvh4 && !p.wf.shadow_budget)
+      hipLaunchKernelGGL((wf_trace_shadow_refill<KS, DEEP>), dim3(refill_blocks(2 * N)), dim3(kTB), 0, s, p,
+                         (const int*)p.wf.shadow_list, (const int*)shadow, cap, p.wf.counters + kWfCtr * i + kCtrQShadow);
+    else if (p.scene.bvh4)
       hipLaunchKernelGGL((wf_trace_shadow<KS, true, DEEP>), dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
                          (const int*)shadow, cap, strag);
     else

@@ -48,7 +48,9 @@ constexpr int kPointBins = 4;     // point-light shadow lists, one per light ind
 constexpr int kLiveBins = PT_LIVE_BINS;  // live-ray lists by direction octant: 8 measured 4 % slower than 1
 // wavefront list counters per bounce (8 segments each): live bins, HDR shadow, point bins, straggler count
 constexpr int kCtrHdr = 8 * kLiveBins, kCtrPoint = kCtrHdr + 8, kCtrStrag = kCtrPoint + 8 * kPointBins;
-constexpr int kWfCtr = (kCtrStrag + 1 + 63) / 64 * 64;
+// per-XCD work-queue heads of the refill traversal kernels launched in bounce i: shadow rays, closest-hit rays
+constexpr int kCtrQShadow = kCtrStrag + 1, kCtrQClosest = kCtrQShadow + 8;
+constexpr int kWfCtr = (kCtrQClosest + 8 + 63) / 64 * 64;
 constexpr int kWfCounters = 4 * kWfCtr;  // 4 bounces  // "no node" (leaf refs are >= -(2^31 - 1))
 
 struct Plane {          // banded RGBA32F plane
@@ -108,7 +110,8 @@ struct WFState {
   int* shadow_list;             // compacted shadow rays of one bounce: HDR list, then kPointBins point-light
                                 // lists (by light index), each kSeg segments of `cap`
   int* counters;                // per bounce i, base kWfCtr*i: [0, kCtrHdr) live-bin segment counts, then 8 HDR,
-                                // 8 kPointBins point-light counts, [kCtrStrag] cooperative-walk stragglers
+                                // 8 kPointBins point-light counts, [kCtrStrag] cooperative-walk stragglers,
+                                // 8 + 8 work-queue heads (kCtrQShadow, kCtrQClosest)
   uint32_t* row_cost;           // optional: traversal steps per band row (load-balancing probe), may be null
   int* straggler;               // shadow rays past the step budget: pid | (point << 31), count at kCtrStrag
   uint32_t shadow_budget;       // node + triangle visits before a shadow ray is handed to the cooperative walk (0: never)
@@ -118,9 +121,12 @@ struct WFState {
 };
 // Traversal counters of one path-tracing draw (pt_pass_set_trace_stats): rays traced and node + triangle visits
 // per traversal kind, tie re-walks on the reference tree, primary rays retried unbounded after the G-buffer bound, rays
-// whose stack went past the LDS stack into the spill columns (deep reference trees).
+// whose stack went past the LDS stack into the spill columns (deep reference trees), and per traversal kind the lane
+// slots its waves occupied (64 x the wave's largest visit count, summed over waves): visits / slots is the share of
+// SIMD lanes doing useful traversal work (divergence: a wave runs as long as its longest ray).
 enum { kStatPrimRays, kStatPrimVisits, kStatBounceRays, kStatBounceVisits, kStatShadowRays, kStatShadowVisits,
-       kStatTieRewalks, kStatPrimRetries, kStatSpills, kStatCount };
+       kStatTieRewalks, kStatPrimRetries, kStatSpills, kStatPrimSlots, kStatBounceSlots, kStatShadowSlots,
+       kStatCount };
 
 struct PTParams {
   int W, H, y0, y1;     // frame size (global) and rows to compute
@@ -139,6 +145,7 @@ struct PTParams {
   int prune;            // closest-hit pruning (parity-safe margin)
   int closest_tree;     // closest-hit rays walk the SAH tree over the reference leaves (closest_hit, pt_shading.h)
   int stack_need;       // deepest interior level of the binary BVH (selects the LDS stack size)
+  int refill;           // > 0: percent of each bounce/shadow list traced by lane-refill waves (kernels_wavefront.hip)
   float sobol_u[4], sobol_v[4];  // sobolVec2(frameCounter+1, b): uniform across pixels
   WFState wf;
   // optional bound for the primary rays from this frame's G-buffer (world position + normal/linearZ planes,

@@ -198,7 +198,7 @@ class RenderPass:
         check(pt().pt_pass_set_row_cost(self._handle(), C.c_void_p(device_ptr or None)))
 
     def set_trace_stats(self, device_ptr: int) -> None:
-        """Path-tracing pass: add traversal counters (9 x uint64, pt_pass_set_trace_stats) on every draw (0 disables)."""
+        """Path-tracing pass: add traversal counters (12 x uint64, pt_pass_set_trace_stats) on every draw (0 disables)."""
         check(pt().pt_pass_set_trace_stats(self._handle(), C.c_void_p(device_ptr or None)))
 
     def set_motion_bound(self, device_ptr: int) -> None:

@@ -252,6 +252,8 @@ class Renderer:
             p.set_uniform_int("pointLightSize", scene.lights.shape[0])
             p.set_uniform_int("aspect_corrected", int(self.aspect_corrected))
             p.set_uniform_int("prune", int(self._pt_prune))
+            # lane-refill traversal waves: +8 % frames/s with frames in flight, -6 % serial (kernels_wavefront.hip)
+            p.set_uniform_int("trace_refill", 75 if self.K > 1 else 0)
             self.pt_slots.append((p, outs))
         self.pass_path_tracing = PassGroup([p for p, _ in self.pt_slots])  # settings apply to every slot
 
@@ -549,7 +551,8 @@ class Renderer:
         return e0.elapsed_time(e1) / (reps * len(iters))
 
     STAT_KEYS = ("primary_rays", "primary_visits", "bounce_rays", "bounce_visits", "shadow_rays", "shadow_visits",
-                 "tie_rewalks", "primary_retries", "spills")  # pt_pass_set_trace_stats order
+                 "tie_rewalks", "primary_retries", "spills", "primary_slots", "bounce_slots",
+                 "shadow_slots")  # pt_pass_set_trace_stats order
 
     def trace_stats(self) -> dict:
         """Render one frame with the path tracer's traversal counters on (pt_pass_set_trace_stats): rays traced and

@@ -450,3 +450,30 @@ def test_accumulate_matches_oracle(gpu, scene_small, mode, K):
         one = single.frame()
     assert not np.array_equal(one["color"], acc2)
     r.close()
+
+
+@pytest.mark.parametrize("scene_name", ["scene_small", "scene_cornell", "scene_nan"])
+def test_lane_refill_is_result_preserving(gpu, scene_name, request):
+    """trace_refill=100 / 75 (list-driven traversal waves hand the next list items to their idle lanes, for all of
+    each list / its first 75 %) gives the
+    one-ray-per-thread kernels' bits and traces the same rays. Visit counts may differ by a few: a lane holding a
+    postponed leaf keeps descending while other lanes of its wave still look for one (while-while), and the wave
+    a ray shares differs between the two forms; the verdicts and hits do not depend on it."""
+    gl = gpu
+    scene = request.getfixturevalue(scene_name)
+    W, H = 96, 64
+    outs, stats = [], []
+    for refill in (100, 75, 0):
+        r = _renderer(scene, W, H, mode="fast", run_taa=False, run_output=False)
+        r.pass_path_tracing.set_uniform_int("trace_refill", refill)
+        r.frame()
+        stats.append(r.trace_stats())
+        outs.append({k: gl.readback(r.planes()[k]) for k in ("color", "emission", "albedo")})
+        r.close()
+    for o, st in zip(outs[:2], stats[:2]):
+        for k in o:
+            assert np.array_equal(o[k].view(np.uint32), outs[2][k].view(np.uint32)), k
+        for k in ("primary_rays", "bounce_rays", "shadow_rays"):
+            assert st[k] == stats[2][k], (k, stats)
+        for k in ("shadow_visits", "bounce_visits"):
+            assert abs(st[k] - stats[2][k]) <= 0.01 * stats[2][k], (k, stats)
