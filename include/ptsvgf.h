@@ -104,7 +104,7 @@ int pt_texbuffer_create(const void* host_data, size_t bytes, uint32_t fmt, uint3
 int pt_texarray_create(int width, int height, int layers, uint32_t* out_tex);     /* RGBA8 2-D array */
 int pt_texarray_upload_layer(uint32_t tex, int layer, int width, int height, int channels,
                              const uint8_t* host_data);
-int pt_texture_readback(uint32_t tex, float* host_out, size_t bytes);             /* syncs */
+int pt_texture_readback(uint32_t tex, float* host_out, size_t bytes);             /* syncs the device */
 int pt_texture_upload_rgba(uint32_t tex, const float* host_rgba, size_t bytes);   /* raw RGBA32F rows */
 int pt_texture_device_ptr(uint32_t tex, void** out_ptr);
 int pt_texture_info(uint32_t tex, int* width, int* height, int* row0);

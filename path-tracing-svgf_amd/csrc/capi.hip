@@ -1382,7 +1382,7 @@ int pt_texture_readback(uint32_t tex, float* out, size_t bytes) {
   Texture* t = tex_of(tex);
   if (!t || !t->dev) return err(PT_ERR_INVALID_HANDLE, "invalid texture");
   if (!out || bytes < t->bytes) return err(PT_ERR_ARG, "readback buffer too small");
-  HIPCHK(hipStreamSynchronize(g.stream));
+  HIPCHK(hipDeviceSynchronize());  // every stream: a frame may be in flight on another renderer's stream
   HIPCHK(hipMemcpy(out, t->dev, t->bytes, hipMemcpyDeviceToHost));
   return PT_OK;
 }

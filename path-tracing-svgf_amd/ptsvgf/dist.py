@@ -39,6 +39,7 @@ tests/test_dist_gloo.py (CPU, oracle) both execute it through run_stage().
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 # a-trous radius 2*step (svgf_Atrous.frag:92-97) for step 1 << i; the reference allows up to 8 iterations
@@ -247,6 +248,10 @@ class BandRenderer:
 
         kw.setdefault("run_taa", False)
         kw.setdefault("run_output", False)
+        # frames in flight: issue the back end one frame behind the front end, so the host's wait for the motion
+        # bound (before the reprojection exchange) finds a G-buffer issued a frame earlier (Renderer back_lag)
+        if kw.get("frames_in_flight", 1) > 1:
+            kw.setdefault("back_lag", min(int(os.environ.get("PTSVGF_BAND_LAG", "2")), kw["frames_in_flight"] - 1))
         if kw.get("frames_in_flight", 1) == 1:  # exchanges run on torch's stream: the draws must too
             from ._lib import check, pt
             check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
@@ -259,7 +264,6 @@ class BandRenderer:
         self._mb_event = [torch.cuda.Event() for _ in range(ng)]
         for b, p in enumerate(self.r.init_pass):
             p.set_motion_bound(self._mb_dev[b:b + 1].data_ptr())
-        self._mb_set = None
         self.motion_log = []  # per frame: (all-reduced |motion.y| in rows, history rows exchanged)
         self.camera = self.r.camera
         self.pass_path_tracing = self.r.pass_path_tracing
@@ -271,14 +275,13 @@ class BandRenderer:
         with torch.cuda.stream(stream):
             self._mb_host[b:b + 1].copy_(self._mb_dev[b:b + 1], non_blocking=True)
             self._mb_event[b].record(stream)
-        self._mb_set = b
 
     def _motion(self) -> None:
-        """This frame's history reach: wait for the G-buffer's bound (the path tracer is already queued), MAX over
-        ranks on the host."""
+        """History reach of the frame whose back end is being issued: wait for its G-buffer's bound (issued with
+        its front end, back_lag frames earlier), MAX over ranks on the host."""
         import numpy as np
 
-        b = self._mb_set
+        b = self.r.back_set
         self._mb_event[b].synchronize()
         m = float(self._mb_host[b:b + 1].numpy().view(np.float32)[0])
         m = allreduce_motion(m, self.dist, self._group)

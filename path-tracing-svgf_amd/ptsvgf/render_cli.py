@@ -71,7 +71,7 @@ def main(argv=None) -> int:
         gl.sync()
         write_png(a.png, gl.readback(r.planes()["output"]))
         if a.pfm:
-            write_pfm(a.pfm, gl.readback(r._view_plane()))
+            write_pfm(a.pfm, gl.readback(r._view_plane(r.frame_index - 1)))
         r.close()
     finally:
         gl.shutdown()

@@ -57,7 +57,7 @@ class Renderer:
     def __init__(self, scene: Scene, width: int, height: int, config: parameter_config | None = None,
                  mode: str = "fast", aspect_corrected: bool | None = None, band=None, prune: bool = True,
                  atrous_exact: bool = False, run_taa: bool = True, run_output: bool = True, tex_factory=None,
-                 halo=None, gbuffer_rows=None, frames_in_flight: int = 1, after_gbuffer=None):
+                 halo=None, gbuffer_rows=None, frames_in_flight: int = 1, after_gbuffer=None, back_lag: int = 0):
         """band = (y0, y1, row0, rows) for screen-band sharding; tex_factory(w, h) -> handle allocates the
         frame-sized planes (ptsvgf.dist wraps torch tensors); halo(stage, {plane name: handle}) is called before
         the SVGF passes that read rows beyond the band (dist.HALO_SCHEDULE names the planes); after_gbuffer(set,
@@ -70,7 +70,13 @@ class Renderer:
         the SVGF of frame f-K, whose buffers it reuses. The front end's launches end in long tails (a few
         rays through dense geometry); with K frames in flight another frame's work fills them. Same
         kernels, same inputs, same bits as K = 1 (tests/test_gpu_parity.py); throughput rises, latency
-        from camera to finished frame is up to K frames."""
+        from camera to finished frame is up to K frames.
+
+        back_lag = D (0 <= D < K, frames in flight only): frame() issues the front end of frame f and the SVGF
+        back end of frame f - D, so a host wait before a back-end pass (the band renderer's motion bound, read
+        from the G-buffer before the reprojection exchange is sized) finds a G-buffer issued D frames earlier
+        instead of stalling the issue of the next front end. planes() and time_atrous() first issue the back
+        ends still pending (flush); results are those of D = 0."""
         if mode not in ("fast", "reference"):
             raise ValueError(mode)
         self.mode = mode
@@ -121,6 +127,18 @@ class Renderer:
         self.K = int(frames_in_flight)
         if self.K < 1 or (self.K > 1 and mode != "fast"):
             raise ValueError("frames_in_flight must be >= 1, and > 1 only with the fast driver")
+        self.lag = int(back_lag)
+        if not 0 <= self.lag < self.K:
+            raise ValueError(f"back_lag must be in [0, frames_in_flight) = [0, {self.K}), got {back_lag}")
+        self._pending: list = []  # front ends whose back end is not issued yet (back_lag)
+        # a serial renderer draws on torch's stream of its construction, whatever stream another renderer in the
+        # process left the library on (the library's stream is process-global, pt_set_stream)
+        self._serial_stream = None
+        if self.K == 1:
+            import torch
+
+            self._serial_stream = torch.cuda.current_stream()
+        self.back_set = 0         # G-buffer set of the back end being issued (halo / after_gbuffer users)
         # G-buffer sets: the reference has one; fast mode alternates two (this frame / previous frame);
         # with K frames in flight, frame f writes set f % (K+1) once SVGF(f-K) has read it (as "previous")
         nbuf = (self.K + 1 if self.K > 1 else 2) if mode == "fast" else 1
@@ -273,9 +291,9 @@ class Renderer:
             self._ensure_slots(max(self.K, 2))
         self.camera.frameCounter = 0
 
-    def _view_plane(self) -> int:
+    def _view_plane(self, f: int) -> int:
         v = getattr(self, "view", "final_pic")
-        pl = self.planes()
+        pl = self._planes_of(f)
         return {"path_tracing_pic_1spp": pl["color"], "accumulate_color": pl["color"],
                 "svgf_reprojected_pic": pl["reproj_illum"], "svgf_variance_pic": pl["variance"],
                 "svgf_atrous_pic": pl["atrous"], "svgf_modulate_pic": pl["modulate"],
@@ -408,15 +426,13 @@ class Renderer:
         self._draw(nf, "copy")
         self.final = self.taa_output if self.run_taa else self.modulate_color
 
-    def _frame_fast(self):
-        cfg = self.cfg
+    def _front_fast(self) -> dict:
+        """G-buffer + path tracer of frame f (the front end); returns what its back end needs."""
         f = self.frame_index
-        b = f & 1                                              # history parity (back end, sequential)
-        pb = 1 - b
         ng = len(self.gbuf)
-        g, gp = self.gbuf[f % ng], self.gbuf[(f - 1) % ng]
         s = f % len(self.pt_slots)
         self._use_slot(s)
+        done = None
         if self.K > 1:                                         # front end on stream s, after SVGF(f - K)
             import torch
 
@@ -445,10 +461,23 @@ class Renderer:
             done = torch.cuda.Event()
             done.record(fe)
             self._fe_prev = done
-            self._back.wait_event(done)
-            self._stream_to(self._back)
         else:
             self._gbuffer_and_pt(f % ng)
+        return dict(f=f, slot=s, done=done, frame_counter=self.camera.frameCounter)
+
+    def _back_fast(self, ctx: dict):
+        """The SVGF chain of the frame whose front end made ctx (back-end stream, sequential over frames)."""
+        cfg = self.cfg
+        f = ctx["f"]
+        b = f & 1                                              # history parity (back end, sequential)
+        pb = 1 - b
+        ng = len(self.gbuf)
+        g, gp = self.gbuf[f % ng], self.gbuf[(f - 1) % ng]
+        _, (color, emission, albedo) = self.pt_slots[ctx["slot"]]
+        self.back_set = f % ng
+        if self.K > 1:
+            self._back.wait_event(ctx["done"])
+            self._stream_to(self._back)
         self._halo("reproject", {"prev_illum": self.hist_illum[pb], "prev_moments": self.moments[pb],
                                  "prev_nd": gp["normal_depth"]})
         rp = self.reproject[b]
@@ -456,9 +485,9 @@ class Renderer:
         rp.set_uniform_float("depth_threshold", cfg.reproj_depth_threshold)
         rp.set_uniform_float("normal_threshold", cfg.reproj_normal_threshold)
         rp.set_texture_uniform(GL_TEXTURE_2D, g["velocity"], "gMotion")
-        rp.set_texture_uniform(GL_TEXTURE_2D, self.curColor, "gColor")
-        rp.set_texture_uniform(GL_TEXTURE_2D, self.Albedo, "gAlbedo")
-        rp.set_texture_uniform(GL_TEXTURE_2D, self.Emission, "gEmission")
+        rp.set_texture_uniform(GL_TEXTURE_2D, color, "gColor")
+        rp.set_texture_uniform(GL_TEXTURE_2D, albedo, "gAlbedo")
+        rp.set_texture_uniform(GL_TEXTURE_2D, emission, "gEmission")
         rp.set_texture_uniform(GL_TEXTURE_2D, self.hist_illum[pb], "gPrevIllum")
         rp.set_texture_uniform(GL_TEXTURE_2D, self.moments[pb], "gPrevMoments_HistoryLength")
         rp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
@@ -504,8 +533,8 @@ class Renderer:
         self.atrous_final = src
         mp = self.svgf_modulate_pass
         mp.reset_texture_slot()
-        mp.set_texture_uniform(GL_TEXTURE_2D, self.Albedo, "gAlbedo")
-        mp.set_texture_uniform(GL_TEXTURE_2D, self.Emission, "gEmission")
+        mp.set_texture_uniform(GL_TEXTURE_2D, albedo, "gAlbedo")
+        mp.set_texture_uniform(GL_TEXTURE_2D, emission, "gEmission")
         mp.set_texture_uniform(GL_TEXTURE_2D, src, "gIllumination")
         mp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
         self._draw(mp, "modulate")
@@ -517,7 +546,7 @@ class Renderer:
             tp.set_texture_uniform(GL_TEXTURE_2D, self.taa[pb], "previousColor")
             tp.set_texture_uniform(GL_TEXTURE_2D, g["velocity"], "velocityTexture")
             tp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "normal_depth")
-            tp.set_uniform_uint("frameCounter", self.camera.frameCounter)
+            tp.set_uniform_uint("frameCounter", ctx["frame_counter"])
             self._draw(tp, "taa")
         self.final = self.taa[b] if self.run_taa else self.modulate_color
 
@@ -527,8 +556,9 @@ class Renderer:
         library's stream, kernels alone on the GPU (everything in flight is drained first). Fast driver."""
         import torch
 
+        self.flush()
         g, iters, src0 = self._atrous_last
-        stream = self._back if self.K > 1 else torch.cuda.current_stream()
+        stream = self._back if self.K > 1 else self._serial_stream
         torch.cuda.synchronize()
         self._stream_to(stream)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -610,28 +640,45 @@ class Renderer:
         return {"ping": self.ping, "pong": self.pong, "hist0": self.hist_illum[0], "hist1": self.hist_illum[1]}[key]
 
     def frame(self) -> None:
-        """One iteration of main.cpp's while-loop body (436-602), headless."""
+        """One iteration of main.cpp's while-loop body (436-602), headless (with back_lag D: this frame's front
+        end and frame f - D's back end)."""
         self.camera.update()
+        if self._serial_stream is not None:
+            self._stream_to(self._serial_stream)
         if self.mode == "reference":
             self._frame_reference()
+            self._finish(None)
         else:
-            self._frame_fast()
+            self._pending.append(self._front_fast())
+            while len(self._pending) > self.lag:
+                self._finish(self._pending.pop(0))
+        # main.cpp:599-600: pre_viewproj = projection * inverse(cameraRotate) = projection * view
+        self.pre_viewproj = mat_mul(self.camera.cam_proj_mat, self.camera.cam_view_mat)
+        self.camera.frameCounter += 1
+        self.frame_index += 1
+
+    def flush(self) -> None:
+        """Issue the back ends still pending (back_lag)."""
+        while self._pending:
+            self._finish(self._pending.pop(0))
+
+    def _finish(self, ctx) -> None:
+        """Back end (fast driver) + output pass of one frame; then its frame slot is free for frame f + K."""
+        f = self.frame_index if ctx is None else ctx["f"]
+        if ctx is not None:
+            self._back_fast(ctx)
         if self.run_output:                                    # main.cpp:556-590 (final view)
             op = self.output_pass
             op.reset_texture_slot()
             op.set_uniform_bool("accumulate", self.cfg.accumulate_color)
-            op.set_texture_uniform(GL_TEXTURE_2D, self._view_plane(), "texPass0")
+            op.set_texture_uniform(GL_TEXTURE_2D, self._view_plane(f), "texPass0")
             self._draw(op, "output")
         if self.K > 1:  # the slot's buffers are free again once this frame's back end has run
             import torch
 
             ev = torch.cuda.Event()
             ev.record(self._back)
-            self._slot_free[self.frame_index % self.K] = ev
-        # main.cpp:599-600: pre_viewproj = projection * inverse(cameraRotate) = projection * view
-        self.pre_viewproj = mat_mul(self.camera.cam_proj_mat, self.camera.cam_view_mat)
-        self.camera.frameCounter += 1
-        self.frame_index += 1
+            self._slot_free[f % self.K] = ev
 
     # --------------------------------------------------------- accessors ---
     def close(self) -> None:
@@ -653,7 +700,11 @@ class Renderer:
         self._owned = []
 
     def planes(self) -> dict:
-        """Handles of this frame's per-pass outputs (for readback / tests)."""
+        """Handles of the last frame's per-pass outputs (for readback / tests); issues pending back ends first."""
+        self.flush()
+        return self._planes_of(self.frame_index - 1)
+
+    def _planes_of(self, f: int) -> dict:
         if self.mode == "reference":
             g = self.gbuf[0]
             return dict(world=g["world"], normal_depth=g["normal_depth"], velocity=g["velocity"], fwidth=g["fwidth"],
@@ -662,10 +713,11 @@ class Renderer:
                         variance=self.variance_compute_illumination, atrous=self.atrous_output,
                         history_illum=self.lastIllumination, modulate=self.modulate_color, final=self.final,
                         output=self.output_tex)
-        b = (self.frame_index - 1) & 1
-        g = self.gbuf[(self.frame_index - 1) % len(self.gbuf)]
+        b = f & 1
+        g = self.gbuf[f % len(self.gbuf)]
+        _, (color, emission, albedo) = self.pt_slots[f % len(self.pt_slots)]
         return dict(world=g["world"], normal_depth=g["normal_depth"], velocity=g["velocity"], fwidth=g["fwidth"],
-                    color=self.curColor, emission=self.Emission, albedo=self.Albedo, reproj_illum=self.illum,
+                    color=color, emission=emission, albedo=albedo, reproj_illum=self.illum,
                     reproj_moments=self.moments[b], variance=self.var_out, atrous=self.atrous_final,
                     history_illum=self.hist_illum[b], modulate=self.modulate_color, final=self.final,
                     output=self.output_tex)

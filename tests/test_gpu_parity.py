@@ -316,16 +316,16 @@ def test_accumulate_fast_equals_reference(gpu, scene_small, K):
     b.close()
 
 
-@pytest.mark.parametrize("K", [2, 3])
-def test_frames_in_flight_equal_serial(gpu, scene_small, K):
-    """K frames in flight (front ends on K streams, SVGF chain on a back-end stream) give the serial fast
-    driver's bits: per frame (read back after each frame) and after K+3 frames issued without any host wait
-    (moving camera, so every frame's inputs differ)."""
+@pytest.mark.parametrize("K,lag", [(2, 0), (3, 0), (3, 1), (4, 3)])
+def test_frames_in_flight_equal_serial(gpu, scene_small, K, lag):
+    """K frames in flight (front ends on K streams, SVGF chain on a back-end stream; with back_lag the back end
+    issued `lag` frames behind the front end) give the serial fast driver's bits: per frame (read back after each
+    frame) and after K+3 frames issued without any host wait (moving camera, so every frame's inputs differ)."""
     gl = gpu
     W, H = 96, 64
     kw = dict(mode="fast", run_taa=True, run_output=True)
     a = _renderer(scene_small, W, H, **kw)
-    b = _renderer(scene_small, W, H, frames_in_flight=K, **kw)
+    b = _renderer(scene_small, W, H, frames_in_flight=K, back_lag=lag, **kw)
     keys = ("normal_depth", "color", "albedo", "reproj_illum", "variance", "atrous", "modulate", "final", "output")
     for f in range(K + 2):
         for r in (a, b):

@@ -48,6 +48,10 @@ def fake_exchange(items, plan, dist, group=None):
 
 
 D.halo_exchange = fake_exchange
+if os.environ.get("NOSYNC") == "1":  # experiment: no host wait for the G-buffer's motion bound (fixed reach)
+    def _motion_nosync(self):
+        self.plan.motion = D.REPROJ_REACH + 8
+    D.BandRenderer._motion = _motion_nosync
 torch.cuda.set_device(0)
 gl.init(0)
 from ptsvgf._lib import check, pt
@@ -84,6 +88,11 @@ def sim_rank(rk, bounds, probe=False, K=30):
         torch.cuda.synchronize()
         r.pass_path_tracing.set_row_cost(0)
         counts = c.cpu().numpy().astype(np.float64)
+    if os.environ.get("STATS") == "1":  # traversal counters of this band (rays, node + triangle visits by kind)
+        st = r.trace_stats()
+        vis = st["primary_visits"] + st["bounce_visits"] + st["shadow_visits"]
+        print(f"rank {rk} stats: visits {vis / 1e6:.1f} M ({vis / 1e9 / (wall):.1f} G visits/s at the band's wall) "
+              f"{st}", flush=True)
     r.profile(True)
     r.frame()
     torch.cuda.synchronize()
@@ -111,9 +120,10 @@ if __name__ == "__main__":
     # calibration as in ptsvgf.dist.make_band_renderer: per-rank band time alone (frames in flight) + row visits,
     # band_row_cost per round, bounds from the mean of the rounds' estimates
     ranks = [int(v) for v in os.environ["RANKS"].split(",")] if "RANKS" in os.environ else range(N)
-    res = [sim_rank(rk, None, probe=True) for rk in ranks]
-    report("equal bands", res)
-    bounds = tuple(D.BandPlan(W, H, 0, N).bounds)
+    bounds = tuple(int(v) for v in os.environ["BOUNDS"].split(",")) if "BOUNDS" in os.environ else None
+    res = [sim_rank(rk, bounds, probe=True) for rk in ranks]
+    report("given bands" if bounds else "equal bands", res)
+    bounds = bounds or tuple(D.BandPlan(W, H, 0, N).bounds)
     est = []
     for rnd in range(int(os.environ.get("ROUNDS", "2")) if N > 1 and os.environ.get("BALANCE", "1") != "0" else 0):
         visits = np.concatenate([s["counts"] for s in res])
