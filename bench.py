@@ -32,8 +32,8 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 # frames in flight use K + 1 streams (K front ends + the SVGF back end; 3K + 1 with the optional G-buffer and
 # closest-hit side streams); HIP's default of 4 hardware queues per process would make streams share queues
-# and serialise. Set before HIP initialises.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# and serialise. Set before HIP initialises; the GPU box exports GPU_MAX_HW_QUEUES=4, so it is overridden (PTSVGF_HW_QUEUES to choose).
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("PTSVGF_HW_QUEUES", "16")
 sys.path.insert(0, os.path.join(REPO, "path-tracing-svgf_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 

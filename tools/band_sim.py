@@ -10,6 +10,7 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("PTSVGF_HW_QUEUES", "16")  # as bench.py
 sys.path.insert(0, os.path.join(REPO, "path-tracing-svgf_amd"))
 import numpy as np
 import torch
