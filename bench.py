@@ -265,6 +265,9 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         out = {"dt": dt, "rows": r.rows_rendered() if hasattr(r, "rows_rendered") else H}
+        if world > 1:  # the band plan the calibration chose: (slowest band ms, bounds) per measured plan
+            out["bands"] = {"bounds": list(r.plan.bounds), "back_lag": r.r.lag,
+                            "calibration": [[round(m, 3), list(b)] for m, b in getattr(r, "calibration", [])]}
         log(f"  {args.steps} frames in {dt:.3f} s = {args.steps / dt:.2f} frames/s")
         if probes:
             st = r.trace_stats()
@@ -383,6 +386,8 @@ def main():
                 "passes_ms": {k: round(v, 4) for k, v in res["per_pass"].items()}}
         if "max_history_rows" in res:
             line["max_history_rows"] = res["max_history_rows"]
+        if "bands" in res:
+            line["bands"] = res["bands"]
         print(json.dumps(line), flush=True)
     gl.shutdown()
     if dist:

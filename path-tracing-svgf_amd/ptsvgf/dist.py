@@ -320,7 +320,7 @@ class BandRenderer:
         self.r.close()
         self._tensors.clear()
 
-    def measure_row_cost(self, frames: int = 24):
+    def measure_row_cost(self, frames: int = 32):
         """Estimated time (ms) of every frame row, identical on all ranks.
 
         One probed frame counts each row's BVH visits (pt_pass_set_row_cost). Then every rank times `frames`
@@ -358,7 +358,8 @@ class BandRenderer:
         per_rank[p.rank] = frame_ms
         self.dist.all_reduce(visits)
         self.dist.all_reduce(per_rank)
-        return band_row_cost(visits.cpu().numpy(), p.bounds, per_rank.cpu().numpy())
+        self.last_band_ms = per_rank.cpu().numpy()  # every rank's band time alone (ms per frame)
+        return band_row_cost(visits.cpu().numpy(), p.bounds, self.last_band_ms)
 
 
 def band_row_cost(visits, bounds, ms):
@@ -400,22 +401,32 @@ def fit_row_cost(visits, rows, ms):
     return 0.0, float(t.sum() / max(A[:, 1].sum(), 1.0))
 
 
-def make_band_renderer(scene, W, H, cfg, rank, world, dist, balance: bool = True, rounds: int = 2, **kw):
+def make_band_renderer(scene, W, H, cfg, rank, world, dist, balance: bool = True, rounds: int = 3, **kw):
     """BandRenderer whose band heights equalise the measured per-row cost (sky rows are cheap, the plant
     and clock rows expensive). Each calibration round renders on the current bands, measures every rank's
     band time and visits (measure_row_cost) and cuts new bands at equal quantiles of the mean of all rounds'
-    per-row cost estimates; the renderer is then rebuilt on the final plan. Every rank derives the same bounds
-    from all-reduced data."""
+    per-row cost estimates. A band's time is not additive in its rows (a band holding the plant's longest rays
+    has a latency floor set by their walks) and single timings are noisy, so the last cut is measured too and the
+    plan with the smallest measured slowest band wins; the renderer is rebuilt on it. Every rank derives the same
+    bounds from all-reduced data."""
     import numpy as np
 
     r = BandRenderer(scene, W, H, cfg, rank, world, dist, **kw)
     if not balance or world == 1:
         return r
-    est = []
-    for _ in range(max(rounds, 1)):
+    est, tried = [], []
+    for i in range(max(rounds, 1) + 1):
         r.frame()
-        est.append(r.measure_row_cost())
+        cost = r.measure_row_cost()
+        tried.append((float(np.max(r.last_band_ms)), r.plan.bounds))
+        if i == max(rounds, 1):
+            break
+        est.append(cost)
         bounds = balanced_bounds(np.mean(est, axis=0), world)
         r.close()
         r = BandRenderer(scene, W, H, cfg, rank, world, dist, bounds=bounds, **kw)
+    best = min(tried, key=lambda x: x[0])[1]
+    r.close()  # calibration frames are discarded: the renderer starts fresh (frame 0, empty history)
+    r = BandRenderer(scene, W, H, cfg, rank, world, dist, bounds=best, **kw)
+    r.calibration = tried  # (slowest band ms, bounds) per measured plan
     return r

@@ -114,7 +114,9 @@ def report(tag, res):
               f"{s['xbytes'] / 1e6:.2f} MB")
     mx = max(s["wall"] for s in res)
     print(f"predicted frame (slowest rank, no exchange time): {mx:.3f} ms = {1e3 / mx:.1f} fps; "
-          f"sum of rank GPU times {sum(s['gpu'] for s in res):.3f} ms")
+          f"sum of rank GPU times {sum(s['gpu'] for s in res):.3f} ms; sum of rank walls "
+          f"{sum(s['wall'] for s in res):.3f} ms")
+    return mx
 
 
 if __name__ == "__main__":
@@ -123,7 +125,7 @@ if __name__ == "__main__":
     ranks = [int(v) for v in os.environ["RANKS"].split(",")] if "RANKS" in os.environ else range(N)
     bounds = tuple(int(v) for v in os.environ["BOUNDS"].split(",")) if "BOUNDS" in os.environ else None
     res = [sim_rank(rk, bounds, probe=True) for rk in ranks]
-    report("given bands" if bounds else "equal bands", res)
+    plans = [(report("given bands" if bounds else "equal bands", res), "initial")]
     bounds = bounds or tuple(D.BandPlan(W, H, 0, N).bounds)
     est = []
     for rnd in range(int(os.environ.get("ROUNDS", "2")) if N > 1 and os.environ.get("BALANCE", "1") != "0" else 0):
@@ -132,5 +134,8 @@ if __name__ == "__main__":
         bounds = D.balanced_bounds(np.mean(est, axis=0), N)
         print("round %d bounds %s" % (rnd, bounds))
         res = [sim_rank(rk, bounds, probe=True) for rk in range(N)]
-        report(f"balanced bands (round {rnd})", res)
+        plans.append((report(f"balanced bands (round {rnd})", res), bounds))
+    # as make_band_renderer: the measured plan with the smallest slowest band wins
+    best = min(plans, key=lambda x: x[0])
+    print(f"best measured plan: {best[1]} slowest band {best[0]:.3f} ms = {1e3 / best[0]:.1f} fps")
     gl.shutdown()
