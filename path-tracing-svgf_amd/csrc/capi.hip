@@ -76,6 +76,14 @@ struct RasterScene {
   int ntris = 0;
 };
 
+// Scratch of the tile-binned G-buffer (launch_gbuffer_raster), per rasterize pass, sized by its triangles and band.
+struct RasterBins {
+  void* base = nullptr;
+  int ntris = 0, ntiles = 0, pair_cap = 0, big_cap = 0, cap_uniform = 0;
+  int4* tri_box = nullptr;
+  int *tile_count = nullptr, *tile_off = nullptr, *pairs = nullptr, *big = nullptr, *ctr = nullptr;
+};
+
 struct WFBuffers {
   void* base = nullptr;  // one allocation carved into the WFState arrays
   size_t n = 0;          // pixels covered
@@ -154,6 +162,7 @@ struct Pass {
   std::unordered_map<std::string, Uniform> uni;
   int y_begin = -1, y_end = -1;
   RasterScene raster;
+  RasterBins bins;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   uint32_t* row_cost = nullptr;  // pt_pass_set_row_cost (not owned)
@@ -970,6 +979,48 @@ int draw_pathtrace(Pass* p) {
   return rc ? hip_err((hipError_t)rc, "pathtrace launch") : PT_OK;
 }
 
+// Allocates (once per size) and clears the rasteriser's scratch for this launch; fills k's binning fields.
+int raster_bins(Pass* p, int ntiles, GBufParams* k) {
+  RasterBins& b = p->bins;
+  const int ntris = p->raster.ntris;
+  if (!b.base || b.ntris != ntris || b.ntiles != ntiles || b.cap_uniform != ui(p, "raster_pair_cap", 0)) {
+    if (b.base) (void)hipFree(b.base);
+    b = RasterBins{};
+    int pair_cap = (int)std::min<long long>(std::max<long long>(256LL * ntris, 1 << 22), 1 << 28);
+    int big_cap = std::max(ntris, 1);
+    if (int cap = ui(p, "raster_pair_cap", 0); cap > 0) pair_cap = std::min(pair_cap, cap);  // tests: force overflow
+    auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t o_box = 0, o_cnt = o_box + up((size_t)std::max(ntris, 1) * 16), o_off = o_cnt + up((size_t)ntiles * 4),
+                 o_pairs = o_off + up(((size_t)ntiles + 1) * 4), o_big = o_pairs + up((size_t)pair_cap * 4),
+                 o_ctr = o_big + up((size_t)big_cap * 4), total = o_ctr + 256;
+    HIPCHK(hipMalloc(&b.base, total));
+    char* c = (char*)b.base;
+    b.tri_box = (int4*)(c + o_box);
+    b.tile_count = (int*)(c + o_cnt);
+    b.tile_off = (int*)(c + o_off);
+    b.pairs = (int*)(c + o_pairs);
+    b.big = (int*)(c + o_big);
+    b.ctr = (int*)(c + o_ctr);
+    b.ntris = ntris;
+    b.ntiles = ntiles;
+    b.pair_cap = pair_cap;
+    b.big_cap = big_cap;
+    b.cap_uniform = ui(p, "raster_pair_cap", 0);
+  }
+  HIPCHK(hipMemsetAsync(b.tile_count, 0, (size_t)ntiles * 4, g.stream));
+  HIPCHK(hipMemsetAsync(b.ctr, 0, 16, g.stream));
+  k->ntris = ntris;
+  k->tri_box = b.tri_box;
+  k->tile_count = b.tile_count;
+  k->tile_off = b.tile_off;
+  k->pairs = b.pairs;
+  k->pair_cap = b.pair_cap;
+  k->big = b.big;
+  k->big_cap = b.big_cap;
+  k->raster_ctr = b.ctr;
+  return PT_OK;
+}
+
 int draw_raster(Pass* p) {
   if (!p->raster.geom && p->raster.ntris > 0) return err(PT_ERR_STATE, "raster pass not bound");
   GBufParams k;
@@ -1012,10 +1063,16 @@ int draw_raster(Pass* p) {
     k.motion_max = p->motion_max;
   }
   const int ntiles = ((k.W + 15) / 16) * ((std::max(0, k.y1 - k.y0) + 15) / 16);  // gbuffer_kernel's grid
-  TRY(tile_order_begin(p, ntiles, &k.tiles));
-  int rc = launch_gbuffer(k, g.stream);
-  if (rc) return hip_err((hipError_t)rc, "gbuffer launch");
-  TRY(tile_order_finish(p, k.tiles));
+  if (ui(p, "gbuffer_mode", 1) == 1) {  // tile-binned rasterisation (default); the ray cast on list overflow
+    TRY(raster_bins(p, ntiles, &k));
+    int rc = launch_gbuffer_raster(k, g.stream);
+    if (rc) return hip_err((hipError_t)rc, "gbuffer raster launch");
+  } else {  // A/B: the ray cast with cost-ordered tiles
+    TRY(tile_order_begin(p, ntiles, &k.tiles));
+    int rc = launch_gbuffer(k, g.stream);
+    if (rc) return hip_err((hipError_t)rc, "gbuffer launch");
+    TRY(tile_order_finish(p, k.tiles));
+  }
   fwt->aux_valid = true;
   return PT_OK;
 }
@@ -1160,6 +1217,7 @@ int pt_shutdown(void) {
     if (p->raster.geom) (void)hipFree(p->raster.geom);
     if (p->raster.nrm) (void)hipFree(p->raster.nrm);
     if (p->raster.bvh) (void)hipFree(p->raster.bvh);
+    if (p->bins.base) (void)hipFree(p->bins.base);
     if (p->wf.base) (void)hipFree(p->wf.base);
     if (p->wf.spill) (void)hipFree(p->wf.spill);
     if (p->order.cost) (void)hipFree(p->order.cost);
@@ -1654,6 +1712,7 @@ int pt_pass_destroy(uint32_t pass) {
   if (p->raster.geom) (void)hipFree(p->raster.geom);
   if (p->raster.nrm) (void)hipFree(p->raster.nrm);
   if (p->raster.bvh) (void)hipFree(p->raster.bvh);
+  if (p->bins.base) (void)hipFree(p->bins.base);
   if (p->wf.base) (void)hipFree(p->wf.base);
   if (p->wf.spill) (void)hipFree(p->wf.spill);
   if (p->order.cost) (void)hipFree(p->order.cost);

@@ -200,9 +200,72 @@ __device__ __forceinline__ float lin_z(const GBufParams& p, v3 P) {
   return zw / fw;
 }
 
+// The G-buffer texels of pixel (x, y) from its closest front-facing hit (bests: geom index, best: t, (bu, bv):
+// barycentrics; bests < 0: background) and the wave's motion bound. Called by the whole wave (invalid lanes too).
+__device__ __forceinline__ void gb_finish(const GBufParams& p, int x, int y, bool valid, int ln, v3 o, v3 d,
+                                          float best, int bests, float bu, float bv) {
+  if (p.motion_max) {  // band planning (pt_pass_set_motion_bound): wave max of |motion.y|, one atomic per wave
+    float mv = 0.0f;
+    if (valid && bests >= 0) {  // the motion written below, recomputed for this lane
+      const v3 P = add(o, muls(d, best));
+      float c[4], pc[4];
+      mat_vec4(p.M, P, c);
+      mat_vec4(p.PV, P, pc);
+      mv = f_abs(((c[1] / c[3]) * 0.5f + 0.5f) - ((pc[1] / pc[3]) * 0.5f + 0.5f));
+      if (!(mv <= 3.0e38f)) mv = __builtin_inff();  // NaN / inf: unbounded
+    }
+    uint32_t mb = __float_as_uint(mv);  // non-negative floats order as their bits
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) mb = max(mb, (uint32_t)__shfl_xor((int)mb, s));
+    if (ln == 0 && mb) atomicMax(p.motion_max, mb);
+  }
+  if (!valid) return;
+  if (bests < 0) {
+    float4 bg = f4(0.2f, 0.3f, 0.3f, 1.0f);  // glClearColor (main.cpp:62)
+    pst(p.world, x, y, bg);
+    pst(p.normal_depth, x, y, bg);
+    pst(p.motion, x, y, bg);
+    pst(p.fwidth, x, y, bg);
+    if (p.fwidth_aux) p.fwidth_aux[(size_t)prow(p.fwidth, y) * p.W + x] = -0.3f;  // .y with the zCenter == 1 flag
+    return;
+  }
+  const float4* g = p.geom + 4 * bests;
+  const float4* gn = p.nrm + 3 * bests;
+  v3 p1 = xyz(g[0]), e1 = xyz(g[1]), e2 = xyz(g[2]);
+  v3 n1 = xyz(gn[0]), n2 = xyz(gn[1]), n3 = xyz(gn[2]);
+  auto interp = [&](float u, float v) {
+    float w0 = (1.0f - u) - v;
+    return add(add(muls(n1, w0), muls(n2, u)), muls(n3, v));
+  };
+  v3 P = add(o, muls(d, best));
+  v3 N = interp(bu, bv);
+  float lz = lin_z(p, P);
+  float c[4], pc[4];
+  mat_vec4(p.M, P, c);
+  mat_vec4(p.PV, P, pc);
+  float nowx = (c[0] / c[3]) * 0.5f + 0.5f, nowy = (c[1] / c[3]) * 0.5f + 0.5f;
+  float prex = (pc[0] / pc[3]) * 0.5f + 0.5f, prey = (pc[1] / pc[3]) * 0.5f + 0.5f;
+  v3 dx = gb_dir(p, x ^ 1, y), dy = gb_dir(p, x, y ^ 1);
+  MTr hx = moller(p1, e1, e2, o, dx, false), hy = moller(p1, e1, e2, o, dy, false);
+  v3 Nx = interp(hx.u, hx.v), Ny = interp(hy.u, hy.v);
+  float zx = lin_z(p, add(o, muls(dx, hx.t)));
+  float zy = lin_z(p, add(o, muls(dy, hy.t)));
+  v3 fwN = add(mk(f_abs(Nx.x - N.x), f_abs(Nx.y - N.y), f_abs(Nx.z - N.z)),
+               mk(f_abs(Ny.x - N.x), f_abs(Ny.y - N.y), f_abs(Ny.z - N.z)));
+  float fwz = f_max(f_abs(zx - lz), f_abs(zy - lz));
+  pst(p.world, x, y, f4(P.x, P.y, P.z, 1.0f));
+  pst(p.normal_depth, x, y, f4(N.x, N.y, N.z, lz));
+  pst(p.motion, x, y, f4(nowx - prex, nowy - prey, 0.0f, 1.0f));
+  pst(p.fwidth, x, y, f4(length(fwN), fwz, lz, 1.0f));
+  if (p.fwidth_aux)  // .y, sign bit = (linearZ == 1.0): the a-trous background test (svgf_Atrous.frag:77)
+    p.fwidth_aux[(size_t)prow(p.fwidth, y) * p.W + x] =
+        __uint_as_float(__float_as_uint(fwz) | (lz == 1.0f ? 0x80000000u : 0u));
+}
+
 template <int KS>
 __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
   __shared__ int stk[KS * kBlock];
+  if (p.raster_ctr && p.raster_ctr[2] == 0) return;  // launched as the rasteriser's overflow fallback: not needed
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   const int tile = sched_tile(p.tiles, blockIdx.y * gridDim.x + blockIdx.x);  // cost-ordered dispatch
   const int tx = tile % gridDim.x, ty = tile / gridDim.x;
@@ -276,62 +339,238 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
     }
   }
   sched_cost(p.tiles, tile, steps);
-  if (p.motion_max) {  // band planning (pt_pass_set_motion_bound): wave max of |motion.y|, one atomic per wave
-    float mv = 0.0f;
-    if (valid && bests >= 0) {  // the motion written below, recomputed for this lane
-      const v3 P = add(o, muls(d, best));
-      float c[4], pc[4];
-      mat_vec4(p.M, P, c);
-      mat_vec4(p.PV, P, pc);
-      mv = f_abs(((c[1] / c[3]) * 0.5f + 0.5f) - ((pc[1] / pc[3]) * 0.5f + 0.5f));
-      if (!(mv <= 3.0e38f)) mv = __builtin_inff();  // NaN / inf: unbounded
+  gb_finish(p, x, y, valid, ln, o, d, best, bests, bu, bv);
+}
+
+// ------------------------------------------------- G-buffer by tile binning ---
+// The same G-buffer (closest front-facing Moller hit of the pixel-centre ray, ties to the lower triangle index;
+// gb_finish for the texels) computed without a per-pixel BVH walk: every front-facing triangle is binned to the
+// 16 x 16 tiles its screen box covers, and each pixel runs the exact Moller test of gbuffer_kernel against the
+// triangles of its tile. The winner is the lexicographic minimum of (t, original index) over every triangle whose
+// Moller test accepts the ray — the ray cast's answer whatever the order, provided each such triangle reaches the
+// pixel's tile. The box: the triangle clipped in clip space to the view frustum's four side planes (widened by
+// 1 %; every pixel-centre ray with t > 0 lies inside, so the clipped-away part meets no such ray — and a triangle
+// with nothing left is dropped), projected, widened by kBoxMargin pixels (projection and ray arithmetic agree
+// to far below a pixel). A clipped vertex on the camera plane (the triangle passes through the eye) makes the
+// box the whole band. No walk means no tail: a tile costs about as much as it holds triangles.
+constexpr int kRTile = 16;
+constexpr int kLargeTiles = 64;  // triangles covering more tiles are binned by a whole block (rast_*_large)
+constexpr int kRChunk = 256;     // triangles staged in LDS per round of the resolve
+constexpr int kBoxMargin = 2;    // pixels
+constexpr int kLargeBlocks = 512;
+
+__device__ __forceinline__ int rast_ntx(const GBufParams& p) { return (p.W + kRTile - 1) / kRTile; }
+
+struct TileBox {
+  int tx0, tx1, ty0, ty1;
+  __device__ int area() const { return (tx1 - tx0 + 1) * (ty1 - ty0 + 1); }
+};
+__device__ __forceinline__ TileBox tile_box(const GBufParams& p, int4 b) {
+  return TileBox{b.x / kRTile, b.z / kRTile, (b.y - p.y0) / kRTile, (b.w - p.y0) / kRTile};
+}
+
+// Sutherland-Hodgman against s * w + sgn * c[axis] >= 0 (homogeneous clip coordinates: x, y, w)
+__device__ __forceinline__ int clip_plane(const float3* in, int n, float3* out, int axis, float sgn) {
+  const float s = 1.01f;
+  int m = 0;
+  for (int i = 0; i < n; ++i) {
+    const float3 a = in[i], b = in[(i + 1) % n];
+    const float da = s * a.z + sgn * (axis == 0 ? a.x : a.y), db = s * b.z + sgn * (axis == 0 ? b.x : b.y);
+    if (da >= 0.0f) out[m++] = a;
+    if ((da >= 0.0f) != (db >= 0.0f)) {
+      const float t = da / (da - db);
+      out[m++] = make_float3(a.x + t * (b.x - a.x), a.y + t * (b.y - a.y), a.z + t * (b.z - a.z));
     }
-    uint32_t mb = __float_as_uint(mv);  // non-negative floats order as their bits
-#pragma unroll
-    for (int s = 32; s > 0; s >>= 1) mb = max(mb, (uint32_t)__shfl_xor((int)mb, s));
-    if (ln == 0 && mb) atomicMax(p.motion_max, mb);
   }
-  if (!valid) return;
-  if (bests < 0) {
-    float4 bg = f4(0.2f, 0.3f, 0.3f, 1.0f);  // glClearColor (main.cpp:62)
-    pst(p.world, x, y, bg);
-    pst(p.normal_depth, x, y, bg);
-    pst(p.motion, x, y, bg);
-    pst(p.fwidth, x, y, bg);
-    if (p.fwidth_aux) p.fwidth_aux[(size_t)prow(p.fwidth, y) * p.W + x] = -0.3f;  // .y with the zCenter == 1 flag
+  return m;
+}
+
+// per triangle: cull, screen box, per-tile counts (small triangles; large ones are queued for rast_large)
+__global__ void __launch_bounds__(256) rast_setup(GBufParams p) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= p.ntris) return;
+  const float4* g = p.geom + 4 * i;
+  const float4 a = g[0], e1 = g[1], e2 = g[2], ng = g[3];
+  const v3 o = mk(p.eye[0], p.eye[1], p.eye[2]);
+  const v3 p1 = xyz(a);
+  int4 box = make_int4(1, 1, 0, 0);  // empty
+  if (dot(xyz(ng), sub(p1, o)) < 0.0f) {  // front-facing: gbuffer_kernel's back-face cull
+    const v3 v[3] = {p1, add(p1, xyz(e1)), add(p1, xyz(e2))};
+    float3 A[8], B[8];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      float c[4];
+      mat_vec4(p.M, v[k], c);
+      A[k] = make_float3(c[0], c[1], c[3]);
+    }
+    int n = clip_plane(A, 3, B, 0, 1.0f);
+    n = clip_plane(B, n, A, 0, -1.0f);
+    n = clip_plane(A, n, B, 1, 1.0f);
+    n = clip_plane(B, n, A, 1, -1.0f);
+    if (n > 0) {
+      float x0 = 3.0e38f, y0 = 3.0e38f, x1 = -3.0e38f, y1 = -3.0e38f;
+      bool full = false;
+      for (int k = 0; k < n; ++k) {
+        if (!(A[k].z > 0.0f)) { full = true; break; }
+        // pixel coordinate whose centre ray has this NDC: ndc = (2 x + 1) / W - 1
+        const float px = ((A[k].x / A[k].z + 1.0f) * (float)p.W - 1.0f) * 0.5f;
+        const float py = ((A[k].y / A[k].z + 1.0f) * (float)p.H - 1.0f) * 0.5f;
+        if (!(px == px && py == py)) { full = true; break; }
+        x0 = fminf(x0, px); x1 = fmaxf(x1, px);
+        y0 = fminf(y0, py); y1 = fmaxf(y1, py);
+      }
+      if (full) {
+        box = make_int4(0, p.y0, p.W - 1, p.y1 - 1);
+      } else {
+        const float lim = 1.0e8f;  // keeps the float -> int conversion in range
+        const int bx0 = (int)floorf(fmaxf(x0, -lim)) - kBoxMargin, bx1 = (int)ceilf(fminf(x1, lim)) + kBoxMargin;
+        const int by0 = (int)floorf(fmaxf(y0, -lim)) - kBoxMargin, by1 = (int)ceilf(fminf(y1, lim)) + kBoxMargin;
+        box = make_int4(max(bx0, 0), max(by0, p.y0), min(bx1, p.W - 1), min(by1, p.y1 - 1));
+      }
+    }
+  }
+  p.tri_box[i] = box;
+  if (box.x > box.z || box.y > box.w) return;
+  const TileBox tb = tile_box(p, box);
+  if (tb.area() > kLargeTiles) {
+    const int slot = atomicAdd(&p.raster_ctr[0], 1);
+    if (slot < p.big_cap) p.big[slot] = i;
+    else atomicOr(&p.raster_ctr[2], 1);
     return;
   }
-  const float4* g = p.geom + 4 * bests;
-  const float4* gn = p.nrm + 3 * bests;
-  v3 p1 = xyz(g[0]), e1 = xyz(g[1]), e2 = xyz(g[2]);
-  v3 n1 = xyz(gn[0]), n2 = xyz(gn[1]), n3 = xyz(gn[2]);
-  auto interp = [&](float u, float v) {
-    float w0 = (1.0f - u) - v;
-    return add(add(muls(n1, w0), muls(n2, u)), muls(n3, v));
-  };
-  v3 P = add(o, muls(d, best));
-  v3 N = interp(bu, bv);
-  float lz = lin_z(p, P);
-  float c[4], pc[4];
-  mat_vec4(p.M, P, c);
-  mat_vec4(p.PV, P, pc);
-  float nowx = (c[0] / c[3]) * 0.5f + 0.5f, nowy = (c[1] / c[3]) * 0.5f + 0.5f;
-  float prex = (pc[0] / pc[3]) * 0.5f + 0.5f, prey = (pc[1] / pc[3]) * 0.5f + 0.5f;
-  v3 dx = gb_dir(p, x ^ 1, y), dy = gb_dir(p, x, y ^ 1);
-  MTr hx = moller(p1, e1, e2, o, dx, false), hy = moller(p1, e1, e2, o, dy, false);
-  v3 Nx = interp(hx.u, hx.v), Ny = interp(hy.u, hy.v);
-  float zx = lin_z(p, add(o, muls(dx, hx.t)));
-  float zy = lin_z(p, add(o, muls(dy, hy.t)));
-  v3 fwN = add(mk(f_abs(Nx.x - N.x), f_abs(Nx.y - N.y), f_abs(Nx.z - N.z)),
-               mk(f_abs(Ny.x - N.x), f_abs(Ny.y - N.y), f_abs(Ny.z - N.z)));
-  float fwz = f_max(f_abs(zx - lz), f_abs(zy - lz));
-  pst(p.world, x, y, f4(P.x, P.y, P.z, 1.0f));
-  pst(p.normal_depth, x, y, f4(N.x, N.y, N.z, lz));
-  pst(p.motion, x, y, f4(nowx - prex, nowy - prey, 0.0f, 1.0f));
-  pst(p.fwidth, x, y, f4(length(fwN), fwz, lz, 1.0f));
-  if (p.fwidth_aux)  // .y, sign bit = (linearZ == 1.0): the a-trous background test (svgf_Atrous.frag:77)
-    p.fwidth_aux[(size_t)prow(p.fwidth, y) * p.W + x] =
-        __uint_as_float(__float_as_uint(fwz) | (lz == 1.0f ? 0x80000000u : 0u));
+  const int ntx = rast_ntx(p);
+  for (int ty = tb.ty0; ty <= tb.ty1; ++ty)
+    for (int tx = tb.tx0; tx <= tb.tx1; ++tx) atomicAdd(&p.tile_count[ty * ntx + tx], 1);
+}
+
+// large triangles: one block strides over each one's tiles. SCATTER 0 counts, 1 writes the list entries.
+template <int SCATTER>
+__global__ void __launch_bounds__(256) rast_large(GBufParams p) {
+  if (SCATTER && p.raster_ctr[2]) return;
+  const int nlarge = min(p.raster_ctr[0], p.big_cap);
+  const int ntx = rast_ntx(p);
+  for (int q = blockIdx.x; q < nlarge; q += gridDim.x) {
+    const int i = p.big[q];
+    const TileBox tb = tile_box(p, p.tri_box[i]);
+    const int w = tb.tx1 - tb.tx0 + 1, n = tb.area();
+    for (int k = threadIdx.x; k < n; k += 256) {
+      const int tile = (tb.ty0 + k / w) * ntx + tb.tx0 + k % w;
+      if (SCATTER) p.pairs[p.tile_off[tile] + atomicSub(&p.tile_count[tile], 1) - 1] = i;
+      else atomicAdd(&p.tile_count[tile], 1);
+    }
+  }
+}
+
+// one block: exclusive scan of the per-tile counts (tile_off[ntiles] = pairs); overflow if they exceed the list
+__global__ void __launch_bounds__(1024) rast_scan(GBufParams p, int ntiles) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int per = (ntiles + 1023) / 1024;
+  const int b = t * per, e = min(b + per, ntiles);
+  int sum = 0;
+  for (int i = b; i < e; ++i) sum += p.tile_count[i];
+  part[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan of the per-thread sums
+    const int v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - sum;
+  for (int i = b; i < e; ++i) {
+    p.tile_off[i] = run;
+    run += p.tile_count[i];
+  }
+  if (t == 1023) {
+    p.tile_off[ntiles] = part[1023];
+    p.raster_ctr[1] = part[1023];
+    if (part[1023] > p.pair_cap) atomicOr(&p.raster_ctr[2], 1);
+  }
+}
+
+// per small triangle: its index into each covered tile's list (slot order within a tile is arbitrary)
+__global__ void __launch_bounds__(256) rast_scatter(GBufParams p) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= p.ntris || p.raster_ctr[2]) return;
+  const int4 box = p.tri_box[i];
+  if (box.x > box.z || box.y > box.w) return;
+  const TileBox tb = tile_box(p, box);
+  if (tb.area() > kLargeTiles) return;
+  const int ntx = rast_ntx(p);
+  for (int ty = tb.ty0; ty <= tb.ty1; ++ty)
+    for (int tx = tb.tx0; tx <= tb.tx1; ++tx) {
+      const int tile = ty * ntx + tx;
+      p.pairs[p.tile_off[tile] + atomicSub(&p.tile_count[tile], 1) - 1] = i;
+    }
+}
+
+// one block per tile: the tile's list staged through LDS, every pixel's Moller tests, gb_finish
+__global__ void __launch_bounds__(kBlock) gbuffer_raster_kernel(GBufParams p) {
+  __shared__ float4 sg[kRChunk * 3];
+  __shared__ int4 sbox[kRChunk];
+  __shared__ int sidx[kRChunk];
+  if (p.raster_ctr[2]) return;  // overflow: gbuffer_kernel (the ray cast) writes the frame
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+  const int x = blockIdx.x * 16 + (wv & 1) * 8 + (ln & 7);
+  const int y = p.y0 + blockIdx.y * 16 + (wv >> 1) * 8 + (ln >> 3);
+  const bool valid = x < p.W && y < p.y1;
+  const v3 o = mk(p.eye[0], p.eye[1], p.eye[2]);
+  const v3 d = gb_dir(p, x, y);
+  float best = 3.0e38f, bu = 0.0f, bv = 0.0f;
+  int besti = -1, bests = -1;
+  const int off = p.tile_off[tile], total = p.tile_off[tile + 1] - off;
+  for (int base = 0; base < total; base += kRChunk) {
+    __syncthreads();
+    const int j = base + (int)threadIdx.x;
+    if (j < total) {
+      const int tri = p.pairs[off + j];
+      const float4* g = p.geom + 4 * tri;
+      sg[3 * threadIdx.x] = g[0];
+      sg[3 * threadIdx.x + 1] = g[1];
+      sg[3 * threadIdx.x + 2] = g[2];
+      sbox[threadIdx.x] = p.tri_box[tri];
+      sidx[threadIdx.x] = tri;
+    }
+    __syncthreads();
+    const int n = min(kRChunk, total - base);
+    if (!valid) continue;
+    for (int k = 0; k < n; ++k) {
+      const int4 b = sbox[k];
+      if (x < b.x || x > b.z || y < b.y || y > b.w) continue;  // outside the triangle's widened screen box
+      const float4 a = sg[3 * k];
+      const MTr h = moller(xyz(a), xyz(sg[3 * k + 1]), xyz(sg[3 * k + 2]), o, d, true);
+      if (!h.ok) continue;
+      const int oi = __float_as_int(a.w);
+      if (h.t < best || (h.t == best && oi < besti)) {
+        best = h.t;
+        besti = oi;
+        bests = sidx[k];
+        bu = h.u;
+        bv = h.v;
+      }
+    }
+  }
+  gb_finish(p, x, y, valid, ln, o, d, best, bests, bu, bv);
+}
+
+int launch_gbuffer_raster(const GBufParams& p, hipStream_t s) {
+  if (p.y1 <= p.y0) return 0;
+  const int ntx = (p.W + kRTile - 1) / kRTile, nty = (p.y1 - p.y0 + kRTile - 1) / kRTile;
+  if (p.ntris > 0) {
+    const int nb = (p.ntris + 255) / 256;
+    hipLaunchKernelGGL(rast_setup, dim3(nb), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(rast_large<0>, dim3(kLargeBlocks), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(rast_scan, dim3(1), dim3(1024), 0, s, p, ntx * nty);
+    hipLaunchKernelGGL(rast_scatter, dim3(nb), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(rast_large<1>, dim3(kLargeBlocks), dim3(256), 0, s, p);
+  } else {
+    hipLaunchKernelGGL(rast_scan, dim3(1), dim3(1024), 0, s, p, ntx * nty);  // zero lists
+  }
+  hipLaunchKernelGGL(gbuffer_raster_kernel, dim3(ntx, nty), dim3(kBlock), 0, s, p);
+  // the ray cast runs only if a list overflowed (it reads the flag and returns otherwise)
+  return launch_gbuffer(p, s);
 }
 
 int launch_pathtrace(const PTParams& p, hipStream_t s) {

@@ -175,6 +175,17 @@ struct GBufParams {
   float PV[16];         // pre_viewproj
   TileSched tiles;      // 16 x 16 px tiles
   uint32_t* motion_max; // optional: max |motion.y| (float bits) over the launch's surface pixels, zeroed by the host
+  // tile-binned rasterisation (gbuffer_mode 1, launch_gbuffer_raster): per-pass device scratch
+  int ntris;
+  int4* tri_box;        // per triangle: pixel box (x0, y0, x1, y1) of the pixels its Moller test can accept; empty
+                        // (x0 > x1) when culled; the G-buffer rows [y0, y1) only
+  int* tile_count;      // per 16 x 16 tile of the band: triangles binned to it (consumed by the scatter)
+  int* tile_off;        // ntiles + 1: exclusive scan of tile_count
+  int* pairs;           // triangle indices grouped by tile
+  int pair_cap;
+  int* big;             // triangles whose box covers more than kLargeTiles tiles (binned by whole blocks)
+  int big_cap;
+  int* raster_ctr;      // [0] large triangles, [1] binned pairs, [2] overflow (the ray-cast kernel then runs instead)
 };
 
 struct ReprojParams {
@@ -224,6 +235,7 @@ int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux
 int wf_list_capacity(int W, int rows);  // per-segment capacity of the compacted ray lists (8 segments)
 int wf_subset_tiles(int W, int rows, int stride, int offset);  // tiles of a PTParams tile subset (< 0: invalid)
 int launch_gbuffer(const GBufParams& p, hipStream_t s);
+int launch_gbuffer_raster(const GBufParams& p, hipStream_t s);  // bins, resolves, and the ray cast on overflow
 int launch_reproject(const ReprojParams& p, hipStream_t s);
 int launch_variance(const VarianceParams& p, hipStream_t s);
 int launch_atrous_exact(const AtrousParams& p, hipStream_t s);

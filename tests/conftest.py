@@ -55,3 +55,11 @@ def scene_cornell():
     from ptsvgf.scene import build_scene
 
     return build_scene("cornell_teapot", hdr_size=(128, 64))
+
+
+@pytest.fixture(scope="session")
+def scene_bench():
+    """The bench scene at full size (150 leaves, 2048x1024 HDR)."""
+    from ptsvgf.scene import build_scene
+
+    return build_scene("table_clock_plant")

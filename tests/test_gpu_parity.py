@@ -379,13 +379,6 @@ def test_taa_and_output_match_oracle(gpu, scene_small, mode):
             _cmp(f"{mode}/f{f}/{key}", got[key], want[key], rel=True)
 
 
-@pytest.fixture(scope="module")
-def scene_bench():
-    from ptsvgf.scene import build_scene
-
-    return build_scene("table_clock_plant")
-
-
 def test_full_size_4k_properties(gpu, scene_bench):
     """At the bench size (3840x2160, the bench scene) the oracle is too slow, so size-independent properties:
     the wavefront path tracer (compacted ray lists at their largest, cost-ordered tiles, shadow trees) gives
