@@ -79,8 +79,9 @@ struct RasterScene {
 // Scratch of the tile-binned G-buffer (launch_gbuffer_raster), per rasterize pass, sized by its triangles and band.
 struct RasterBins {
   void* base = nullptr;
-  int ntris = 0, ntiles = 0, pair_cap = 0, big_cap = 0, cap_uniform = 0;
+  int ntris = 0, ntiles = 0, pair_cap = 0, big_cap = 0;
   int4* tri_box = nullptr;
+  float* tri_tmin = nullptr;
   int *tile_count = nullptr, *tile_off = nullptr, *pairs = nullptr, *big = nullptr, *ctr = nullptr;
 };
 
@@ -983,19 +984,20 @@ int draw_pathtrace(Pass* p) {
 int raster_bins(Pass* p, int ntiles, GBufParams* k) {
   RasterBins& b = p->bins;
   const int ntris = p->raster.ntris;
-  if (!b.base || b.ntris != ntris || b.ntiles != ntiles || b.cap_uniform != ui(p, "raster_pair_cap", 0)) {
+  if (!b.base || b.ntris != ntris || b.ntiles != ntiles) {
     if (b.base) (void)hipFree(b.base);
     b = RasterBins{};
     int pair_cap = (int)std::min<long long>(std::max<long long>(256LL * ntris, 1 << 22), 1 << 28);
     int big_cap = std::max(ntris, 1);
-    if (int cap = ui(p, "raster_pair_cap", 0); cap > 0) pair_cap = std::min(pair_cap, cap);  // tests: force overflow
     auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t o_box = 0, o_cnt = o_box + up((size_t)std::max(ntris, 1) * 16), o_off = o_cnt + up((size_t)ntiles * 4),
+    const size_t o_box = 0, o_tmin = o_box + up((size_t)std::max(ntris, 1) * 16),
+                 o_cnt = o_tmin + up((size_t)std::max(ntris, 1) * 4), o_off = o_cnt + up((size_t)ntiles * 4),
                  o_pairs = o_off + up(((size_t)ntiles + 1) * 4), o_big = o_pairs + up((size_t)pair_cap * 4),
                  o_ctr = o_big + up((size_t)big_cap * 4), total = o_ctr + 256;
     HIPCHK(hipMalloc(&b.base, total));
     char* c = (char*)b.base;
     b.tri_box = (int4*)(c + o_box);
+    b.tri_tmin = (float*)(c + o_tmin);
     b.tile_count = (int*)(c + o_cnt);
     b.tile_off = (int*)(c + o_off);
     b.pairs = (int*)(c + o_pairs);
@@ -1005,16 +1007,19 @@ int raster_bins(Pass* p, int ntiles, GBufParams* k) {
     b.ntiles = ntiles;
     b.pair_cap = pair_cap;
     b.big_cap = big_cap;
-    b.cap_uniform = ui(p, "raster_pair_cap", 0);
+    // zero once: every later launch leaves the counts at zero (the scatter decrements each one it counted; an
+    // overflowed launch's fallback clears them)
+    HIPCHK(hipMemsetAsync(b.tile_count, 0, (size_t)ntiles * 4, g.stream));
   }
-  HIPCHK(hipMemsetAsync(b.tile_count, 0, (size_t)ntiles * 4, g.stream));
   HIPCHK(hipMemsetAsync(b.ctr, 0, 16, g.stream));
   k->ntris = ntris;
   k->tri_box = b.tri_box;
+  k->tri_tmin = b.tri_tmin;
   k->tile_count = b.tile_count;
   k->tile_off = b.tile_off;
   k->pairs = b.pairs;
   k->pair_cap = b.pair_cap;
+  if (int cap = ui(p, "raster_pair_cap", 0); cap > 0) k->pair_cap = std::min(b.pair_cap, cap);  // tests: overflow
   k->big = b.big;
   k->big_cap = b.big_cap;
   k->raster_ctr = b.ctr;

@@ -265,7 +265,12 @@ __device__ __forceinline__ void gb_finish(const GBufParams& p, int x, int y, boo
 template <int KS>
 __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
   __shared__ int stk[KS * kBlock];
-  if (p.raster_ctr && p.raster_ctr[2] == 0) return;  // launched as the rasteriser's overflow fallback: not needed
+  if (p.raster_ctr) {  // launched as the rasteriser's overflow fallback
+    if (p.raster_ctr[2] == 0) return;  // not needed
+    // the overflowed frame skipped the scatter, which returns every tile count to zero: clear them here
+    const int b = blockIdx.y * gridDim.x + blockIdx.x;
+    if (threadIdx.x == 0) p.tile_count[b] = 0;
+  }
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   const int tile = sched_tile(p.tiles, blockIdx.y * gridDim.x + blockIdx.x);  // cost-ordered dispatch
   const int tx = tile % gridDim.x, ty = tile / gridDim.x;
@@ -354,7 +359,7 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
 // to far below a pixel). A clipped vertex on the camera plane (the triangle passes through the eye) makes the
 // box the whole band. No walk means no tail: a tile costs about as much as it holds triangles.
 constexpr int kRTile = 16;
-constexpr int kLargeTiles = 64;  // triangles covering more tiles are binned by a whole block (rast_*_large)
+constexpr int kLargeTiles = 8;   // triangles covering more tiles are binned by a whole block (rast_large)
 constexpr int kRChunk = 256;     // triangles staged in LDS per round of the resolve
 constexpr int kBoxMargin = 2;    // pixels
 constexpr int kLargeBlocks = 512;
@@ -394,6 +399,7 @@ __global__ void __launch_bounds__(256) rast_setup(GBufParams p) {
   const v3 o = mk(p.eye[0], p.eye[1], p.eye[2]);
   const v3 p1 = xyz(a);
   int4 box = make_int4(1, 1, 0, 0);  // empty
+  float tmin = 0.0f;                 // lower bound of the ray parameter of any hit (0: none known)
   if (dot(xyz(ng), sub(p1, o)) < 0.0f) {  // front-facing: gbuffer_kernel's back-face cull
     const v3 v[3] = {p1, add(p1, xyz(e1)), add(p1, xyz(e2))};
     float3 A[8], B[8];
@@ -408,10 +414,11 @@ __global__ void __launch_bounds__(256) rast_setup(GBufParams p) {
     n = clip_plane(A, n, B, 1, 1.0f);
     n = clip_plane(B, n, A, 1, -1.0f);
     if (n > 0) {
-      float x0 = 3.0e38f, y0 = 3.0e38f, x1 = -3.0e38f, y1 = -3.0e38f;
+      float x0 = 3.0e38f, y0 = 3.0e38f, x1 = -3.0e38f, y1 = -3.0e38f, wmin = 3.0e38f;
       bool full = false;
       for (int k = 0; k < n; ++k) {
         if (!(A[k].z > 0.0f)) { full = true; break; }
+        wmin = fminf(wmin, A[k].z);
         // pixel coordinate whose centre ray has this NDC: ndc = (2 x + 1) / W - 1
         const float px = ((A[k].x / A[k].z + 1.0f) * (float)p.W - 1.0f) * 0.5f;
         const float py = ((A[k].y / A[k].z + 1.0f) * (float)p.H - 1.0f) * 0.5f;
@@ -426,10 +433,14 @@ __global__ void __launch_bounds__(256) rast_setup(GBufParams p) {
         const int bx0 = (int)floorf(fmaxf(x0, -lim)) - kBoxMargin, bx1 = (int)ceilf(fminf(x1, lim)) + kBoxMargin;
         const int by0 = (int)floorf(fmaxf(y0, -lim)) - kBoxMargin, by1 = (int)ceilf(fminf(y1, lim)) + kBoxMargin;
         box = make_int4(max(bx0, 0), max(by0, p.y0), min(bx1, p.W - 1), min(by1, p.y1 - 1));
+        // the pixel rays' direction has camera-space z = -1, so a hit's t is its clip w, and w is linear over the
+        // (clipped) triangle: no hit lies nearer than the smallest vertex w (margin for the rounding of both)
+        tmin = wmin * 0.9999f;
       }
     }
   }
   p.tri_box[i] = box;
+  p.tri_tmin[i] = tmin;
   if (box.x > box.z || box.y > box.w) return;
   const TileBox tb = tile_box(p, box);
   if (tb.area() > kLargeTiles) {
@@ -461,31 +472,46 @@ __global__ void __launch_bounds__(256) rast_large(GBufParams p) {
   }
 }
 
-// one block: exclusive scan of the per-tile counts (tile_off[ntiles] = pairs); overflow if they exceed the list
+// one block: exclusive scan of the per-tile counts (tile_off[ntiles] = pairs); overflow if they exceed the list.
+// 4096 counts per round: 4 consecutive per thread (one 16-B load), wave prefix sums by shuffles, 16 wave totals
+// through LDS, a carry between rounds.
 __global__ void __launch_bounds__(1024) rast_scan(GBufParams p, int ntiles) {
-  __shared__ int part[1024];
-  const int t = threadIdx.x;
-  const int per = (ntiles + 1023) / 1024;
-  const int b = t * per, e = min(b + per, ntiles);
-  int sum = 0;
-  for (int i = b; i < e; ++i) sum += p.tile_count[i];
-  part[t] = sum;
+  __shared__ int wsum[16];
+  __shared__ int carry_s;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t == 0) carry_s = 0;
   __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan of the per-thread sums
-    const int v = t >= off ? part[t - off] : 0;
+  for (int base = 0; base < ntiles; base += 4096) {
+    const int i0 = base + 4 * t;
+    int c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[k] = i0 + k < ntiles ? p.tile_count[i0 + k] : 0;
+    const int mine = c[0] + c[1] + c[2] + c[3];
+    int inc = mine;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o);
+      if (lane >= o) inc += v;
+    }
+    if (lane == 63) wsum[wv] = inc;
     __syncthreads();
-    part[t] += v;
+    int before = carry_s;
+    for (int w = 0; w < wv; ++w) before += wsum[w];
+    int run = before + inc - mine;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (i0 + k < ntiles) p.tile_off[i0 + k] = run;
+      run += c[k];
+    }
+    __syncthreads();
+    if (t == 1023) carry_s = run;  // the last thread's running sum is the round's total plus the carry
     __syncthreads();
   }
-  int run = part[t] - sum;
-  for (int i = b; i < e; ++i) {
-    p.tile_off[i] = run;
-    run += p.tile_count[i];
-  }
-  if (t == 1023) {
-    p.tile_off[ntiles] = part[1023];
-    p.raster_ctr[1] = part[1023];
-    if (part[1023] > p.pair_cap) atomicOr(&p.raster_ctr[2], 1);
+  if (t == 0) {
+    const int total = carry_s;
+    p.tile_off[ntiles] = total;
+    p.raster_ctr[1] = total;
+    if (total > p.pair_cap) atomicOr(&p.raster_ctr[2], 1);
   }
 }
 
@@ -510,6 +536,7 @@ __global__ void __launch_bounds__(kBlock) gbuffer_raster_kernel(GBufParams p) {
   __shared__ float4 sg[kRChunk * 3];
   __shared__ int4 sbox[kRChunk];
   __shared__ int sidx[kRChunk];
+  __shared__ float stmin[kRChunk];
   if (p.raster_ctr[2]) return;  // overflow: gbuffer_kernel (the ray cast) writes the frame
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   const int tile = blockIdx.y * gridDim.x + blockIdx.x;
@@ -532,6 +559,7 @@ __global__ void __launch_bounds__(kBlock) gbuffer_raster_kernel(GBufParams p) {
       sg[3 * threadIdx.x + 2] = g[2];
       sbox[threadIdx.x] = p.tri_box[tri];
       sidx[threadIdx.x] = tri;
+      stmin[threadIdx.x] = p.tri_tmin[tri];
     }
     __syncthreads();
     const int n = min(kRChunk, total - base);
@@ -539,6 +567,7 @@ __global__ void __launch_bounds__(kBlock) gbuffer_raster_kernel(GBufParams p) {
     for (int k = 0; k < n; ++k) {
       const int4 b = sbox[k];
       if (x < b.x || x > b.z || y < b.y || y > b.w) continue;  // outside the triangle's widened screen box
+      if (stmin[k] > best) continue;                             // wholly behind this pixel's closest hit so far
       const float4 a = sg[3 * k];
       const MTr h = moller(xyz(a), xyz(sg[3 * k + 1]), xyz(sg[3 * k + 2]), o, d, true);
       if (!h.ok) continue;

@@ -179,7 +179,8 @@ struct GBufParams {
   int ntris;
   int4* tri_box;        // per triangle: pixel box (x0, y0, x1, y1) of the pixels its Moller test can accept; empty
                         // (x0 > x1) when culled; the G-buffer rows [y0, y1) only
-  int* tile_count;      // per 16 x 16 tile of the band: triangles binned to it (consumed by the scatter)
+  float* tri_tmin;      // per triangle: no Moller hit of a pixel ray has a smaller t (0 when unknown)
+  int* tile_count;      // per 16 x 16 tile of the band: triangles binned to it; the scatter counts it back to 0
   int* tile_off;        // ntiles + 1: exclusive scan of tile_count
   int* pairs;           // triangle indices grouped by tile
   int pair_cap;

@@ -12,19 +12,19 @@ GBUF = ("world", "normal_depth", "velocity", "fwidth")
 MOVES = [None, (1.0, 0.75), (-1.5, -1.0), (20.0, 10.0)]
 
 
-def _render(gl, scene, W, H, mode, moves, cap=0, rows=None, keys=GBUF + ("color", "atrous")):
+def _render(gl, scene, W, H, mode, moves, caps=None, rows=None, keys=GBUF + ("color", "atrous")):
     from ptsvgf.renderer import Renderer
 
     r = Renderer(scene, W, H, mode="fast", aspect_corrected=W != H, run_taa=False, run_output=False,
                  gbuffer_rows=rows)
     for p in r.init_pass:
         p.set_uniform_int("gbuffer_mode", mode)
-        if cap:
-            p.set_uniform_int("raster_pair_cap", cap)
     out = []
-    for mv in moves:
+    for f, mv in enumerate(moves):
         if mv:
             r.camera.orbit(*mv)
+        for p in r.init_pass:  # per frame: a pair-list cap (0: the allocation's) that may force an overflow
+            p.set_uniform_int("raster_pair_cap", caps[f] if caps else 0)
         r.frame()
         out.append({k: gl.readback(r.planes()[k]) for k in keys})
     r.close()
@@ -49,19 +49,20 @@ def test_raster_equals_ray_cast(gpu, scene_name, request):
 
 
 def test_raster_equals_ray_cast_bench_scene_1080p(gpu, scene_bench):
-    """The bench scene at configs[1] size: 30 k triangles (the plant's foliage binned densely, the floor and table in
-    the big list), a moving camera including a large orbit step."""
+    """The bench scene at configs[1] size: 30 k triangles (the plant's foliage binned densely, the table and floor
+    binned by whole blocks), a moving camera including a large orbit step."""
     W, H = 1920, 1080
     _same(_render(gpu, scene_bench, W, H, 1, MOVES), _render(gpu, scene_bench, W, H, 0, MOVES), "bench1080")
 
 
 def test_raster_band_rows_and_overflow_fallback(gpu, scene_small):
     """A band of G-buffer rows (the multi-GPU case: boxes clipped to the band, tiles counted from its first row),
-    and a pair list too small for the frame (the rasteriser flags the overflow and the ray cast writes the frame)."""
+    and a pair list too small for the frame on frames 1 and 2 (the rasteriser flags the overflow, the ray cast
+    writes the frame and clears the tile counts the skipped scatter left, so frame 3 bins from zero again)."""
     W, H = 160, 96
     rows = (21, 70)
     keys = GBUF
     want = _render(gpu, scene_small, W, H, 0, MOVES, rows=rows, keys=keys)
     _same(_render(gpu, scene_small, W, H, 1, MOVES, rows=rows, keys=keys), want, "band", rows)
-    _same(_render(gpu, scene_small, W, H, 1, MOVES, cap=8, keys=keys),
+    _same(_render(gpu, scene_small, W, H, 1, MOVES, caps=[0, 8, 8, 0], keys=keys),
           _render(gpu, scene_small, W, H, 0, MOVES, keys=keys), "overflow")
