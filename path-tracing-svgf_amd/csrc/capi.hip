@@ -177,6 +177,8 @@ struct SceneGPU {
   float4* bvh = nullptr;
   float4* bvh4 = nullptr;
   float4* bvh_any = nullptr;  // any-hit tree over the reference leaves (build_anyhit_tree)
+  float4* leaves = nullptr;   // the reference leaves: (box lo, leaf ref bits), (box hi, 0) (wf_primary_raster)
+  int nleaves = 0;
   int root_any = 0, need_any = 0;
   bool has4 = false;
   int root4 = 0;
@@ -634,7 +636,7 @@ int build_anyhit_tree(const float* node_enc, int nnodes, int ntris, std::vector<
 }
 
 void free_scene(SceneGPU& sg) {
-  float4** bufs[5] = {&sg.geom, &sg.shade, &sg.bvh, &sg.bvh4, &sg.bvh_any};
+  float4** bufs[6] = {&sg.geom, &sg.shade, &sg.bvh, &sg.bvh4, &sg.bvh_any, &sg.leaves};
   for (auto b : bufs) {
     if (*b) (void)hipFree(*b);
     *b = nullptr;
@@ -699,6 +701,22 @@ int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU*
       (void)hipFree(sg.bvh_any);
       sg.bvh_any = nullptr;
     }
+  }
+  {  // the reference leaves with their own boxes (the primary-ray tile rasteriser's items)
+    std::vector<float4> lv;
+    const float* ne = (const float*)nodes->host.data();
+    for (size_t i = 1; i < nnodes; ++i) {
+      const float* f = ne + i * 12;
+      const int n = (int)f[3], first = (int)f[4];
+      if (n <= 0) continue;  // pack_bvh above has checked the leaf ranges
+      const int ref = -(first * 16 + n) - 1;
+      float rf;
+      memcpy(&rf, &ref, 4);
+      lv.push_back(float4{f[6], f[7], f[8], rf});
+      lv.push_back(float4{f[9], f[10], f[11], 0.0f});
+    }
+    sg.nleaves = (int)(lv.size() / 2);
+    if ((rc = upload_vec(lv, &sg.leaves)) != PT_OK) return rc;
   }
   if ((rc = upload_vec(geom, &sg.geom)) != PT_OK) return rc;
   if ((rc = upload_vec(shade, &sg.shade)) != PT_OK) return rc;
@@ -860,6 +878,54 @@ int tile_order_finish(Pass* p, const TileSched& t) {
   return PT_OK;
 }
 
+// Scratch of a tile rasteriser (Bins, pt_device.h): allocated once per (items, band) size, its tile counts zeroed
+// then (every later launch leaves them at zero: the scatter decrements each one it counted, an overflowed launch's
+// fallback clears them); the counters are cleared per launch. `cap` > 0 lowers the pair list's capacity (tests).
+int bins_for(RasterBins& b, int n, int W, int y0, int y1, int cap, Bins* out) {
+  const int ntiles = ((W + kRTile - 1) / kRTile) * ((std::max(0, y1 - y0) + kRTile - 1) / kRTile);
+  if (!b.base || b.ntris != n || b.ntiles != ntiles) {
+    if (b.base) (void)hipFree(b.base);
+    b = RasterBins{};
+    const int pair_cap = (int)std::min<long long>(std::max<long long>(256LL * n, 1 << 22), 1 << 28);
+    const int large_cap = std::max(n, 1);
+    auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t o_box = 0, o_tmin = o_box + up((size_t)std::max(n, 1) * 16),
+                 o_cnt = o_tmin + up((size_t)std::max(n, 1) * 4), o_off = o_cnt + up((size_t)ntiles * 4),
+                 o_pairs = o_off + up(((size_t)ntiles + 1) * 4), o_big = o_pairs + up((size_t)pair_cap * 4),
+                 o_ctr = o_big + up((size_t)large_cap * 4), total = o_ctr + 256;
+    HIPCHK(hipMalloc(&b.base, total));
+    char* c = (char*)b.base;
+    b.tri_box = (int4*)(c + o_box);
+    b.tri_tmin = (float*)(c + o_tmin);
+    b.tile_count = (int*)(c + o_cnt);
+    b.tile_off = (int*)(c + o_off);
+    b.pairs = (int*)(c + o_pairs);
+    b.big = (int*)(c + o_big);
+    b.ctr = (int*)(c + o_ctr);
+    b.ntris = n;
+    b.ntiles = ntiles;
+    b.pair_cap = pair_cap;
+    b.big_cap = large_cap;
+    HIPCHK(hipMemsetAsync(b.tile_count, 0, (size_t)ntiles * 4, g.stream));
+  }
+  HIPCHK(hipMemsetAsync(b.ctr, 0, 16, g.stream));
+  Bins& k = *out;
+  k.n = n;
+  k.box = b.tri_box;
+  k.tmin = b.tri_tmin;
+  k.tile_count = b.tile_count;
+  k.tile_off = b.tile_off;
+  k.pairs = b.pairs;
+  k.pair_cap = cap > 0 ? std::min(b.pair_cap, cap) : b.pair_cap;
+  k.large = b.big;
+  k.large_cap = b.big_cap;
+  k.ctr = b.ctr;
+  k.W = W;
+  k.y0 = y0;
+  k.y1 = y1;
+  return PT_OK;
+}
+
 // ------------------------------------------------------------- draw calls ---
 int draw_pathtrace(Pass* p) {
   PTParams k;
@@ -891,6 +957,8 @@ int draw_pathtrace(Pass* p) {
   k.scene.bvh4 = (sg->has4 && ui(p, "shadow_bvh4", 0)) ? sg->bvh4 : nullptr;  // 1: 4-wide any-hit (A/B; slower here)
   k.scene.root4 = sg->root4;
   k.scene.ntris = sg->ntris;
+  k.scene.leaves = sg->leaves;
+  k.scene.nleaves = sg->nleaves;
   if (lt && lt->target == PT_TEXTURE_BUFFER) {
     k.scene.lights = (const float*)lt->dev;
     k.scene.nlights_buf = (int)(lt->bytes / (6 * sizeof(float)));
@@ -968,6 +1036,11 @@ int draw_pathtrace(Pass* p) {
     k.refill = std::min(100, std::max(0, ui(p, "trace_refill", 0)));
     const int ntiles = wf_subset_tiles(k.W, std::max(0, k.y1 - k.y0), k.tile_stride, k.tile_offset);  // wf_primary's grid
     TRY(tile_order_begin(p, ntiles, &k.tiles));
+    // primary rays by tile-binned rasterisation of the reference leaves (default; 0 = the per-pixel walk)
+    if (ui(p, "primary_raster", 1) && k.tile_stride == 1 && k.tile_offset == 0) {
+      TRY(bins_for(p->bins, sg->nleaves, k.W, k.y0, k.y1, ui(p, "raster_pair_cap", 0), &k.leaf_bins));
+      k.primary_raster = 1;
+    }
     if (ui(p, "trace_fork", 0) && !p->aux) {  // A/B switch (off: measured slower with frames in flight)
       HIPCHK(hipStreamCreateWithFlags(&p->aux, hipStreamNonBlocking));
       HIPCHK(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
@@ -978,52 +1051,6 @@ int draw_pathtrace(Pass* p) {
     if (!rc && k.tiles.cost) p->order.ordered = true;
   }
   return rc ? hip_err((hipError_t)rc, "pathtrace launch") : PT_OK;
-}
-
-// Allocates (once per size) and clears the rasteriser's scratch for this launch; fills k's binning fields.
-int raster_bins(Pass* p, int ntiles, GBufParams* k) {
-  RasterBins& b = p->bins;
-  const int ntris = p->raster.ntris;
-  if (!b.base || b.ntris != ntris || b.ntiles != ntiles) {
-    if (b.base) (void)hipFree(b.base);
-    b = RasterBins{};
-    int pair_cap = (int)std::min<long long>(std::max<long long>(256LL * ntris, 1 << 22), 1 << 28);
-    int big_cap = std::max(ntris, 1);
-    auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t o_box = 0, o_tmin = o_box + up((size_t)std::max(ntris, 1) * 16),
-                 o_cnt = o_tmin + up((size_t)std::max(ntris, 1) * 4), o_off = o_cnt + up((size_t)ntiles * 4),
-                 o_pairs = o_off + up(((size_t)ntiles + 1) * 4), o_big = o_pairs + up((size_t)pair_cap * 4),
-                 o_ctr = o_big + up((size_t)big_cap * 4), total = o_ctr + 256;
-    HIPCHK(hipMalloc(&b.base, total));
-    char* c = (char*)b.base;
-    b.tri_box = (int4*)(c + o_box);
-    b.tri_tmin = (float*)(c + o_tmin);
-    b.tile_count = (int*)(c + o_cnt);
-    b.tile_off = (int*)(c + o_off);
-    b.pairs = (int*)(c + o_pairs);
-    b.big = (int*)(c + o_big);
-    b.ctr = (int*)(c + o_ctr);
-    b.ntris = ntris;
-    b.ntiles = ntiles;
-    b.pair_cap = pair_cap;
-    b.big_cap = big_cap;
-    // zero once: every later launch leaves the counts at zero (the scatter decrements each one it counted; an
-    // overflowed launch's fallback clears them)
-    HIPCHK(hipMemsetAsync(b.tile_count, 0, (size_t)ntiles * 4, g.stream));
-  }
-  HIPCHK(hipMemsetAsync(b.ctr, 0, 16, g.stream));
-  k->ntris = ntris;
-  k->tri_box = b.tri_box;
-  k->tri_tmin = b.tri_tmin;
-  k->tile_count = b.tile_count;
-  k->tile_off = b.tile_off;
-  k->pairs = b.pairs;
-  k->pair_cap = b.pair_cap;
-  if (int cap = ui(p, "raster_pair_cap", 0); cap > 0) k->pair_cap = std::min(b.pair_cap, cap);  // tests: overflow
-  k->big = b.big;
-  k->big_cap = b.big_cap;
-  k->raster_ctr = b.ctr;
-  return PT_OK;
 }
 
 int draw_raster(Pass* p) {
@@ -1069,7 +1096,7 @@ int draw_raster(Pass* p) {
   }
   const int ntiles = ((k.W + 15) / 16) * ((std::max(0, k.y1 - k.y0) + 15) / 16);  // gbuffer_kernel's grid
   if (ui(p, "gbuffer_mode", 1) == 1) {  // tile-binned rasterisation (default); the ray cast on list overflow
-    TRY(raster_bins(p, ntiles, &k));
+    TRY(bins_for(p->bins, p->raster.ntris, k.W, k.y0, k.y1, ui(p, "raster_pair_cap", 0), &k.bins));
     int rc = launch_gbuffer_raster(k, g.stream);
     if (rc) return hip_err((hipError_t)rc, "gbuffer raster launch");
   } else {  // A/B: the ray cast with cost-ordered tiles

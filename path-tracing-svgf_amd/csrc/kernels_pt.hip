@@ -265,11 +265,11 @@ __device__ __forceinline__ void gb_finish(const GBufParams& p, int x, int y, boo
 template <int KS>
 __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
   __shared__ int stk[KS * kBlock];
-  if (p.raster_ctr) {  // launched as the rasteriser's overflow fallback
-    if (p.raster_ctr[2] == 0) return;  // not needed
+  if (p.bins.ctr) {  // launched as the rasteriser's overflow fallback
+    if (p.bins.ctr[2] == 0) return;  // not needed
     // the overflowed frame skipped the scatter, which returns every tile count to zero: clear them here
     const int b = blockIdx.y * gridDim.x + blockIdx.x;
-    if (threadIdx.x == 0) p.tile_count[b] = 0;
+    if (threadIdx.x == 0) p.bins.tile_count[b] = 0;
   }
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   const int tile = sched_tile(p.tiles, blockIdx.y * gridDim.x + blockIdx.x);  // cost-ordered dispatch
@@ -347,135 +347,33 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
   gb_finish(p, x, y, valid, ln, o, d, best, bests, bu, bv);
 }
 
-// ------------------------------------------------- G-buffer by tile binning ---
-// The same G-buffer (closest front-facing Moller hit of the pixel-centre ray, ties to the lower triangle index;
-// gb_finish for the texels) computed without a per-pixel BVH walk: every front-facing triangle is binned to the
-// 16 x 16 tiles its screen box covers, and each pixel runs the exact Moller test of gbuffer_kernel against the
-// triangles of its tile. The winner is the lexicographic minimum of (t, original index) over every triangle whose
-// Moller test accepts the ray — the ray cast's answer whatever the order, provided each such triangle reaches the
-// pixel's tile. The box: the triangle clipped in clip space to the view frustum's four side planes (widened by
-// 1 %; every pixel-centre ray with t > 0 lies inside, so the clipped-away part meets no such ray — and a triangle
-// with nothing left is dropped), projected, widened by kBoxMargin pixels (projection and ray arithmetic agree
-// to far below a pixel). A clipped vertex on the camera plane (the triangle passes through the eye) makes the
-// box the whole band. No walk means no tail: a tile costs about as much as it holds triangles.
-constexpr int kRTile = 16;
-constexpr int kLargeTiles = 8;   // triangles covering more tiles are binned by a whole block (rast_large)
-constexpr int kRChunk = 256;     // triangles staged in LDS per round of the resolve
-constexpr int kBoxMargin = 2;    // pixels
+// ------------------------------------------------------- tile binning ---
+// Generic stages of the tile rasterisers (Bins, pt_device.h); the item-specific setup kernel runs first.
+constexpr int kRChunk = 256;     // items staged in LDS per round of a resolve
 constexpr int kLargeBlocks = 512;
 
-__device__ __forceinline__ int rast_ntx(const GBufParams& p) { return (p.W + kRTile - 1) / kRTile; }
-
-struct TileBox {
-  int tx0, tx1, ty0, ty1;
-  __device__ int area() const { return (tx1 - tx0 + 1) * (ty1 - ty0 + 1); }
-};
-__device__ __forceinline__ TileBox tile_box(const GBufParams& p, int4 b) {
-  return TileBox{b.x / kRTile, b.z / kRTile, (b.y - p.y0) / kRTile, (b.w - p.y0) / kRTile};
-}
-
-// Sutherland-Hodgman against s * w + sgn * c[axis] >= 0 (homogeneous clip coordinates: x, y, w)
-__device__ __forceinline__ int clip_plane(const float3* in, int n, float3* out, int axis, float sgn) {
-  const float s = 1.01f;
-  int m = 0;
-  for (int i = 0; i < n; ++i) {
-    const float3 a = in[i], b = in[(i + 1) % n];
-    const float da = s * a.z + sgn * (axis == 0 ? a.x : a.y), db = s * b.z + sgn * (axis == 0 ? b.x : b.y);
-    if (da >= 0.0f) out[m++] = a;
-    if ((da >= 0.0f) != (db >= 0.0f)) {
-      const float t = da / (da - db);
-      out[m++] = make_float3(a.x + t * (b.x - a.x), a.y + t * (b.y - a.y), a.z + t * (b.z - a.z));
-    }
-  }
-  return m;
-}
-
-// per triangle: cull, screen box, per-tile counts (small triangles; large ones are queued for rast_large)
-__global__ void __launch_bounds__(256) rast_setup(GBufParams p) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= p.ntris) return;
-  const float4* g = p.geom + 4 * i;
-  const float4 a = g[0], e1 = g[1], e2 = g[2], ng = g[3];
-  const v3 o = mk(p.eye[0], p.eye[1], p.eye[2]);
-  const v3 p1 = xyz(a);
-  int4 box = make_int4(1, 1, 0, 0);  // empty
-  float tmin = 0.0f;                 // lower bound of the ray parameter of any hit (0: none known)
-  if (dot(xyz(ng), sub(p1, o)) < 0.0f) {  // front-facing: gbuffer_kernel's back-face cull
-    const v3 v[3] = {p1, add(p1, xyz(e1)), add(p1, xyz(e2))};
-    float3 A[8], B[8];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      float c[4];
-      mat_vec4(p.M, v[k], c);
-      A[k] = make_float3(c[0], c[1], c[3]);
-    }
-    int n = clip_plane(A, 3, B, 0, 1.0f);
-    n = clip_plane(B, n, A, 0, -1.0f);
-    n = clip_plane(A, n, B, 1, 1.0f);
-    n = clip_plane(B, n, A, 1, -1.0f);
-    if (n > 0) {
-      float x0 = 3.0e38f, y0 = 3.0e38f, x1 = -3.0e38f, y1 = -3.0e38f, wmin = 3.0e38f;
-      bool full = false;
-      for (int k = 0; k < n; ++k) {
-        if (!(A[k].z > 0.0f)) { full = true; break; }
-        wmin = fminf(wmin, A[k].z);
-        // pixel coordinate whose centre ray has this NDC: ndc = (2 x + 1) / W - 1
-        const float px = ((A[k].x / A[k].z + 1.0f) * (float)p.W - 1.0f) * 0.5f;
-        const float py = ((A[k].y / A[k].z + 1.0f) * (float)p.H - 1.0f) * 0.5f;
-        if (!(px == px && py == py)) { full = true; break; }
-        x0 = fminf(x0, px); x1 = fmaxf(x1, px);
-        y0 = fminf(y0, py); y1 = fmaxf(y1, py);
-      }
-      if (full) {
-        box = make_int4(0, p.y0, p.W - 1, p.y1 - 1);
-      } else {
-        const float lim = 1.0e8f;  // keeps the float -> int conversion in range
-        const int bx0 = (int)floorf(fmaxf(x0, -lim)) - kBoxMargin, bx1 = (int)ceilf(fminf(x1, lim)) + kBoxMargin;
-        const int by0 = (int)floorf(fmaxf(y0, -lim)) - kBoxMargin, by1 = (int)ceilf(fminf(y1, lim)) + kBoxMargin;
-        box = make_int4(max(bx0, 0), max(by0, p.y0), min(bx1, p.W - 1), min(by1, p.y1 - 1));
-        // the pixel rays' direction has camera-space z = -1, so a hit's t is its clip w, and w is linear over the
-        // (clipped) triangle: no hit lies nearer than the smallest vertex w (margin for the rounding of both)
-        tmin = wmin * 0.9999f;
-      }
-    }
-  }
-  p.tri_box[i] = box;
-  p.tri_tmin[i] = tmin;
-  if (box.x > box.z || box.y > box.w) return;
-  const TileBox tb = tile_box(p, box);
-  if (tb.area() > kLargeTiles) {
-    const int slot = atomicAdd(&p.raster_ctr[0], 1);
-    if (slot < p.big_cap) p.big[slot] = i;
-    else atomicOr(&p.raster_ctr[2], 1);
-    return;
-  }
-  const int ntx = rast_ntx(p);
-  for (int ty = tb.ty0; ty <= tb.ty1; ++ty)
-    for (int tx = tb.tx0; tx <= tb.tx1; ++tx) atomicAdd(&p.tile_count[ty * ntx + tx], 1);
-}
-
-// large triangles: one block strides over each one's tiles. SCATTER 0 counts, 1 writes the list entries.
+// large items: one block strides over each one's tiles. SCATTER 0 counts, 1 writes the list entries.
 template <int SCATTER>
-__global__ void __launch_bounds__(256) rast_large(GBufParams p) {
-  if (SCATTER && p.raster_ctr[2]) return;
-  const int nlarge = min(p.raster_ctr[0], p.big_cap);
-  const int ntx = rast_ntx(p);
+__global__ void __launch_bounds__(256) bins_large(Bins b) {
+  if (SCATTER && b.ctr[2]) return;
+  const int nlarge = min(b.ctr[0], b.large_cap);
+  const int ntx = (b.W + kRTile - 1) / kRTile;
   for (int q = blockIdx.x; q < nlarge; q += gridDim.x) {
-    const int i = p.big[q];
-    const TileBox tb = tile_box(p, p.tri_box[i]);
+    const int i = b.large[q];
+    const TileBox tb = tile_box(b, b.box[i]);
     const int w = tb.tx1 - tb.tx0 + 1, n = tb.area();
     for (int k = threadIdx.x; k < n; k += 256) {
       const int tile = (tb.ty0 + k / w) * ntx + tb.tx0 + k % w;
-      if (SCATTER) p.pairs[p.tile_off[tile] + atomicSub(&p.tile_count[tile], 1) - 1] = i;
-      else atomicAdd(&p.tile_count[tile], 1);
+      if (SCATTER) b.pairs[b.tile_off[tile] + atomicSub(&b.tile_count[tile], 1) - 1] = i;
+      else atomicAdd(&b.tile_count[tile], 1);
     }
   }
 }
 
 // one block: exclusive scan of the per-tile counts (tile_off[ntiles] = pairs); overflow if they exceed the list.
-// 4096 counts per round: 4 consecutive per thread (one 16-B load), wave prefix sums by shuffles, 16 wave totals
-// through LDS, a carry between rounds.
-__global__ void __launch_bounds__(1024) rast_scan(GBufParams p, int ntiles) {
+// 4096 counts per round: 4 consecutive per thread, wave prefix sums by shuffles, 16 wave totals through LDS, a
+// carry between rounds.
+__global__ void __launch_bounds__(1024) bins_scan(Bins bn, int ntiles) {
   __shared__ int wsum[16];
   __shared__ int carry_s;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -485,7 +383,7 @@ __global__ void __launch_bounds__(1024) rast_scan(GBufParams p, int ntiles) {
     const int i0 = base + 4 * t;
     int c[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) c[k] = i0 + k < ntiles ? p.tile_count[i0 + k] : 0;
+    for (int k = 0; k < 4; ++k) c[k] = i0 + k < ntiles ? bn.tile_count[i0 + k] : 0;
     const int mine = c[0] + c[1] + c[2] + c[3];
     int inc = mine;  // inclusive wave scan
 #pragma unroll
@@ -500,35 +398,84 @@ __global__ void __launch_bounds__(1024) rast_scan(GBufParams p, int ntiles) {
     int run = before + inc - mine;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if (i0 + k < ntiles) p.tile_off[i0 + k] = run;
+      if (i0 + k < ntiles) bn.tile_off[i0 + k] = run;
       run += c[k];
     }
     __syncthreads();
-    if (t == 1023) carry_s = run;  // the last thread's running sum is the round's total plus the carry
+    if (t == 1023) carry_s = run;  // the last thread's running sum: this round's total plus the carry
     __syncthreads();
   }
   if (t == 0) {
     const int total = carry_s;
-    p.tile_off[ntiles] = total;
-    p.raster_ctr[1] = total;
-    if (total > p.pair_cap) atomicOr(&p.raster_ctr[2], 1);
+    bn.tile_off[ntiles] = total;
+    bn.ctr[1] = total;
+    if (total > bn.pair_cap) atomicOr(&bn.ctr[2], 1);
   }
 }
 
-// per small triangle: its index into each covered tile's list (slot order within a tile is arbitrary)
-__global__ void __launch_bounds__(256) rast_scatter(GBufParams p) {
+// per small item: its index into each covered tile's list (slot order within a tile is arbitrary)
+__global__ void __launch_bounds__(256) bins_scatter(Bins b) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= p.ntris || p.raster_ctr[2]) return;
-  const int4 box = p.tri_box[i];
+  if (i >= b.n || b.ctr[2]) return;
+  const int4 box = b.box[i];
   if (box.x > box.z || box.y > box.w) return;
-  const TileBox tb = tile_box(p, box);
+  const TileBox tb = tile_box(b, box);
   if (tb.area() > kLargeTiles) return;
-  const int ntx = rast_ntx(p);
+  const int ntx = (b.W + kRTile - 1) / kRTile;
   for (int ty = tb.ty0; ty <= tb.ty1; ++ty)
     for (int tx = tb.tx0; tx <= tb.tx1; ++tx) {
       const int tile = ty * ntx + tx;
-      p.pairs[p.tile_off[tile] + atomicSub(&p.tile_count[tile], 1) - 1] = i;
+      b.pairs[b.tile_off[tile] + atomicSub(&b.tile_count[tile], 1) - 1] = i;
     }
+}
+
+int launch_bins(const Bins& b, hipStream_t s) {
+  const int ntiles = ((b.W + kRTile - 1) / kRTile) * ((b.y1 - b.y0 + kRTile - 1) / kRTile);
+  if (b.n > 0) hipLaunchKernelGGL(bins_large<0>, dim3(kLargeBlocks), dim3(256), 0, s, b);
+  hipLaunchKernelGGL(bins_scan, dim3(1), dim3(1024), 0, s, b, ntiles);
+  if (b.n > 0) {
+    hipLaunchKernelGGL(bins_scatter, dim3((b.n + 255) / 256), dim3(256), 0, s, b);
+    hipLaunchKernelGGL(bins_large<1>, dim3(kLargeBlocks), dim3(256), 0, s, b);
+  }
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------- G-buffer by tile binning ---
+// The same G-buffer (closest front-facing Moller hit of the pixel-centre ray, ties to the lower triangle index;
+// gb_finish for the texels) computed without a per-pixel BVH walk: every front-facing triangle is binned to the
+// 16 x 16 tiles its screen box covers, and each pixel runs the exact Moller test of gbuffer_kernel against the
+// triangles of its tile. The winner is the lexicographic minimum of (t, original index) over every triangle whose
+// Moller test accepts the ray — the ray cast's answer whatever the order, provided each such triangle reaches the
+// pixel's tile. The box: the triangle clipped in clip space to the view frustum's four side planes (widened by
+// 1 %; every pixel-centre ray with t > 0 lies inside, so the clipped-away part meets no such ray — and a triangle
+// with nothing left is dropped), projected, widened by kBoxMargin pixels (projection and ray arithmetic agree
+// to far below a pixel). A clipped vertex on the camera plane (the triangle passes through the eye) makes the
+// box the whole band. No walk means no tail: a tile costs about as much as it holds triangles.
+
+// per triangle: back-face cull, box, bound, binning counts
+__global__ void __launch_bounds__(256) rast_setup(GBufParams p) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= p.bins.n) return;
+  const float4* g = p.geom + 4 * i;
+  const float4 a = g[0], e1 = g[1], e2 = g[2], ng = g[3];
+  const v3 o = mk(p.eye[0], p.eye[1], p.eye[2]);
+  const v3 p1 = xyz(a);
+  int4 box = make_int4(1, 1, 0, 0);  // empty
+  float tmin = 0.0f;
+  if (dot(xyz(ng), sub(p1, o)) < 0.0f) {  // front-facing: gbuffer_kernel's back-face cull
+    const v3 v[3] = {p1, add(p1, xyz(e1)), add(p1, xyz(e2))};
+    float3 A[16];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      float c[4];
+      mat_vec4(p.M, v[k], c);
+      A[k] = make_float3(c[0], c[1], c[3]);
+    }
+    // the pixel rays' direction has camera-space z = -1, so a hit's t is its clip w, which is linear over the
+    // (clipped) triangle: no hit lies nearer than the smallest vertex w (margin for the rounding of both)
+    if (poly_box(p.bins, p.H, A, 3, 1.0f, 1.0f, &box, &tmin)) tmin *= 0.9999f;
+  }
+  bins_count_item(p.bins, i, box, tmin);
 }
 
 // one block per tile: the tile's list staged through LDS, every pixel's Moller tests, gb_finish
@@ -537,7 +484,8 @@ __global__ void __launch_bounds__(kBlock) gbuffer_raster_kernel(GBufParams p) {
   __shared__ int4 sbox[kRChunk];
   __shared__ int sidx[kRChunk];
   __shared__ float stmin[kRChunk];
-  if (p.raster_ctr[2]) return;  // overflow: gbuffer_kernel (the ray cast) writes the frame
+  const Bins& bn = p.bins;
+  if (bn.ctr[2]) return;  // overflow: gbuffer_kernel (the ray cast) writes the frame
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   const int tile = blockIdx.y * gridDim.x + blockIdx.x;
   const int x = blockIdx.x * 16 + (wv & 1) * 8 + (ln & 7);
@@ -547,19 +495,19 @@ __global__ void __launch_bounds__(kBlock) gbuffer_raster_kernel(GBufParams p) {
   const v3 d = gb_dir(p, x, y);
   float best = 3.0e38f, bu = 0.0f, bv = 0.0f;
   int besti = -1, bests = -1;
-  const int off = p.tile_off[tile], total = p.tile_off[tile + 1] - off;
+  const int off = bn.tile_off[tile], total = bn.tile_off[tile + 1] - off;
   for (int base = 0; base < total; base += kRChunk) {
     __syncthreads();
     const int j = base + (int)threadIdx.x;
     if (j < total) {
-      const int tri = p.pairs[off + j];
+      const int tri = bn.pairs[off + j];
       const float4* g = p.geom + 4 * tri;
       sg[3 * threadIdx.x] = g[0];
       sg[3 * threadIdx.x + 1] = g[1];
       sg[3 * threadIdx.x + 2] = g[2];
-      sbox[threadIdx.x] = p.tri_box[tri];
+      sbox[threadIdx.x] = bn.box[tri];
       sidx[threadIdx.x] = tri;
-      stmin[threadIdx.x] = p.tri_tmin[tri];
+      stmin[threadIdx.x] = bn.tmin[tri];
     }
     __syncthreads();
     const int n = min(kRChunk, total - base);
@@ -587,16 +535,9 @@ __global__ void __launch_bounds__(kBlock) gbuffer_raster_kernel(GBufParams p) {
 int launch_gbuffer_raster(const GBufParams& p, hipStream_t s) {
   if (p.y1 <= p.y0) return 0;
   const int ntx = (p.W + kRTile - 1) / kRTile, nty = (p.y1 - p.y0 + kRTile - 1) / kRTile;
-  if (p.ntris > 0) {
-    const int nb = (p.ntris + 255) / 256;
-    hipLaunchKernelGGL(rast_setup, dim3(nb), dim3(256), 0, s, p);
-    hipLaunchKernelGGL(rast_large<0>, dim3(kLargeBlocks), dim3(256), 0, s, p);
-    hipLaunchKernelGGL(rast_scan, dim3(1), dim3(1024), 0, s, p, ntx * nty);
-    hipLaunchKernelGGL(rast_scatter, dim3(nb), dim3(256), 0, s, p);
-    hipLaunchKernelGGL(rast_large<1>, dim3(kLargeBlocks), dim3(256), 0, s, p);
-  } else {
-    hipLaunchKernelGGL(rast_scan, dim3(1), dim3(1024), 0, s, p, ntx * nty);  // zero lists
-  }
+  if (p.bins.n > 0) hipLaunchKernelGGL(rast_setup, dim3((p.bins.n + 255) / 256), dim3(256), 0, s, p);
+  int rc = launch_bins(p.bins, s);
+  if (rc) return rc;
   hipLaunchKernelGGL(gbuffer_raster_kernel, dim3(ntx, nty), dim3(kBlock), 0, s, p);
   // the ray cast runs only if a list overflowed (it reads the flag and returns otherwise)
   return launch_gbuffer(p, s);

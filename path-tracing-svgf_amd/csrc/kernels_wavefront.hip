@@ -177,6 +177,8 @@ __device__ __forceinline__ v3 primary_dir(const PTParams& p, int x, int y) {
 }
 
 // ------------------------------------------------------------ primaries ---
+constexpr int kTieFix = -2;  // hit.x of a pixel wf_primary_raster leaves to the walk (two triangles share its t)
+
 // 16x16 screen tiles, each wave an 8x8 sub-tile: coherent camera rays.
 template <int KS, bool DEEP>
 __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
@@ -187,8 +189,18 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
   const int tx = gt % ntx, ty = gt / ntx;
   const int x = tx * 16 + (wv & 1) * 8 + (ln & 7);
   const int y = p.y0 + ty * 16 + (wv >> 1) * 8 + (ln >> 3);
-  const bool valid = x < p.W && y < p.y1;
+  bool valid = x < p.W && y < p.y1;
   const int pid = (y - p.y0) * p.W + x;
+  bool count_ray = true;
+  if (p.pr_fix) {  // after wf_primary_raster: walk only the pixels it flagged, or all of them after an overflow
+    if (p.pr_fix[2]) {
+      if (threadIdx.x == 0) p.leaf_bins.tile_count[gt] = 0;  // the skipped scatter did not count them back to zero
+    } else {
+      valid = valid && ldnt(&p.wf.hit[pid]).x == kTieFix;
+      if (!__any(valid)) return;
+      count_ray = false;  // counted by the rasteriser
+    }
+  }
   uint32_t steps = 0;
   bool rewalk = false, retry = false, spill = false;
 #ifdef PT_WAVE_TIMES
@@ -224,7 +236,7 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
     stnt(&p.wf.hit[pid], make_int2(tri, __float_as_int(t)));
     spill = st.spilled;
   }
-  stat_add(p, kStatPrimRays, valid ? 1u : 0u);
+  stat_add(p, kStatPrimRays, valid && count_ray ? 1u : 0u);
   stat_add(p, kStatPrimVisits, steps);
   stat_slots(p, kStatPrimSlots, steps);
   stat_add(p, kStatTieRewalks, rewalk ? 1u : 0u);
@@ -242,6 +254,139 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
   sched_cost(p.tiles, tile, steps);
   if (valid) add_row_cost(p, y - p.y0, pid, steps);
 #endif
+}
+
+// ------------------------------------------------ primaries by tile binning ---
+// The primary rays' closest hits without a per-pixel BVH walk. The candidates of hitBVH for a ray are the
+// triangles of the reference leaves whose own box the ray passes (hitAABB > 0: every reference ancestor box holds
+// that box, so the walk reaches it — closest_hit's argument, pt_shading.h), the closest hit is the minimum t over
+// them, and when one triangle alone attains it, that triangle. So each reference leaf is binned to the 16 x 16
+// tiles whose pixels' primary rays can pass its box, and each pixel runs, over its tile's leaves, the walk's own
+// leaf step: hitAABB on the leaf box with the walk's pruning bound, then hitTriangle on the leaf's triangles in
+// order, seeking (as wf_primary) only hits nearer than this frame's G-buffer surface. A pixel whose minimum t two
+// triangles share (the reference keeps the one its depth-first order meets first) or that finds nothing below the
+// G-buffer bound is flagged and walked by wf_primary, as is every pixel if a list overflows. Same bits as wf_primary.
+constexpr int kPChunk = 256;  // leaves staged in LDS per round
+
+// per reference leaf: the pixel box of the primary rays that can pass its box — each face clipped to the widened
+// frustum and projected; a box holding the eye covers the band — and the nearest t they can meet it at (t along
+// the normalised ray is at least the camera-space depth w of the point)
+__global__ void __launch_bounds__(256) pr_setup(PTParams p) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= p.scene.nleaves) return;
+  const float4 lo4 = p.scene.leaves[2 * i], hi4 = p.scene.leaves[2 * i + 1];
+  const float lo[3] = {lo4.x, lo4.y, lo4.z}, hi[3] = {hi4.x, hi4.y, hi4.z};
+  const float* m = p.camRot;  // primary_dir: right = m[0..2], up = m[4..6], back = m[8..10]
+  const float sx = p.aspect_corrected ? (float)p.W / (float)p.H : 1.0f;
+  int4 box = make_int4(0, p.y0, p.W - 1, p.y1 - 1);
+  float tmin = 0.0f;
+  bool inside = true;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const float e = p.eye[a], tol = 1.0e-4f * (fabsf(e) + 1.0f);
+    inside = inside && e >= lo[a] - tol && e <= hi[a] + tol;
+  }
+  if (!inside) {
+    float3 C[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float X = (k & 1 ? hi[0] : lo[0]) - p.eye[0], Y = (k & 2 ? hi[1] : lo[1]) - p.eye[1],
+                  Z = (k & 4 ? hi[2] : lo[2]) - p.eye[2];
+      const float cx = (m[0] * X + m[1] * Y) + m[2] * Z, cy = (m[4] * X + m[5] * Y) + m[6] * Z,
+                  cz = (m[8] * X + m[9] * Y) + m[10] * Z;
+      C[k] = make_float3(cx / sx, cy, -cz);
+    }
+    const int F[6][4] = {{0, 2, 6, 4}, {1, 3, 7, 5}, {0, 1, 5, 4}, {2, 3, 7, 6}, {0, 1, 3, 2}, {4, 5, 7, 6}};
+    int4 u = make_int4(1, 1, 0, 0);
+    float w = 3.0e38f;
+    bool any = false;
+    for (int f = 0; f < 6; ++f) {
+      float3 A[16];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) A[k] = C[F[f][k]];
+      int4 fb;
+      float ft;
+      if (!poly_box(p.leaf_bins, p.H, A, 4, 1.0f, 1.0f, &fb, &ft)) continue;
+      if (fb.x > fb.z || fb.y > fb.w) continue;
+      u = any ? make_int4(min(u.x, fb.x), min(u.y, fb.y), max(u.z, fb.z), max(u.w, fb.w)) : fb;
+      w = fminf(w, ft);
+      any = true;
+    }
+    box = any ? u : make_int4(1, 1, 0, 0);
+    tmin = any ? w * 0.9999f : 0.0f;
+  }
+  bins_count_item(p.leaf_bins, i, box, tmin);
+}
+
+__global__ void __launch_bounds__(256) wf_primary_raster(PTParams p) {
+  __shared__ float4 slo[kPChunk], shi[kPChunk];
+  __shared__ int4 sbox[kPChunk];
+  __shared__ float stmin[kPChunk];
+  const Bins& bn = p.leaf_bins;
+  if (bn.ctr[2]) return;  // overflow: wf_primary walks every pixel
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  const int tile = blockIdx.x, ntx = (p.W + 15) / 16;
+  const int x = (tile % ntx) * 16 + (wv & 1) * 8 + (ln & 7);
+  const int y = p.y0 + (tile / ntx) * 16 + (wv >> 1) * 8 + (ln >> 3);
+  const bool valid = x < p.W && y < p.y1;
+  const int pid = (y - p.y0) * p.W + x;
+  const v3 S = mk(p.eye[0], p.eye[1], p.eye[2]);
+  const v3 d = primary_dir(p, x, y);
+  const v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  // the G-buffer bound of wf_primary: only hits nearer than the rasterised surface (plus a margin) are sought; a
+  // pixel that finds none below it is flagged for the walk (which retries unbounded)
+  float bound = PT_INF;
+  if (valid && p.hint_pos.p && p.prune) {
+    const float4 nd = pld(p.hint_nd, x, y);
+    if (nd.w != 1.0f) {
+      const float dist = length(sub(xyz(pld(p.hint_pos, x, y)), S));
+      if (dist == dist) bound = dist * 1.001f + 1.0e-3f;
+    }
+  }
+  float tbest = bound;
+  int best = -1;
+  bool tied = false;
+  uint32_t steps = 0;
+  const int off = bn.tile_off[tile], total = bn.tile_off[tile + 1] - off;
+  for (int base = 0; base < total; base += kPChunk) {
+    __syncthreads();
+    const int j = base + (int)threadIdx.x;
+    if (j < total) {
+      const int leaf = bn.pairs[off + j];
+      slo[threadIdx.x] = p.scene.leaves[2 * leaf];
+      shi[threadIdx.x] = p.scene.leaves[2 * leaf + 1];
+      sbox[threadIdx.x] = bn.box[leaf];
+      stmin[threadIdx.x] = bn.tmin[leaf];
+    }
+    __syncthreads();
+    const int n = min(kPChunk, total - base);
+    if (!valid) continue;
+    for (int k = 0; k < n; ++k) {
+      const int4 b = sbox[k];
+      if (x < b.x || x > b.z || y < b.y || y > b.w) continue;  // no primary ray of this pixel passes the box
+      const float lim = tbest * 1.0002f + 2.0e-4f;                // the walk's pruning bound (traverse<0>)
+      if (stmin[k] > lim) continue;                               // entered beyond it
+      const float4 lo = slo[k], hi = shi[k];
+      float t0;
+      const float dl = slab(S, inv, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, &t0);
+      ++steps;
+      if (!(dl > 0.0f) || t0 > lim) continue;
+      const int ref = __float_as_int(lo.w), first = ref_leaf_first(ref), cnt = ref_leaf_count(ref);
+      steps += (uint32_t)cnt;
+      leaf_scan(p.scene.tri_geom, first, cnt, S, d, [&](int i, float t) {
+        if (t < tbest) { tbest = t; best = i; tied = false; }
+        else if (t == tbest && best >= 0) tied = true;
+        return false;
+      });
+    }
+  }
+  const bool walk = tied || (best < 0 && bound < PT_INF);  // a tie, or nothing below the G-buffer bound
+  if (valid) stnt(&p.wf.hit[pid], walk ? make_int2(kTieFix, 0) : make_int2(best, __float_as_int(tbest)));
+  stat_add(p, kStatPrimRays, valid ? 1u : 0u);
+  stat_add(p, kStatPrimVisits, steps);
+  stat_slots(p, kStatPrimSlots, steps);
+  sched_cost(p.tiles, tile, steps);
+  if (valid) add_row_cost(p, y - p.y0, pid, steps);
 }
 
 // ----------------------------------------------------------- bounce trace ---
@@ -899,7 +1044,17 @@ int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent
   if (e != hipSuccess) return (int)e;
   const int ntiles = wf_subset_tiles(p.W, rows, p.tile_stride, p.tile_offset);
   if (ntiles <= 0) return 0;
-  hipLaunchKernelGGL((wf_primary<KS, DEEP>), dim3(ntiles), dim3(256), 0, s, p);
+  if (p.primary_raster) {  // every tile of the band (the host enables it only without tile subsets)
+    if (p.scene.nleaves > 0) hipLaunchKernelGGL(pr_setup, dim3((p.scene.nleaves + 255) / 256), dim3(256), 0, s, p);
+    const int rc = launch_bins(p.leaf_bins, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(wf_primary_raster, dim3(ntiles), dim3(256), 0, s, p);
+    PTParams q = p;
+    q.pr_fix = p.leaf_bins.ctr;  // ties (and an overflow) walked
+    hipLaunchKernelGGL((wf_primary<KS, DEEP>), dim3(ntiles), dim3(256), 0, s, q);
+  } else {
+    hipLaunchKernelGGL((wf_primary<KS, DEEP>), dim3(ntiles), dim3(256), 0, s, p);
+  }
   if (p.tiles.cost) {  // this frame's primary costs -> tile order of the bounce-0 shade and the next frame
     const int rc = launch_tile_sort(p.tiles.cost, p.tiles.perm_next, p.tiles.ntiles, s);
     if (rc) return rc;

@@ -95,6 +95,10 @@ struct SceneDev {
   const uint32_t* texarr;
   int tex_w, tex_h, tex_layers;
   int use_normal_map;   // uniform use_normal_map (path_tracing.frag:338)
+  // the reference tree's leaves (2 x float4 each: (box lo, leaf ref bits), (box hi, -)): the primary-ray tile
+  // rasteriser's items (wf_primary_raster)
+  const float4* leaves;
+  int nleaves;
 };
 
 // Wavefront path-tracer state (kernels_wavefront.hip): SoA per band pixel.
@@ -128,6 +132,26 @@ enum { kStatPrimRays, kStatPrimVisits, kStatBounceRays, kStatBounceVisits, kStat
        kStatTieRewalks, kStatPrimRetries, kStatSpills, kStatPrimSlots, kStatBounceSlots, kStatShadowSlots,
        kStatCount };
 
+// Screen-tile binning of items (the G-buffer's triangles, the path tracer's BVH leaves) for the tile rasterisers:
+// an item-specific setup kernel writes each item's pixel box and counts it into the 16 x 16 tiles of the band it
+// covers (bins_count_item); launch_bins then bins the large items, scans and scatters (kernels_pt.hip).
+constexpr int kRTile = 16;
+constexpr int kLargeTiles = 8;   // items covering more tiles are binned by a whole block
+constexpr int kBoxMargin = 2;    // pixels added around a projected box (projection vs ray arithmetic)
+struct Bins {
+  int n;                // items
+  int4* box;            // per item: pixel box (x0, y0, x1, y1) of the pixels whose ray it can meet; empty: x0 > x1
+  float* tmin;          // per item: lower bound of the ray parameter of any hit (0 when unknown)
+  int* tile_count;      // per tile of the band: items binned to it; the scatter counts it back to zero
+  int* tile_off;        // ntiles + 1: exclusive scan of tile_count
+  int* pairs;           // item indices grouped by tile
+  int pair_cap;
+  int* large;           // items whose box covers more than kLargeTiles tiles (binned by whole blocks)
+  int large_cap;
+  int* ctr;             // [0] large items, [1] binned pairs, [2] overflow (the caller's fallback then runs)
+  int W, y0, y1;        // band: tiles counted from row y0
+};
+
 struct PTParams {
   int W, H, y0, y1;     // frame size (global) and rows to compute
   Plane color, emission, albedo, last;  // outputs (+ lastFrame input)
@@ -157,6 +181,12 @@ struct PTParams {
   // offset 0 = every tile. Interleaved subsets give every rank of a multi-GPU frame an equal share of the
   // expensive tiles (ptsvgf.dist, DESIGN.md "Multi-GPU").
   int tile_stride, tile_offset;
+  // primary rays by tile rasterisation of the reference leaves (wf_primary_raster; primary_raster uniform): the
+  // bins, and for the wf_primary launch that follows it the bins' counters (pr_fix non-null: that launch walks
+  // only the pixels the rasteriser flagged — exact-t ties — or every pixel after a list overflow)
+  Bins leaf_bins;
+  int primary_raster;
+  const int* pr_fix;
 };
 
 struct GBufParams {
@@ -175,18 +205,8 @@ struct GBufParams {
   float PV[16];         // pre_viewproj
   TileSched tiles;      // 16 x 16 px tiles
   uint32_t* motion_max; // optional: max |motion.y| (float bits) over the launch's surface pixels, zeroed by the host
-  // tile-binned rasterisation (gbuffer_mode 1, launch_gbuffer_raster): per-pass device scratch
-  int ntris;
-  int4* tri_box;        // per triangle: pixel box (x0, y0, x1, y1) of the pixels its Moller test can accept; empty
-                        // (x0 > x1) when culled; the G-buffer rows [y0, y1) only
-  float* tri_tmin;      // per triangle: no Moller hit of a pixel ray has a smaller t (0 when unknown)
-  int* tile_count;      // per 16 x 16 tile of the band: triangles binned to it; the scatter counts it back to 0
-  int* tile_off;        // ntiles + 1: exclusive scan of tile_count
-  int* pairs;           // triangle indices grouped by tile
-  int pair_cap;
-  int* big;             // triangles whose box covers more than kLargeTiles tiles (binned by whole blocks)
-  int big_cap;
-  int* raster_ctr;      // [0] large triangles, [1] binned pairs, [2] overflow (the ray-cast kernel then runs instead)
+  Bins bins;            // tile-binned rasterisation (gbuffer_mode 1): items = the raster triangles; bins.ctr null
+                        // when the ray cast runs alone
 };
 
 struct ReprojParams {
@@ -237,6 +257,7 @@ int wf_list_capacity(int W, int rows);  // per-segment capacity of the compacted
 int wf_subset_tiles(int W, int rows, int stride, int offset);  // tiles of a PTParams tile subset (< 0: invalid)
 int launch_gbuffer(const GBufParams& p, hipStream_t s);
 int launch_gbuffer_raster(const GBufParams& p, hipStream_t s);  // bins, resolves, and the ray cast on overflow
+int launch_bins(const Bins& b, hipStream_t s);  // after the item setup kernel: large items, scan, scatter
 int launch_reproject(const ReprojParams& p, hipStream_t s);
 int launch_variance(const VarianceParams& p, hipStream_t s);
 int launch_atrous_exact(const AtrousParams& p, hipStream_t s);
@@ -261,6 +282,88 @@ __device__ __forceinline__ SceneDev anyhit_scene(const SceneDev& s) {
   return r;
 }
 __device__ __forceinline__ int sched_tile(const TileSched& t, int slot) { return t.perm ? t.perm[slot] : slot; }
+
+struct TileBox {
+  int tx0, tx1, ty0, ty1;
+  __device__ int area() const { return (tx1 - tx0 + 1) * (ty1 - ty0 + 1); }
+};
+__device__ __forceinline__ TileBox tile_box(const Bins& b, int4 box) {
+  return TileBox{box.x / kRTile, box.z / kRTile, (box.y - b.y0) / kRTile, (box.w - b.y0) / kRTile};
+}
+// Pixel box of projected extents (pixel coordinates of the centre rays), widened by kBoxMargin, clipped to the band.
+__device__ __forceinline__ int4 pixel_box(const Bins& b, float x0, float y0, float x1, float y1) {
+  const float lim = 1.0e8f;  // keeps the float -> int conversion in range
+  const int bx0 = (int)floorf(fmaxf(x0, -lim)) - kBoxMargin, bx1 = (int)ceilf(fminf(x1, lim)) + kBoxMargin;
+  const int by0 = (int)floorf(fmaxf(y0, -lim)) - kBoxMargin, by1 = (int)ceilf(fminf(y1, lim)) + kBoxMargin;
+  return make_int4(max(bx0, 0), max(by0, b.y0), min(bx1, b.W - 1), min(by1, b.y1 - 1));
+}
+// Sutherland-Hodgman against s * w + sgn * c[axis] >= 0 (homogeneous coordinates: x, y, w)
+__device__ __forceinline__ int clip_plane(const float3* in, int n, float3* out, int axis, float sgn) {
+  const float s = 1.01f;
+  int m = 0;
+  for (int i = 0; i < n; ++i) {
+    const float3 a = in[i], b = in[(i + 1) % n];
+    const float da = s * a.z + sgn * (axis == 0 ? a.x : a.y), db = s * b.z + sgn * (axis == 0 ? b.x : b.y);
+    if (da >= 0.0f) out[m++] = a;
+    if ((da >= 0.0f) != (db >= 0.0f)) {
+      const float t = da / (da - db);
+      out[m++] = make_float3(a.x + t * (b.x - a.x), a.y + t * (b.y - a.y), a.z + t * (b.z - a.z));
+    }
+  }
+  return m;
+}
+
+// Screen box and nearest-t bound of a convex polygon given by n <= 8 vertices (x, y, w) in a frame whose centre
+// rays have NDC ((2x+1)/W - 1, (2y+1)/H - 1) scaled by (sx, sy): clipped to the widened frustum first.
+// Returns false when nothing of it lies in front of the camera inside the frustum.
+__device__ __forceinline__ bool poly_box(const Bins& b, int H, float3* A, int n, float sx, float sy, int4* box,
+                                         float* tmin) {
+  float3 B[16];
+  n = clip_plane(A, n, B, 0, 1.0f);
+  n = clip_plane(B, n, A, 0, -1.0f);
+  n = clip_plane(A, n, B, 1, 1.0f);
+  n = clip_plane(B, n, A, 1, -1.0f);
+  if (n <= 0) return false;
+  float x0 = 3.0e38f, y0 = 3.0e38f, x1 = -3.0e38f, y1 = -3.0e38f, wmin = 3.0e38f;
+  for (int k = 0; k < n; ++k) {
+    if (!(A[k].z > 0.0f)) {  // on the camera plane: the whole band, no bound
+      *box = make_int4(0, b.y0, b.W - 1, b.y1 - 1);
+      *tmin = 0.0f;
+      return true;
+    }
+    wmin = fminf(wmin, A[k].z);
+    // pixel coordinate whose centre ray has this NDC: ndc = (2 x + 1) / W - 1
+    const float px = ((A[k].x / (A[k].z * sx) + 1.0f) * (float)b.W - 1.0f) * 0.5f;
+    const float py = ((A[k].y / (A[k].z * sy) + 1.0f) * (float)H - 1.0f) * 0.5f;
+    if (!(px == px && py == py)) {
+      *box = make_int4(0, b.y0, b.W - 1, b.y1 - 1);
+      *tmin = 0.0f;
+      return true;
+    }
+    x0 = fminf(x0, px); x1 = fmaxf(x1, px);
+    y0 = fminf(y0, py); y1 = fmaxf(y1, py);
+  }
+  *box = pixel_box(b, x0, y0, x1, y1);
+  *tmin = wmin;
+  return true;
+}
+
+// Records item i's box and bound and counts it into its tiles (small items) or queues it (large ones).
+__device__ __forceinline__ void bins_count_item(const Bins& b, int i, int4 box, float tmin) {
+  b.box[i] = box;
+  b.tmin[i] = tmin;
+  if (box.x > box.z || box.y > box.w) return;
+  const TileBox tb = tile_box(b, box);
+  if (tb.area() > kLargeTiles) {
+    const int slot = atomicAdd(&b.ctr[0], 1);
+    if (slot < b.large_cap) b.large[slot] = i;
+    else atomicOr(&b.ctr[2], 1);
+    return;
+  }
+  const int ntx = (b.W + kRTile - 1) / kRTile;
+  for (int ty = tb.ty0; ty <= tb.ty1; ++ty)
+    for (int tx = tb.tx0; tx <= tb.tx1; ++tx) atomicAdd(&b.tile_count[ty * ntx + tx], 1);
+}
 // Call with every lane of the wave active (steps = 0 for lanes without a ray).
 __device__ __forceinline__ void sched_cost(const TileSched& t, int tile, uint32_t steps) {
   if (!t.cost) return;

@@ -66,3 +66,42 @@ def test_raster_band_rows_and_overflow_fallback(gpu, scene_small):
     _same(_render(gpu, scene_small, W, H, 1, MOVES, rows=rows, keys=keys), want, "band", rows)
     _same(_render(gpu, scene_small, W, H, 1, MOVES, caps=[0, 8, 8, 0], keys=keys),
           _render(gpu, scene_small, W, H, 0, MOVES, keys=keys), "overflow")
+
+
+def _pt(gl, scene, W, H, raster, moves, cap=0):
+    from ptsvgf.renderer import Renderer
+
+    r = Renderer(scene, W, H, mode="fast", aspect_corrected=W != H, run_taa=False, run_output=False)
+    r.pass_path_tracing.set_uniform_int("primary_raster", raster)
+    r.pass_path_tracing.set_uniform_int("raster_pair_cap", cap)
+    out = []
+    for mv in moves:
+        if mv:
+            r.camera.orbit(*mv)
+        r.frame()
+        out.append({k: gl.readback(r.planes()[k]) for k in ("color", "emission", "albedo")})
+    st = r.trace_stats()
+    r.close()
+    return out, st
+
+
+@pytest.mark.parametrize("scene_name", ["scene_small", "scene_cornell", "scene_nan"])
+def test_primary_raster_equals_walk(gpu, scene_name, request):
+    """Primary rays by tile-binned reference leaves (wf_primary_raster, the default) give the per-pixel walk's bits
+    (wf_primary), through camera moves; with a pair list too small for the frame every pixel is walked instead."""
+    scene = request.getfixturevalue(scene_name)
+    W, H = 160, 96
+    want, st0 = _pt(gpu, scene, W, H, 0, MOVES)
+    got, st1 = _pt(gpu, scene, W, H, 1, MOVES)
+    _same(got, want, scene_name)
+    assert st1["primary_rays"] == st0["primary_rays"] == W * H, (st0, st1)
+    over, _ = _pt(gpu, scene, W, H, 1, MOVES, cap=4)
+    _same(over, want, scene_name + "/overflow")
+
+
+def test_primary_raster_equals_walk_bench_scene_1080p(gpu, scene_bench):
+    W, H = 1920, 1080
+    want, _ = _pt(gpu, scene_bench, W, H, 0, MOVES)
+    got, st = _pt(gpu, scene_bench, W, H, 1, MOVES)
+    print(st)
+    _same(got, want, "bench1080")
