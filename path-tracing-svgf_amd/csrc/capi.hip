@@ -122,7 +122,7 @@ int wf_alloc(WFBuffers& b, int W, int rows) {
   auto up = [&](size_t v) { return (v + al - 1) / al * al; };
   size_t total = up(f4) * 10 + up(n * 8) + up(n * 4) + up(n) * 2 + up(nl * 4 * kLiveBins) * 2 +
                  up(nl * 4 * (1 + kPointBins)) +
-                 up(n * 8) + up(kWfCounters * 4);
+                 up(n * 8) + up(n * 4) + up(kWfCounters * 4);
   if (hipMalloc(&b.base, total) != hipSuccess) { b.base = nullptr; return PT_ERR_HIP; }
   char* c = (char*)b.base;
   float4** f4p[10] = {&b.st.ray_o, &b.st.ray_d, &b.st.light, &b.st.red, &b.st.pend0,
@@ -136,6 +136,7 @@ int wf_alloc(WFBuffers& b, int W, int rows) {
   b.st.list1 = (int*)c; c += up(nl * 4 * kLiveBins);
   b.st.shadow_list = (int*)c; c += up(nl * 4 * (1 + kPointBins));
   b.st.straggler = (int*)c; c += up(n * 8);  // both shadow kinds of one bounce
+  b.st.strag_c = (int*)c; c += up(n * 4);    // bounce rays of one bounce
   b.st.counters = (int*)c;
   b.n = n;
   return PT_OK;
@@ -1031,6 +1032,8 @@ int draw_pathtrace(Pass* p) {
     // > 0: shadow rays past this many visits finish in the wave-cooperative walk (A/B switch; off: with frames
     // in flight it measured slower)
     k.wf.shadow_budget = (uint32_t)ui(p, "shadow_budget", 0);
+    // > 0: bounce rays past this many visits finish in the wave-cooperative closest-hit walk (refill kernel only)
+    k.wf.closest_budget = (uint32_t)ui(p, "closest_budget", 0);
     // percent of the bounce / shadow lists traced by lane-refill waves: 75 pays with frames in flight (the renderer
     // sets it then), 0 (default) keeps the shortest single-frame latency
     k.refill = std::min(100, std::max(0, ui(p, "trace_refill", 0)));

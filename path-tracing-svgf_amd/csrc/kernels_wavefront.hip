@@ -585,10 +585,13 @@ __host__ __device__ constexpr int refill_blocks(int items_max) {
 // of their while-while walks, hand list items from the work queue to their idle lanes, so lanes stay busy until the
 // queue runs dry. Per ray the walk is anyhit2's (same boxes, same pruning bound, same triangle tests, visit order
 // per ray unchanged); any-hit verdicts do not depend on which lane or when.
+// With a visit budget (PTParams::wf.shadow_budget) a ray still undecided past it is handed to the wave-cooperative
+// walk (wf_shadow_coop) and its lane takes the next item, as in wf_trace_shadow.
 template <int KS, bool DEEP>
 __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTParams p, const int* __restrict__ list,
                                                                              const int* __restrict__ counts, int cap,
-                                                                             int* __restrict__ heads) {
+                                                                             int* __restrict__ heads,
+                                                                             int* __restrict__ strag_count) {
   __shared__ int stk[KS * kTB];
   const int lane = threadIdx.x & 63;
   const int nh = seg_total(counts);
@@ -604,13 +607,15 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
   int pid = 0, sp = 0, node = kNone, leaf = kNone;
   v3 S = splat(0.0f), d = splat(0.0f), inv = splat(0.0f);
   float lim = 0.0f, maxd = 0.0f;
-  uint32_t nvis = 0, nray = 0;
+  uint32_t nvis = 0, nray = 0, rvis = 0;
+  const uint32_t budget = p.wf.shadow_budget;
   while (true) {
     const unsigned long long idle = __ballot(!have);
     if (__popcll(idle) >= (__ballot(have) ? kRefillMin : 1) && (q.next < q.end || q.grab())) {
       // refill: the next items go to the idle lanes in lane order
       const int k = q.next + __popcll(idle & below);
       if (!have && k < q.end && shadow_item(list, counts, cap, nh, k, &pid, &point)) {
+        rvis = 0;
         const float4 o = ldnt(&p.wf.ray_o[pid]);
         const float4 dir = point ? ldnt(&p.wf.sh_p[pid]) : ldnt(&p.wf.sh_h[pid]);  // point: (direction, distance)
         S = xyz(o);
@@ -631,6 +636,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
     if (!__any(have)) break;
     while (node >= 0) {  // anyhit2's descent (only lanes holding a ray have node >= 0)
       ++nvis;
+      ++rvis;
       const float4* nd = sc.bvh + 4 * node;
       const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
       float t0l, t0r;
@@ -659,6 +665,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
     while (leaf != kNone) {  // anyhit2's leaf phase
       const int first = ref_leaf_first(leaf), cnt = ref_leaf_count(leaf);
       nvis += (uint32_t)cnt;
+      rvis += (uint32_t)cnt;
       if (leaf_scan(sc.tri_geom, first, cnt, S, d, [&](int, float t) {
             return t < PT_INF && (!point || length(sub(add(S, muls(d, t)), S)) < maxd);
           })) {
@@ -677,6 +684,19 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
       node = leaf = kNone;
       spill = spill || st.spilled;
     }
+    const bool defer = have && budget && rvis > budget;  // past the budget: the cooperative walk decides it
+    const unsigned long long m = __ballot(defer);
+    if (m) {
+      int base = 0;
+      if (lane == __ffsll((long long)m) - 1) base = atomicAdd(strag_count, __popcll(m));
+      base = __shfl(base, __ffsll((long long)m) - 1);
+      if (defer) {
+        p.wf.straggler[base + __popcll(m & below)] = pid | (point ? (int)0x80000000 : 0);
+        have = false;
+        node = leaf = kNone;
+        spill = spill || st.spilled;
+      }
+    }
   }
   stat_add(p, kStatShadowRays, nray);
   stat_add(p, kStatSpills, spill ? 1u : 0u);
@@ -688,10 +708,13 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
 // over the reference leaves (pruned), and for a ray whose best t was met exactly by a second triangle the walk again
 // on the reference tree in the reference's order (traverse<0>; the same lane restarts it before taking a new ray).
 // Production switches only (closest_tree = prune = 1); the host keeps wf_trace_closest otherwise.
+// With a visit budget (PTParams::wf.closest_budget) a ray still walking past it goes to the cooperative closest-hit
+// walk (wf_closest_coop) and its lane takes the next item.
 template <int KS, bool DEEP>
 __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTParams p, const int* __restrict__ list,
                                                                               const int* __restrict__ counts, int cap,
-                                                                              int* __restrict__ heads) {
+                                                                              int* __restrict__ heads,
+                                                                              int* __restrict__ strag_count) {
   __shared__ int stk[KS * kTB];
   const int lane = threadIdx.x & 63;
   int total = 0;
@@ -706,7 +729,8 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTP
   const float4* tree = p.scene.bvh_any;  // this lane's tree: the SAH tree, or the reference tree for a re-walk
   v3 S = splat(0.0f), d = splat(0.0f), inv = splat(0.0f);
   float tbest = PT_INF;
-  uint32_t nvis = 0, nray = 0, nrewalk = 0;
+  uint32_t nvis = 0, nray = 0, nrewalk = 0, rvis = 0;
+  const uint32_t budget = p.wf.closest_budget;
   while (true) {
     const unsigned long long idle = __ballot(!have);
     if (__popcll(idle) >= (__ballot(have) ? kRefillMin : 1) && (q.next < q.end || q.grab())) {
@@ -727,6 +751,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTP
         if (node < 0) { leaf = node; node = kNone; }
         if constexpr (DEEP) st = ray_stack<kTB, KS, DEEP>(stk + threadIdx.x, p, pid);
         have = true;
+        rvis = 0;
         ++nray;
       }
       q.next = min(q.next + __popcll(idle), q.end);
@@ -734,6 +759,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTP
     if (!__any(have)) break;
     while (node >= 0) {  // traverse<0>'s descent, pruned by the current best t
       ++nvis;
+      ++rvis;
       const float4* nd = tree + 4 * node;
       const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
       float t0l, t0r;
@@ -762,6 +788,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTP
     while (leaf != kNone) {  // traverse<0>'s leaf phase: strict '<' keeps the first triangle at a given t
       const int first = ref_leaf_first(leaf), cnt = ref_leaf_count(leaf);
       nvis += (uint32_t)cnt;
+      rvis += (uint32_t)cnt;
       leaf_scan(p.scene.tri_geom, first, cnt, S, d, [&](int i, float t) {
         if (t < tbest) {
           tbest = t;
@@ -795,6 +822,19 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTP
         spill = spill || st.spilled;
       }
     }
+    const bool defer = have && budget && rvis > budget;  // past the budget: the cooperative walk finishes it
+    const unsigned long long m = __ballot(defer);
+    if (m) {
+      int base = 0;
+      if (lane == __ffsll((long long)m) - 1) base = atomicAdd(strag_count, __popcll(m));
+      base = __shfl(base, __ffsll((long long)m) - 1);
+      if (defer) {
+        p.wf.strag_c[base + __popcll(m & below)] = pid;
+        have = false;
+        node = leaf = kNone;
+        spill = spill || st.spilled;
+      }
+    }
   }
   stat_add(p, kStatBounceRays, nray);
   stat_add(p, kStatSpills, spill ? 1u : 0u);
@@ -821,6 +861,26 @@ __global__ void __launch_bounds__(64 * kCoopWaves) wf_shadow_coop(PTParams p, co
     const bool occ = shadow_coop_walk(anyhit_scene(p.scene), st[wv], kCoopCap, xyz(o), xyz(dir), point, dir.w);
     if ((threadIdx.x & 63) == 0) (point ? p.wf.occ_p : p.wf.occ_h)[pid] = occ;
   }
+}
+
+// The bounce rays wf_trace_closest_refill deferred: one wave per ray (closest_coop_walk).
+__global__ void __launch_bounds__(64 * kCoopWaves) wf_closest_coop(PTParams p, const int* __restrict__ strag_count) {
+  __shared__ int st[kCoopWaves][kCoopCap];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n = *strag_count;
+  uint32_t nrewalk = 0;
+  for (int r = blockIdx.x * kCoopWaves + wv; r < n; r += gridDim.x * kCoopWaves) {
+    const int pid = p.wf.strag_c[r];
+    const float4 o = ldnt(&p.wf.ray_o[pid]), dd = ldnt(&p.wf.ray_d[pid]);
+    float t;
+    bool rw;
+    const int tri = closest_coop_walk(p.scene, st[wv], kCoopCap, xyz(o), xyz(dd), &t, &rw);
+    if ((threadIdx.x & 63) == 0) {
+      stnt(&p.wf.hit[pid], make_int2(tri, __float_as_int(t)));
+      nrewalk += rw ? 1u : 0u;
+    }
+  }
+  stat_add(p, kStatTieRewalks, nrewalk);
 }
 
 // shade()'s MIS combination (:950-966) for given shadow verdicts: hdriLight zeroes
@@ -1067,10 +1127,13 @@ int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent
   auto closest = [&](int i, hipStream_t st) {
     const int* lin = lists[(i + 1) & 1];
     const int* live_in = p.wf.counters + kWfCtr * (i - 1);
-    if (refill_closest)
+    if (refill_closest) {
+      int* strag = p.wf.counters + kWfCtr * i + kCtrStragC;
       hipLaunchKernelGGL((wf_trace_closest_refill<KS, DEEP>), dim3(refill_blocks(N)), dim3(kTB), 0, st, p,
-                         lin, live_in, cap, p.wf.counters + kWfCtr * i + kCtrQClosest);
-    else
+                         lin, live_in, cap, p.wf.counters + kWfCtr * i + kCtrQClosest, strag);
+      if (p.wf.closest_budget)
+        hipLaunchKernelGGL(wf_closest_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, st, p, (const int*)strag);
+    } else
       hipLaunchKernelGGL((wf_trace_closest<KS, DEEP>), dim3(gT), dim3(kTB), 0, st, p, lin, live_in, cap);
   };
   for (int i = 0; i < p.max_depth; ++i) {
@@ -1095,9 +1158,10 @@ int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent
       if ((e = hipEventRecord(ev_join, aux)) != hipSuccess) return (int)e;
     }
     int* strag = p.wf.counters + kWfCtr * i + kCtrStrag;  // shadow rays handed to the cooperative walk
-    if (p.refill && !p.scene.bvh4 && !p.wf.shadow_budget)
+    if (p.refill && !p.scene.bvh4)
       hipLaunchKernelGGL((wf_trace_shadow_refill<KS, DEEP>), dim3(refill_blocks(2 * N)), dim3(kTB), 0, s, p,
-                         (const int*)p.wf.shadow_list, (const int*)shadow, cap, p.wf.counters + kWfCtr * i + kCtrQShadow);
+                         (const int*)p.wf.shadow_list, (const int*)shadow, cap, p.wf.counters + kWfCtr * i + kCtrQShadow,
+                         strag);
     else if (p.scene.bvh4)
       hipLaunchKernelGGL((wf_trace_shadow<KS, true, DEEP>), dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
                          (const int*)shadow, cap, strag);

@@ -49,8 +49,8 @@ constexpr int kLiveBins = PT_LIVE_BINS;  // live-ray lists by direction octant: 
 // wavefront list counters per bounce (8 segments each): live bins, HDR shadow, point bins, straggler count
 constexpr int kCtrHdr = 8 * kLiveBins, kCtrPoint = kCtrHdr + 8, kCtrStrag = kCtrPoint + 8 * kPointBins;
 // per-XCD work-queue heads of the refill traversal kernels launched in bounce i: shadow rays, closest-hit rays
-constexpr int kCtrQShadow = kCtrStrag + 1, kCtrQClosest = kCtrQShadow + 8;
-constexpr int kWfCtr = (kCtrQClosest + 8 + 63) / 64 * 64;
+constexpr int kCtrQShadow = kCtrStrag + 1, kCtrQClosest = kCtrQShadow + 8, kCtrStragC = kCtrQClosest + 8;
+constexpr int kWfCtr = (kCtrStragC + 1 + 63) / 64 * 64;
 constexpr int kWfCounters = 4 * kWfCtr;  // 4 bounces  // "no node" (leaf refs are >= -(2^31 - 1))
 
 struct Plane {          // banded RGBA32F plane
@@ -119,6 +119,8 @@ struct WFState {
   uint32_t* row_cost;           // optional: traversal steps per band row (load-balancing probe), may be null
   int* straggler;               // shadow rays past the step budget: pid | (point << 31), count at kCtrStrag
   uint32_t shadow_budget;       // node + triangle visits before a shadow ray is handed to the cooperative walk (0: never)
+  int* strag_c;                 // bounce rays past closest_budget (count at kCtrStragC): the cooperative closest walk
+  uint32_t closest_budget;      // node + triangle visits before a bounce ray is handed to it (0: never; refill kernel)
   unsigned long long* stats;    // optional traversal counters (kStat*), wave-aggregated atomics; may be null
   int* spill;                   // deep trees only: stack entries past the LDS stack, entry kStack + j of pixel pid at
   size_t spill_stride;          // spill[j * spill_stride + pid] (spill_stride = band pixels); null otherwise

@@ -445,6 +445,99 @@ __device__ bool shadow_coop_walk(const SceneDev& sc, int* __restrict__ st, int c
   return __any(occ);
 }
 
+// Wave-cooperative closest hit of ONE ray (the stragglers of the bounce walk's visit budget), the same answer as
+// closest_hit(sah = true): the 64 lanes pop the top 64 entries of a shared LDS stack of the SAH tree over the
+// reference leaves, test node children with the walk's pruning bound (from the wave's best t so far) or scan a
+// leaf's triangles keeping a lane-local best and how many triangles met it exactly; the candidates are the
+// serial walk's, so the minimum t is too, and when one triangle alone attains it, the triangle. When two do, lane 0
+// walks the ray on the reference tree in the reference's order (traverse<0>), as closest_hit does; also when the
+// shared stack would overflow (closest_hit itself). Returns the triangle; *t_out the t. Call with the whole wave.
+__device__ int closest_coop_walk(const SceneDev& sc, int* __restrict__ st, int cap, v3 S, v3 d, float* t_out,
+                                 bool* rewalked) {
+  const int lane = threadIdx.x & 63;
+  const SceneDev sa = anyhit_scene(sc);
+  const v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  float lb = PT_INF, tw = PT_INF;  // lane's best, wave's best so far
+  int li = -1, lc = 0;             // lane's best triangle, triangles that met lb exactly
+  int count = 1;
+  if (lane == 0) st[0] = sa.root_ref;
+  __builtin_amdgcn_wave_barrier();
+  bool overflow = false;
+  while (count > 0) {
+    const int k = count < 64 ? count : 64;
+    const int ref = lane < k ? st[count - 1 - lane] : kNone;
+    count -= k;
+    __builtin_amdgcn_wave_barrier();
+    const float lim = tw * 1.0002f + 2.0e-4f;
+    int push0 = kNone, push1 = kNone;  // far, near
+    if (ref >= 0) {
+      const float4* nd = sa.bvh + 4 * ref;
+      const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+      float t0l, t0r;
+      const float dl = slab(S, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, &t0l);
+      const float dr = slab(S, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, &t0r);
+      const bool hl = dl > 0.0f && !(t0l > lim), hr = dr > 0.0f && !(t0r > lim);
+      const int cl = __float_as_int(q3.x), cr = __float_as_int(q3.y);
+      if (hl && hr) {
+        const bool lnear = dl < dr;
+        push0 = lnear ? cr : cl;
+        push1 = lnear ? cl : cr;
+      } else if (hl) {
+        push1 = cl;
+      } else if (hr) {
+        push1 = cr;
+      }
+    } else if (ref != kNone) {
+      leaf_scan(sc.tri_geom, ref_leaf_first(ref), ref_leaf_count(ref), S, d, [&](int i, float t) {
+        if (t < lb) { lb = t; li = i; lc = 1; }
+        else if (t == lb) ++lc;
+        return false;
+      });
+    }
+    float m = lb;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fminf(m, __shfl_xor(m, o));
+    tw = m;
+    const unsigned long long m0 = __ballot(push0 != kNone), m1 = __ballot(push1 != kNone);
+    const int n0 = __popcll(m0), n1 = __popcll(m1);
+    if (count + n0 + n1 > cap) {
+      overflow = true;
+      break;
+    }
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    if (push0 != kNone) st[count + __popcll(m0 & lt)] = push0;           // all far children first,
+    if (push1 != kNone) st[count + n0 + __popcll(m1 & lt)] = push1;      // then the near ones on top
+    count += n0 + n1;
+    __builtin_amdgcn_wave_barrier();
+  }
+  int n_at = (!overflow && lb == tw && tw < PT_INF) ? lc : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) n_at += __shfl_xor(n_at, o);
+  if (!overflow && n_at < 2) {  // one triangle attains the minimum (or none: a miss)
+    const unsigned long long own = __ballot(tw < PT_INF && lb == tw);
+    const int tri = own ? __shfl(li, __ffsll((long long)own) - 1) : -1;
+    *t_out = tw;
+    *rewalked = false;
+    return tri;
+  }
+  // a tie (or overflow): lane 0 walks, on the (now free) LDS region
+  __builtin_amdgcn_wave_barrier();
+  int tri = -1;
+  float t = PT_INF;
+  LdsStack<1> ls{st};
+  if (lane == 0) {
+    if (overflow) {
+      bool rw = false;
+      tri = closest_hit(sc, true, ls, S, d, 1, &t, nullptr, PT_INF, &rw);
+    } else {
+      tri = traverse<0>(sc, ls, S, d, 0.0f, 1, &t, nullptr, PT_INF);
+    }
+  }
+  *t_out = __shfl(t, 0);
+  *rewalked = !overflow;
+  return __shfl(tri, 0);
+}
+
 // Returns 1 occluded, 0 visible, -1 when the stack would overflow (the caller
 // re-traces that ray on the binary tree, whose depth the host bounds by kStack).
 template <int STRIDE, int KS = kStack>

@@ -107,13 +107,24 @@ def test_degenerate_sah_builds_fit_the_stack(gpu):
     W, H = 64, 48
     ref = O.OracleFrameLoop(scene, W, H, run_taa=False)
     r = Renderer(scene, W, H, mode="fast", atrous_exact=True, run_taa=False, run_output=False)
+    coop = Renderer(scene, W, H, mode="fast", atrous_exact=True, run_taa=False, run_output=False)
+    coop.pass_path_tracing.set_uniform_int("closest_budget", 8)  # the cooperative walk meets the ties too
+    coop.pass_path_tracing.set_uniform_int("trace_refill", 75)
     for f in range(2):
         r.frame()
+        coop.frame()
         want = ref.frame()
         got = {k: gl.readback(v) for k, v in r.planes().items()}
         for k in ("normal_depth", "velocity", "fwidth", "world", "color", "emission", "albedo"):
             assert np.array_equal(got[k].view(np.uint32), want[k].view(np.uint32)), (f, k)
+        gc = {k: gl.readback(coop.planes()[k]) for k in ("color", "emission", "albedo")}
+        for k in gc:
+            assert np.array_equal(gc[k].view(np.uint32), want[k].view(np.uint32)), ("coop", f, k)
         assert float(np.mean(want["albedo"][..., 2] > 0.7)) > 0.05  # the stacked triangles are in view
+    st_coop = coop.trace_stats()
+    print("cooperative", st_coop)
+    assert st_coop["tie_rewalks"] > 0
+    coop.close()
     st = r.trace_stats()
     print(st)
     assert st["tie_rewalks"] > 0  # coincident triangles meet the same t: re-walked on the reference tree

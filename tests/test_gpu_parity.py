@@ -184,15 +184,16 @@ def test_closest_tree_is_result_preserving(gpu, scene_name, request):
 @pytest.mark.parametrize("scene_name", ["scene_small", "scene_nan"])
 def test_cooperative_shadow_walk_is_result_preserving(gpu, scene_name, request):
     """Shadow rays past the step budget are finished by the wave-cooperative walk (kernels_wavefront.hip
-    wf_shadow_coop): budgets 4 (nearly every ray, including LDS-stack overflows), 16 and 128 (default) give the
-    serial walk's bits (budget 0)."""
+    wf_shadow_coop): budgets 4 (nearly every ray, including LDS-stack overflows), 16 and 128 give the serial walk's
+    bits (budget 0), from the one-ray-per-lane kernel and from the lane-refill kernel (trace_refill 75)."""
     gl = gpu
     scene = request.getfixturevalue(scene_name)
     W, H = 96, 64
     outs = []
-    for budget in (0, 4, 16, 128):
+    for budget, refill in ((0, 0), (4, 0), (16, 0), (128, 0), (4, 75), (16, 75), (128, 75)):
         r = _renderer(scene, W, H, mode="fast", run_taa=False, run_output=False)
         r.pass_path_tracing.set_uniform_int("shadow_budget", budget)
+        r.pass_path_tracing.set_uniform_int("trace_refill", refill)
         for _ in range(2):
             r.frame()
         outs.append({k: gl.readback(r.planes()[k]) for k in ("color", "emission", "albedo")})
@@ -200,6 +201,28 @@ def test_cooperative_shadow_walk_is_result_preserving(gpu, scene_name, request):
     for o in outs[1:]:
         for k in o:
             assert np.array_equal(outs[0][k], o[k], equal_nan=True), k
+
+
+@pytest.mark.parametrize("scene_name", ["scene_small", "scene_cornell", "scene_nan"])
+def test_cooperative_closest_walk_is_result_preserving(gpu, scene_name, request):
+    """Bounce rays past the visit budget are finished by the wave-cooperative closest-hit walk (kernels_wavefront.hip
+    wf_closest_coop, from the lane-refill kernel): budgets 2 (nearly every ray), 16 and 64 give the serial walk's
+    bits, ray counts and tie re-walks."""
+    gl = gpu
+    scene = request.getfixturevalue(scene_name)
+    W, H = 96, 64
+    outs = []
+    for budget in (0, 2, 16, 64):
+        r = _renderer(scene, W, H, mode="fast", run_taa=False, run_output=False)
+        r.pass_path_tracing.set_uniform_int("closest_budget", budget)
+        r.pass_path_tracing.set_uniform_int("trace_refill", 75)
+        for _ in range(2):
+            r.frame()
+        outs.append({k: gl.readback(r.planes()[k]) for k in ("color", "emission", "albedo")})
+        r.close()
+    for o in outs[1:]:
+        for k in o:
+            assert np.array_equal(outs[0][k].view(np.uint32), o[k].view(np.uint32)), k
 
 
 def test_wavefront_equals_megakernel(gpu, scene_small):
