@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--equal-bands", action="store_true", help="multi-GPU: equal band heights (no cost balancing)")
     ap.add_argument("--breakdown", action="store_true", help="print per-pass ms to stderr")
     ap.add_argument("--pt-kernel", type=int, default=0, help="0 wavefront (production), 1 megakernel (A/B)")
+    ap.add_argument("--trace-batch", type=int, default=None,
+                    help="path tracers of this many frames drawn as one batch (default 1)")
     ap.add_argument("--frames-in-flight", type=int, default=None,
                     help="K > 1: front ends (G-buffer + path tracer) of K frames overlap on K streams "
                          "(default 4 on one GPU, 8 on bands: thinner bands have relatively longer launch tails)")
@@ -183,6 +185,8 @@ def main():
         world = args.gpus if world == 1 and args.gpus == 1 else world
     if args.frames_in_flight is None:
         args.frames_in_flight = 4 if world == 1 else 8
+    if args.trace_batch is None:
+        args.trace_batch = 1
     # every frame slot must have run once before the timed region (a slot's first frame allocates its
     # wavefront state, and hipMalloc stalls the queues): at least K + 1 untimed frames
     args.warmup = max(args.warmup, args.frames_in_flight + 1)
@@ -226,11 +230,11 @@ def main():
         if world > 1:
             from ptsvgf.dist import make_band_renderer
             r = make_band_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,
-                                   frames_in_flight=K)
+                                   frames_in_flight=K, trace_batch=min(args.trace_batch, K))
         else:
             from ptsvgf.renderer import Renderer
             r = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, run_taa=False, run_output=False,
-                         frames_in_flight=K)
+                         frames_in_flight=K, trace_batch=min(args.trace_batch, K))
         r.pass_path_tracing.set_uniform_int("pt_kernel", args.pt_kernel)
         for kv in args.pt_uniform:
             name, val = kv.split("=")
@@ -380,7 +384,8 @@ def main():
                                        + (f" {args.view} view" if args.view != "default" else ""),
                            "resolution": [W, H], "spp": 1, "max_tracing_depth": cfg.max_tracing_depth,
                            "atrous_iterations": cfg.num_atrous_iterations, "triangles": scene.ntris,
-                           "parallelism": f"bands{world}", "frames_in_flight": K},
+                           "parallelism": f"bands{world}", "frames_in_flight": K,
+                           "trace_batch": min(args.trace_batch, K)},
                 "roofline": atrous_roofline(res, W, res["rows"]), "cpu_baseline": cpu,
                 "path_tracer": pt_rates(res, fps), **extra,
                 "passes_ms": {k: round(v, 4) for k, v in res["per_pass"].items()}}

@@ -148,6 +148,14 @@ int pt_pass_set_motion_bound(uint32_t pass, void* device_u32);
  * Wave-aggregated atomics; NULL disables (the default). */
 int pt_pass_set_trace_stats(uint32_t pass, void* device_u64);
 int pt_pass_draw(uint32_t pass);
+/* Draw `count` (1..8) path-tracing passes — the frames of a batch, each with its
+ * own uniforms, samplers and attachments, one scene, size and band — as one
+ * wavefront run whose list-driven traversal launches trace every frame's rays at
+ * once (no GL counterpart: the reference draws one frame at a time). Results are
+ * those of drawing each pass alone. passes[0] owns the shared wavefront state,
+ * sized for max(count, its "trace_batch" uniform) frames; the batch is timed as
+ * its draw. Accumulation (lastFrame) and tile subsets are refused. */
+int pt_pass_draw_batch(const uint32_t* passes, int count);
 /* Time the last draw of this pass (ms, HIP events on the library stream; syncs). */
 int pt_pass_last_ms(uint32_t pass, float* ms);
 int pt_pass_destroy(uint32_t pass);

@@ -87,58 +87,95 @@ struct RasterBins {
 
 struct WFBuffers {
   void* base = nullptr;  // one allocation carved into the WFState arrays
-  size_t n = 0;          // pixels covered
+  size_t n = 0;          // pixels per frame
+  int nb = 1;            // frames (pt_pass_draw_batch): per-pixel arrays for nb * n pixels, lists and counters per frame
+  WFState stb[kMaxBatch]{};  // frame b's state: per-pixel arrays at pid offset b * n; stb[0] == st
   WFState st{};
   int* spill = nullptr;  // deep reference trees: stack entries past the LDS stack (WFState::spill)
   int spill_levels = 0;
+  size_t spill_cols = 0;
 };
 
 // Spill columns for a reference tree needing `need` stack entries (> the LDS stack): (need - kStack + 1) entries per
 // pixel of the band, allocated on first use and kept while the depth fits.
 int wf_spill(WFBuffers& b, int need) {
   const int levels = need - kStack + 1;
+  const size_t m = b.n * (size_t)b.nb;  // columns of the batch's pixels (global pids)
   if (levels <= 0) {
-    b.st.spill = nullptr;
-    b.st.spill_stride = 0;
+    for (int f = 0; f < b.nb; ++f) {
+      b.stb[f].spill = nullptr;
+      b.stb[f].spill_stride = 0;
+    }
+    b.st = b.stb[0];
     return PT_OK;
   }
-  if (!b.spill || b.spill_levels < levels) {
+  if (!b.spill || b.spill_levels < levels || b.spill_cols != m) {
     if (b.spill) (void)hipFree(b.spill);
     b.spill = nullptr;
-    if (hipMalloc((void**)&b.spill, (size_t)levels * b.n * sizeof(int)) != hipSuccess) return PT_ERR_HIP;
+    if (hipMalloc((void**)&b.spill, (size_t)levels * m * sizeof(int)) != hipSuccess) return PT_ERR_HIP;
     b.spill_levels = levels;
+    b.spill_cols = m;
   }
-  b.st.spill = b.spill;
-  b.st.spill_stride = b.n;
+  for (int f = 0; f < b.nb; ++f) {  // frame f's local pid p is column f * n + p
+    b.stb[f].spill = b.spill + (size_t)f * b.n;
+    b.stb[f].spill_stride = m;
+  }
+  b.st = b.stb[0];
   return PT_OK;
 }
 
-int wf_alloc(WFBuffers& b, int W, int rows) {
+int wf_alloc(WFBuffers& b, int W, int rows, int nb = 1) {
   const size_t n = (size_t)W * (size_t)rows;
-  if (b.base && b.n == n) return PT_OK;
+  if (b.base && b.n == n && b.nb == nb) return PT_OK;
   if (b.base) { (void)hipFree(b.base); b.base = nullptr; }
-  const size_t f4 = n * 16, al = 256;
+  const size_t m = n * (size_t)nb;  // pixels of the batch
+  const size_t f4 = m * 16, al = 256;
   const size_t nl = (size_t)wf_list_capacity(W, rows) * 8;  // 8 list segments
   auto up = [&](size_t v) { return (v + al - 1) / al * al; };
-  size_t total = up(f4) * 10 + up(n * 8) + up(n * 4) + up(n) * 2 + up(nl * 4 * kLiveBins) * 2 +
-                 up(nl * 4 * (1 + kPointBins)) +
-                 up(n * 8) + up(n * 4) + up(kWfCounters * 4);
+  const size_t lists = up(nl * 4 * kLiveBins) * 2 + up(nl * 4 * (1 + kPointBins));
+  size_t total = up(f4) * 10 + up(m * 8) + up(m * 4) + up(m) * 2 + lists * nb + up(m * 8) + up(m * 4) +
+                 up((size_t)nb * kWfCounters * 4);
   if (hipMalloc(&b.base, total) != hipSuccess) { b.base = nullptr; return PT_ERR_HIP; }
   char* c = (char*)b.base;
-  float4** f4p[10] = {&b.st.ray_o, &b.st.ray_d, &b.st.light, &b.st.red, &b.st.pend0,
-                      &b.st.pend1, &b.st.pend2, &b.st.pend3, &b.st.sh_h, &b.st.sh_p};
+  WFState s0{};
+  float4** f4p[10] = {&s0.ray_o, &s0.ray_d, &s0.light, &s0.red, &s0.pend0,
+                      &s0.pend1, &s0.pend2, &s0.pend3, &s0.sh_h, &s0.sh_p};
   for (auto q : f4p) { *q = (float4*)c; c += up(f4); }
-  b.st.hit = (int2*)c; c += up(n * 8);
-  b.st.seed = (uint32_t*)c; c += up(n * 4);
-  b.st.occ_h = (uint8_t*)c; c += up(n);
-  b.st.occ_p = (uint8_t*)c; c += up(n);
-  b.st.list0 = (int*)c; c += up(nl * 4 * kLiveBins);
-  b.st.list1 = (int*)c; c += up(nl * 4 * kLiveBins);
-  b.st.shadow_list = (int*)c; c += up(nl * 4 * (1 + kPointBins));
-  b.st.straggler = (int*)c; c += up(n * 8);  // both shadow kinds of one bounce
-  b.st.strag_c = (int*)c; c += up(n * 4);    // bounce rays of one bounce
-  b.st.counters = (int*)c;
+  s0.hit = (int2*)c; c += up(m * 8);
+  s0.seed = (uint32_t*)c; c += up(m * 4);
+  s0.occ_h = (uint8_t*)c; c += up(m);
+  s0.occ_p = (uint8_t*)c; c += up(m);
+  s0.straggler = (int*)c; c += up(m * 8);  // both shadow kinds of one bounce (a batch's: frame 0's pointer)
+  s0.strag_c = (int*)c; c += up(m * 4);    // bounce rays of one bounce
+  int* counters = (int*)c; c += up((size_t)nb * kWfCounters * 4);  // contiguous: one memset per draw
+  for (int f = 0; f < nb; ++f) {
+    WFState st = s0;
+    const size_t o = (size_t)f * n;
+    st.ray_o = s0.ray_o + o;
+    st.ray_d = s0.ray_d + o;
+    st.light = s0.light + o;
+    st.red = s0.red + o;
+    st.pend0 = s0.pend0 + o;
+    st.pend1 = s0.pend1 + o;
+    st.pend2 = s0.pend2 + o;
+    st.pend3 = s0.pend3 + o;
+    st.sh_h = s0.sh_h + o;
+    st.sh_p = s0.sh_p + o;
+    st.hit = s0.hit + o;
+    st.seed = s0.seed + o;
+    st.occ_h = s0.occ_h + o;
+    st.occ_p = s0.occ_p + o;
+    st.straggler = s0.straggler + 2 * o;
+    st.strag_c = s0.strag_c + o;
+    st.counters = counters + (size_t)f * kWfCounters;
+    st.list0 = (int*)c; c += up(nl * 4 * kLiveBins);
+    st.list1 = (int*)c; c += up(nl * 4 * kLiveBins);
+    st.shadow_list = (int*)c; c += up(nl * 4 * (1 + kPointBins));
+    b.stb[f] = st;
+  }
+  b.st = b.stb[0];
   b.n = n;
+  b.nb = nb;
   return PT_OK;
 }
 
@@ -928,8 +965,8 @@ int bins_for(RasterBins& b, int n, int W, int y0, int y1, int cap, Bins* out) {
 }
 
 // ------------------------------------------------------------- draw calls ---
-int draw_pathtrace(Pass* p) {
-  PTParams k;
+// PTParams of a path-tracing pass's draw from its uniforms, samplers and attachments (the wavefront state aside).
+int pt_params(Pass* p, PTParams& k, SceneGPU*& sg) {
   memset(&k, 0, sizeof(k));
   k.W = p->W;
   k.H = p->H;
@@ -943,7 +980,6 @@ int draw_pathtrace(Pass* p) {
   Texture* lt = sampler(p, "pointLights", &lh);
   if (!tt || tt->target != PT_TEXTURE_BUFFER || !nt || nt->target != PT_TEXTURE_BUFFER)
     return err(PT_ERR_MISSING_TEXTURE, "path_tracing needs the 'triangles' and 'nodes' texture buffers");
-  SceneGPU* sg;
   TRY(get_scene(tt, th, nt, nh, &sg));
   k.scene.tri_geom = sg->geom;
   k.scene.tri_shade = sg->shade;
@@ -1016,17 +1052,13 @@ int draw_pathtrace(Pass* p) {
   k.tile_offset = ui(p, "tile_offset", 0);
   if (wf_subset_tiles(k.W, std::max(0, k.y1 - k.y0), k.tile_stride, k.tile_offset) < 0)
     return err(PT_ERR_ARG, "tile_offset must lie in [0, tile_stride)");
-  int rc;
-  if (ui(p, "pt_kernel", 0) == 1) {  // 1: single megakernel (kernels_pt.hip), kept for A/B
-    if (k.tile_stride != 1) return err(PT_ERR_ARG, "tile subsets need the wavefront path tracer");
-    if (k.stack_need >= kStack)
-      return err(PT_ERR_ARG, "the megakernel (pt_kernel=1) walks a 32-entry LDS stack; this BVH is deeper: use the "
-                             "wavefront path tracer (pt_kernel=0, the default)");
-    rc = launch_pathtrace(k, g.stream);
-  } else {                            // 0: wavefront (kernels_wavefront.hip), production
-    TRY(wf_alloc(p->wf, k.W, std::max(0, k.y1 - k.y0)));
-    if (wf_spill(p->wf, k.stack_need) != PT_OK) return err(PT_ERR_HIP, "spill stack allocation failed");
-    k.wf = p->wf.st;
+  return PT_OK;
+}
+
+// The wavefront-side fields of a path-tracing pass's PTParams: its wavefront state `st` (its own, or its frame's
+// share of a batch's), counters, budgets, refill, cost-ordered tiles and the primary rasteriser's bins.
+int pt_wf_setup(Pass* p, PTParams& k, SceneGPU* sg, const WFState& st) {
+    k.wf = st;
     k.wf.row_cost = p->row_cost;
     k.wf.stats = p->stats;
     // > 0: shadow rays past this many visits finish in the wave-cooperative walk (A/B switch; off: with frames
@@ -1044,6 +1076,24 @@ int draw_pathtrace(Pass* p) {
       TRY(bins_for(p->bins, sg->nleaves, k.W, k.y0, k.y1, ui(p, "raster_pair_cap", 0), &k.leaf_bins));
       k.primary_raster = 1;
     }
+    return PT_OK;
+}
+
+int draw_pathtrace(Pass* p) {
+  PTParams k;
+  SceneGPU* sg = nullptr;
+  TRY(pt_params(p, k, sg));
+  int rc;
+  if (ui(p, "pt_kernel", 0) == 1) {  // 1: single megakernel (kernels_pt.hip), kept for A/B
+    if (k.tile_stride != 1) return err(PT_ERR_ARG, "tile subsets need the wavefront path tracer");
+    if (k.stack_need >= kStack)
+      return err(PT_ERR_ARG, "the megakernel (pt_kernel=1) walks a 32-entry LDS stack; this BVH is deeper: use the "
+                             "wavefront path tracer (pt_kernel=0, the default)");
+    rc = launch_pathtrace(k, g.stream);
+  } else {                            // 0: wavefront (kernels_wavefront.hip), production
+    TRY(wf_alloc(p->wf, k.W, std::max(0, k.y1 - k.y0)));
+    if (wf_spill(p->wf, k.stack_need) != PT_OK) return err(PT_ERR_HIP, "spill stack allocation failed");
+    TRY(pt_wf_setup(p, k, sg, p->wf.st));
     if (ui(p, "trace_fork", 0) && !p->aux) {  // A/B switch (off: measured slower with frames in flight)
       HIPCHK(hipStreamCreateWithFlags(&p->aux, hipStreamNonBlocking));
       HIPCHK(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
@@ -1054,6 +1104,32 @@ int draw_pathtrace(Pass* p) {
     if (!rc && k.tiles.cost) p->order.ordered = true;
   }
   return rc ? hip_err((hipError_t)rc, "pathtrace launch") : PT_OK;
+}
+
+// pt_pass_draw_batch: the frames of several path-tracing passes in one wavefront run whose list-driven traversals
+// trace every frame's rays per launch. The first pass owns the shared state, sized for its "trace_batch" frames.
+int draw_pathtrace_batch(Pass** ps, int n) {
+  Pass* h = ps[0];
+  PTParams k[kMaxBatch];
+  SceneGPU* sg = nullptr;
+  for (int b = 0; b < n; ++b) {
+    SceneGPU* sb = nullptr;
+    TRY(pt_params(ps[b], k[b], sb));
+    if (b == 0) sg = sb;
+    if (sb != sg || k[b].W != k[0].W || k[b].y0 != k[0].y0 || k[b].y1 != k[0].y1 || k[b].max_depth != k[0].max_depth ||
+        k[b].refill != k[0].refill)
+      return err(PT_ERR_ARG, "a path-tracing batch needs one scene, size, band and depth");
+    if (ui(ps[b], "pt_kernel", 0) != 0 || k[b].tile_stride != 1 || k[b].accumulate)
+      return err(PT_ERR_ARG, "a path-tracing batch needs the wavefront path tracer on whole frames, no accumulation");
+  }
+  const int cap = std::max(n, std::min(kMaxBatch, ui(h, "trace_batch", n)));
+  TRY(wf_alloc(h->wf, k[0].W, std::max(0, k[0].y1 - k[0].y0), cap));
+  if (wf_spill(h->wf, k[0].stack_need) != PT_OK) return err(PT_ERR_HIP, "spill stack allocation failed");
+  for (int b = 0; b < n; ++b) TRY(pt_wf_setup(ps[b], k[b], sg, h->wf.stb[b]));
+  const int rc = launch_pathtrace_wavefront_batch(k, n, g.stream);
+  for (int b = 0; b < n && !rc; ++b)
+    if (k[b].tiles.cost) ps[b]->order.ordered = true;
+  return rc ? hip_err((hipError_t)rc, "pathtrace batch launch") : PT_OK;
 }
 
 int draw_raster(Pass* p) {
@@ -1725,6 +1801,32 @@ int pt_pass_draw(uint32_t pass) {
   if (g.profiling) {
     HIPCHK(hipEventRecord(p->ev1, g.stream));
     p->timed = true;
+  }
+  return PT_OK;
+}
+
+int pt_pass_draw_batch(const uint32_t* passes, int count) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  if (!passes || count < 1 || count > kMaxBatch) return err(PT_ERR_ARG, "a batch holds 1 to 8 path-tracing passes");
+  Pass* ps[kMaxBatch];
+  for (int b = 0; b < count; ++b) {
+    ps[b] = pass_of(passes[b]);
+    if (!ps[b]) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
+    if (!ps[b]->bound) return err(PT_ERR_STATE, "pass drawn before bindData");
+    if (g.programs[ps[b]->program] != PK_PATHTRACE) return err(PT_ERR_ARG, "a batch holds path-tracing passes only");
+    for (int c = 0; c < b; ++c)
+      if (ps[c] == ps[b]) return err(PT_ERR_ARG, "a pass appears twice in a batch");
+  }
+  Pass* h = ps[0];
+  if (g.profiling) {  // the batch is timed as the first pass's draw
+    if (!h->ev0) { HIPCHK(hipEventCreate(&h->ev0)); HIPCHK(hipEventCreate(&h->ev1)); }
+    HIPCHK(hipEventRecord(h->ev0, g.stream));
+  }
+  TRY(draw_pathtrace_batch(ps, count));
+  if (g.profiling) {
+    HIPCHK(hipEventRecord(h->ev1, g.stream));
+    h->timed = true;
   }
   return PT_OK;
 }

@@ -490,6 +490,15 @@ __device__ __forceinline__ bool shadow_item(const int* __restrict__ list, const 
   return false;
 }
 
+// Dense index k over a batch's frames (per-frame totals tot[b]) -> frame b and its local index (wave-uniform data).
+__device__ __forceinline__ int batch_frame(const int* tot, int nb, int* k) {
+  for (int b = 0; b < nb; ++b) {
+    if (*k < tot[b]) return b;
+    *k -= tot[b];
+  }
+  return -1;
+}
+
 // Work queue of the refill traversal kernels: the list's dense index range is cut into 8 regions, one per XCD,
 // each with its own head word (one returning atomic per grab of kGrab items; a per-XCD head keeps the grabs of
 // 256 CUs off one word, MI355X_MICROARCH.md "dequeue"). A wave drains its XCD's region first, then the others;
@@ -588,16 +597,20 @@ __host__ __device__ constexpr int refill_blocks(int items_max) {
 // With a visit budget (PTParams::wf.shadow_budget) a ray still undecided past it is handed to the wave-cooperative
 // walk (wf_shadow_coop) and its lane takes the next item, as in wf_trace_shadow.
 template <int KS, bool DEEP>
-__global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTParams p, const int* __restrict__ list,
-                                                                             const int* __restrict__ counts, int cap,
+__global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTParams p, ListBatch lb, int cap,
                                                                              int* __restrict__ heads,
                                                                              int* __restrict__ strag_count) {
   __shared__ int stk[KS * kTB];
   const int lane = threadIdx.x & 63;
-  const int nh = seg_total(counts);
-  int total = nh;
+  int nh[kMaxBatch], tot[kMaxBatch];
+  int total = 0;
+  for (int b = 0; b < lb.nb; ++b) {
+    nh[b] = seg_total(lb.counts[b]);
+    tot[b] = nh[b];
 #pragma unroll
-  for (int b = 0; b < kPointBins; ++b) total += seg_total(counts + (1 + b) * kSeg);
+    for (int c = 0; c < kPointBins; ++c) tot[b] += seg_total(lb.counts[b] + (1 + c) * kSeg);
+    total += tot[b];
+  }
   WaveQueue q = refill_queue(heads, total, p.refill);
   if (q.next >= q.end) return;
   const SceneDev sc = anyhit_scene(p.scene);
@@ -613,8 +626,10 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
     const unsigned long long idle = __ballot(!have);
     if (__popcll(idle) >= (__ballot(have) ? kRefillMin : 1) && (q.next < q.end || q.grab())) {
       // refill: the next items go to the idle lanes in lane order
-      const int k = q.next + __popcll(idle & below);
-      if (!have && k < q.end && shadow_item(list, counts, cap, nh, k, &pid, &point)) {
+      int k = q.next + __popcll(idle & below);
+      const int fb = k < q.end ? batch_frame(tot, lb.nb, &k) : -1;
+      if (!have && fb >= 0 && shadow_item(lb.list[fb], lb.counts[fb], cap, nh[fb], k, &pid, &point)) {
+        pid += fb * lb.n;
         rvis = 0;
         const float4 o = ldnt(&p.wf.ray_o[pid]);
         const float4 dir = point ? ldnt(&p.wf.sh_p[pid]) : ldnt(&p.wf.sh_h[pid]);  // point: (direction, distance)
@@ -711,15 +726,19 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
 // With a visit budget (PTParams::wf.closest_budget) a ray still walking past it goes to the cooperative closest-hit
 // walk (wf_closest_coop) and its lane takes the next item.
 template <int KS, bool DEEP>
-__global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTParams p, const int* __restrict__ list,
-                                                                              const int* __restrict__ counts, int cap,
+__global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTParams p, ListBatch lb, int cap,
                                                                               int* __restrict__ heads,
                                                                               int* __restrict__ strag_count) {
   __shared__ int stk[KS * kTB];
   const int lane = threadIdx.x & 63;
+  int tot[kMaxBatch];
   int total = 0;
+  for (int b = 0; b < lb.nb; ++b) {
+    tot[b] = 0;
 #pragma unroll
-  for (int b = 0; b < kLiveBins * kSeg; ++b) total += counts[b];
+    for (int c = 0; c < kLiveBins * kSeg; ++c) tot[b] += lb.counts[b][c];
+    total += tot[b];
+  }
   WaveQueue q = refill_queue(heads, total, p.refill);
   if (q.next >= q.end) return;
   const unsigned long long below = (1ull << lane) - 1ull;
@@ -734,8 +753,10 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTP
   while (true) {
     const unsigned long long idle = __ballot(!have);
     if (__popcll(idle) >= (__ballot(have) ? kRefillMin : 1) && (q.next < q.end || q.grab())) {
-      const int k = q.next + __popcll(idle & below);
-      if (!have && k < q.end && bins_get(list, counts, kLiveBins, cap, k, &pid)) {
+      int k = q.next + __popcll(idle & below);
+      const int fb = k < q.end ? batch_frame(tot, lb.nb, &k) : -1;
+      if (!have && fb >= 0 && bins_get(lb.list[fb], lb.counts[fb], kLiveBins, cap, k, &pid)) {
+        pid += fb * lb.n;
         const float4 o = ldnt(&p.wf.ray_o[pid]), dd = ldnt(&p.wf.ray_d[pid]);
         S = xyz(o);
         d = xyz(dd);
@@ -1094,54 +1115,64 @@ int wf_subset_tiles(int W, int rows, int stride, int offset) {
 // rays and live list shade(i) wrote) runs concurrently with the shadow trace and finish of bounce i; the join
 // comes before shade(i+1), which needs both. Two traversal launches then end together, so the frame's
 // dependency chain carries one tail fewer per bounce. Without `aux` the launches are serial.
+// nb > 1: a batch of frames (pt_pass_draw_batch) — per-frame launches for the primaries, shades and finishes, ONE
+// launch per bounce for the list-driven traversals of every frame's rays (lane-refill kernels; the one-ray-per-lane
+// kernels run per frame). Frame b's wavefront state lies at pid offset b * N of ps[0]'s, its counters at
+// ps[0].wf.counters + b * kWfCounters; the batched launches use frame 0's work-queue heads and straggler lists.
 template <int KS, bool DEEP>
-int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent_t ev_fork, hipEvent_t ev_join) {
+int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, hipStream_t aux, hipEvent_t ev_fork,
+                     hipEvent_t ev_join) {
+  const PTParams& p = ps[0];
   const int rows = p.y1 - p.y0;
   if (rows <= 0) return 0;
   const int N = p.W * rows;
   const int cap = wf_list_capacity(p.W, rows);  // per segment; the host sized the lists with the same function
-  hipError_t e = hipMemsetAsync(p.wf.counters, 0, kWfCounters * sizeof(int), s);
+  hipError_t e = hipMemsetAsync(p.wf.counters, 0, (size_t)nb * kWfCounters * sizeof(int), s);
   if (e != hipSuccess) return (int)e;
   const int ntiles = wf_subset_tiles(p.W, rows, p.tile_stride, p.tile_offset);
   if (ntiles <= 0) return 0;
-  if (p.primary_raster) {  // every tile of the band (the host enables it only without tile subsets)
-    if (p.scene.nleaves > 0) hipLaunchKernelGGL(pr_setup, dim3((p.scene.nleaves + 255) / 256), dim3(256), 0, s, p);
-    const int rc = launch_bins(p.leaf_bins, s);
-    if (rc) return rc;
-    hipLaunchKernelGGL(wf_primary_raster, dim3(ntiles), dim3(256), 0, s, p);
-    PTParams q = p;
-    q.pr_fix = p.leaf_bins.ctr;  // ties (and an overflow) walked
-    hipLaunchKernelGGL((wf_primary<KS, DEEP>), dim3(ntiles), dim3(256), 0, s, q);
-  } else {
-    hipLaunchKernelGGL((wf_primary<KS, DEEP>), dim3(ntiles), dim3(256), 0, s, p);
-  }
-  if (p.tiles.cost) {  // this frame's primary costs -> tile order of the bounce-0 shade and the next frame
-    const int rc = launch_tile_sort(p.tiles.cost, p.tiles.perm_next, p.tiles.ntiles, s);
-    if (rc) return rc;
+  for (int b = 0; b < nb; ++b) {
+    const PTParams& f = ps[b];
+    if (f.primary_raster) {  // every tile of the band (the host enables it only without tile subsets)
+      if (f.scene.nleaves > 0) hipLaunchKernelGGL(pr_setup, dim3((f.scene.nleaves + 255) / 256), dim3(256), 0, s, f);
+      const int rc = launch_bins(f.leaf_bins, s);
+      if (rc) return rc;
+      hipLaunchKernelGGL(wf_primary_raster, dim3(ntiles), dim3(256), 0, s, f);
+      PTParams q = f;
+      q.pr_fix = f.leaf_bins.ctr;  // ties (and an overflow) walked
+      hipLaunchKernelGGL((wf_primary<KS, DEEP>), dim3(ntiles), dim3(256), 0, s, q);
+    } else {
+      hipLaunchKernelGGL((wf_primary<KS, DEEP>), dim3(ntiles), dim3(256), 0, s, f);
+    }
+    if (f.tiles.cost) {  // this frame's primary costs -> tile order of the bounce-0 shade and the next frame
+      const int rc = launch_tile_sort(f.tiles.cost, f.tiles.perm_next, f.tiles.ntiles, s);
+      if (rc) return rc;
+    }
   }
   const int gN = (N + 255) / 256, gT = (N + kTB - 1) / kTB, gT2 = (2 * N + kTB - 1) / kTB;
   const int gS0 = ntiles;  // bounce-0 shade: one block per primary tile
-  const bool fork = aux && ev_fork && ev_join;
-  int* lists[2] = {p.wf.list0, p.wf.list1};
+  const bool fork = aux && ev_fork && ev_join && nb == 1;
+  auto lst = [&](const PTParams& f, int i) { return (i & 1) ? f.wf.list1 : f.wf.list0; };  // bounce i's live list
   const bool refill_closest = p.refill && p.closest_tree && p.prune && p.scene.bvh_any;
   auto closest = [&](int i, hipStream_t st) {
-    const int* lin = lists[(i + 1) & 1];
-    const int* live_in = p.wf.counters + kWfCtr * (i - 1);
     if (refill_closest) {
+      ListBatch lb{nb, N, {}, {}};
+      for (int b = 0; b < nb; ++b) {
+        lb.list[b] = lst(ps[b], i + 1);
+        lb.counts[b] = ps[b].wf.counters + kWfCtr * (i - 1);
+      }
       int* strag = p.wf.counters + kWfCtr * i + kCtrStragC;
-      hipLaunchKernelGGL((wf_trace_closest_refill<KS, DEEP>), dim3(refill_blocks(N)), dim3(kTB), 0, st, p,
-                         lin, live_in, cap, p.wf.counters + kWfCtr * i + kCtrQClosest, strag);
+      hipLaunchKernelGGL((wf_trace_closest_refill<KS, DEEP>), dim3(refill_blocks(nb * N)), dim3(kTB), 0, st, p, lb,
+                         cap, p.wf.counters + kWfCtr * i + kCtrQClosest, strag);
       if (p.wf.closest_budget)
         hipLaunchKernelGGL(wf_closest_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, st, p, (const int*)strag);
-    } else
-      hipLaunchKernelGGL((wf_trace_closest<KS, DEEP>), dim3(gT), dim3(kTB), 0, st, p, lin, live_in, cap);
+    } else {
+      for (int b = 0; b < nb; ++b)
+        hipLaunchKernelGGL((wf_trace_closest<KS, DEEP>), dim3(gT), dim3(kTB), 0, st, ps[b], lst(ps[b], i + 1),
+                           (const int*)(ps[b].wf.counters + kWfCtr * (i - 1)), cap);
+    }
   };
   for (int i = 0; i < p.max_depth; ++i) {
-    const int* lin = lists[(i + 1) & 1];
-    int* lout = lists[i & 1];
-    int* live = p.wf.counters + kWfCtr * i;        // kSeg live-list counts of bounce i
-    int* shadow = p.wf.counters + kWfCtr * i + kCtrHdr;  // kSeg HDR + kPointBins x kSeg point-light counts
-    const int* live_in = p.wf.counters + kWfCtr * (i > 0 ? i - 1 : 0);
     if (i > 0) {
       if (fork) {
         if ((e = hipStreamWaitEvent(s, ev_join, 0)) != hipSuccess) return (int)e;  // closest(i) done
@@ -1149,39 +1180,66 @@ int launch_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent
         closest(i, s);
       }
     }
-    hipLaunchKernelGGL(wf_shade, dim3(i == 0 ? gS0 : gN), dim3(256), 0, s, p, i, lin, live_in, lout, live,
-                       p.wf.shadow_list, shadow, cap);
+    for (int b = 0; b < nb; ++b) {
+      const PTParams& f = ps[b];
+      const int* live_in = f.wf.counters + kWfCtr * (i > 0 ? i - 1 : 0);
+      hipLaunchKernelGGL(wf_shade, dim3(i == 0 ? gS0 : gN), dim3(256), 0, s, f, i, (const int*)lst(f, i + 1), live_in,
+                         lst(f, i), f.wf.counters + kWfCtr * i, f.wf.shadow_list, f.wf.counters + kWfCtr * i + kCtrHdr,
+                         cap);
+    }
     if (fork && i + 1 < p.max_depth) {  // closest(i+1) on aux, beside shadow(i) + finish(i)
       if ((e = hipEventRecord(ev_fork, s)) != hipSuccess) return (int)e;
       if ((e = hipStreamWaitEvent(aux, ev_fork, 0)) != hipSuccess) return (int)e;
       closest(i + 1, aux);
       if ((e = hipEventRecord(ev_join, aux)) != hipSuccess) return (int)e;
     }
-    int* strag = p.wf.counters + kWfCtr * i + kCtrStrag;  // shadow rays handed to the cooperative walk
-    if (p.refill && !p.scene.bvh4)
-      hipLaunchKernelGGL((wf_trace_shadow_refill<KS, DEEP>), dim3(refill_blocks(2 * N)), dim3(kTB), 0, s, p,
-                         (const int*)p.wf.shadow_list, (const int*)shadow, cap, p.wf.counters + kWfCtr * i + kCtrQShadow,
-                         strag);
-    else if (p.scene.bvh4)
-      hipLaunchKernelGGL((wf_trace_shadow<KS, true, DEEP>), dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
-                         (const int*)shadow, cap, strag);
-    else
-      hipLaunchKernelGGL((wf_trace_shadow<KS, false, DEEP>), dim3(gT2), dim3(kTB), 0, s, p, (const int*)p.wf.shadow_list,
-                         (const int*)shadow, cap, strag);
-    if (p.wf.shadow_budget)
-      hipLaunchKernelGGL(wf_shadow_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, s, p, (const int*)strag);
-    hipLaunchKernelGGL(wf_finish, dim3(gN), dim3(256), 0, s, p, (const int*)lout, (const int*)live, cap);
+    if (p.refill && !p.scene.bvh4) {
+      ListBatch lb{nb, N, {}, {}};
+      for (int b = 0; b < nb; ++b) {
+        lb.list[b] = ps[b].wf.shadow_list;
+        lb.counts[b] = ps[b].wf.counters + kWfCtr * i + kCtrHdr;
+      }
+      int* strag = p.wf.counters + kWfCtr * i + kCtrStrag;  // shadow rays handed to the cooperative walk
+      hipLaunchKernelGGL((wf_trace_shadow_refill<KS, DEEP>), dim3(refill_blocks(2 * nb * N)), dim3(kTB), 0, s, p, lb,
+                         cap, p.wf.counters + kWfCtr * i + kCtrQShadow, strag);
+      if (p.wf.shadow_budget)
+        hipLaunchKernelGGL(wf_shadow_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, s, p, (const int*)strag);
+    } else {
+      for (int b = 0; b < nb; ++b) {
+        const PTParams& f = ps[b];
+        const int* shadow = f.wf.counters + kWfCtr * i + kCtrHdr;
+        int* strag = f.wf.counters + kWfCtr * i + kCtrStrag;
+        if (f.scene.bvh4)
+          hipLaunchKernelGGL((wf_trace_shadow<KS, true, DEEP>), dim3(gT2), dim3(kTB), 0, s, f,
+                             (const int*)f.wf.shadow_list, shadow, cap, strag);
+        else
+          hipLaunchKernelGGL((wf_trace_shadow<KS, false, DEEP>), dim3(gT2), dim3(kTB), 0, s, f,
+                             (const int*)f.wf.shadow_list, shadow, cap, strag);
+        if (f.wf.shadow_budget)
+          hipLaunchKernelGGL(wf_shadow_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, s, f, (const int*)strag);
+      }
+    }
+    for (int b = 0; b < nb; ++b)
+      hipLaunchKernelGGL(wf_finish, dim3(gN), dim3(256), 0, s, ps[b], (const int*)lst(ps[b], i),
+                         (const int*)(ps[b].wf.counters + kWfCtr * i), cap);
   }
-  hipLaunchKernelGGL(wf_finalize, dim3(gN), dim3(256), 0, s, p);
+  for (int b = 0; b < nb; ++b) hipLaunchKernelGGL(wf_finalize, dim3(gN), dim3(256), 0, s, ps[b]);
   return (int)hipGetLastError();
 }
 
 int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent_t ev_fork,
                                hipEvent_t ev_join) {
   // the LDS stack bounds resident waves: a tree that fits the small stack gets more of them
-  if (p.wf.spill) return launch_wavefront<kStack, true>(p, s, nullptr, nullptr, nullptr);  // deep tree, no fork
-  return p.stack_need <= kStackSmall ? launch_wavefront<kStackSmall, false>(p, s, aux, ev_fork, ev_join)
-                                     : launch_wavefront<kStack, false>(p, s, aux, ev_fork, ev_join);
+  if (p.wf.spill) return launch_wavefront<kStack, true>(&p, 1, s, nullptr, nullptr, nullptr);  // deep tree, no fork
+  return p.stack_need <= kStackSmall ? launch_wavefront<kStackSmall, false>(&p, 1, s, aux, ev_fork, ev_join)
+                                     : launch_wavefront<kStack, false>(&p, 1, s, aux, ev_fork, ev_join);
+}
+
+int launch_pathtrace_wavefront_batch(const PTParams* ps, int nb, hipStream_t s) {
+  if (nb < 1 || nb > kMaxBatch) return (int)hipErrorInvalidValue;
+  if (ps[0].wf.spill) return launch_wavefront<kStack, true>(ps, nb, s, nullptr, nullptr, nullptr);
+  return ps[0].stack_need <= kStackSmall ? launch_wavefront<kStackSmall, false>(ps, nb, s, nullptr, nullptr, nullptr)
+                                         : launch_wavefront<kStack, false>(ps, nb, s, nullptr, nullptr, nullptr);
 }
 
 }  // namespace ptk

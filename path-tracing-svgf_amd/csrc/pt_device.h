@@ -134,6 +134,17 @@ enum { kStatPrimRays, kStatPrimVisits, kStatBounceRays, kStatBounceVisits, kStat
        kStatTieRewalks, kStatPrimRetries, kStatSpills, kStatPrimSlots, kStatBounceSlots, kStatShadowSlots,
        kStatCount };
 
+// A path-tracing draw over several frames' pixels (pt_pass_draw_batch): frame b's pixels are the pids
+// [b * n, (b + 1) * n) of one shared per-pixel wavefront state; its lists hold frame-local pids. The list-driven
+// traversal kernels take every frame's list of a bounce at once, so one launch traces the whole batch's rays.
+constexpr int kMaxBatch = 8;
+struct ListBatch {
+  int nb;               // frames
+  int n;                // pixels per frame (the pid offset of frame b is b * n)
+  const int* list[kMaxBatch];
+  const int* counts[kMaxBatch];
+};
+
 // Screen-tile binning of items (the G-buffer's triangles, the path tracer's BVH leaves) for the tile rasterisers:
 // an item-specific setup kernel writes each item's pixel box and counts it into the 16 x 16 tiles of the band it
 // covers (bins_count_item); launch_bins then bins the large items, scans and scatters (kernels_pt.hip).
@@ -260,6 +271,8 @@ int wf_subset_tiles(int W, int rows, int stride, int offset);  // tiles of a PTP
 int launch_gbuffer(const GBufParams& p, hipStream_t s);
 int launch_gbuffer_raster(const GBufParams& p, hipStream_t s);  // bins, resolves, and the ray cast on overflow
 int launch_bins(const Bins& b, hipStream_t s);  // after the item setup kernel: large items, scan, scatter
+// nb frames' path tracing with batched traversal launches (ps[b]: frame b, its wavefront state at pid offset b * n)
+int launch_pathtrace_wavefront_batch(const PTParams* ps, int nb, hipStream_t s);
 int launch_reproject(const ReprojParams& p, hipStream_t s);
 int launch_variance(const VarianceParams& p, hipStream_t s);
 int launch_atrous_exact(const AtrousParams& p, hipStream_t s);

@@ -107,6 +107,7 @@ _PT_SIGS = [
     ("pt_pass_set_motion_bound", C.c_int, [_u32, C.c_void_p]),
     ("pt_pass_set_trace_stats", C.c_int, [_u32, C.c_void_p]),
     ("pt_pass_draw", C.c_int, [_u32]),
+    ("pt_pass_draw_batch", C.c_int, [C.POINTER(_u32), C.c_int]),
     ("pt_pass_last_ms", C.c_int, [_u32, _fp]),
     ("pt_pass_destroy", C.c_int, [_u32]),
 ]

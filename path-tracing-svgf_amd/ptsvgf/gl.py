@@ -108,6 +108,12 @@ def texture_info(tex: int):
     return w.value, h.value, r0.value
 
 
+def draw_batch(passes) -> None:
+    """pt_pass_draw_batch: the frames of up to 8 path-tracing passes in one run, their traversals batched."""
+    hs = (C.c_uint32 * len(passes))(*[p._handle() for p in passes])
+    check(pt().pt_pass_draw_batch(hs, len(passes)))
+
+
 def readback(tex: int) -> np.ndarray:
     """Stored rows of an RGBA32F texture as (rows, W, 4) float32."""
     w, rows, _ = texture_info(tex)

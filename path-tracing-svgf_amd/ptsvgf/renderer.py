@@ -57,7 +57,8 @@ class Renderer:
     def __init__(self, scene: Scene, width: int, height: int, config: parameter_config | None = None,
                  mode: str = "fast", aspect_corrected: bool | None = None, band=None, prune: bool = True,
                  atrous_exact: bool = False, run_taa: bool = True, run_output: bool = True, tex_factory=None,
-                 halo=None, gbuffer_rows=None, frames_in_flight: int = 1, after_gbuffer=None, back_lag: int = 0):
+                 halo=None, gbuffer_rows=None, frames_in_flight: int = 1, after_gbuffer=None, back_lag: int = 0,
+                 trace_batch: int = 1):
         """band = (y0, y1, row0, rows) for screen-band sharding; tex_factory(w, h) -> handle allocates the
         frame-sized planes (ptsvgf.dist wraps torch tensors); halo(stage, {plane name: handle}) is called before
         the SVGF passes that read rows beyond the band (dist.HALO_SCHEDULE names the planes); after_gbuffer(set,
@@ -76,7 +77,12 @@ class Renderer:
         back end of frame f - D, so a host wait before a back-end pass (the band renderer's motion bound, read
         from the G-buffer before the reprojection exchange is sized) finds a G-buffer issued D frames earlier
         instead of stalling the issue of the next front end. planes() and time_atrous() first issue the back
-        ends still pending (flush); results are those of D = 0."""
+        ends still pending (flush); results are those of D = 0.
+
+        trace_batch = B (2..8, at most K, frames in flight only): the path tracer of B consecutive frames runs as
+        one batched draw (pt_pass_draw_batch) issued with the last of them — its list-driven traversal launches
+        trace all B frames' rays at once, so a thin band's launches carry B times the rays. The back lag is raised
+        to at least B - 1 (a frame's back end needs its batch). Same bits."""
         if mode not in ("fast", "reference"):
             raise ValueError(mode)
         self.mode = mode
@@ -127,9 +133,13 @@ class Renderer:
         self.K = int(frames_in_flight)
         if self.K < 1 or (self.K > 1 and mode != "fast"):
             raise ValueError("frames_in_flight must be >= 1, and > 1 only with the fast driver")
-        self.lag = int(back_lag)
+        self.B = int(trace_batch)
+        if not 1 <= self.B <= min(self.K, 8) or (self.B > 1 and mode != "fast"):
+            raise ValueError(f"trace_batch must be in [1, min(frames_in_flight, 8)] (fast driver), got {trace_batch}")
+        self.lag = max(int(back_lag), self.B - 1)
         if not 0 <= self.lag < self.K:
             raise ValueError(f"back_lag must be in [0, frames_in_flight) = [0, {self.K}), got {back_lag}")
+        self._batch: list = []  # path-tracing passes of the open batch: (pass, G-buffer-done event, stream, holder)
         self._pending: list = []  # front ends whose back end is not issued yet (back_lag)
         # a serial renderer draws on torch's stream of its construction, whatever stream another renderer in the
         # process left the library on (the library's stream is process-global, pt_set_stream)
@@ -272,6 +282,7 @@ class Renderer:
             p.set_uniform_int("prune", int(self._pt_prune))
             # lane-refill traversal waves: +8 % frames/s with frames in flight, -6 % serial (kernels_wavefront.hip)
             p.set_uniform_int("trace_refill", 75 if self.K > 1 else 0)
+            p.set_uniform_int("trace_batch", self.B)
             self.pt_slots.append((p, outs))
         self.pass_path_tracing = PassGroup([p for p, _ in self.pt_slots])  # settings apply to every slot
 
@@ -352,7 +363,32 @@ class Renderer:
         if hint is not None:
             pt.set_texture_uniform(GL_TEXTURE_2D, hint["world"], "gWorldPos")
             pt.set_texture_uniform(GL_TEXTURE_2D, hint["normal_depth"], "gNormalAndLinearZ")
+        if self._batching():
+            return  # drawn with its batch (_front_fast)
         self._draw(pt, "pathtrace")
+
+    def _batching(self) -> bool:
+        return self.B > 1 and self.mode == "fast" and not self.cfg.accumulate_color
+
+    def _issue_batch(self) -> None:
+        """Draw the open batch's path tracers on the stream of its last frame, after all its G-buffers."""
+        if not self._batch:
+            return
+        import torch
+
+        stream = self._batch[-1][2]
+        for _, ev, _, _ in self._batch:
+            stream.wait_event(ev)
+        self._stream_to(stream)
+        passes = [p for p, _, _, _ in self._batch]
+        gl.draw_batch(passes)
+        if self._profile:
+            self._times.setdefault("pathtrace", []).append(passes[0].last_ms())
+        done = torch.cuda.Event()
+        done.record(stream)
+        for _, _, _, holder in self._batch:
+            holder["ev"] = done
+        self._batch = []
 
     def _frame_reference(self):
         cfg = self.cfg
@@ -461,6 +497,12 @@ class Renderer:
             done = torch.cuda.Event()
             done.record(fe)
             self._fe_prev = done
+            if self._batching():  # the path tracer waits for its batch; the back end for the batch's draw
+                holder = {}
+                self._batch.append((self.pt_pass, done, fe, holder))
+                done = holder
+                if len(self._batch) == self.B:
+                    self._issue_batch()
         else:
             self._gbuffer_and_pt(f % ng)
         return dict(f=f, slot=s, done=done, frame_counter=self.camera.frameCounter)
@@ -476,7 +518,12 @@ class Renderer:
         _, (color, emission, albedo) = self.pt_slots[ctx["slot"]]
         self.back_set = f % ng
         if self.K > 1:
-            self._back.wait_event(ctx["done"])
+            done = ctx["done"]
+            if isinstance(done, dict):  # batched path tracer: its batch must have been drawn
+                if "ev" not in done:
+                    self._issue_batch()
+                done = done["ev"]
+            self._back.wait_event(done)
             self._stream_to(self._back)
         self._halo("reproject", {"prev_illum": self.hist_illum[pb], "prev_moments": self.moments[pb],
                                  "prev_nd": gp["normal_depth"]})
@@ -590,11 +637,13 @@ class Renderer:
         import torch
 
         buf = torch.zeros(len(self.STAT_KEYS), dtype=torch.int64, device="cuda")
+        self.flush()  # frames already issued are not counted
         torch.cuda.synchronize()
         for p, _ in self.pt_slots:
             p.set_trace_stats(buf.data_ptr())
         try:
             self.frame()
+            self._issue_batch()  # this frame alone
             torch.cuda.synchronize()
         finally:
             for p, _ in self.pt_slots:
@@ -658,7 +707,8 @@ class Renderer:
         self.frame_index += 1
 
     def flush(self) -> None:
-        """Issue the back ends still pending (back_lag)."""
+        """Issue the open path-tracing batch and the back ends still pending (back_lag)."""
+        self._issue_batch()
         while self._pending:
             self._finish(self._pending.pop(0))
 

@@ -29,7 +29,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, outdir, moving, balance, fif=1, size=(W, H), bench_scene=False, moves=None):
+def _worker(rank, world, port, outdir, moving, balance, fif=1, size=(W, H), bench_scene=False, moves=None, batch=1):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(os.path.dirname(here), "path-tracing-svgf_amd"))
@@ -48,7 +48,7 @@ def _worker(rank, world, port, outdir, moving, balance, fif=1, size=(W, H), benc
     scene = _scene(bench_scene)
     Wf, Hf = size
     r = make_band_renderer(scene, Wf, Hf, parameter_config(), rank, world, dist, balance=balance, run_taa=True,
-                           frames_in_flight=fif)
+                           frames_in_flight=fif, trace_batch=batch)
     for f in range(len(moves) if moves else FRAMES):
         mv = moves[f] if moves else ((1.5, 0.5) if moving and f else None)
         if mv:
@@ -81,8 +81,9 @@ def _compare(bands, want):
             assert len(bad) == 0, (k, y0, y1)
 
 
-@pytest.mark.parametrize("moving,balance,fif", [(False, False, 1), (True, False, 1), (True, True, 1), (True, True, 3)])
-def test_two_bands_equal_full_frame(gpu, moving, balance, fif):
+@pytest.mark.parametrize("moving,balance,fif,batch", [(False, False, 1, 1), (True, False, 1, 1), (True, True, 1, 1),
+                                                      (True, True, 3, 1), (True, True, 4, 4)])
+def test_two_bands_equal_full_frame(gpu, moving, balance, fif, batch):
     import torch.multiprocessing as mp
 
     from ptsvgf.camera import parameter_config
@@ -91,7 +92,7 @@ def test_two_bands_equal_full_frame(gpu, moving, balance, fif):
 
     gl = gpu
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(2, _port(), d, moving, balance, fif), nprocs=2, join=True)
+        mp.spawn(_worker, args=(2, _port(), d, moving, balance, fif, (W, H), False, None, batch), nprocs=2, join=True)
         bands = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(2)]
     scene = build_scene("table_clock_plant", hdr_size=(256, 128), plant_leaves=40)
     full = Renderer(scene, W, H, parameter_config(), mode="fast", aspect_corrected=True, run_taa=True,

@@ -60,7 +60,8 @@ def test_deep_reference_bvh_matches_oracle(gpu, scene_cornell):
     deep = dataclasses.replace(scene_cornell, name="cornell_chain", tri_enc=tri, node_enc=chain_bvh(tri))
     W, H = 64, 48
     ref = O.OracleFrameLoop(deep, W, H, run_taa=False)
-    want = [ref.frame() for _ in range(2)]
+    want = [ref.frame() for _ in range(3)]
+    ref3 = want[2]
     # production switches (closest hits on the SAH tree over these leaves, exact ties re-walked on the chain), then
     # every walk on the chain itself (closest_tree = shadow_tree = 0): the spill path carries those
     for switches in ({}, {"closest_tree": 0, "shadow_tree": 0}):
@@ -75,6 +76,13 @@ def test_deep_reference_bvh_matches_oracle(gpu, scene_cornell):
         if switches:
             assert st["spills"] > 0, st  # rays went past the 32-entry LDS stack
         r.close()
+    # the spill columns of a batch (global pids): 3 frames drawn as one batch, frames in flight
+    rb = Renderer(deep, W, H, mode="fast", run_taa=False, run_output=False, frames_in_flight=3, trace_batch=3)
+    for _ in range(3):
+        rb.frame()
+    rb.flush()
+    _check_bits(_pt_planes(gl, rb), {k: ref3[k] for k in ("color", "emission", "albedo")}, "batch")
+    rb.close()
     r = Renderer(deep, W, H, mode="fast", run_taa=False, run_output=False)
     r.pass_path_tracing.set_uniform_int("pt_kernel", 1)
     with pytest.raises(PtError, match="megakernel"):

@@ -339,16 +339,18 @@ def test_accumulate_fast_equals_reference(gpu, scene_small, K):
     b.close()
 
 
-@pytest.mark.parametrize("K,lag", [(2, 0), (3, 0), (3, 1), (4, 3)])
-def test_frames_in_flight_equal_serial(gpu, scene_small, K, lag):
+@pytest.mark.parametrize("K,lag,B", [(2, 0, 1), (3, 0, 1), (3, 1, 1), (4, 3, 1), (4, 0, 2), (4, 3, 4), (8, 0, 8)])
+def test_frames_in_flight_equal_serial(gpu, scene_small, K, lag, B):
     """K frames in flight (front ends on K streams, SVGF chain on a back-end stream; with back_lag the back end
-    issued `lag` frames behind the front end) give the serial fast driver's bits: per frame (read back after each
-    frame) and after K+3 frames issued without any host wait (moving camera, so every frame's inputs differ)."""
+    issued `lag` frames behind the front end; with trace_batch B the path tracers of B frames drawn as one batch
+    whose traversal launches trace all their rays) give the serial fast driver's bits: per frame (read back after
+    each frame: a partial batch is drawn) and after K+3 frames issued without any host wait (moving camera, so
+    every frame's inputs differ)."""
     gl = gpu
     W, H = 96, 64
     kw = dict(mode="fast", run_taa=True, run_output=True)
     a = _renderer(scene_small, W, H, **kw)
-    b = _renderer(scene_small, W, H, frames_in_flight=K, back_lag=lag, **kw)
+    b = _renderer(scene_small, W, H, frames_in_flight=K, back_lag=lag, trace_batch=B, **kw)
     keys = ("normal_depth", "color", "albedo", "reproj_illum", "variance", "atrous", "modulate", "final", "output")
     for f in range(K + 2):
         for r in (a, b):

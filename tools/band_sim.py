@@ -63,11 +63,14 @@ cfg = parameter_config()
 
 def sim_rank(rk, bounds, probe=False, K=30):
     r = D.BandRenderer(scene, W, H, cfg, rk, N, FakeDist(), bounds=bounds,
-                       frames_in_flight=int(os.environ.get("FIF", "1")))
+                       frames_in_flight=int(os.environ.get("FIF", "1")), trace_batch=int(os.environ.get("BATCH", "1")))
     r.pass_path_tracing.set_uniform_int("pt_kernel", int(os.environ.get("PTK", "0")))
     r.pass_path_tracing.set_uniform_int("trace_fork", int(os.environ.get("PTSVGF_TRACE_FORK", "0")))
     if "SHADOW_BUDGET" in os.environ:
         r.pass_path_tracing.set_uniform_int("shadow_budget", int(os.environ["SHADOW_BUDGET"]))
+    for kv in filter(None, os.environ.get("PT_UNIFORMS", "").split(",")):  # name=value,... on the path tracer
+        name, val = kv.split("=")
+        r.pass_path_tracing.set_uniform_int(name, int(val))
     for _ in range(max(3, 2 * r.r.K)):  # every frame slot used before timing (first use allocates)
         r.frame()
     torch.cuda.synchronize()
@@ -109,8 +112,8 @@ def report(tag, res):
     print(f"--- {tag}: N={N} {W}x{H}")
     for rk, s in enumerate(res):
         print(f"rank {rk}: rows {s['y0']}..{s['y1']} ({s['y1'] - s['y0']}) wall {s['wall']:.3f} ms gpu {s['gpu']:.3f} "
-              f"issue {s['issue']:.3f}  gbuf {s['pp']['gbuffer']:.3f} pt {s['pp']['pathtrace']:.3f} "
-              f"svgf {s['gpu'] - s['pp']['gbuffer'] - s['pp']['pathtrace']:.3f}  halo {s['nex']:.0f}x "
+              f"issue {s['issue']:.3f}  gbuf {s['pp'].get('gbuffer', 0):.3f} pt {s['pp'].get('pathtrace', 0):.3f} "
+              f"svgf {s['gpu'] - s['pp'].get('gbuffer', 0) - s['pp'].get('pathtrace', 0):.3f}  halo {s['nex']:.0f}x "
               f"{s['xbytes'] / 1e6:.2f} MB")
     mx = max(s["wall"] for s in res)
     print(f"predicted frame (slowest rank, no exchange time): {mx:.3f} ms = {1e3 / mx:.1f} fps; "
