@@ -296,11 +296,32 @@ __global__ void __launch_bounds__(256) pr_setup(PTParams p) {
                   cz = (m[8] * X + m[9] * Y) + m[10] * Z;
       C[k] = make_float3(cx / sx, cy, -cz);
     }
-    const int F[6][4] = {{0, 2, 6, 4}, {1, 3, 7, 5}, {0, 1, 5, 4}, {2, 3, 7, 6}, {0, 1, 3, 2}, {4, 5, 7, 6}};
+    // every corner inside the widened frustum (poly_box's clip planes) and in front: no clipping happens, and the
+    // box's projection is the hull of its corners' projections (all w > 0)
+    bool front = true;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      front = front && C[k].z > 0.0f && fabsf(C[k].x) <= 1.01f * C[k].z && fabsf(C[k].y) <= 1.01f * C[k].z;
+    constexpr int F[6][4] = {{0, 2, 6, 4}, {1, 3, 7, 5}, {0, 1, 5, 4}, {2, 3, 7, 6}, {0, 1, 3, 2}, {4, 5, 7, 6}};
     int4 u = make_int4(1, 1, 0, 0);
     float w = 3.0e38f;
     bool any = false;
-    for (int f = 0; f < 6; ++f) {
+    if (front) {  // nothing to clip: the box of the corners' projections (poly_box's arithmetic, unrolled)
+      float x0 = 3.0e38f, y0 = 3.0e38f, x1 = -3.0e38f, y1 = -3.0e38f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float px = ((C[k].x / C[k].z + 1.0f) * (float)p.W - 1.0f) * 0.5f;
+        const float py = ((C[k].y / C[k].z + 1.0f) * (float)p.H - 1.0f) * 0.5f;
+        x0 = fminf(x0, px); x1 = fmaxf(x1, px);
+        y0 = fminf(y0, py); y1 = fmaxf(y1, py);
+        w = fminf(w, C[k].z);
+      }
+      u = pixel_box(p.leaf_bins, x0, y0, x1, y1);
+      any = !(u.x > u.z || u.y > u.w);
+    }
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {  // (unrolled: the corner indices stay compile-time, C in registers)
+      if (front) break;
       float3 A[16];
 #pragma unroll
       for (int k = 0; k < 4; ++k) A[k] = C[F[f][k]];
