@@ -175,6 +175,11 @@ def config0(gl):
 
 def main():
     args = parse()
+    # stdout carries the one JSON line only: native libraries (gloo's connection messages, HIP) print to file
+    # descriptor 1, so it is pointed at stderr for the run and the JSON line goes to the saved descriptor
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import numpy as np
     import torch
 
@@ -393,7 +398,8 @@ def main():
             line["max_history_rows"] = res["max_history_rows"]
         if "bands" in res:
             line["bands"] = res["bands"]
-        print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     gl.shutdown()
     if dist:
         dist.destroy_process_group()

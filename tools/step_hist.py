@@ -35,5 +35,5 @@ t = s.reshape(H // 8, 8, W // 8, 8).max(axis=(1, 3))
 print("8x8 tile max percentiles 50/99/max:", [int(np.percentile(t, q)) for q in (50, 99)], int(t.max()))
 rows = s.max(axis=1)
 print("row max by 270-row band:", [int(rows[i:i + 270].max()) for i in range(0, H, 270)])
-np.save("/tmp/steps.npy", s)
+np.save(os.path.join(REPO, "gpurun_out", "steps.npy"), np.minimum(s, 65535).astype(np.uint16))
 gl.shutdown()
