@@ -165,18 +165,42 @@ __global__ void __launch_bounds__(256) reproject_kernel(ReprojParams p) {
 }
 
 // -------------------------------------------------------------- variance ---
+// Per 16 x 16 block: a pixel with a long history (or the background) copies its illumination (32 B read, 16 B
+// written); the 7x7 spatial estimate (svgf_variance.frag:58-110, young histories) reads its taps from the block's
+// illumination, moments and normal/depth staged once in LDS with a 3-texel apron — only in blocks where some pixel
+// needs it. Same taps in the same order as the per-pixel form.
+constexpr int kVT = 16 + 2 * 3;
 __global__ void __launch_bounds__(256) variance_kernel(VarianceParams p) {
-  int x = blockIdx.x * 16 + (threadIdx.x & 15);
-  int y = p.y0 + blockIdx.y * 16 + (threadIdx.x >> 4);
-  if (x >= p.W || y >= p.y1) return;
-  float h = ldp(p.moments, x, y).z;
-  float4 ic = ldp(p.illum, x, y);
-  if (!(h < 4.0f)) {
-    stp(p.out, x, y, ic);
+  __shared__ float4 s_il[kVT * kVT], s_mo[kVT * kVT], s_nd[kVT * kVT];
+  const int bx = blockIdx.x * 16, by = p.y0 + blockIdx.y * 16;
+  const int x = bx + (threadIdx.x & 15), y = by + (threadIdx.x >> 4);
+  const bool valid = x < p.W && y < p.y1;
+  float h = 4.0f;
+  float4 ic = make_float4(0.0f, 0.0f, 0.0f, 0.0f), nd = ic;
+  bool need = false;
+  if (valid) {
+    h = ldp(p.moments, x, y).z;
+    ic = ldp(p.illum, x, y);
+    if (h < 4.0f) {
+      nd = ldp(p.nd, x, y);
+      need = nd.w != 1.0f;
+    }
+  }
+  if (!__syncthreads_or(need)) {  // nothing to filter in this block
+    if (valid) stp(p.out, x, y, ic);
     return;
   }
-  float4 nd = ldp(p.nd, x, y);
-  if (nd.w == 1.0f) {
+  for (int i = threadIdx.x; i < kVT * kVT; i += 256) {  // texels outside the frame are never read
+    const int tx = bx - 3 + i % kVT, ty = by - 3 + i / kVT;
+    if (tx >= 0 && tx < p.W && ty >= 0 && ty < p.H) {
+      s_il[i] = ldp(p.illum, tx, ty);
+      s_mo[i] = ldp(p.moments, tx, ty);
+      s_nd[i] = ldp(p.nd, tx, ty);
+    }
+  }
+  __syncthreads();
+  if (!valid) return;
+  if (!need) {
     stp(p.out, x, y, ic);
     return;
   }
@@ -190,9 +214,10 @@ __global__ void __launch_bounds__(256) variance_kernel(VarianceParams p) {
     for (int xx = -3; xx <= 3; ++xx) {
       int px = x + xx;
       if (px < 0 || px >= p.W) continue;
-      float4 ip = ldp(p.illum, px, py);
-      float4 mp = ldp(p.moments, px, py);
-      float4 q = ldp(p.nd, px, py);
+      const int li = (py - (by - 3)) * kVT + (px - (bx - 3));
+      float4 ip = s_il[li];
+      float4 mp = s_mo[li];
+      float4 q = s_nd[li];
       float len = f_sqrt((float)(xx * xx) + (float)(yy * yy));
       float w = edge_weight(nd.w, q.w, phiDepth * len, nc, mk(q.x, q.y, q.z), p.phi_normal, lc,
                             lum(ip.x, ip.y, ip.z), p.phi_color);
