@@ -188,8 +188,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         world = args.gpus if world == 1 and args.gpus == 1 else world
+    k1080 = args.frames_in_flight  # 1080p: 6 frames in flight by default on one GPU (4 / 6 / 8: 512 / 538 / 536 fps)
     if args.frames_in_flight is None:
         args.frames_in_flight = 4 if world == 1 else 8
+        k1080 = 6 if world == 1 else 8
     if args.trace_batch is None:
         args.trace_batch = 1
     # every frame slot must have run once before the timed region (a slot's first frame allocates its
@@ -348,9 +350,10 @@ def main():
         extra["fps_serial"] = round(args.steps / ser["dt"], 3)
         extra["ms_per_step_serial"] = round(ser["dt"] / args.steps * 1e3, 3)
     if not args.no_1080p and (W, H) == (3840, 2160):
-        r2 = run(1920, 1080, K, args.view)
+        r2 = run(1920, 1080, k1080, args.view)
         fps2 = args.steps / r2["dt"]
         extra.update({"fps_1080p": round(fps2, 3), "ms_per_step_1080p": round(r2["dt"] / args.steps * 1e3, 3),
+                      "frames_in_flight_1080p": k1080,
                       "roofline_1080p": atrous_roofline(r2, 1920, r2["rows"])})
         if not args.no_extras and world == 1 and K > 1:
             s2 = run(1920, 1080, 1, args.view, probes=False)
