@@ -50,6 +50,7 @@ REPROJ_REACH = 3  # rows beyond |motion| the history taps reach: bilinear + 1-te
 TAA_NEIGHBOURS = 2  # rows of the TAA 3x3 neighbourhood: +-1 texel, plus the LINEAR sampler's zero-weight row
 GHOST = 96        # default stored rows either side of a band (storage only); motion up to GHOST - 3 rows per frame
 MIN_BAND_ROWS = 16
+BAND_VISIT_BUDGET = 256  # shadow / closest-hit visits before a band's ray goes to the cooperative walk
 
 # stage -> ((plane, rows), ...) exchanged before that stage; rows: int, or "reproj" / "reproj_nd" (set from this
 # frame's motion bound) / "nd" (the widest a-trous halo of the configured iterations)
@@ -267,6 +268,12 @@ class BandRenderer:
         self.motion_log = []  # per frame: (all-reduced |motion.y| in rows, history rows exchanged)
         self.camera = self.r.camera
         self.pass_path_tracing = self.r.pass_path_tracing
+        if self.r.K > 1:
+            # a band's traversal launches end on a few long rays: past 256 visits a ray is finished by a
+            # wave-cooperative walk (same bits; simulated 8-band frame 1.22 -> 1.08 ms; the one-GPU frame, whose
+            # launches are full, keeps them off)
+            self.pass_path_tracing.set_uniform_int("shadow_budget", BAND_VISIT_BUDGET)
+            self.pass_path_tracing.set_uniform_int("closest_budget", BAND_VISIT_BUDGET)
 
     def _after_gbuffer(self, b: int, stream) -> None:
         """The G-buffer of set b was issued on `stream`: fetch its motion bound behind it (no wait here)."""
