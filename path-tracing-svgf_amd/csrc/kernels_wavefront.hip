@@ -196,6 +196,7 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
     if (p.pr_fix[2]) {
       if (threadIdx.x == 0) p.leaf_bins.tile_count[gt] = 0;  // the skipped scatter did not count them back to zero
     } else {
+      if (p.closest_tree) return;  // the flagged pixels went to wf_primary_coop
       valid = valid && ldnt(&p.wf.hit[pid]).x == kTieFix;
       if (!__any(valid)) return;
       count_ray = false;  // counted by the rasteriser
@@ -401,8 +402,17 @@ __global__ void __launch_bounds__(256) wf_primary_raster(PTParams p) {
       });
     }
   }
-  const bool walk = tied || (best < 0 && bound < PT_INF);  // a tie, or nothing below the G-buffer bound
+  const bool walk = valid && (tied || (best < 0 && bound < PT_INF));  // a tie, or nothing below the G-buffer bound
   if (valid) stnt(&p.wf.hit[pid], walk ? make_int2(kTieFix, 0) : make_int2(best, __float_as_int(tbest)));
+  if (p.closest_tree) {  // flagged pixels: the wave-cooperative closest-hit walk (wf_primary_coop)
+    const unsigned long long m = __ballot(walk);
+    if (m) {
+      int base = 0;
+      if (ln == __ffsll((long long)m) - 1) base = atomicAdd(p.wf.counters + kCtrStragC, __popcll(m));
+      base = __shfl(base, __ffsll((long long)m) - 1);
+      if (walk) p.wf.strag_c[base + __popcll(m & ((1ull << ln) - 1ull))] = pid;
+    }
+  }
   stat_add(p, kStatPrimRays, valid ? 1u : 0u);
   stat_add(p, kStatPrimVisits, steps);
   stat_slots(p, kStatPrimSlots, steps);
@@ -925,6 +935,30 @@ __global__ void __launch_bounds__(64 * kCoopWaves) wf_closest_coop(PTParams p, c
   stat_add(p, kStatTieRewalks, nrewalk);
 }
 
+// The primary rays wf_primary_raster flagged (an exact-t tie, or no hit below the G-buffer bound): one wave per ray
+// (closest_coop_walk: closest_hit's answer, unbounded, ties walked on the reference tree).
+__global__ void __launch_bounds__(64 * kCoopWaves) wf_primary_coop(PTParams p, const int* __restrict__ strag_count) {
+  __shared__ int st[kCoopWaves][kCoopCap];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n = *strag_count;
+  uint32_t nrewalk = 0, nretry = 0;
+  for (int r = blockIdx.x * kCoopWaves + wv; r < n; r += gridDim.x * kCoopWaves) {
+    const int pid = p.wf.strag_c[r];
+    const int x = pid % p.W, y = p.y0 + pid / p.W;
+    const v3 S = mk(p.eye[0], p.eye[1], p.eye[2]);
+    float t;
+    bool rw;
+    const int tri = closest_coop_walk(p.scene, st[wv], kCoopCap, S, primary_dir(p, x, y), &t, &rw);
+    if ((threadIdx.x & 63) == 0) {
+      stnt(&p.wf.hit[pid], make_int2(tri, __float_as_int(t)));
+      nrewalk += rw ? 1u : 0u;
+      ++nretry;
+    }
+  }
+  stat_add(p, kStatTieRewalks, nrewalk);
+  stat_add(p, kStatPrimRetries, nretry);
+}
+
 // shade()'s MIS combination (:950-966) for given shadow verdicts: hdriLight zeroes
 // its value and pdf when occluded, calculatePointLight only its value.
 struct NeeTerms {
@@ -1159,6 +1193,9 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, hipStream_t aux,
       const int rc = launch_bins(f.leaf_bins, s);
       if (rc) return rc;
       hipLaunchKernelGGL(wf_primary_raster, dim3(ntiles), dim3(256), 0, s, f);
+      if (f.closest_tree)
+        hipLaunchKernelGGL(wf_primary_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, s, f,
+                           (const int*)(f.wf.counters + kCtrStragC));
       PTParams q = f;
       q.pr_fix = f.leaf_bins.ctr;  // ties (and an overflow) walked
       hipLaunchKernelGGL((wf_primary<KS, DEEP>), dim3(ntiles), dim3(256), 0, s, q);

@@ -68,12 +68,13 @@ def test_raster_band_rows_and_overflow_fallback(gpu, scene_small):
           _render(gpu, scene_small, W, H, 0, MOVES, keys=keys), "overflow")
 
 
-def _pt(gl, scene, W, H, raster, moves, cap=0):
+def _pt(gl, scene, W, H, raster, moves, cap=0, tree=1):
     from ptsvgf.renderer import Renderer
 
     r = Renderer(scene, W, H, mode="fast", aspect_corrected=W != H, run_taa=False, run_output=False)
     r.pass_path_tracing.set_uniform_int("primary_raster", raster)
     r.pass_path_tracing.set_uniform_int("raster_pair_cap", cap)
+    r.pass_path_tracing.set_uniform_int("closest_tree", tree)
     out = []
     for mv in moves:
         if mv:
@@ -88,15 +89,20 @@ def _pt(gl, scene, W, H, raster, moves, cap=0):
 @pytest.mark.parametrize("scene_name", ["scene_small", "scene_cornell", "scene_nan"])
 def test_primary_raster_equals_walk(gpu, scene_name, request):
     """Primary rays by tile-binned reference leaves (wf_primary_raster, the default) give the per-pixel walk's bits
-    (wf_primary), through camera moves; with a pair list too small for the frame every pixel is walked instead."""
+    (wf_primary), through camera moves. The pixels the rasteriser flags (ties, nothing below the G-buffer bound)
+    go to the wave-cooperative walk (wf_primary_coop) with the SAH tree on, to wf_primary's fixup without it; with
+    a pair list too small for the frame every pixel is walked instead."""
     scene = request.getfixturevalue(scene_name)
     W, H = 160, 96
     want, st0 = _pt(gpu, scene, W, H, 0, MOVES)
     got, st1 = _pt(gpu, scene, W, H, 1, MOVES)
     _same(got, want, scene_name)
     assert st1["primary_rays"] == st0["primary_rays"] == W * H, (st0, st1)
+    print(scene_name, "flagged primary pixels:", st1["primary_retries"], "tie rewalks:", st1["tie_rewalks"])
     over, _ = _pt(gpu, scene, W, H, 1, MOVES, cap=4)
     _same(over, want, scene_name + "/overflow")
+    no_tree, _ = _pt(gpu, scene, W, H, 1, MOVES, tree=0)
+    _same(no_tree, want, scene_name + "/no-tree")
 
 
 def test_primary_raster_equals_walk_bench_scene_1080p(gpu, scene_bench):
