@@ -1240,6 +1240,8 @@ int draw_svgf(Pass* p, int kind) {
     else if (ui(p, "atrous_variant", 0) == 1) rc = launch_atrous_simple(k, g.stream);  // A/B: generic
     else if (ui(p, "atrous_variant", 0) == 2) rc = launch_atrous_step(k, g.stream);    // A/B: step kernel
     else if (ui(p, "atrous_variant", 0) == 3) rc = launch_atrous_pair(k, g.stream);    // A/B: packed pairs
+    else if (ui(p, "atrous_variant", 0) == 4)                                         // A/B: sliding LDS ring
+      rc = launch_atrous_slide(k, ui(p, "atrous_chunks", 6), ui(p, "atrous_nx", 0), ui(p, "atrous_xcd", 0), g.stream);
     else rc = launch_atrous_fast(k, g.stream);                             // LDS-tiled (production)
   } else if (kind == PK_MODULATE) {
     ModulateParams k;

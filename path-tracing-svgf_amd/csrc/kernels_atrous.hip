@@ -399,6 +399,181 @@ __global__ void __launch_bounds__(64 * kTileWaves * tile_nx<S>()) atrous_tile_ke
   *out = float4{s01.x * inv, s01.y * inv, s23.x * inv, s23.y * (inv * inv)};
 }
 
+static bool same_geometry(const AtrousParams& p);
+
+// ---------------------------------------------------------------------------
+// Sliding form. The tiled kernel stages (TJ + 4) rows of each plane for TJ output rows: the 4 halo rows (1.5x
+// staged rows) are fetched again by the tile above and the tile below, and on 4K frames those re-reads come from
+// the fabric, not L2 (PMC FETCH ~ staged bytes). Here a block walks DOWN its residue class: chunk k outputs class
+// rows 8k .. 8k+7 and needs class rows 8k-2 .. 8k+9; the 12 staged rows live in an LDS ring (class row i in slot
+// (i + 2) mod 12), so a chunk following a staged chunk loads only its 8 new rows. Chunks whose pixels are all
+// background copy from HBM and stage nothing (the ring keeps what it holds). Same taps, same arithmetic, same
+// order as atrous_taps: bit-identical to the step and tiled kernels.
+// XCD: with `xcd`, linear block L runs tile (L % 8) * (N / 8) + L / 8, so each XCD (blocks L = 8i + x land on XCD
+// x) walks a contiguous run of column tiles and the horizontal halos neighbouring tiles share stay in its L2.
+template <int S, int NX, bool AUX>
+__global__ void __launch_bounds__(64 * kTileWaves * NX) atrous_slide_kernel(AtrousParams p, int chunks, int xcd) {
+  constexpr int TJ = kTileRows, NW = kTileWaves * NX, R = TJ + 4, C = 64 * NX + 4 * S, NT = 64 * NW;
+  __shared__ float4 LI[R * C];
+  __shared__ float4 LN[R * C];
+  __shared__ int any_surface[2][NW];
+  const int W = p.illum.W, row0 = p.illum.row0;
+  const float4* __restrict__ I = p.illum.p;
+  const float4* __restrict__ ND = p.nd.p;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (xcd) {
+    const int N = gridDim.x * gridDim.y, L = by * gridDim.x + bx, per = N >> 3;
+    const int t = L < (per << 3) ? (L & 7) * per + (L >> 3) : L;
+    by = t / gridDim.x;
+    bx = t - by * gridDim.x;
+  }
+  const int seg = by / S, b = by - seg * S;
+  const int j = wv / NX, xl = (wv - j * NX) * 64 + lane;  // tile row, tile column
+  const int x0 = bx * 64 * NX, x = x0 + xl;
+  const int lo = max(0, row0), hi = min(p.H, row0 + p.illum.rows) - 1;
+  const bool xedge = x0 - 2 * S < 0 || x0 + 64 * NX - 1 + 2 * S >= p.W;
+  int rlo = 0, rhi = 0;  // ring holds u = class row + 2 in [rlo, rhi)
+  const int k0 = seg * chunks;
+  for (int k = k0; k < k0 + chunks; ++k) {
+    const int ybase = p.y0 + b + S * TJ * k;  // frame row of chunk row 0 (block-uniform)
+    if (ybase >= p.y1) break;
+    const int y = ybase + S * j;
+    const bool own = x < p.W && y < p.y1;
+    const size_t ci = (size_t)(y - row0) * W + x;
+    bool bg = true;
+    float fwz = 0.0f;
+    if (own) {
+      if (AUX) {
+        const float a = p.fwidth.aux[ci];
+        bg = aux_flag(a);
+        fwz = fabsf(a);
+      } else {
+        bg = ND[ci].w == 1.0f;
+        fwz = p.fwidth.p[ci].y;
+      }
+    }
+    const bool wave_any = __ballot(!bg) != 0ull;
+    if (lane == 0) any_surface[k & 1][wv] = wave_any;
+    __syncthreads();  // also: every thread is done with the previous chunk's ring reads
+    bool tile_any = false;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) tile_any |= any_surface[k & 1][w] != 0;
+    if (!tile_any) {
+      if (own) p.out.p[ci] = I[ci];
+      continue;
+    }
+    const int ua = TJ * k, ub = ua + R;  // rows this chunk reads
+    const int us = (rhi > ua && rlo <= ua) ? rhi : ua;
+    for (int e = tid; e < (ub - us) * C; e += NT) {
+      const int rr = e / C, c = e - rr * C, u = us + rr;
+      int gy = p.y0 + b + S * (u - 2), gx = x0 - 2 * S + c;
+      gy = gy < lo ? lo : (gy > hi ? hi : gy);
+      gx = gx < 0 ? 0 : (gx >= p.W ? p.W - 1 : gx);
+      const size_t gi = (size_t)(gy - row0) * W + gx;
+      const int li = (u % R) * C + c;
+      LI[li] = I[gi];
+      LN[li] = ND[gi];
+    }
+    rlo = ua;
+    rhi = ub;
+    __syncthreads();
+    if (!own) continue;
+    const int sb = (ua + j) % R;  // slot of this pixel's tap row yy = -2
+    int so[5];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) so[t] = (sb + t >= R ? sb + t - R : sb + t) * C + xl;
+    const float4 ic = LI[so[2] + 2 * S];
+    float4* out = p.out.p + ci;
+    if (bg) {
+      *out = ic;
+      continue;
+    }
+    const float4 nd = LN[so[2] + 2 * S];
+    const bool edge = xedge || ybase - 2 * S < 0 || ybase + S * (TJ + 1) >= p.H;
+    const float LOG2E = 1.4426950408889634f;
+    const float lc = (0.2125f * ic.x + 0.7154f * ic.y) + 0.0721f * ic.z;
+    const float phiL = p.phi_color * __builtin_sqrtf(fmaxf(0.0f, 1e-10f + ic.w));
+    const float kL = LOG2E / phiL;
+    const float kD = LOG2E / (fmaxf(fwz, 1e-8f) * (float)S);
+    const float kDr[5] = {kD, kD * 0.70710678f, kD * 0.5f, kD * 0.44721360f, kD * 0.35355339f};
+    float sumW = 1.0f;
+    f2v s01 = {ic.x, ic.y}, s23 = {ic.z, ic.w};
+    auto taps = [&](auto flat_tag) __attribute__((always_inline)) {
+      constexpr bool FLAT = decltype(flat_tag)::value;
+      const float wLr = 0.2125f * kL, wLg = 0.7154f * kL, wLb = 0.0721f * kL, cL = -(lc * kL);
+#pragma unroll
+      for (int yy = -2; yy <= 2; ++yy) {
+        if (edge && (y + yy * S < 0 || y + yy * S >= p.H)) continue;
+#pragma unroll
+        for (int xx = -2; xx <= 2; ++xx) {
+          if (xx == 0 && yy == 0) continue;
+          if (edge && (x + xx * S < 0 || x + xx * S >= p.W)) continue;
+          const int r2 = xx * xx + yy * yy;
+          const float kDl = r2 == 1 ? kDr[0] : r2 == 2 ? kDr[1] : r2 == 4 ? kDr[2] : r2 == 5 ? kDr[3] : kDr[4];
+          const int ax = xx < 0 ? -xx : xx, ay = yy < 0 ? -yy : yy;
+          const float kern = (ax == 0 ? 1.0f : ax == 1 ? 2.0f / 3.0f : 1.0f / 6.0f) *
+                             (ay == 0 ? 1.0f : ay == 1 ? 2.0f / 3.0f : 1.0f / 6.0f);
+          const int o = so[yy + 2] + (xx + 2) * S;
+          const float4 ip = LI[o];
+          const float4 q = LN[o];
+          const float dn =
+              fminf(fmaxf(__builtin_fmaf(nd.z, q.z, __builtin_fmaf(nd.y, q.y, nd.x * q.x)), 0.0f), 1.0f);
+          float a;
+          if (FLAT) {
+            const float lp = (0.2125f * ip.x + 0.7154f * ip.y) + 0.0721f * ip.z;
+            a = lp == lc ? fabsf(nd.w - q.w) * kDl : __builtin_inff();
+          } else {
+            const float tl = __builtin_fmaf(ip.z, wLb, __builtin_fmaf(ip.y, wLg, __builtin_fmaf(ip.x, wLr, cL)));
+            a = __builtin_fmaf(fabsf(nd.w - q.w), kDl, fabsf(tl));
+          }
+          const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(p.phi_normal, __builtin_amdgcn_logf(dn), -a)) * kern;
+          sumW += w;
+          s01 = __builtin_elementwise_fma(f2v{w, w}, f2v{ip.x, ip.y}, s01);
+          s23 = __builtin_elementwise_fma(f2v{w, w * w}, f2v{ip.z, ip.w}, s23);
+        }
+      }
+    };
+    if (__builtin_expect(phiL > 0.0f, 1)) taps(std::false_type{});
+    else taps(std::true_type{});
+    const float inv = 1.0f / sumW;
+    *out = float4{s01.x * inv, s01.y * inv, s23.x * inv, s23.y * (inv * inv)};
+  }
+}
+
+template <int S, int NX>
+static void launch_slide_snx(const AtrousParams& p, bool aux, int chunks, int xcd, hipStream_t s) {
+  const int class_rows = (p.y1 - p.y0 + S - 1) / S;        // rows of the largest residue class
+  const int nchunk = (class_rows + kTileRows - 1) / kTileRows;
+  const int segs = (nchunk + chunks - 1) / chunks;
+  dim3 grid((p.W + 64 * NX - 1) / (64 * NX), segs * S);
+  if (aux) hipLaunchKernelGGL((atrous_slide_kernel<S, NX, true>), grid, dim3(64 * kTileWaves * NX), 0, s, p, chunks, xcd);
+  else hipLaunchKernelGGL((atrous_slide_kernel<S, NX, false>), grid, dim3(64 * kTileWaves * NX), 0, s, p, chunks, xcd);
+}
+
+template <int S>
+static void launch_slide_s(const AtrousParams& p, bool aux, int chunks, int nx, int xcd, hipStream_t s) {
+  if ((nx ? nx : tile_nx<S>()) == 2) launch_slide_snx<S, 2>(p, aux, chunks, xcd, s);
+  else launch_slide_snx<S, 1>(p, aux, chunks, xcd, s);
+}
+
+int launch_atrous_slide(const AtrousParams& p, int chunks, int nx, int xcd, hipStream_t s) {
+  if (p.y1 <= p.y0) return 0;
+  if (!same_geometry(p)) return launch_atrous_simple(p, s);
+  const bool aux = p.fwidth.aux != nullptr;
+  chunks = chunks < 1 ? 1 : chunks;
+  switch (p.step) {
+    case 1: launch_slide_s<1>(p, aux, chunks, nx, xcd, s); break;
+    case 2: launch_slide_s<2>(p, aux, chunks, nx, xcd, s); break;
+    case 4: launch_slide_s<4>(p, aux, chunks, nx, xcd, s); break;
+    case 8: launch_slide_s<8>(p, aux, chunks, nx, xcd, s); break;
+    case 16: launch_slide_s<16>(p, aux, chunks, nx, xcd, s); break;
+    default: return launch_atrous_step(p, s);
+  }
+  return (int)hipGetLastError();
+}
+
 template <int S>
 static void launch_tile_s(const AtrousParams& p, bool aux, hipStream_t s) {
   constexpr int NX = tile_nx<S>();

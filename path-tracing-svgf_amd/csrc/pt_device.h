@@ -278,6 +278,7 @@ int launch_variance(const VarianceParams& p, hipStream_t s);
 int launch_atrous_exact(const AtrousParams& p, hipStream_t s);
 int launch_atrous_fast(const AtrousParams& p, hipStream_t s);   // LDS-tiled (production)
 int launch_atrous_pair(const AtrousParams& p, hipStream_t s);   // LDS-tiled, channel-planar, packed pixel pairs
+int launch_atrous_slide(const AtrousParams& p, int chunks, int nx, int xcd, hipStream_t s);  // LDS ring down a residue class
 int launch_atrous_step(const AtrousParams& p, hipStream_t s);   // step-specialised, texture-path taps
 int launch_atrous_simple(const AtrousParams& p, hipStream_t s);
 int launch_modulate(const ModulateParams& p, hipStream_t s);

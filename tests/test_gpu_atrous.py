@@ -58,7 +58,7 @@ def _planes(seed=11, W=320, H=200):
     return illum, nd, fw
 
 
-def _run(gl, illum, nd, fw, step, variant):
+def _run(gl, illum, nd, fw, step, variant, **uniforms):
     from ptsvgf.gl import GL_TEXTURE_2D, RenderPass, getShaderProgram, getTextureRGB32F
     H, W, _ = illum.shape
     ti, tn, tf, to = (getTextureRGB32F(W, H) for _ in range(4))
@@ -72,6 +72,8 @@ def _run(gl, illum, nd, fw, step, variant):
     p.set_uniform_float("gPhiNormal", 128.0)
     p.set_uniform_int("gStepSize", step)
     p.set_uniform_int("atrous_variant", variant)
+    for name, val in uniforms.items():
+        p.set_uniform_int(name, val)
     p.set_texture_uniform(GL_TEXTURE_2D, ti, "gIllumination")
     p.set_texture_uniform(GL_TEXTURE_2D, tn, "gNormalAndLinearZ")
     p.set_texture_uniform(GL_TEXTURE_2D, tf, "gNormalDepthFwidth")
@@ -84,7 +86,7 @@ def _run(gl, illum, nd, fw, step, variant):
 
 
 @pytest.mark.parametrize("size", SIZES)
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("step", [1, 2, 4, 8, 16])
 def test_atrous_kernel_vs_oracle(gpu, step, variant, size):
     W, H = size
@@ -110,13 +112,17 @@ def test_interior_tiles_cover_every_step():
 @pytest.mark.parametrize("size", SIZES)
 @pytest.mark.parametrize("step", [1, 2, 4, 8, 16])
 def test_tile_kernel_equals_step_kernel(gpu, step, size):
-    """The LDS-tiled kernels (variant 0, and variant 3: channel-planar tile, packed pixel pairs) perform the step
-    kernel's (variant 2) arithmetic in the same tap order: identical bits, NaNs included."""
+    """The LDS-tiled kernels (variant 0; variant 3: channel-planar tile, packed pixel pairs; variant 4: the LDS ring
+    sliding down a residue class, with 1, 2, 3 and 6 chunks per block, both strip widths and the XCD-contiguous
+    block order) perform the step kernel's (variant 2) arithmetic in the same tap order: identical bits, NaNs
+    included."""
     illum, nd, fw = _planes(seed=5, W=size[0], H=size[1])
     b = _run(gpu, illum, nd, fw, step, 2)
-    for v in (0, 3):
-        a = _run(gpu, illum, nd, fw, step, v)
-        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), v
+    cases = [(0, {}), (3, {})] + [(4, dict(atrous_chunks=c, atrous_nx=nx, atrous_xcd=xcd))
+                                  for c in (1, 2, 3, 6) for nx in (1, 2) for xcd in (0, 1)]
+    for v, kw in cases:
+        a = _run(gpu, illum, nd, fw, step, v, **kw)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (v, kw)
 
 
 def test_tile_kernel_aux_flag_on_rendered_planes(gpu, scene_small):
@@ -135,7 +141,7 @@ def test_tile_kernel_aux_flag_on_rendered_planes(gpu, scene_small):
     nd = gpu.readback(pl["normal_depth"])
     assert 0.05 < float(np.mean(nd[..., 3] == 1.0)) < 0.95  # both background and surface pixels present
     outs = {}
-    for variant in (0, 2, 3):
+    for variant in (0, 2, 3, 4):
         for step in (1, 2, 4, 8, 16):
             to = getTextureRGB32F(Wr, Hr)
             p = RenderPass(getShaderProgram("shaders/svgf_Atrous.frag", "shaders/vert.vert"), Wr, Hr)
@@ -156,3 +162,4 @@ def test_tile_kernel_aux_flag_on_rendered_planes(gpu, scene_small):
     for step in (1, 2, 4, 8, 16):
         assert np.array_equal(outs[0, step].view(np.uint32), outs[2, step].view(np.uint32)), step
         assert np.array_equal(outs[3, step].view(np.uint32), outs[2, step].view(np.uint32)), step
+        assert np.array_equal(outs[4, step].view(np.uint32), outs[2, step].view(np.uint32)), step

@@ -3,7 +3,8 @@
 For each view: render 3 frames, then time every variant x step as 20 back-to-back launches between two HIP
 events on the library stream (no per-launch sync), interleaved over ROUNDS rounds; report the median per-launch
 time and the algorithmic (52 B/px) fraction of 8 TB/s. The variants' outputs are compared bit for bit.
-usage: python tools/bench_atrous.py [variant ...]   (variants: 0 tile, 2 step, 3 pair; default 0 3)"""
+usage: python tools/bench_atrous.py [variant ...]   (variants: 0 tile, 2 step, 3 pair, 4 sliding ring; default 0 3)
+A variant may carry extra int uniforms: 4:atrous_chunks=8:atrous_xcd=1"""
 import json
 import os
 import sys
@@ -23,7 +24,18 @@ from ptsvgf.renderer import Renderer, _prog
 from ptsvgf.scene import build_scene
 
 W, H = int(os.environ.get("W", 3840)), int(os.environ.get("H", 2160))
-VARIANTS = [int(v) for v in sys.argv[1:]] or [0, 3]
+VARIANTS = sys.argv[1:] or ["0", "3"]
+
+
+def select(ap, spec):
+    """Set atrous_variant and the spec's extra uniforms (reset to 0 first so variants do not leak into each other)."""
+    v, *kv = spec.split(":")
+    for name in ("atrous_chunks", "atrous_nx", "atrous_xcd"):
+        ap.set_uniform_int(name, 6 if name == "atrous_chunks" else 0)
+    ap.set_uniform_int("atrous_variant", int(v))
+    for item in kv:
+        name, val = item.split("=")
+        ap.set_uniform_int(name, int(val))
 torch.cuda.set_device(0)
 gl.init(0)
 check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
@@ -52,7 +64,7 @@ for view in ("default", "surface"):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for rnd in range(int(os.environ.get("ROUNDS", 5))):
         for v in VARIANTS:
-            ap.set_uniform_int("atrous_variant", v)
+            select(ap, v)
             for step in (1, 2, 4, 8, 16):
                 ap.set_uniform_int("gStepSize", step)
                 ap.draw()
@@ -72,7 +84,7 @@ for view in ("default", "surface"):
     outs = {}
     for v in VARIANTS:
         for step in (1, 2, 4, 8, 16):
-            ap.set_uniform_int("atrous_variant", v)
+            select(ap, v)
             ap.set_uniform_int("gStepSize", step)
             ap.draw()
             outs[(v, step)] = gl.readback(out)
