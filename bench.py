@@ -173,6 +173,38 @@ def config0(gl):
     return res
 
 
+def dynamic_bvh(scene, W, H, K, steps, warmup, host_ms):
+    """SURVEY.md §8(f)2, dynamic scenes: the GPU LBVH builder (pt_bvh_build) rebuilding the path tracer's BVH in place
+    (median device and host-wall ms of 10 rebuilds, against the host SAH build of the same triangles), and the frame
+    rate of the headline configuration rendered over the LBVH instead of the reference's SAH tree."""
+    import numpy as np
+    import torch
+
+    from ptsvgf.camera import parameter_config
+    from ptsvgf.renderer import Renderer
+
+    r = Renderer(scene, W, H, parameter_config(), mode="fast", aspect_corrected=True, run_taa=False, run_output=False,
+                 frames_in_flight=K)
+    dev, wall, nodes = [], [], 0
+    for _ in range(10):
+        t0 = time.perf_counter()
+        nodes, ms = r.rebuild_bvh(leaf_n=8)
+        wall.append((time.perf_counter() - t0) * 1e3)
+        dev.append(ms)
+    for _ in range(warmup):
+        r.frame()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r.frame()
+    torch.cuda.synchronize()
+    fps = steps / (time.perf_counter() - t0)
+    r.close()
+    return {"triangles": scene.ntris, "leaf_n": 8, "nodes": nodes, "gpu_build_ms": round(float(np.median(dev)), 4),
+            "gpu_build_wall_ms": round(float(np.median(wall)), 3),
+            "host_sah_build_ms": round(host_ms, 1) if host_ms else None, "fps_over_lbvh": round(fps, 3)}
+
+
 def main():
     args = parse()
     # stdout carries the one JSON line only: native libraries (gloo's connection messages, HIP) print to file
@@ -214,7 +246,8 @@ def main():
     from ptsvgf.camera import parameter_config
     from ptsvgf.scene import build_scene
 
-    scene = build_scene(args.scene)
+    scene_timings = {}
+    scene = build_scene(args.scene, timings=scene_timings)
     cfg = parameter_config()
     gl.init(local)
     stream = torch.cuda.current_stream()
@@ -367,6 +400,11 @@ def main():
                                  "roofline": atrous_roofline(sv, W, sv["rows"]),
                                  "path_tracer": pt_rates(sv, sfps),
                                  "passes_ms": {k: round(v, 4) for k, v in sv["per_pass"].items()}}
+
+    if not args.no_extras and world == 1:
+        log("dynamic scenes: GPU LBVH rebuilds")
+        extra["dynamic_bvh"] = dynamic_bvh(scene, W, H, K, args.steps, args.warmup,
+                                           scene_timings.get("host_sah_build_ms"))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

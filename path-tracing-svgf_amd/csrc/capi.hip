@@ -1297,6 +1297,27 @@ Uniform* set_u(uint32_t pass, const char* name, int type, int* rc) {
 }  // namespace
 
 // ================================================================= C ABI ===
+ptk::LbvhWork g_lbvh;  // GPU BVH builder scratch (grows, reused across rebuilds)
+
+// Replace a texbuffer's contents with `bytes` of device data (device + host copy), as a fresh upload would.
+static int texbuffer_take(Texture* t, const void* dev_src, size_t bytes) {
+  if (t->bytes != bytes || !t->dev) {
+    if (t->owned && t->dev) (void)hipFree(t->dev);
+    t->dev = nullptr;
+    if (bytes) HIPCHK(hipMalloc(&t->dev, bytes));
+    t->owned = true;
+  }
+  t->bytes = bytes;
+  t->W = (int)(bytes / 12);
+  t->host.resize(bytes);
+  if (bytes) {
+    HIPCHK(hipMemcpyAsync(t->dev, dev_src, bytes, hipMemcpyDeviceToDevice, g.stream));
+    HIPCHK(hipMemcpyAsync(t->host.data(), dev_src, bytes, hipMemcpyDeviceToHost, g.stream));
+  }
+  t->version++;
+  return PT_OK;
+}
+
 extern "C" {
 
 const char* pt_last_error(void) { return g_err.c_str(); }
@@ -1342,6 +1363,8 @@ int pt_shutdown(void) {
     if (p->ev1) (void)hipEventDestroy(p->ev1);
   }
   for (auto& kv : g.scenes) free_scene(kv.second);
+  if (g_lbvh.base) (void)hipFree(g_lbvh.base);
+  g_lbvh = ptk::LbvhWork{};
   if (g.own) (void)hipStreamDestroy(g.own);
   g = Lib();
   return PT_OK;
@@ -1511,6 +1534,55 @@ int pt_texbuffer_create(const void* data, size_t bytes, uint32_t fmt, uint32_t* 
     HIPCHK(hipMemcpy(t->dev, data, bytes, hipMemcpyHostToDevice));
   }
   return new_texture(std::move(t), out);
+}
+
+int pt_bvh_build(uint32_t tri_in, int leaf_n, uint32_t tri_out, uint32_t node_out, int* out_nodes, float* out_ms) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  Texture *ti = tex_of(tri_in), *to = tex_of(tri_out), *no = tex_of(node_out);
+  if (!ti || !to || !no || ti->target != PT_TEXTURE_BUFFER || to->target != PT_TEXTURE_BUFFER ||
+      no->target != PT_TEXTURE_BUFFER)
+    return err(PT_ERR_ARG, "pt_bvh_build: tri_in, tri_out and node_out must be texture buffers");
+  if (tri_in == tri_out || tri_in == node_out || tri_out == node_out)
+    return err(PT_ERR_ARG, "pt_bvh_build: tri_in, tri_out and node_out must be three different buffers");
+  if (leaf_n < 1 || leaf_n > 15) return err(PT_ERR_ARG, "pt_bvh_build: leaf_n must be in [1, 15]");
+  if (ti->bytes == 0 || ti->bytes % (45 * sizeof(float)) || !ti->dev)
+    return err(PT_ERR_FORMAT, "pt_bvh_build: tri_in must hold whole Triangle_encoded records (45 floats)");
+  const size_t nt = ti->bytes / (45 * sizeof(float));
+  if (nt > (1u << 24)) return err(PT_ERR_ARG, "pt_bvh_build: more than 2^24 triangles (float-encoded indices)");
+  const int n = (int)nt;
+  float *tbuf = nullptr, *nbuf = nullptr;
+  HIPCHK(hipMalloc(&tbuf, nt * 45 * sizeof(float)));
+  if (hipMalloc(&nbuf, (size_t)2 * n * 12 * sizeof(float)) != hipSuccess) {
+    (void)hipFree(tbuf);
+    return err(PT_ERR_HIP, "pt_bvh_build: out of device memory");
+  }
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (out_ms) {
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, g.stream);
+  }
+  int nodes = 0;
+  int rc = ptk::lbvh_build(g_lbvh, (const float*)ti->dev, n, leaf_n, tbuf, nbuf, &nodes, g.stream);
+  if (out_ms) {
+    (void)hipEventRecord(e1, g.stream);
+    (void)hipEventSynchronize(e1);
+    (void)hipEventElapsedTime(out_ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+  }
+  if (rc == 0) rc = texbuffer_take(to, tbuf, nt * 45 * sizeof(float));
+  else rc = hip_err((hipError_t)rc, "lbvh_build");
+  if (rc == PT_OK) rc = texbuffer_take(no, nbuf, (size_t)nodes * 12 * sizeof(float));
+  if (rc == PT_OK) {
+    hipError_t e = hipStreamSynchronize(g.stream);
+    if (e != hipSuccess) rc = hip_err(e, "pt_bvh_build");
+  }
+  (void)hipFree(tbuf);
+  (void)hipFree(nbuf);
+  if (rc == PT_OK && out_nodes) *out_nodes = nodes;
+  return rc;
 }
 
 int pt_texarray_create(int w, int h, int layers, uint32_t* out) {

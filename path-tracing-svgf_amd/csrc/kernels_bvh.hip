@@ -1,0 +1,329 @@
+// kernels_bvh.hip — GPU LBVH builder for dynamic scenes.
+//
+// The reference builds its BVH once, on the host, with a recursive SAH sweep (buildBVHwithSAH, Utils/BVH.h:42-173,
+// called at main.cpp:88-96 with leaf size 8) and uploads it as BVHNode_encoded texels (main.cpp:122-151). A scene
+// whose triangles move every frame cannot afford that (a recursive sort per node). This builder produces the SAME
+// buffer formats on the device — triangles in leaf order (Triangle_encoded, 15 RGB32F texels each) and
+// BVHNode_encoded nodes with the dummy node 0 and the root at node 1 — so every consumer of the reference's buffers
+// (the path tracer, the host decode in capi.hip, the CPU oracle) takes them unchanged. It is a different tree than
+// the SAH builder's (no GPU builder can reproduce a host sort-and-sweep bit for bit); rendering over it is checked
+// against the oracle walking the same buffers (tests/test_gpu_bvh.py).
+//
+// Algorithm: Karras, "Maximizing Parallelism in the Construction of BVHs, Octrees, and k-d Trees" (HPG 2012):
+//   1. centroid c = (p1 + p2 + p3) / 3 (cmpx's centre, BVH.h:25-29) and the centroid bounds (wave max/min, one
+//      ordered-int atomic per wave);
+//   2. 30-bit Morton code of the centroid quantised to 1024 cells per axis, key = code << b | index (b bits of
+//      index: keys are unique, so the radix tree is fully determined and the build deterministic);
+//   3. rocPRIM radix sort of the keys (30 + b bits);
+//   4. one thread per internal node finds its key range and split (the highest differing key bit);
+//   5. bottom-up refit: each primitive walks towards the root; the second child to arrive (one acq_rel atomic per
+//      node) computes the box as the union of its children — min/max are exact, so a node box equals the
+//      reference's per-triangle min/max loop (BVH.h:52-67) over the same triangles;
+//   6. nodes whose range holds <= leaf_n triangles become leaves (their subtrees are dropped); a scan over
+//      "reachable" flags (internal nodes first, in Karras order, then single-triangle leaves) numbers the output
+//      nodes from 1 (the root), and the emit kernel writes BVHNode_encoded texels and the triangles in key order.
+// HBM traffic is a few passes over 16-64 B per triangle: for the 30.6 k-triangle bench scene the build is bound
+// by launch latency and the sort's passes, not bytes.
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include <cstdint>
+
+#include "pt_device.h"
+
+namespace ptk {
+
+namespace {
+
+constexpr int kTriFloats = 45;   // Triangle_encoded (Utils/Triangle.h:12-24)
+constexpr int kNodeFloats = 12;  // BVHNode_encoded (Utils/BVH.h:18-22)
+
+__device__ __forceinline__ unsigned ordered(float f) {
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unordered(unsigned u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+// glm::min / glm::max (a < b ? ... as the reference evaluates them)
+__device__ __forceinline__ float gmin(float a, float b) { return b < a ? b : a; }
+__device__ __forceinline__ float gmax(float a, float b) { return a < b ? b : a; }
+
+__device__ __forceinline__ float3 centroid(const float* t) {
+  return float3{((t[0] + t[3]) + t[6]) / 3.0f, ((t[1] + t[4]) + t[7]) / 3.0f, ((t[2] + t[5]) + t[8]) / 3.0f};
+}
+
+// 1. centroids and their bounds. bounds[0..2] = ordered min, bounds[3..5] = ordered max (pre-set by the host).
+__global__ void __launch_bounds__(256) lbvh_centroids(const float* __restrict__ tri, int n, float4* __restrict__ cen,
+                                                       unsigned* __restrict__ bounds) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  unsigned lo[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, hi[3] = {0u, 0u, 0u};
+  if (i < n) {
+    const float3 c = centroid(tri + (size_t)i * kTriFloats);
+    cen[i] = float4{c.x, c.y, c.z, 0.0f};
+    lo[0] = hi[0] = ordered(c.x);
+    lo[1] = hi[1] = ordered(c.y);
+    lo[2] = hi[2] = ordered(c.z);
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      lo[a] = min(lo[a], (unsigned)__shfl_xor((int)lo[a], o));
+      hi[a] = max(hi[a], (unsigned)__shfl_xor((int)hi[a], o));
+    }
+  }
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      atomicMin(&bounds[a], lo[a]);
+      atomicMax(&bounds[3 + a], hi[a]);
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t spread10(uint32_t v) {  // 10 bits -> every third bit of 30
+  uint64_t x = v & 0x3ffu;
+  x = (x | (x << 16)) & 0x030000FFull;
+  x = (x | (x << 8)) & 0x0300F00Full;
+  x = (x | (x << 4)) & 0x030C30C3ull;
+  x = (x | (x << 2)) & 0x09249249ull;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t cell(float c, float lo, float hi) {
+  const float ext = hi - lo;
+  const float q = ext > 0.0f ? (c - lo) / ext : 0.0f;
+  const float v = floorf(q * 1024.0f);
+  return v < 0.0f ? 0u : (v > 1023.0f ? 1023u : (uint32_t)v);
+}
+
+// 2. keys: Morton code (x in the highest of each bit triple) above b index bits
+__global__ void __launch_bounds__(256) lbvh_keys(const float4* __restrict__ cen, int n, const unsigned* bounds,
+                                                  int ibits, uint64_t* __restrict__ keys) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float4 c = cen[i];
+  const float lx = unordered(bounds[0]), ly = unordered(bounds[1]), lz = unordered(bounds[2]);
+  const float hx = unordered(bounds[3]), hy = unordered(bounds[4]), hz = unordered(bounds[5]);
+  const uint64_t m = (spread10(cell(c.x, lx, hx)) << 2) | (spread10(cell(c.y, ly, hy)) << 1) |
+                     spread10(cell(c.z, lz, hz));
+  keys[i] = (m << ibits) | (uint64_t)i;
+}
+
+__device__ __forceinline__ int delta(const uint64_t* __restrict__ k, int n, int i, int j) {
+  if (j < 0 || j >= n) return -1;
+  return __clzll(k[i] ^ k[j]);
+}
+
+// 4. internal node i of n-1: its range [first, last] and children. child refs: >= 0 internal node, < 0 primitive
+// (~sorted position). parent[] indexes internal nodes 0..n-2, then primitives at n-1+p.
+__global__ void __launch_bounds__(256) lbvh_karras(const uint64_t* __restrict__ k, int n, int2* __restrict__ child,
+                                                    int2* __restrict__ range, int* __restrict__ parent) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n - 1) return;
+  const int d = delta(k, n, i, i + 1) - delta(k, n, i, i - 1) >= 0 ? 1 : -1;
+  const int dmin = delta(k, n, i, i - d);
+  int lmax = 2;
+  while (delta(k, n, i, i + lmax * d) > dmin) lmax <<= 1;
+  int l = 0;
+  for (int t = lmax >> 1; t >= 1; t >>= 1)
+    if (delta(k, n, i, i + (l + t) * d) > dmin) l += t;
+  const int j = i + l * d;
+  const int dnode = delta(k, n, i, j);
+  int s = 0;
+  for (int div = 2;; div <<= 1) {
+    const int t = (l + div - 1) / div;
+    if (delta(k, n, i, i + (s + t) * d) > dnode) s += t;
+    if (t == 1) break;
+  }
+  const int gamma = i + s * d + min(d, 0);
+  const int first = min(i, j), last = max(i, j);
+  const int left = first == gamma ? ~gamma : gamma;
+  const int right = last == gamma + 1 ? ~(gamma + 1) : gamma + 1;
+  child[i] = int2{left, right};
+  range[i] = int2{first, last};
+  parent[left >= 0 ? left : n - 1 + ~left] = i;
+  parent[right >= 0 ? right : n - 1 + ~right] = i;
+  if (i == 0) parent[0] = -1;
+}
+
+// 5. bottom-up boxes. box[e] (e: internal 0..n-2, primitive n-1+p) = lo.xyz, hi.xyz as 2 float4.
+__global__ void __launch_bounds__(256) lbvh_refit(const float* __restrict__ tri, const uint64_t* __restrict__ k, int n,
+                                                   int ibits, const int2* __restrict__ child,
+                                                   const int* __restrict__ parent, float4* box, int* flags) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= n) return;
+  const uint64_t mask = (ibits >= 64) ? ~0ull : ((1ull << ibits) - 1ull);
+  const int orig = (int)(k[p] & mask);
+  const float* t = tri + (size_t)orig * kTriFloats;
+  float lo[3], hi[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {  // BVH.h:54-66: min(p1, min(p2, p3)) per axis
+    lo[a] = gmin(t[a], gmin(t[3 + a], t[6 + a]));
+    hi[a] = gmax(t[a], gmax(t[3 + a], t[6 + a]));
+  }
+  int e = n - 1 + p;
+  box[2 * e] = float4{lo[0], lo[1], lo[2], 0.0f};
+  box[2 * e + 1] = float4{hi[0], hi[1], hi[2], 0.0f};
+  int node = parent[e];
+  while (node >= 0) {
+    // the first child to arrive stops; the second sees both boxes (acq_rel orders the box stores and loads)
+    if (__hip_atomic_fetch_add(&flags[node], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+    const int2 c = child[node];
+    const int a = c.x >= 0 ? c.x : n - 1 + ~c.x, b = c.y >= 0 ? c.y : n - 1 + ~c.y;
+    const float4 al = box[2 * a], ah = box[2 * a + 1], bl = box[2 * b], bh = box[2 * b + 1];
+    box[2 * node] = float4{gmin(al.x, bl.x), gmin(al.y, bl.y), gmin(al.z, bl.z), 0.0f};
+    box[2 * node + 1] = float4{gmax(ah.x, bh.x), gmax(ah.y, bh.y), gmax(ah.z, bh.z), 0.0f};
+    node = parent[node];
+  }
+}
+
+// 6a. reachable output nodes: internal node i unless its parent's range fits a leaf; primitive p only when its
+// parent is an interior output node (a range > leaf_n). n == 1: the single primitive is the root leaf.
+__global__ void __launch_bounds__(256) lbvh_mark(int n, int leaf_n, const int2* __restrict__ range,
+                                                  const int* __restrict__ parent, int* __restrict__ keep) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= 2 * n - 1) return;
+  const int par = parent[e];
+  int k;
+  if (par < 0) k = 1;  // the root (internal 0, or the lone primitive when n == 1)
+  else {
+    const int2 r = range[par];
+    k = r.y - r.x + 1 > leaf_n;
+  }
+  keep[e] = k;
+}
+
+// 6b. BVHNode_encoded texels (childs, leafInfo, AA, BB) and the dummy node 0 (main.cpp:88-94).
+__global__ void __launch_bounds__(256) lbvh_emit(int n, int leaf_n, const int2* __restrict__ child,
+                                                  const int2* __restrict__ range, const int* __restrict__ keep,
+                                                  const int* __restrict__ id, const float4* __restrict__ box,
+                                                  float* __restrict__ out) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e == 0) {
+    const float dummy[kNodeFloats] = {255, 128, 0, 30, 0, 0, 1, 1, 0, 0, 1, 0};
+    for (int q = 0; q < kNodeFloats; ++q) out[q] = dummy[q];
+  }
+  if (e >= 2 * n - 1 || !keep[e]) return;
+  float* o = out + (size_t)(1 + id[e]) * kNodeFloats;
+  int first, count;
+  bool leaf;
+  if (e < n - 1) {
+    const int2 r = range[e];
+    first = r.x;
+    count = r.y - r.x + 1;
+    leaf = count <= leaf_n;
+  } else {
+    first = e - (n - 1);
+    count = 1;
+    leaf = true;
+  }
+  if (leaf) {
+    o[0] = 0.0f; o[1] = 0.0f; o[2] = 0.0f;
+    o[3] = (float)count; o[4] = (float)first; o[5] = 0.0f;
+  } else {
+    const int2 c = child[e];
+    const int a = c.x >= 0 ? c.x : n - 1 + ~c.x, b = c.y >= 0 ? c.y : n - 1 + ~c.y;
+    o[0] = (float)(1 + id[a]); o[1] = (float)(1 + id[b]); o[2] = 0.0f;
+    o[3] = 0.0f; o[4] = 0.0f; o[5] = 0.0f;
+  }
+  const float4 lo = box[2 * e], hi = box[2 * e + 1];
+  o[6] = lo.x; o[7] = lo.y; o[8] = lo.z;
+  o[9] = hi.x; o[10] = hi.y; o[11] = hi.z;
+}
+
+// 6c. triangles in key (leaf) order
+__global__ void __launch_bounds__(256) lbvh_reorder(const float* __restrict__ tri, const uint64_t* __restrict__ k,
+                                                     int n, int ibits, float* __restrict__ out) {
+  const size_t f = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (f >= (size_t)n * kTriFloats) return;
+  const int p = (int)(f / kTriFloats), q = (int)(f - (size_t)p * kTriFloats);
+  const uint64_t mask = (1ull << ibits) - 1ull;
+  out[f] = tri[(size_t)(k[p] & mask) * kTriFloats + q];
+}
+
+}  // namespace
+
+size_t LbvhWork::need(int n) {
+  size_t b = 0;
+  auto add = [&](size_t bytes) { b += (bytes + 255) & ~(size_t)255; };
+  add(2 * sizeof(uint64_t) * n);            // keys in / out
+  add(sizeof(float4) * n);                  // centroids
+  add(sizeof(int2) * n);                    // child
+  add(sizeof(int2) * n);                    // range
+  add(sizeof(int) * 2 * n);                 // parent
+  add(sizeof(float4) * 2 * 2 * n);          // boxes
+  add(sizeof(int) * n);                     // flags
+  add(sizeof(int) * 2 * n * 2);             // keep, id
+  add(64);                                  // bounds + count
+  return b;
+}
+
+int lbvh_build(LbvhWork& w, const float* tri, int n, int leaf_n, float* tri_out, float* node_out, int* nnodes,
+               hipStream_t s) {
+  if (n < 1) return (int)hipErrorInvalidValue;
+  int ibits = 1;
+  while ((1ll << ibits) < n) ++ibits;
+  const size_t need = LbvhWork::need(n);
+  // rocPRIM scratch: sort of 30 + ibits key bits, scan of 2n - 1 flags
+  size_t sort_bytes = 0, scan_bytes = 0;
+  hipError_t e = rocprim::radix_sort_keys(nullptr, sort_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)n, 0,
+                                          30 + ibits, s);
+  if (e != hipSuccess) return (int)e;
+  e = rocprim::exclusive_scan(nullptr, scan_bytes, (int*)nullptr, (int*)nullptr, 0, (size_t)(2 * n - 1),
+                              rocprim::plus<int>(), s);
+  if (e != hipSuccess) return (int)e;
+  const size_t temp = sort_bytes > scan_bytes ? sort_bytes : scan_bytes;
+  if (w.bytes < need + temp) {
+    if (w.base) (void)hipFree(w.base);
+    w.base = nullptr;
+    w.bytes = 0;
+    if ((e = hipMalloc(&w.base, need + temp)) != hipSuccess) return (int)e;
+    w.bytes = need + temp;
+  }
+  char* p = (char*)w.base;
+  auto take = [&](size_t bytes) { char* q = p; p += (bytes + 255) & ~(size_t)255; return (void*)q; };
+  uint64_t* kin = (uint64_t*)take(sizeof(uint64_t) * n);
+  uint64_t* kout = (uint64_t*)take(sizeof(uint64_t) * n);
+  float4* cen = (float4*)take(sizeof(float4) * n);
+  int2* child = (int2*)take(sizeof(int2) * n);
+  int2* range = (int2*)take(sizeof(int2) * n);
+  int* parent = (int*)take(sizeof(int) * 2 * n);
+  float4* box = (float4*)take(sizeof(float4) * 2 * 2 * n);
+  int* flags = (int*)take(sizeof(int) * n);
+  int* keep = (int*)take(sizeof(int) * 2 * n);
+  int* id = (int*)take(sizeof(int) * 2 * n);
+  unsigned* bounds = (unsigned*)take(64);
+  void* scratch = (void*)(p);
+  const unsigned init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
+  if ((e = hipMemcpyAsync(bounds, init, sizeof(init), hipMemcpyHostToDevice, s)) != hipSuccess) return (int)e;
+  if ((e = hipMemsetAsync(flags, 0, sizeof(int) * n, s)) != hipSuccess) return (int)e;
+  const int gb = (n + 255) / 256, ge = (2 * n - 1 + 255) / 256;
+  hipLaunchKernelGGL(lbvh_centroids, dim3(gb), dim3(256), 0, s, tri, n, cen, bounds);
+  hipLaunchKernelGGL(lbvh_keys, dim3(gb), dim3(256), 0, s, cen, n, bounds, ibits, kin);
+  size_t sb = sort_bytes;
+  if ((e = rocprim::radix_sort_keys(scratch, sb, kin, kout, (size_t)n, 0, 30 + ibits, s)) != hipSuccess) return (int)e;
+  if (n > 1) hipLaunchKernelGGL(lbvh_karras, dim3((n - 1 + 255) / 256), dim3(256), 0, s, kout, n, child, range, parent);
+  else if ((e = hipMemsetAsync(parent, 0xff, sizeof(int), s)) != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(lbvh_refit, dim3(gb), dim3(256), 0, s, tri, kout, n, ibits, child, parent, box, flags);
+  hipLaunchKernelGGL(lbvh_mark, dim3(ge), dim3(256), 0, s, n, leaf_n, range, parent, keep);
+  size_t cb = scan_bytes;
+  if ((e = rocprim::exclusive_scan(scratch, cb, keep, id, 0, (size_t)(2 * n - 1), rocprim::plus<int>(), s)) !=
+      hipSuccess)
+    return (int)e;
+  hipLaunchKernelGGL(lbvh_emit, dim3(ge), dim3(256), 0, s, n, leaf_n, child, range, keep, id, box, node_out);
+  hipLaunchKernelGGL(lbvh_reorder, dim3((unsigned)(((size_t)n * kTriFloats + 255) / 256)), dim3(256), 0, s, tri, kout,
+                     n, ibits, tri_out);
+  // output node count = 1 (dummy) + id[last] + keep[last]
+  int tail[2];
+  if ((e = hipMemcpyAsync(&tail[0], id + 2 * n - 2, sizeof(int), hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
+  if ((e = hipMemcpyAsync(&tail[1], keep + 2 * n - 2, sizeof(int), hipMemcpyDeviceToHost, s)) != hipSuccess)
+    return (int)e;
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return (int)e;
+  *nnodes = 1 + tail[0] + tail[1];
+  return (int)hipGetLastError();
+}
+
+}  // namespace ptk

@@ -387,5 +387,16 @@ __device__ __forceinline__ void sched_cost(const TileSched& t, int tile, uint32_
   for (int o = 32; o > 0; o >>= 1) steps = max(steps, (uint32_t)__shfl_xor((int)steps, o));
   if ((threadIdx.x & 63) == 0 && steps) atomicMax(t.cost + tile, steps);
 }
+// GPU LBVH builder (kernels_bvh.hip): Triangle_encoded texels in, triangles in leaf order + BVHNode_encoded
+// nodes out (the reference's upload formats, main.cpp:101-151). Scratch grows on demand and is reused.
+struct LbvhWork {
+  void* base = nullptr;
+  size_t bytes = 0;
+  static size_t need(int n);
+};
+// node_out needs room for 2n nodes (12 floats each); *nnodes = nodes written (dummy node 0 included).
+int lbvh_build(LbvhWork& w, const float* tri, int n, int leaf_n, float* tri_out, float* node_out, int* nnodes,
+               hipStream_t s);
+
 }  // namespace ptk
 #endif

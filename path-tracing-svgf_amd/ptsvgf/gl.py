@@ -90,6 +90,23 @@ def texture_buffer(data: np.ndarray) -> int:
     return h.value
 
 
+def buffer_readback(tex: int) -> np.ndarray:
+    """Device contents of a texture buffer as flat float32 (3 floats per RGB32F texel)."""
+    w, _, _ = texture_info(tex)
+    out = np.empty(w * 3, np.float32)
+    check(pt().pt_texture_readback(tex, fptr(out), out.nbytes))
+    return out
+
+
+def bvh_build(tri_in: int, tri_out: int, node_out: int, leaf_n: int = 8):
+    """pt_bvh_build: GPU LBVH over the device triangles of tri_in (Triangle_encoded texels) into tri_out (leaf
+    order) and node_out (BVHNode_encoded, dummy node 0, root 1) — the reference's buffer formats (main.cpp:88-151).
+    Returns (node count, device build ms)."""
+    n, ms = C.c_int(), C.c_float()
+    check(pt().pt_bvh_build(tri_in, leaf_n, tri_out, node_out, C.byref(n), C.byref(ms)))
+    return n.value, ms.value
+
+
 def texture_array(layers: np.ndarray) -> int:
     """main.cpp:184-205: glTexStorage3D(GL_TEXTURE_2D_ARRAY, 1, GL_RGBA8, w, h, n) + one glTexSubImage3D per layer
     (help_func.h:4-20). `layers` is (n, h, w, 3|4) uint8, rows already in GL order (stbi flipped on load)."""

@@ -731,6 +731,28 @@ class Renderer:
             self._slot_free[f % self.K] = ev
 
     # --------------------------------------------------------- accessors ---
+    def rebuild_bvh(self, tri_enc=None, raster=None, leaf_n: int = 8):
+        """Dynamic scenes: rebuild the path tracer's BVH on the GPU (pt_bvh_build) into the scene
+        buffers the passes are bound to. `tri_enc` (Triangle_encoded rows, any order; default: the scene's
+        triangles) carries moved vertices; `raster` (the pre-BVH vertex list, obj_loader.h:143-160) moves the
+        G-buffer's triangles with them. Frames already issued finish first. Returns (nodes, device build ms)."""
+        if self._streams is not None:
+            import torch
+
+            self.flush()
+            torch.cuda.synchronize()
+        src = gl.texture_buffer(self.scene.tri_enc if tri_enc is None else np.asarray(tri_enc, np.float32))
+        try:
+            nodes, ms = gl.bvh_build(src, self.trianglesTextureBuffer, self.nodesTextureBuffer, leaf_n)
+        finally:
+            gl.destroy_texture(src)
+        for p, _ in self.pt_slots:
+            p.set_uniform_int("nNodes", nodes)
+        if raster is not None:
+            for p in self.init_pass:
+                p.bindData(raster)
+        return nodes, ms
+
     def close(self) -> None:
         """Release every pass and texture this renderer created (the GL objects main.cpp never frees)."""
         if self._streams is not None:

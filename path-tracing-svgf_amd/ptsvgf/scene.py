@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import time
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -178,7 +179,8 @@ def material_layers(size: int = 256, image: int = 192, objects: int = 3, seed: i
     return out
 
 
-def build_scene(name: str = "table_clock_plant", hdr_size=(2048, 1024), plant_leaves: int = 150) -> Scene:
+def build_scene(name: str = "table_clock_plant", hdr_size=(2048, 1024), plant_leaves: int = 150,
+                timings: dict | None = None) -> Scene:
     """Named scenes of BASELINE.json's configs.
 
     ``clock``               main.cpp:72-80 (textures absent -> constant brass material)
@@ -216,7 +218,10 @@ def build_scene(name: str = "table_clock_plant", hdr_size=(2048, 1024), plant_le
         b.add_obj(clock, textured, transform(trans=(-0.914, -0.155, -1.03), scale=(1.12, 1.12, 1.12)), True, 1)
     else:
         raise ValueError(f"unknown scene {name!r}")
-    b.build(8)
+    t0 = time.perf_counter()
+    b.build(8)  # buildBVHwithSAH (BVH.h:42-173) on the host, as main.cpp:96
+    if timings is not None:
+        timings["host_sah_build_ms"] = (time.perf_counter() - t0) * 1e3
     tri, node, raster = b.encode()
     hdr = env_map(*hdr_size)
     tex = material_layers() if name == "textured" else None
