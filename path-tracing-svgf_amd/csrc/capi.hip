@@ -58,6 +58,7 @@ struct Texture {
   uint64_t version = 1;
   float* aux = nullptr;  // compact depth-fwidth side plane
   bool aux_valid = false;
+  bool lbvh = false;     // written by pt_bvh_build (the device copy is authoritative: get_scene decodes it there)
 };
 
 struct Uniform {
@@ -690,6 +691,51 @@ int upload_vec(const std::vector<T>& v, T** dst) {
   return PT_OK;
 }
 
+// A scene pt_bvh_build wrote (dynamic scenes): its triangles are decoded on the device (decode_tris: the host
+// decode's built-ins, the same records), and its own tree (an LBVH, not the reference's SAH tree) serves every walk:
+// no 4-wide or any-hit SAH tree is derived from it, so a rebuild costs the GPU build, this decode and the host
+// packing of the node texels (DESIGN.md "Dynamic scenes").
+int get_scene_lbvh(Texture* tris, Texture* nodes, SceneGPU& sg, SceneGPU** out) {
+  const size_t ntris = tris->bytes / (45 * sizeof(float));
+  const size_t nnodes = nodes->host.size() / (12 * sizeof(float));
+  std::vector<float4> bvh;
+  int root = 0;
+  int rc = pack_bvh((const float*)nodes->host.data(), (int)nnodes, bvh, &root, (int)ntris, &sg.stack_need);
+  if (rc != PT_OK) return rc;
+  std::vector<float4> lv;
+  const float* ne = (const float*)nodes->host.data();
+  for (size_t i = 1; i < nnodes; ++i) {
+    const float* f = ne + i * 12;
+    const int n = (int)f[3], first = (int)f[4];
+    if (n <= 0) continue;
+    const int ref = -(first * 16 + n) - 1;
+    float rf;
+    memcpy(&rf, &ref, 4);
+    lv.push_back(float4{f[6], f[7], f[8], rf});
+    lv.push_back(float4{f[9], f[10], f[11], 0.0f});
+  }
+  sg.nleaves = (int)(lv.size() / 2);
+  if ((rc = upload_vec(lv, &sg.leaves)) != PT_OK) return rc;
+  if (bvh.empty()) bvh.push_back(float4{0, 0, 0, 0});
+  if ((rc = upload_vec(bvh, &sg.bvh)) != PT_OK) return rc;
+  float4** opt[2] = {&sg.bvh4, &sg.bvh_any};
+  for (auto b : opt)
+    if (*b) { (void)hipFree(*b); *b = nullptr; }
+  sg.has4 = false;
+  if (sg.geom) (void)hipFree(sg.geom);
+  if (sg.shade) (void)hipFree(sg.shade);
+  sg.geom = sg.shade = nullptr;
+  HIPCHK(hipMalloc((void**)&sg.geom, std::max<size_t>(ntris, 1) * 4 * sizeof(float4)));
+  HIPCHK(hipMalloc((void**)&sg.shade, std::max<size_t>(ntris, 1) * 9 * sizeof(float4)));
+  HIPCHK((hipError_t)ptk::decode_tris((const float*)tris->dev, (int)ntris, sg.geom, sg.shade, g.stream));
+  sg.root_ref = root;
+  sg.ntris = (int)ntris;
+  sg.tri_ver = tris->version;
+  sg.node_ver = nodes->version;
+  *out = &sg;
+  return PT_OK;
+}
+
 int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU** out) {
   SceneGPU& sg = g.scenes[{th, nh}];
   if (sg.geom && sg.tri_ver == tris->version && sg.node_ver == nodes->version) {
@@ -699,6 +745,7 @@ int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU*
   using namespace glsl;
   size_t ntris = tris->host.size() / (45 * sizeof(float));
   size_t nnodes = nodes->host.size() / (12 * sizeof(float));
+  if (tris->lbvh && nodes->lbvh) return get_scene_lbvh(tris, nodes, sg, out);
   const float* te = (const float*)tris->host.data();
   std::vector<float4> geom(ntris * 4), shade(ntris * 9);
   for (size_t i = 0; i < ntris; ++i) {
@@ -1315,6 +1362,7 @@ static int texbuffer_take(Texture* t, const void* dev_src, size_t bytes) {
     HIPCHK(hipMemcpyAsync(t->host.data(), dev_src, bytes, hipMemcpyDeviceToHost, g.stream));
   }
   t->version++;
+  t->lbvh = true;
   return PT_OK;
 }
 

@@ -30,6 +30,7 @@
 
 #include <cstdint>
 
+#include "glsl_builtins.h"
 #include "pt_device.h"
 
 namespace ptk {
@@ -244,7 +245,39 @@ __global__ void __launch_bounds__(256) lbvh_reorder(const float* __restrict__ tr
   out[f] = tri[(size_t)(k[p] & mask) * kTriFloats + q];
 }
 
+// Triangle_encoded texels -> the path tracer's tri_geom / tri_shade records (capi.hip get_scene's host decode,
+// same built-ins, so the same bits): the device decode of GPU-built scenes, whose triangles never leave the device.
+__global__ void __launch_bounds__(256) decode_tris_kernel(const float* __restrict__ te, int n, float4* __restrict__ geom,
+                                                           float4* __restrict__ shade) {
+  using namespace glsl;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float* f = te + (size_t)i * kTriFloats;
+  const v3 p1 = mk(f[0], f[1], f[2]), p2 = mk(f[3], f[4], f[5]), p3 = mk(f[6], f[7], f[8]);
+  const v3 N = normalize(cross(sub(p2, p1), sub(p3, p1)));  // hitTriangle (path_tracing.frag:227)
+  geom[4 * i + 0] = float4{p1.x, p1.y, p1.z, dot(N, p1)};
+  geom[4 * i + 1] = float4{p2.x, p2.y, p2.z, 0.0f};
+  geom[4 * i + 2] = float4{p3.x, p3.y, p3.z, 0.0f};
+  geom[4 * i + 3] = float4{N.x, N.y, N.z, 0.0f};
+  float4* s = shade + 9 * (size_t)i;
+  s[0] = float4{f[9], f[10], f[11], f[12]};
+  s[1] = float4{f[13], f[14], f[15], f[16]};
+  s[2] = float4{f[17], f[18], f[19], f[20]};
+  s[3] = float4{f[21], f[22], f[23], f[24]};
+  s[4] = float4{f[25], f[26], f[27], f[28]};
+  s[5] = float4{f[29], f[30], f[31], f[32]};
+  s[6] = float4{f[33], f[34], f[35], f[42]};
+  s[7] = float4{f[36], f[37], f[38], f[39]};
+  s[8] = float4{f[40], f[41], 0.0f, 0.0f};
+}
+
 }  // namespace
+
+int decode_tris(const float* te, int n, float4* geom, float4* shade, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(decode_tris_kernel, dim3((n + 255) / 256), dim3(256), 0, s, te, n, geom, shade);
+  return (int)hipGetLastError();
+}
 
 size_t LbvhWork::need(int n) {
   size_t b = 0;
