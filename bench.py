@@ -14,8 +14,9 @@ the line also carries the serial rate (one frame at a time: camera-to-display
 latency of one frame), 1080p (configs[1]), the path tracer's rays/s and BVH
 visits/s, a surface-dominated view, the a-trous roofline three ways (SURVEY.md's
 52 B/px convention, PMC traffic, background-weighted bytes), the CPU oracle on
-16 threads and on 1 core, and configs[0] (Cornell box + teapot 512x512, SVGF off,
-CPU reference traversal).
+16 threads and on 1 core, configs[0] (Cornell box + teapot 512x512, SVGF off,
+CPU reference traversal), and the dynamic-scene path (GPU LBVH rebuild time, frame
+rate over the LBVH).
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
 each rank renders one horizontal band of the SAME 4K frame and exchanges SVGF

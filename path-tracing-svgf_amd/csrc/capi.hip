@@ -1283,6 +1283,7 @@ int draw_svgf(Pass* p, int kind) {
     k.step = ui(p, "gStepSize", 1);
     k.phi_color = uf(p, "gPhiColor", 0.0f);
     k.phi_normal = uf(p, "gPhiNormal", 0.0f);
+    k.xcd_run = ui(p, "atrous_xcd_run", 0);
     if (ui(p, "exact", 0)) rc = launch_atrous_exact(k, g.stream);          // bit-exact form (tests)
     else if (ui(p, "atrous_variant", 0) == 1) rc = launch_atrous_simple(k, g.stream);  // A/B: generic
     else if (ui(p, "atrous_variant", 0) == 2) rc = launch_atrous_step(k, g.stream);    // A/B: step kernel

@@ -253,10 +253,27 @@ __global__ void __launch_bounds__(64 * kTileWaves * tile_nx<S>()) atrous_tile_ke
   const float4* __restrict__ ND = p.nd.p;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = blockIdx.y / S, b = blockIdx.y - g * S;
+  int bx = blockIdx.x, g, b;
+  if (p.xcd_run > 0) {
+    // Tiles in dispatch order t = blockIdx.y * NXT + x; the XCD of linear block L = L % 8 takes runs of xcd_run
+    // consecutive tiles, so the halo columns (and, for S = 1, rows) neighbouring tiles share are fetched once into
+    // that XCD's L2. (A residue-class-major tile order, whose vertical neighbours are closer, measured slower: the
+    // concurrently running tiles then cover far-apart rows.)
+    const int NXT = gridDim.x, N = NXT * gridDim.y, C = p.xcd_run;
+    const int L = blockIdx.y * NXT + blockIdx.x, full = N / (8 * C) * (8 * C);
+    const int i = L >> 3;
+    const int t = L < full ? ((i / C) * 8 + (L & 7)) * C + (i % C) : L;
+    const int q = t / NXT;
+    bx = t - q * NXT;
+    g = q / S;
+    b = q - g * S;
+  } else {
+    g = blockIdx.y / S;
+    b = blockIdx.y - g * S;
+  }
   const int ybase = p.y0 + g * S * TJ + b;  // frame row of tile row j = 0
   const int j = wv / NX, xl = (wv - j * NX) * 64 + lane;  // tile row, tile column
-  const int x0 = blockIdx.x * 64 * NX, x = x0 + xl, y = ybase + S * j;
+  const int x0 = bx * 64 * NX, x = x0 + xl, y = ybase + S * j;
   const bool own = x < p.W && y < p.y1;
   const size_t ci = (size_t)(y - row0) * W + x;
   bool bg = true;

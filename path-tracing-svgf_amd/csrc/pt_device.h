@@ -240,6 +240,7 @@ struct AtrousParams {
   Plane illum, nd, fwidth, out;
   int step;
   float phi_color, phi_normal;
+  int xcd_run;  // tiled kernel: > 0 runs of this many consecutive tiles per XCD (L2 halo reuse), 0 = dispatch order
 };
 
 struct ModulateParams {

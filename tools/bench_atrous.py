@@ -30,7 +30,7 @@ VARIANTS = sys.argv[1:] or ["0", "3"]
 def select(ap, spec):
     """Set atrous_variant and the spec's extra uniforms (reset to 0 first so variants do not leak into each other)."""
     v, *kv = spec.split(":")
-    for name in ("atrous_chunks", "atrous_nx", "atrous_xcd"):
+    for name in ("atrous_chunks", "atrous_nx", "atrous_xcd", "atrous_xcd_run"):
         ap.set_uniform_int(name, 6 if name == "atrous_chunks" else 0)
     ap.set_uniform_int("atrous_variant", int(v))
     for item in kv:
