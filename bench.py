@@ -175,45 +175,48 @@ def config0(gl):
 
 
 def dynamic_bvh(scene, W, H, K, steps, warmup, host_ms):
-    """SURVEY.md §8(f)2, dynamic scenes: the GPU LBVH builder (pt_bvh_build) rebuilding the path tracer's BVH in place
-    (median device and host-wall ms of 10 rebuilds, against the host SAH build of the same triangles), and the frame
-    rate of the headline configuration rendered over the LBVH instead of the reference's SAH tree."""
+    """SURVEY.md §8(f)2, dynamic scenes: the GPU builder (pt_bvh_build) rebuilding the path tracer's BVH in place —
+    a plain LBVH and with the PLOC-built top (radius 16) — median device and host-wall ms of 10 rebuilds against the
+    host SAH build of the same triangles, a rebuild plus the frame that decodes it against a frame alone, and the
+    frame rate of the headline configuration rendered over the GPU-built tree instead of the reference's SAH tree."""
     import numpy as np
     import torch
 
     from ptsvgf.camera import parameter_config
     from ptsvgf.renderer import Renderer
 
-    r = Renderer(scene, W, H, parameter_config(), mode="fast", aspect_corrected=True, run_taa=False, run_output=False,
-                 frames_in_flight=K)
-    dev, wall, nodes, upd = [], [], 0, []
-    for _ in range(10):
-        t0 = time.perf_counter()
-        nodes, ms = r.rebuild_bvh(leaf_n=8)
-        wall.append((time.perf_counter() - t0) * 1e3)
-        dev.append(ms)
-        r.frame()  # the first draw over the new buffers decodes them (capi get_scene)
+    out = {"triangles": scene.ntris, "leaf_n": 8, "host_sah_build_ms": round(host_ms, 1) if host_ms else None}
+    for name, radius in (("lbvh", 0), ("ploc16", 16)):
+        r = Renderer(scene, W, H, parameter_config(), mode="fast", aspect_corrected=True, run_taa=False,
+                     run_output=False, frames_in_flight=K)
+        dev, wall, nodes, upd, plain = [], [], 0, [], []
+        for _ in range(10):
+            t0 = time.perf_counter()
+            nodes, ms = r.rebuild_bvh(leaf_n=8, ploc_radius=radius)
+            wall.append((time.perf_counter() - t0) * 1e3)
+            dev.append(ms)
+            r.frame()  # the first draw over the new buffers decodes them (capi get_scene)
+            torch.cuda.synchronize()
+            upd.append((time.perf_counter() - t0) * 1e3)
+        for _ in range(10):
+            t0 = time.perf_counter()
+            r.frame()
+            torch.cuda.synchronize()
+            plain.append((time.perf_counter() - t0) * 1e3)
+        for _ in range(warmup):
+            r.frame()
         torch.cuda.synchronize()
-        upd.append((time.perf_counter() - t0) * 1e3)
-    plain = []
-    for _ in range(10):
         t0 = time.perf_counter()
-        r.frame()
+        for _ in range(steps):
+            r.frame()
         torch.cuda.synchronize()
-        plain.append((time.perf_counter() - t0) * 1e3)
-    for _ in range(warmup):
-        r.frame()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        r.frame()
-    torch.cuda.synchronize()
-    fps = steps / (time.perf_counter() - t0)
-    r.close()
-    return {"triangles": scene.ntris, "leaf_n": 8, "nodes": nodes, "gpu_build_ms": round(float(np.median(dev)), 4),
-            "gpu_build_wall_ms": round(float(np.median(wall)), 3),
-            "rebuild_plus_frame_ms": round(float(np.median(upd)), 3), "frame_ms": round(float(np.median(plain)), 3),
-            "host_sah_build_ms": round(host_ms, 1) if host_ms else None, "fps_over_lbvh": round(fps, 3)}
+        fps = steps / (time.perf_counter() - t0)
+        r.close()
+        out[name] = {"nodes": nodes, "gpu_build_ms": round(float(np.median(dev)), 4),
+                     "gpu_build_wall_ms": round(float(np.median(wall)), 3),
+                     "rebuild_plus_frame_ms": round(float(np.median(upd)), 3),
+                     "frame_ms": round(float(np.median(plain)), 3), "fps": round(fps, 3)}
+    return out
 
 
 def main():

@@ -103,16 +103,19 @@ int pt_texture2d_upload(uint32_t tex, int width, int height, uint32_t fmt,      
                         const float* host_data);
 int pt_texture2d_wrap(void* device_ptr, int width, int height, uint32_t* out_tex); /* RGBA32F, not owned */
 int pt_texbuffer_create(const void* host_data, size_t bytes, uint32_t fmt, uint32_t* out_tex); /* RGB32F */
-/* GPU LBVH builder for dynamic scenes. The reference builds once on the host
+/* GPU BVH builder for dynamic scenes. The reference builds once on the host
  * (buildBVHwithSAH, Utils/BVH.h:42-173, main.cpp:88-96) and encodes triangles and nodes (main.cpp:101-151);
  * this builds a Karras LBVH on the device from the DEVICE contents of tri_in (Triangle_encoded texels, e.g.
  * after moving vertices through pt_texture_device_ptr) and writes, in those same formats, the triangles in leaf
  * order into tri_out and BVHNode_encoded nodes (dummy node 0, root node 1, leaves of <= leaf_n triangles) into
- * node_out. tri_out / node_out are existing texbuffers (any size, e.g. created empty), distinct from tri_in and
- * each other; their device and host copies are replaced, so passes bound to them draw the new scene next time.
- * leaf_n in [1, 15]. out_nodes: node count (dummy included); out_ms: device time of the build (NULL: skipped).
+ * node_out. ploc_radius > 0 (e.g. 16) rebuilds the tree above the LBVH leaves by PLOC clustering with that search
+ * radius (a surface-area-driven top, cheaper to walk); 0 keeps the plain LBVH. tri_out / node_out are existing
+ * texbuffers (any size, e.g. created empty), distinct from tri_in and each other; their device and host copies are
+ * replaced, so passes bound to them draw the new scene next time. leaf_n in [1, 15], ploc_radius in [0, 256].
+ * out_nodes: node count (dummy included); out_ms: device time of the build (NULL: skipped).
  * Synchronous (waits for the build on the library stream). */
-int pt_bvh_build(uint32_t tri_in, int leaf_n, uint32_t tri_out, uint32_t node_out, int* out_nodes, float* out_ms);
+int pt_bvh_build(uint32_t tri_in, int leaf_n, int ploc_radius, uint32_t tri_out, uint32_t node_out, int* out_nodes,
+                 float* out_ms);
 int pt_texarray_create(int width, int height, int layers, uint32_t* out_tex);     /* RGBA8 2-D array */
 int pt_texarray_upload_layer(uint32_t tex, int layer, int width, int height, int channels,
                              const uint8_t* host_data);

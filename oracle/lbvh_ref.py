@@ -19,6 +19,7 @@ Algorithm (Karras, HPG 2012, as published), with the kernel's float32 arithmetic
   boxes     primitive: glm min/max over its three vertices (BVH.h:54-66); internal: union of its two children
   leaves    a node whose range holds <= leaf_n primitives is a leaf (n = count, index = first sorted position)
   numbering reachable nodes in the order [internal 0 .. n-2, primitive 0 .. n-1], from node 1 (the root)
+With ploc_radius > 0 the LBVH leaves are kept and the tree above them is PLOC's (ploc_top).
 """
 from __future__ import annotations
 
@@ -60,8 +61,9 @@ def keys(tri_enc: np.ndarray):
     return (m << np.uint64(b)) | np.arange(n, dtype=np.uint64), b
 
 
-def lbvh(tri_enc: np.ndarray, leaf_n: int = 8):
-    """(triangles in leaf order (n, 45), BVHNode_encoded nodes (m, 12)) as pt_bvh_build writes them."""
+def lbvh(tri_enc: np.ndarray, leaf_n: int = 8, ploc_radius: int = 0):
+    """(triangles in leaf order (n, 45), BVHNode_encoded nodes (m, 12)) as pt_bvh_build writes them; ploc_radius > 0
+    rebuilds the tree above the LBVH leaves by PLOC (see ploc_top)."""
     t = np.asarray(tri_enc, np.float32).reshape(-1, 45)
     n = t.shape[0]
     k, b = keys(t)
@@ -116,6 +118,14 @@ def lbvh(tri_enc: np.ndarray, leaf_n: int = 8):
         return rng[e][1] - rng[e][0] + 1 if e < n - 1 else 1
 
     keep = np.array([1 if parent[e] < 0 else int(size(parent[e]) > leaf_n) for e in range(2 * n - 1)], np.int64)
+    if ploc_radius > 0 and n > 1:
+        leaves = []  # reachable LBVH leaves: (first, count, lo, hi), in Morton (first) order
+        for e in np.nonzero(keep)[0]:
+            if e >= n - 1 or size(e) <= leaf_n:
+                f0 = rng[e][0] if e < n - 1 else e - (n - 1)
+                leaves.append((f0, size(e), box_lo[e], box_hi[e]))
+        leaves.sort(key=lambda q: q[0])
+        return np.ascontiguousarray(so), ploc_top(leaves, ploc_radius)
     ids = np.concatenate([[0], np.cumsum(keep)[:-1]])
     nodes = np.zeros((1 + int(keep.sum()), 12), np.float32)
     nodes[0] = DUMMY_NODE
@@ -130,6 +140,74 @@ def lbvh(tri_enc: np.ndarray, leaf_n: int = 8):
         o[6:9] = box_lo[e]
         o[9:12] = box_hi[e]
     return np.ascontiguousarray(so), nodes
+
+
+def ploc_top(leaves, r: int) -> np.ndarray:
+    """BVHNode_encoded nodes of the tree PLOC (Meister & Bittner 2018) builds over the given leaves, as the kernels
+    ploc_nn / ploc_flags / ploc_compact / ploc_emit do: each cluster picks, among the clusters within r positions,
+    the one whose merged box has the least half area ((dx*dy + dy*dz) + dz*dx in float32; ties: the smaller index),
+    mutual pairs merge into a new node at the lower position (children in position order), the array is compacted.
+    Node ids: PLOC node k (creation order) -> 1 + (M - 2 - k), leaf L -> M + L; node 0 the dummy."""
+    M = len(leaves)
+    C = np.array([~L for L in range(M)], np.int64)
+    cl = np.array([q[2] for q in leaves], np.float32).reshape(M, 3)
+    ch = np.array([q[3] for q in leaves], np.float32).reshape(M, 3)
+    kids, klo, khi = [], [], []
+    n = M
+    while n > 1:
+        idx = np.arange(n)
+        best = np.full(n, np.inf, np.float32)
+        bj = idx.copy()
+        for off in range(-r, r + 1):  # ascending j: the first minimum wins
+            if off == 0:
+                continue
+            j = idx + off
+            valid = (j >= 0) & (j < n)
+            jj = np.clip(j, 0, n - 1)
+            d = _gmax(ch, ch[jj]) - _gmin(cl, cl[jj])
+            a = (d[:, 0] * d[:, 1] + d[:, 1] * d[:, 2]) + d[:, 2] * d[:, 0]
+            better = valid & (a < best)
+            best = np.where(better, a, best)
+            bj = np.where(better, j, bj)
+        mutual = (bj != idx) & (bj[bj] == idx)
+        newf = mutual & (idx < bj)
+        keepf = ~(mutual & (idx > bj))
+        pos = np.cumsum(keepf) - keepf
+        k0 = len(kids)
+        knew = k0 + np.cumsum(newf) - newf
+        C2 = np.empty(int(keepf.sum()), np.int64)
+        cl2 = np.empty((len(C2), 3), np.float32)
+        ch2 = np.empty((len(C2), 3), np.float32)
+        for i in np.nonzero(keepf)[0]:
+            p = pos[i]
+            if newf[i]:
+                j = bj[i]
+                lo, hi = _gmin(cl[i], cl[j]), _gmax(ch[i], ch[j])
+                k = int(knew[i])
+                while len(kids) <= k:
+                    kids.append(None)
+                    klo.append(None)
+                    khi.append(None)
+                kids[k], klo[k], khi[k] = (int(C[i]), int(C[j])), lo, hi
+                C2[p], cl2[p], ch2[p] = k, lo, hi
+            else:
+                C2[p], cl2[p], ch2[p] = C[i], cl[i], ch[i]
+        C, cl, ch, n = C2, cl2, ch2, len(C2)
+
+    def nid(ref):
+        return 1 + (M - 2 - ref) if ref >= 0 else M + ~ref
+
+    nodes = np.zeros((2 * M, 12), np.float32)
+    nodes[0] = DUMMY_NODE
+    for k, (a, b) in enumerate(kids):
+        o = nodes[nid(k)]
+        o[0], o[1] = nid(a), nid(b)
+        o[6:9], o[9:12] = klo[k], khi[k]
+    for L, (f0, cnt, lo, hi) in enumerate(leaves):
+        o = nodes[M + L]
+        o[3], o[4] = cnt, f0
+        o[6:9], o[9:12] = lo, hi
+    return nodes
 
 
 def check_tree(tri_sorted: np.ndarray, nodes: np.ndarray, leaf_n: int) -> dict:

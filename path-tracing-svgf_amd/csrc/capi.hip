@@ -1585,7 +1585,8 @@ int pt_texbuffer_create(const void* data, size_t bytes, uint32_t fmt, uint32_t* 
   return new_texture(std::move(t), out);
 }
 
-int pt_bvh_build(uint32_t tri_in, int leaf_n, uint32_t tri_out, uint32_t node_out, int* out_nodes, float* out_ms) {
+int pt_bvh_build(uint32_t tri_in, int leaf_n, int ploc_radius, uint32_t tri_out, uint32_t node_out, int* out_nodes,
+                 float* out_ms) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   TRY(ensure_init());
   Texture *ti = tex_of(tri_in), *to = tex_of(tri_out), *no = tex_of(node_out);
@@ -1595,6 +1596,7 @@ int pt_bvh_build(uint32_t tri_in, int leaf_n, uint32_t tri_out, uint32_t node_ou
   if (tri_in == tri_out || tri_in == node_out || tri_out == node_out)
     return err(PT_ERR_ARG, "pt_bvh_build: tri_in, tri_out and node_out must be three different buffers");
   if (leaf_n < 1 || leaf_n > 15) return err(PT_ERR_ARG, "pt_bvh_build: leaf_n must be in [1, 15]");
+  if (ploc_radius < 0 || ploc_radius > 256) return err(PT_ERR_ARG, "pt_bvh_build: ploc_radius must be in [0, 256]");
   if (ti->bytes == 0 || ti->bytes % (45 * sizeof(float)) || !ti->dev)
     return err(PT_ERR_FORMAT, "pt_bvh_build: tri_in must hold whole Triangle_encoded records (45 floats)");
   const size_t nt = ti->bytes / (45 * sizeof(float));
@@ -1613,7 +1615,7 @@ int pt_bvh_build(uint32_t tri_in, int leaf_n, uint32_t tri_out, uint32_t node_ou
     (void)hipEventRecord(e0, g.stream);
   }
   int nodes = 0;
-  int rc = ptk::lbvh_build(g_lbvh, (const float*)ti->dev, n, leaf_n, tbuf, nbuf, &nodes, g.stream);
+  int rc = ptk::lbvh_build(g_lbvh, (const float*)ti->dev, n, leaf_n, ploc_radius, tbuf, nbuf, &nodes, g.stream);
   if (out_ms) {
     (void)hipEventRecord(e1, g.stream);
     (void)hipEventSynchronize(e1);

@@ -28,6 +28,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "glsl_builtins.h"
@@ -271,6 +272,164 @@ __global__ void __launch_bounds__(256) decode_tris_kernel(const float* __restric
   s[8] = float4{f[40], f[41], 0.0f, 0.0f};
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// PLOC top (quality > 0): the LBVH's leaves (ranges of <= leaf_n Morton-ordered triangles, their boxes exact) are
+// kept, and the tree above them is rebuilt by Parallel Locally-Ordered Clustering (Meister & Bittner, 2018): every
+// cluster in Morton order finds, within r positions, the neighbour whose merged box has the smallest surface area
+// (ties: the nearer-indexed pair, a total order on pairs, so the globally best pair is always mutual and every
+// iteration merges at least once); mutual pairs merge into a new node at the lower position, the array is
+// compacted, until one cluster is left. Clusters: >= 0 PLOC node (creation order), < 0 leaf ~L (Morton rank).
+__device__ __forceinline__ float half_area(float4 lo, float4 hi) {
+  const float dx = hi.x - lo.x, dy = hi.y - lo.y, dz = hi.z - lo.z;
+  return (dx * dy + dy * dz) + dz * dx;
+}
+
+// leaves in Morton order: start[first] = 1 for every reachable LBVH leaf
+__global__ void __launch_bounds__(256) ploc_leafstart(int n, int leaf_n, const int2* __restrict__ range,
+                                                       const int* __restrict__ keep, int* __restrict__ start) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= 2 * n - 1 || !keep[e]) return;
+  if (e < n - 1) {
+    const int2 r = range[e];
+    if (r.y - r.x + 1 <= leaf_n) start[r.x] = 1;
+  } else {
+    start[e - (n - 1)] = 1;
+  }
+}
+
+__global__ void __launch_bounds__(256) ploc_init(int n, int leaf_n, const int2* __restrict__ range,
+                                                  const int* __restrict__ keep, const int* __restrict__ rank,
+                                                  const int* __restrict__ start, const float4* __restrict__ box,
+                                                  int2* __restrict__ leaf, float4* __restrict__ leafbox,
+                                                  int* __restrict__ C, float4* __restrict__ cbox, int* __restrict__ cnt) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e == 0) {
+    cnt[0] = rank[n - 1] + start[n - 1];  // clusters (= leaves, M)
+    cnt[1] = 0;                           // PLOC nodes created
+    cnt[4] = cnt[0];
+  }
+  if (e >= 2 * n - 1 || !keep[e]) return;
+  int first, count;
+  if (e < n - 1) {
+    const int2 r = range[e];
+    count = r.y - r.x + 1;
+    if (count > leaf_n) return;
+    first = r.x;
+  } else {
+    first = e - (n - 1);
+    count = 1;
+  }
+  const int L = rank[first];
+  leaf[L] = int2{first, count};
+  C[L] = ~L;
+  cbox[2 * L] = leafbox[2 * L] = box[2 * e];
+  cbox[2 * L + 1] = leafbox[2 * L + 1] = box[2 * e + 1];
+}
+
+__global__ void __launch_bounds__(256) ploc_nn(const int* __restrict__ cnt, const float4* __restrict__ cbox, int r,
+                                                int* __restrict__ nn) {
+  const int n = cnt[0];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float4 lo = cbox[2 * i], hi = cbox[2 * i + 1];
+  float best = __builtin_inff();
+  int bj = i;
+  const int j0 = max(0, i - r), j1 = min(n - 1, i + r);
+  for (int j = j0; j <= j1; ++j) {  // ascending j + strict <: ties go to the smallest j (the smaller pair)
+    if (j == i) continue;
+    const float4 l2 = cbox[2 * j], h2 = cbox[2 * j + 1];
+    const float a = half_area(float4{gmin(lo.x, l2.x), gmin(lo.y, l2.y), gmin(lo.z, l2.z), 0.0f},
+                              float4{gmax(hi.x, h2.x), gmax(hi.y, h2.y), gmax(hi.z, h2.z), 0.0f});
+    if (a < best) {
+      best = a;
+      bj = j;
+    }
+  }
+  nn[i] = bj;
+}
+
+// f[i] = (merges here << 32) | survives, for i < N (zero past the live clusters)
+__global__ void __launch_bounds__(256) ploc_flags(const int* __restrict__ cnt, const int* __restrict__ nn, int N,
+                                                   uint64_t* __restrict__ f) {
+  const int n = cnt[0];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= N) return;
+  if (i >= n) {
+    f[i] = 0;
+    return;
+  }
+  const int j = nn[i];
+  const bool mutual = j != i && nn[j] == i;
+  f[i] = ((uint64_t)(mutual && i < j) << 32) | (uint64_t)!(mutual && i > j);
+}
+
+__global__ void __launch_bounds__(256) ploc_compact(const int* __restrict__ cin, int* __restrict__ cout,
+                                                     const int* __restrict__ C, const float4* __restrict__ cbox,
+                                                     const int* __restrict__ nn, const uint64_t* __restrict__ f,
+                                                     const uint64_t* __restrict__ pf, int* __restrict__ C2,
+                                                     float4* __restrict__ cbox2, int2* __restrict__ nchild,
+                                                     float4* __restrict__ nbox) {
+  const int n = cin[0], created = cin[1];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t fi = f[i], pi = pf[i];
+  if (i == n - 1) {
+    const uint64_t tot = pi + fi;
+    cout[0] = (int)(tot & 0xffffffffu);
+    cout[1] = created + (int)(tot >> 32);
+  }
+  if (!(fi & 1u)) return;
+  const int p = (int)(pi & 0xffffffffu);
+  if (fi >> 32) {
+    const int j = nn[i], k = created + (int)(pi >> 32);
+    const float4 al = cbox[2 * i], ah = cbox[2 * i + 1], bl = cbox[2 * j], bh = cbox[2 * j + 1];
+    const float4 lo = float4{gmin(al.x, bl.x), gmin(al.y, bl.y), gmin(al.z, bl.z), 0.0f};
+    const float4 hi = float4{gmax(ah.x, bh.x), gmax(ah.y, bh.y), gmax(ah.z, bh.z), 0.0f};
+    nchild[k] = int2{C[i], C[j]};
+    nbox[2 * k] = lo;
+    nbox[2 * k + 1] = hi;
+    C2[p] = k;
+    cbox2[2 * p] = lo;
+    cbox2[2 * p + 1] = hi;
+  } else {
+    C2[p] = C[i];
+    cbox2[2 * p] = cbox[2 * i];
+    cbox2[2 * p + 1] = cbox[2 * i + 1];
+  }
+}
+
+// BVHNode_encoded: PLOC node k -> node 1 + (M - 2 - k) (the root, created last, is node 1); leaf L -> node M + L
+__global__ void __launch_bounds__(256) ploc_emit(const int* __restrict__ cnt, int N, const int2* __restrict__ nchild,
+                                                  const float4* __restrict__ nbox, const int2* __restrict__ leaf,
+                                                  const float4* __restrict__ cbox_leaf, float* __restrict__ out) {
+  const int M = cnt[4];
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e == 0) {
+    const float dummy[kNodeFloats] = {255, 128, 0, 30, 0, 0, 1, 1, 0, 0, 1, 0};
+    for (int q = 0; q < kNodeFloats; ++q) out[q] = dummy[q];
+  }
+  auto id = [&](int ref) { return ref >= 0 ? 1 + (M - 2 - ref) : M + ~ref; };
+  if (e < M - 1) {
+    float* o = out + (size_t)id(e) * kNodeFloats;
+    const int2 c = nchild[e];
+    const float4 lo = nbox[2 * e], hi = nbox[2 * e + 1];
+    o[0] = (float)id(c.x); o[1] = (float)id(c.y); o[2] = 0.0f;
+    o[3] = 0.0f; o[4] = 0.0f; o[5] = 0.0f;
+    o[6] = lo.x; o[7] = lo.y; o[8] = lo.z;
+    o[9] = hi.x; o[10] = hi.y; o[11] = hi.z;
+  }
+  if (e < M) {
+    float* o = out + (size_t)(M + e) * kNodeFloats;
+    const int2 l = leaf[e];
+    const float4 lo = cbox_leaf[2 * e], hi = cbox_leaf[2 * e + 1];
+    o[0] = 0.0f; o[1] = 0.0f; o[2] = 0.0f;
+    o[3] = (float)l.y; o[4] = (float)l.x; o[5] = 0.0f;
+    o[6] = lo.x; o[7] = lo.y; o[8] = lo.z;
+    o[9] = hi.x; o[10] = hi.y; o[11] = hi.z;
+  }
+}
+
 }  // namespace
 
 int decode_tris(const float* te, int n, float4* geom, float4* shade, hipStream_t s) {
@@ -291,11 +450,19 @@ size_t LbvhWork::need(int n) {
   add(sizeof(int) * n);                     // flags
   add(sizeof(int) * 2 * n * 2);             // keep, id
   add(64);                                  // bounds + count
+  // PLOC top: start, rank, nn, cluster ids x2 | leaf ranges | cluster boxes x2, leaf boxes, node boxes | flags,
+  // scanned flags | node children | counters
+  add(sizeof(int) * n * 5);
+  add(sizeof(int2) * n);
+  add(sizeof(float4) * 2 * n * 4);
+  add(sizeof(uint64_t) * n * 2);
+  add(sizeof(int2) * n);
+  add(64);
   return b;
 }
 
-int lbvh_build(LbvhWork& w, const float* tri, int n, int leaf_n, float* tri_out, float* node_out, int* nnodes,
-               hipStream_t s) {
+int lbvh_build(LbvhWork& w, const float* tri, int n, int leaf_n, int ploc_r, float* tri_out, float* node_out,
+               int* nnodes, hipStream_t s) {
   if (n < 1) return (int)hipErrorInvalidValue;
   int ibits = 1;
   while ((1ll << ibits) < n) ++ibits;
@@ -308,7 +475,11 @@ int lbvh_build(LbvhWork& w, const float* tri, int n, int leaf_n, float* tri_out,
   e = rocprim::exclusive_scan(nullptr, scan_bytes, (int*)nullptr, (int*)nullptr, 0, (size_t)(2 * n - 1),
                               rocprim::plus<int>(), s);
   if (e != hipSuccess) return (int)e;
-  const size_t temp = sort_bytes > scan_bytes ? sort_bytes : scan_bytes;
+  size_t scan64_bytes = 0;
+  e = rocprim::exclusive_scan(nullptr, scan64_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint64_t)0, (size_t)n,
+                              rocprim::plus<uint64_t>(), s);
+  if (e != hipSuccess) return (int)e;
+  const size_t temp = std::max(sort_bytes, std::max(scan_bytes, scan64_bytes));
   if (w.bytes < need + temp) {
     if (w.base) (void)hipFree(w.base);
     w.base = nullptr;
@@ -329,6 +500,15 @@ int lbvh_build(LbvhWork& w, const float* tri, int n, int leaf_n, float* tri_out,
   int* keep = (int*)take(sizeof(int) * 2 * n);
   int* id = (int*)take(sizeof(int) * 2 * n);
   unsigned* bounds = (unsigned*)take(64);
+  int* start = (int*)take(sizeof(int) * n * 5);
+  int *rank = start + n, *nn = start + 2 * n, *C0 = start + 3 * n, *C1 = start + 4 * n;
+  int2* leaf = (int2*)take(sizeof(int2) * n);
+  float4* cb0 = (float4*)take(sizeof(float4) * 2 * n * 4);
+  float4 *cb1 = cb0 + 2 * n, *leafbox = cb0 + 4 * n, *nbox = cb0 + 6 * n;
+  uint64_t* f = (uint64_t*)take(sizeof(uint64_t) * n * 2);
+  uint64_t* pf = f + n;
+  int2* nchild = (int2*)take(sizeof(int2) * n);
+  int* cnt = (int*)take(64);
   void* scratch = (void*)(p);
   const unsigned init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
   if ((e = hipMemcpyAsync(bounds, init, sizeof(init), hipMemcpyHostToDevice, s)) != hipSuccess) return (int)e;
@@ -346,7 +526,47 @@ int lbvh_build(LbvhWork& w, const float* tri, int n, int leaf_n, float* tri_out,
   if ((e = rocprim::exclusive_scan(scratch, cb, keep, id, 0, (size_t)(2 * n - 1), rocprim::plus<int>(), s)) !=
       hipSuccess)
     return (int)e;
-  hipLaunchKernelGGL(lbvh_emit, dim3(ge), dim3(256), 0, s, n, leaf_n, child, range, keep, id, box, node_out);
+  if (ploc_r <= 0 || n == 1) {
+    hipLaunchKernelGGL(lbvh_emit, dim3(ge), dim3(256), 0, s, n, leaf_n, child, range, keep, id, box, node_out);
+  } else {
+    if ((e = hipMemsetAsync(start, 0, sizeof(int) * n, s)) != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(ploc_leafstart, dim3(ge), dim3(256), 0, s, n, leaf_n, range, keep, start);
+    size_t rb = scan_bytes;
+    if ((e = rocprim::exclusive_scan(scratch, rb, start, rank, 0, (size_t)n, rocprim::plus<int>(), s)) != hipSuccess)
+      return (int)e;
+    hipLaunchKernelGGL(ploc_init, dim3(ge), dim3(256), 0, s, n, leaf_n, range, keep, rank, start, box, leaf, leafbox, C0,
+                       cb0, cnt);
+    // iterations in batches; a converged array (one cluster) makes further iterations no-ops
+    int host_cnt[5] = {0, 0, 0, 0, 0};
+    bool converged = false;
+    for (int it = 0; it < 4096 && !converged;) {
+      for (int b = 0; b < 8; ++b, ++it) {
+        int* cin = cnt + 2 * (it & 1);
+        int* cout = cnt + 2 * ((it + 1) & 1);
+        int* Ci = (it & 1) ? C1 : C0;
+        int* Co = (it & 1) ? C0 : C1;
+        float4* bi = (it & 1) ? cb1 : cb0;
+        float4* bo = (it & 1) ? cb0 : cb1;
+        hipLaunchKernelGGL(ploc_nn, dim3(gb), dim3(256), 0, s, cin, bi, ploc_r, nn);
+        hipLaunchKernelGGL(ploc_flags, dim3(gb), dim3(256), 0, s, cin, nn, n, f);
+        size_t fb = scan64_bytes;
+        if ((e = rocprim::exclusive_scan(scratch, fb, f, pf, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s)) !=
+            hipSuccess)
+          return (int)e;
+        hipLaunchKernelGGL(ploc_compact, dim3(gb), dim3(256), 0, s, cin, cout, Ci, bi, nn, f, pf, Co, bo, nchild, nbox);
+      }
+      if ((e = hipMemcpyAsync(host_cnt, cnt, sizeof(host_cnt), hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
+      if ((e = hipStreamSynchronize(s)) != hipSuccess) return (int)e;
+      converged = host_cnt[2 * (it & 1)] <= 1;
+    }
+    if (!converged) return (int)hipErrorUnknown;  // every iteration merges at least one pair: unreachable
+    hipLaunchKernelGGL(ploc_emit, dim3(gb), dim3(256), 0, s, cnt, n, nchild, nbox, leaf, leafbox, node_out);
+    hipLaunchKernelGGL(lbvh_reorder, dim3((unsigned)(((size_t)n * kTriFloats + 255) / 256)), dim3(256), 0, s, tri,
+                       kout, n, ibits, tri_out);
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return (int)e;
+    *nnodes = 2 * host_cnt[4];  // dummy + (M - 1) PLOC nodes + M leaves
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(lbvh_reorder, dim3((unsigned)(((size_t)n * kTriFloats + 255) / 256)), dim3(256), 0, s, tri, kout,
                      n, ibits, tri_out);
   // output node count = 1 (dummy) + id[last] + keep[last]

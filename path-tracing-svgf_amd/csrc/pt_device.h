@@ -395,11 +395,12 @@ struct LbvhWork {
   size_t bytes = 0;
   static size_t need(int n);
 };
-// node_out needs room for 2n nodes (12 floats each); *nnodes = nodes written (dummy node 0 included).
 // Triangle_encoded texels (device) -> tri_geom (4 float4) / tri_shade (9 float4) records, as get_scene decodes them
 int decode_tris(const float* te, int n, float4* geom, float4* shade, hipStream_t s);
-int lbvh_build(LbvhWork& w, const float* tri, int n, int leaf_n, float* tri_out, float* node_out, int* nnodes,
-               hipStream_t s);
+// node_out needs room for 2n nodes (12 floats each); *nnodes = nodes written (dummy node 0 included).
+// ploc_r > 0: the tree above the LBVH leaves is rebuilt by PLOC with search radius ploc_r.
+int lbvh_build(LbvhWork& w, const float* tri, int n, int leaf_n, int ploc_r, float* tri_out, float* node_out,
+               int* nnodes, hipStream_t s);
 
 }  // namespace ptk
 #endif

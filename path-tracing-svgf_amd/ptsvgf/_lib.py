@@ -83,7 +83,7 @@ _PT_SIGS = [
     ("pt_texture2d_upload", C.c_int, [_u32, C.c_int, C.c_int, _u32, _fp]),
     ("pt_texture2d_wrap", C.c_int, [_vp, C.c_int, C.c_int, _u32p]),
     ("pt_texbuffer_create", C.c_int, [_vp, C.c_size_t, _u32, _u32p]),
-    ("pt_bvh_build", C.c_int, [_u32, C.c_int, _u32, _u32, C.POINTER(C.c_int), _fp]),
+    ("pt_bvh_build", C.c_int, [_u32, C.c_int, C.c_int, _u32, _u32, C.POINTER(C.c_int), _fp]),
     ("pt_texarray_create", C.c_int, [C.c_int, C.c_int, C.c_int, _u32p]),
     ("pt_texarray_upload_layer", C.c_int, [_u32, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint8)]),
     ("pt_texture_readback", C.c_int, [_u32, _fp, C.c_size_t]),

@@ -98,12 +98,12 @@ def buffer_readback(tex: int) -> np.ndarray:
     return out
 
 
-def bvh_build(tri_in: int, tri_out: int, node_out: int, leaf_n: int = 8):
+def bvh_build(tri_in: int, tri_out: int, node_out: int, leaf_n: int = 8, ploc_radius: int = 0):
     """pt_bvh_build: GPU LBVH over the device triangles of tri_in (Triangle_encoded texels) into tri_out (leaf
-    order) and node_out (BVHNode_encoded, dummy node 0, root 1) — the reference's buffer formats (main.cpp:88-151).
-    Returns (node count, device build ms)."""
+    order) and node_out (BVHNode_encoded, dummy node 0, root 1) — the reference's buffer formats (main.cpp:88-151);
+    ploc_radius > 0 rebuilds the tree above the LBVH leaves by PLOC. Returns (node count, device build ms)."""
     n, ms = C.c_int(), C.c_float()
-    check(pt().pt_bvh_build(tri_in, leaf_n, tri_out, node_out, C.byref(n), C.byref(ms)))
+    check(pt().pt_bvh_build(tri_in, leaf_n, ploc_radius, tri_out, node_out, C.byref(n), C.byref(ms)))
     return n.value, ms.value
 
 

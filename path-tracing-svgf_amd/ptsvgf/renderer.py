@@ -731,11 +731,12 @@ class Renderer:
             self._slot_free[f % self.K] = ev
 
     # --------------------------------------------------------- accessors ---
-    def rebuild_bvh(self, tri_enc=None, raster=None, leaf_n: int = 8):
+    def rebuild_bvh(self, tri_enc=None, raster=None, leaf_n: int = 8, ploc_radius: int = 16):
         """Dynamic scenes: rebuild the path tracer's BVH on the GPU (pt_bvh_build) into the scene
         buffers the passes are bound to. `tri_enc` (Triangle_encoded rows, any order; default: the scene's
         triangles) carries moved vertices; `raster` (the pre-BVH vertex list, obj_loader.h:143-160) moves the
-        G-buffer's triangles with them. Frames already issued finish first. Returns (nodes, device build ms)."""
+        G-buffer's triangles with them; ploc_radius > 0 rebuilds the tree above the LBVH leaves by PLOC (0: the plain
+        LBVH). Frames already issued finish first. Returns (nodes, device build ms)."""
         if self._streams is not None:
             import torch
 
@@ -743,7 +744,7 @@ class Renderer:
             torch.cuda.synchronize()
         src = gl.texture_buffer(self.scene.tri_enc if tri_enc is None else np.asarray(tri_enc, np.float32))
         try:
-            nodes, ms = gl.bvh_build(src, self.trianglesTextureBuffer, self.nodesTextureBuffer, leaf_n)
+            nodes, ms = gl.bvh_build(src, self.trianglesTextureBuffer, self.nodesTextureBuffer, leaf_n, ploc_radius)
         finally:
             gl.destroy_texture(src)
         for p, _ in self.pt_slots:

@@ -1,8 +1,8 @@
 """GPU LBVH builder (pt_bvh_build, csrc/kernels_bvh.hip) — SURVEY.md §8(f)2, dynamic scenes.
 
 * The built buffers equal the CPU restatement (oracle/lbvh_ref.py) bit for bit: triangles in leaf order and
-  BVHNode_encoded nodes, on the full bench scene, the Cornell stand-in and tiny / degenerate inputs, for several
-  leaf sizes; the trees are valid (every triangle in one leaf, exact boxes).
+  BVHNode_encoded nodes, on the full bench scene and tiny / degenerate inputs, for several leaf sizes, as a plain
+  LBVH and with the PLOC-built top; the trees are valid (every triangle in one leaf, exact boxes).
 * Rendering over the GPU-built buffers (fast driver, frames in flight, every default switch) is bit-exact against
   the oracle path tracer walking the same buffers, before and after a rebuild for moved geometry.
 The tree itself is not the reference's (buildBVHwithSAH, Utils/BVH.h:42-173, is a host sort-and-sweep): parity
@@ -22,11 +22,11 @@ import lbvh_ref as L  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def _build(gl, tri, leaf_n):
+def _build(gl, tri, leaf_n, ploc=0):
     src = gl.texture_buffer(tri)
     to = gl.texture_buffer(np.zeros(3, np.float32))
     no = gl.texture_buffer(np.zeros(3, np.float32))
-    nodes, ms = gl.bvh_build(src, to, no, leaf_n)
+    nodes, ms = gl.bvh_build(src, to, no, leaf_n, ploc)
     out = gl.buffer_readback(to).reshape(-1, 45), gl.buffer_readback(no).reshape(-1, 12)
     for h in (src, to, no):
         gl.destroy_texture(h)
@@ -44,23 +44,27 @@ def _random_tris(n, seed=0, flat_axis=None):
     return t
 
 
+@pytest.mark.parametrize("ploc", [0, 16])
 @pytest.mark.parametrize("leaf_n", [1, 8, 15])
-def test_gpu_lbvh_equals_oracle_bench_scene(gpu, scene_bench, leaf_n):
-    (tri, nodes), ms = _build(gpu, scene_bench.tri_enc, leaf_n)
-    want_tri, want_nodes = L.lbvh(scene_bench.tri_enc, leaf_n)
+def test_gpu_lbvh_equals_oracle_bench_scene(gpu, scene_bench, leaf_n, ploc):
+    if leaf_n == 1 and ploc:
+        pytest.skip("PLOC over 30 k single-triangle leaves: the Python restatement takes minutes")
+    (tri, nodes), ms = _build(gpu, scene_bench.tri_enc, leaf_n, ploc)
+    want_tri, want_nodes = L.lbvh(scene_bench.tri_enc, leaf_n, ploc)
     assert np.array_equal(tri.view(np.uint32), want_tri.view(np.uint32))
     assert np.array_equal(nodes.view(np.uint32), want_nodes.view(np.uint32))
     info = L.check_tree(tri, nodes, leaf_n)
-    print(f"bench scene {scene_bench.ntris} tris leaf_n {leaf_n}: {len(nodes)} nodes, {info['leaves']} leaves, "
-          f"depth {info['depth']}, build {ms:.3f} ms")
+    print(f"bench scene {scene_bench.ntris} tris leaf_n {leaf_n} ploc {ploc}: {len(nodes)} nodes, "
+          f"{info['leaves']} leaves, depth {info['depth']}, build {ms:.3f} ms")
 
 
+@pytest.mark.parametrize("ploc", [0, 1, 16])
 @pytest.mark.parametrize("n", [1, 2, 3, 17, 1000, 70000])
 @pytest.mark.parametrize("flat", [None, 2])
-def test_gpu_lbvh_equals_oracle_synthetic(gpu, n, flat):
+def test_gpu_lbvh_equals_oracle_synthetic(gpu, n, flat, ploc):
     t = _random_tris(n, seed=n + 7, flat_axis=flat)
-    (tri, nodes), _ = _build(gpu, t, 4)
-    want_tri, want_nodes = L.lbvh(t, 4)
+    (tri, nodes), _ = _build(gpu, t, 4, ploc)
+    want_tri, want_nodes = L.lbvh(t, 4, ploc)
     assert np.array_equal(tri.view(np.uint32), want_tri.view(np.uint32))
     assert np.array_equal(nodes.view(np.uint32), want_nodes.view(np.uint32))
 
@@ -78,6 +82,8 @@ def test_gpu_lbvh_rejects_bad_arguments(gpu):
     for args in ((src, src, to, 8), (src, to, to, 8), (src, to, src, 8)):
         with pytest.raises(PtError):
             gpu.bvh_build(args[0], args[1], args[2], args[3])
+    with pytest.raises(PtError):
+        gpu.bvh_build(src, to, gpu.texture_buffer(np.zeros(3, np.float32)), 8, -1)
     no = gpu.texture_buffer(np.zeros(3, np.float32))
     for leaf_n in (0, 16):
         with pytest.raises(PtError):
@@ -105,13 +111,13 @@ def test_render_over_gpu_lbvh_matches_oracle(gpu, scene_small):
 
     W, H = 96, 64
     r = Renderer(scene_small, W, H, mode="fast", frames_in_flight=2, run_taa=False, run_output=False)
-    r.rebuild_bvh(leaf_n=8)
-    tri, nodes = L.lbvh(scene_small.tri_enc, 8)
+    r.rebuild_bvh(leaf_n=8, ploc_radius=16)
+    tri, nodes = L.lbvh(scene_small.tri_enc, 8, 16)
     for step, (t_enc, want_tri, want_nodes) in enumerate([(scene_small.tri_enc, tri, nodes),
                                                           (_moved(scene_small, 0.05),) + L.lbvh(
-                                                              _moved(scene_small, 0.05), 8)]):
-        if step == 1:
-            r.rebuild_bvh(tri_enc=t_enc, leaf_n=8)
+                                                              _moved(scene_small, 0.05), 8, 0)]):
+        if step == 1:  # the plain LBVH this time
+            r.rebuild_bvh(tri_enc=t_enc, leaf_n=8, ploc_radius=0)
         got_tri = gpu.buffer_readback(r.trianglesTextureBuffer).reshape(-1, 45)
         got_nodes = gpu.buffer_readback(r.nodesTextureBuffer).reshape(-1, 12)
         assert np.array_equal(got_tri.view(np.uint32), want_tri.view(np.uint32))

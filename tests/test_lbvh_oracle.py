@@ -22,27 +22,42 @@ def _random_tris(n, seed=0, flat_axis=None):
     return t
 
 
+@pytest.mark.parametrize("ploc", [0, 16])
 @pytest.mark.parametrize("leaf_n", [1, 4, 8, 15])
-def test_oracle_tree_valid_on_scene(scene_small, leaf_n):
-    tri, nodes = L.lbvh(scene_small.tri_enc, leaf_n)
+def test_oracle_tree_valid_on_scene(scene_small, leaf_n, ploc):
+    tri, nodes = L.lbvh(scene_small.tri_enc, leaf_n, ploc)
     info = L.check_tree(tri, nodes, leaf_n)
     assert info["depth"] < 256  # the reference walk's stack (path_tracing.frag:378)
     # a permutation of the input records
     a = np.sort(scene_small.tri_enc.view(np.uint32), axis=0)
     assert np.array_equal(np.sort(tri.view(np.uint32), axis=0), a)
-    print(f"leaf_n {leaf_n}: {len(nodes)} nodes, {info['leaves']} leaves, depth {info['depth']}")
+    print(f"leaf_n {leaf_n} ploc {ploc}: {len(nodes)} nodes, {info['leaves']} leaves, depth {info['depth']}")
 
 
+@pytest.mark.parametrize("ploc", [0, 1, 16])
 @pytest.mark.parametrize("n", [1, 2, 3, 17, 256, 1000])
 @pytest.mark.parametrize("flat", [None, 1])
-def test_oracle_tree_valid_small(n, flat):
+def test_oracle_tree_valid_small(n, flat, ploc):
     t = _random_tris(n, seed=n, flat_axis=flat)
-    tri, nodes = L.lbvh(t, 4)
+    tri, nodes = L.lbvh(t, 4, ploc)
     L.check_tree(tri, nodes, 4)
     assert sorted(tri[:, 42].astype(int)) == list(range(n))
     k, b = L.keys(t)
     assert len(np.unique(k)) == n and (1 << b) >= n
     assert np.array_equal(nodes[0], L.DUMMY_NODE)
+
+
+def test_ploc_top_lowers_the_surface_area_cost(scene_small):
+    """PLOC's top is a surface-area-driven clustering: its SAH-style cost (sum of interior half areas) is below the
+    LBVH's over the same leaves."""
+    def cost(nodes):
+        d = nodes[1:, 9:12] - nodes[1:, 6:9]
+        a = (d[:, 0] * d[:, 1] + d[:, 1] * d[:, 2]) + d[:, 2] * d[:, 0]
+        return float(a[nodes[1:, 3] == 0].astype(np.float64).sum())
+    _, lb = L.lbvh(scene_small.tri_enc, 8, 0)
+    _, pl = L.lbvh(scene_small.tri_enc, 8, 16)
+    assert len(lb) == len(pl) and cost(pl) < cost(lb)
+    print(f"interior half-area sum: LBVH {cost(lb):.1f}, PLOC {cost(pl):.1f}")
 
 
 def test_oracle_leaf_order_follows_morton_keys():
