@@ -211,8 +211,16 @@ def dynamic_bvh(scene, W, H, K, steps, warmup, host_ms):
             r.frame()
         torch.cuda.synchronize()
         fps = steps / (time.perf_counter() - t0)
+        moved = []  # geometry moved: the path tracer's tree and the K + 1 G-buffer passes' trees, all on the GPU
+        for _ in range(5):
+            t0 = time.perf_counter()
+            r.rebuild_bvh(tri_enc=scene.tri_enc, raster=scene.raster, leaf_n=8, ploc_radius=radius)
+            r.frame()
+            torch.cuda.synchronize()
+            moved.append((time.perf_counter() - t0) * 1e3)
         r.close()
         out[name] = {"nodes": nodes, "gpu_build_ms": round(float(np.median(dev)), 4),
+                     "rebuild_all_trees_plus_frame_ms": round(float(np.median(moved)), 3),
                      "gpu_build_wall_ms": round(float(np.median(wall)), 3),
                      "rebuild_plus_frame_ms": round(float(np.median(upd)), 3),
                      "frame_ms": round(float(np.median(plain)), 3), "fps": round(fps, 3)}

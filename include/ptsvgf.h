@@ -130,6 +130,10 @@ int pt_pass_create(uint32_t program, int width, int height, uint32_t* out_pass);
 int pt_pass_add_color_attachment(uint32_t pass, uint32_t tex);
 int pt_pass_bind(uint32_t pass, int final_pass);
 int pt_raster_pass_bind(uint32_t pass, const float* vertices, size_t n_floats);   /* pos3+nrm3 per vertex */
+/* Dynamic scenes: pt_raster_pass_bind from a DEVICE vertex list (same layout), its G-buffer tree built by the GPU
+ * builder (LBVH, PLOC top with ploc_radius > 0) and its records decoded on the device; the G-buffer does not depend
+ * on the tree (closest t, ties to the lower original index), so the planes equal the host bind's bit for bit. */
+int pt_raster_pass_bind_device(uint32_t pass, const void* device_vertices, size_t n_floats, int ploc_radius);
 int pt_pass_reset_texture_slot(uint32_t pass);
 int pt_pass_set_texture(uint32_t pass, uint32_t target, uint32_t tex, const char* name);
 int pt_pass_set_uniform_mat4(uint32_t pass, const char* name, const float* m16);

@@ -1615,7 +1615,8 @@ int pt_bvh_build(uint32_t tri_in, int leaf_n, int ploc_radius, uint32_t tri_out,
     (void)hipEventRecord(e0, g.stream);
   }
   int nodes = 0;
-  int rc = ptk::lbvh_build(g_lbvh, (const float*)ti->dev, n, leaf_n, ploc_radius, tbuf, nbuf, &nodes, g.stream);
+  int rc = ptk::lbvh_build(g_lbvh, (const float*)ti->dev, ptk::kTriEncoded, n, leaf_n, ploc_radius, tbuf, nbuf,
+                           nullptr, &nodes, g.stream);
   if (out_ms) {
     (void)hipEventRecord(e1, g.stream);
     (void)hipEventSynchronize(e1);
@@ -1802,6 +1803,70 @@ int pt_raster_pass_bind(uint32_t pass, const float* verts, size_t n_floats) {
   TRY(upload_vec(nrm, &p->raster.nrm));
   TRY(upload_vec(bvh, &p->raster.bvh));
   p->raster.root_ref = root;
+  return PT_OK;
+}
+
+int pt_raster_pass_bind_device(uint32_t pass, const void* dverts, size_t n_floats, int ploc_radius) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  Pass* p = pass_of(pass);
+  if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
+  if (g.programs[p->program] != PK_RASTER) return err(PT_ERR_ARG, "not a rasterize pass");
+  if (n_floats % 18) return err(PT_ERR_ARG, "vertex list must be whole triangles of pos3+nrm3");
+  if (ploc_radius < 0 || ploc_radius > 256) return err(PT_ERR_ARG, "ploc_radius must be in [0, 256]");
+  if (n_floats / 18 > (1u << 24)) return err(PT_ERR_ARG, "more than 2^24 raster triangles");
+  const int ntris = (int)(n_floats / 18);
+  if (ntris > 0 && !dverts) return err(PT_ERR_ARG, "null device vertex list");
+  p->raster.ntris = ntris;
+  p->bound = true;
+  if (ntris == 0) return PT_OK;
+  float* nbuf = nullptr;
+  int* order = nullptr;
+  HIPCHK(hipMalloc(&nbuf, (size_t)2 * ntris * 12 * sizeof(float)));
+  if (hipMalloc(&order, (size_t)ntris * sizeof(int)) != hipSuccess) {
+    (void)hipFree(nbuf);
+    return err(PT_ERR_HIP, "pt_raster_pass_bind_device: out of device memory");
+  }
+  auto release = [&]() { (void)hipFree(nbuf); (void)hipFree(order); };
+  int nodes = 0;
+  int rc = ptk::lbvh_build(g_lbvh, (const float*)dverts, ptk::kRasterVerts, ntris, 8, ploc_radius, nullptr, nbuf,
+                           order, &nodes, g.stream);
+  if (rc) { release(); return hip_err((hipError_t)rc, "raster lbvh_build"); }
+  std::vector<float> hn((size_t)nodes * 12);
+  if (hipMemcpy(hn.data(), nbuf, hn.size() * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) {
+    release();
+    return err(PT_ERR_HIP, "pt_raster_pass_bind_device: node readback");
+  }
+  std::vector<float4> bvh;
+  int root = 0, need = 0;
+  rc = pack_bvh(hn.data(), nodes, bvh, &root, ntris, &need);
+  if (rc != PT_OK || need >= kStack) {
+    // the G-buffer walk's stack holds kStack entries: a deeper device tree (coincident centroids) takes the host
+    // bind, whose SAH builder caps the depth; the G-buffer does not depend on the tree
+    std::vector<float> hv(n_floats);
+    const bool ok = hipMemcpy(hv.data(), dverts, n_floats * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess;
+    release();
+    if (!ok) return err(PT_ERR_HIP, "pt_raster_pass_bind_device: vertex readback");
+    return pt_raster_pass_bind(pass, hv.data(), n_floats);
+  }
+  if (p->raster.geom) (void)hipFree(p->raster.geom);
+  if (p->raster.nrm) (void)hipFree(p->raster.nrm);
+  p->raster.geom = p->raster.nrm = nullptr;
+  if (hipMalloc((void**)&p->raster.geom, (size_t)ntris * 4 * sizeof(float4)) != hipSuccess ||
+      hipMalloc((void**)&p->raster.nrm, (size_t)ntris * 3 * sizeof(float4)) != hipSuccess) {
+    release();
+    return err(PT_ERR_HIP, "pt_raster_pass_bind_device: out of device memory");
+  }
+  rc = ptk::decode_raster((const float*)dverts, order, ntris, p->raster.geom, p->raster.nrm, g.stream);
+  if (rc) { release(); return hip_err((hipError_t)rc, "decode_raster"); }
+  if (bvh.empty()) bvh.push_back(float4{0, 0, 0, 0});
+  if ((rc = upload_vec(bvh, &p->raster.bvh)) != PT_OK) { release(); return rc; }
+  p->raster.root_ref = root;
+  p->raster.stack_need = need;
+  // draws of other frames may run on other streams: the records are complete when this returns
+  const hipError_t e = hipStreamSynchronize(g.stream);
+  release();
+  if (e != hipSuccess) return hip_err(e, "pt_raster_pass_bind_device");
   return PT_OK;
 }
 

@@ -52,17 +52,19 @@ __device__ __forceinline__ float unordered(unsigned u) {
 __device__ __forceinline__ float gmin(float a, float b) { return b < a ? b : a; }
 __device__ __forceinline__ float gmax(float a, float b) { return a < b ? b : a; }
 
-__device__ __forceinline__ float3 centroid(const float* t) {
-  return float3{((t[0] + t[3]) + t[6]) / 3.0f, ((t[1] + t[4]) + t[7]) / 3.0f, ((t[2] + t[5]) + t[8]) / 3.0f};
+// p1 at t[0..2], p2 at t[o2..], p3 at t[o3..] (Triangle_encoded: 3, 6; the raster vertex list: 6, 12)
+__device__ __forceinline__ float3 centroid(const float* t, int o2, int o3) {
+  return float3{((t[0] + t[o2]) + t[o3]) / 3.0f, ((t[1] + t[o2 + 1]) + t[o3 + 1]) / 3.0f,
+                ((t[2] + t[o2 + 2]) + t[o3 + 2]) / 3.0f};
 }
 
 // 1. centroids and their bounds. bounds[0..2] = ordered min, bounds[3..5] = ordered max (pre-set by the host).
-__global__ void __launch_bounds__(256) lbvh_centroids(const float* __restrict__ tri, int n, float4* __restrict__ cen,
-                                                       unsigned* __restrict__ bounds) {
+__global__ void __launch_bounds__(256) lbvh_centroids(const float* __restrict__ tri, int n, TriLayout lay,
+                                                       float4* __restrict__ cen, unsigned* __restrict__ bounds) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   unsigned lo[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, hi[3] = {0u, 0u, 0u};
   if (i < n) {
-    const float3 c = centroid(tri + (size_t)i * kTriFloats);
+    const float3 c = centroid(tri + (size_t)i * lay.stride, lay.o2, lay.o3);
     cen[i] = float4{c.x, c.y, c.z, 0.0f};
     lo[0] = hi[0] = ordered(c.x);
     lo[1] = hi[1] = ordered(c.y);
@@ -152,19 +154,21 @@ __global__ void __launch_bounds__(256) lbvh_karras(const uint64_t* __restrict__ 
 }
 
 // 5. bottom-up boxes. box[e] (e: internal 0..n-2, primitive n-1+p) = lo.xyz, hi.xyz as 2 float4.
-__global__ void __launch_bounds__(256) lbvh_refit(const float* __restrict__ tri, const uint64_t* __restrict__ k, int n,
-                                                   int ibits, const int2* __restrict__ child,
-                                                   const int* __restrict__ parent, float4* box, int* flags) {
+__global__ void __launch_bounds__(256) lbvh_refit(const float* __restrict__ tri, TriLayout lay,
+                                                   const uint64_t* __restrict__ k, int n, int ibits,
+                                                   const int2* __restrict__ child, const int* __restrict__ parent,
+                                                   float4* box, int* flags, int* __restrict__ order) {
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= n) return;
   const uint64_t mask = (ibits >= 64) ? ~0ull : ((1ull << ibits) - 1ull);
   const int orig = (int)(k[p] & mask);
-  const float* t = tri + (size_t)orig * kTriFloats;
+  if (order) order[p] = orig;
+  const float* t = tri + (size_t)orig * lay.stride;
   float lo[3], hi[3];
 #pragma unroll
   for (int a = 0; a < 3; ++a) {  // BVH.h:54-66: min(p1, min(p2, p3)) per axis
-    lo[a] = gmin(t[a], gmin(t[3 + a], t[6 + a]));
-    hi[a] = gmax(t[a], gmax(t[3 + a], t[6 + a]));
+    lo[a] = gmin(t[a], gmin(t[lay.o2 + a], t[lay.o3 + a]));
+    hi[a] = gmax(t[a], gmax(t[lay.o2 + a], t[lay.o3 + a]));
   }
   int e = n - 1 + p;
   box[2 * e] = float4{lo[0], lo[1], lo[2], 0.0f};
@@ -430,7 +434,34 @@ __global__ void __launch_bounds__(256) ploc_emit(const int* __restrict__ cnt, in
   }
 }
 
+// Raster vertex list (pos3 + nrm3 per vertex, obj_loader.h:143-160) -> the G-buffer's records in leaf order, as
+// pt_raster_pass_bind writes them on the host: (p1, original index bits), e1, e2, cross(e1, e2); the three normals.
+__global__ void __launch_bounds__(256) decode_raster_kernel(const float* __restrict__ verts,
+                                                             const int* __restrict__ order, int n,
+                                                             float4* __restrict__ geom, float4* __restrict__ nrm) {
+  using namespace glsl;
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= n) return;
+  const int oi = order[k];
+  const float* f = verts + (size_t)oi * 18;
+  const v3 p1 = mk(f[0], f[1], f[2]), p2 = mk(f[6], f[7], f[8]), p3 = mk(f[12], f[13], f[14]);
+  const v3 e1 = sub(p2, p1), e2 = sub(p3, p1), ng = cross(e1, e2);
+  geom[4 * k + 0] = float4{p1.x, p1.y, p1.z, __int_as_float(oi)};
+  geom[4 * k + 1] = float4{e1.x, e1.y, e1.z, 0.0f};
+  geom[4 * k + 2] = float4{e2.x, e2.y, e2.z, 0.0f};
+  geom[4 * k + 3] = float4{ng.x, ng.y, ng.z, 0.0f};
+  nrm[3 * k + 0] = float4{f[3], f[4], f[5], 0.0f};
+  nrm[3 * k + 1] = float4{f[9], f[10], f[11], 0.0f};
+  nrm[3 * k + 2] = float4{f[15], f[16], f[17], 0.0f};
+}
+
 }  // namespace
+
+int decode_raster(const float* verts, const int* order, int n, float4* geom, float4* nrm, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(decode_raster_kernel, dim3((n + 255) / 256), dim3(256), 0, s, verts, order, n, geom, nrm);
+  return (int)hipGetLastError();
+}
 
 int decode_tris(const float* te, int n, float4* geom, float4* shade, hipStream_t s) {
   if (n <= 0) return 0;
@@ -461,8 +492,8 @@ size_t LbvhWork::need(int n) {
   return b;
 }
 
-int lbvh_build(LbvhWork& w, const float* tri, int n, int leaf_n, int ploc_r, float* tri_out, float* node_out,
-               int* nnodes, hipStream_t s) {
+int lbvh_build(LbvhWork& w, const float* tri, TriLayout lay, int n, int leaf_n, int ploc_r, float* tri_out,
+               float* node_out, int* order, int* nnodes, hipStream_t s) {
   if (n < 1) return (int)hipErrorInvalidValue;
   int ibits = 1;
   while ((1ll << ibits) < n) ++ibits;
@@ -514,13 +545,13 @@ int lbvh_build(LbvhWork& w, const float* tri, int n, int leaf_n, int ploc_r, flo
   if ((e = hipMemcpyAsync(bounds, init, sizeof(init), hipMemcpyHostToDevice, s)) != hipSuccess) return (int)e;
   if ((e = hipMemsetAsync(flags, 0, sizeof(int) * n, s)) != hipSuccess) return (int)e;
   const int gb = (n + 255) / 256, ge = (2 * n - 1 + 255) / 256;
-  hipLaunchKernelGGL(lbvh_centroids, dim3(gb), dim3(256), 0, s, tri, n, cen, bounds);
+  hipLaunchKernelGGL(lbvh_centroids, dim3(gb), dim3(256), 0, s, tri, n, lay, cen, bounds);
   hipLaunchKernelGGL(lbvh_keys, dim3(gb), dim3(256), 0, s, cen, n, bounds, ibits, kin);
   size_t sb = sort_bytes;
   if ((e = rocprim::radix_sort_keys(scratch, sb, kin, kout, (size_t)n, 0, 30 + ibits, s)) != hipSuccess) return (int)e;
   if (n > 1) hipLaunchKernelGGL(lbvh_karras, dim3((n - 1 + 255) / 256), dim3(256), 0, s, kout, n, child, range, parent);
   else if ((e = hipMemsetAsync(parent, 0xff, sizeof(int), s)) != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(lbvh_refit, dim3(gb), dim3(256), 0, s, tri, kout, n, ibits, child, parent, box, flags);
+  hipLaunchKernelGGL(lbvh_refit, dim3(gb), dim3(256), 0, s, tri, lay, kout, n, ibits, child, parent, box, flags, order);
   hipLaunchKernelGGL(lbvh_mark, dim3(ge), dim3(256), 0, s, n, leaf_n, range, parent, keep);
   size_t cb = scan_bytes;
   if ((e = rocprim::exclusive_scan(scratch, cb, keep, id, 0, (size_t)(2 * n - 1), rocprim::plus<int>(), s)) !=
@@ -561,14 +592,16 @@ int lbvh_build(LbvhWork& w, const float* tri, int n, int leaf_n, int ploc_r, flo
     }
     if (!converged) return (int)hipErrorUnknown;  // every iteration merges at least one pair: unreachable
     hipLaunchKernelGGL(ploc_emit, dim3(gb), dim3(256), 0, s, cnt, n, nchild, nbox, leaf, leafbox, node_out);
-    hipLaunchKernelGGL(lbvh_reorder, dim3((unsigned)(((size_t)n * kTriFloats + 255) / 256)), dim3(256), 0, s, tri,
-                       kout, n, ibits, tri_out);
+    if (tri_out)
+      hipLaunchKernelGGL(lbvh_reorder, dim3((unsigned)(((size_t)n * kTriFloats + 255) / 256)), dim3(256), 0, s, tri,
+                         kout, n, ibits, tri_out);
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return (int)e;
     *nnodes = 2 * host_cnt[4];  // dummy + (M - 1) PLOC nodes + M leaves
     return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL(lbvh_reorder, dim3((unsigned)(((size_t)n * kTriFloats + 255) / 256)), dim3(256), 0, s, tri, kout,
-                     n, ibits, tri_out);
+  if (tri_out)
+    hipLaunchKernelGGL(lbvh_reorder, dim3((unsigned)(((size_t)n * kTriFloats + 255) / 256)), dim3(256), 0, s, tri,
+                       kout, n, ibits, tri_out);
   // output node count = 1 (dummy) + id[last] + keep[last]
   int tail[2];
   if ((e = hipMemcpyAsync(&tail[0], id + 2 * n - 2, sizeof(int), hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;

@@ -397,10 +397,20 @@ struct LbvhWork {
 };
 // Triangle_encoded texels (device) -> tri_geom (4 float4) / tri_shade (9 float4) records, as get_scene decodes them
 int decode_tris(const float* te, int n, float4* geom, float4* shade, hipStream_t s);
+// Raster vertex list (18 floats per triangle) -> the G-buffer's geom (4 float4) / nrm (3 float4) records in the
+// given leaf order (order[k] = original triangle index), as pt_raster_pass_bind builds them on the host
+int decode_raster(const float* verts, const int* order, int n, float4* geom, float4* nrm, hipStream_t s);
+// Where a triangle record keeps its vertices: p1 at 0, p2 at o2, p3 at o3, records `stride` floats apart.
+struct TriLayout {
+  int stride, o2, o3;
+};
+constexpr TriLayout kTriEncoded{45, 3, 6};   // Triangle_encoded (Utils/Triangle.h:12-24)
+constexpr TriLayout kRasterVerts{18, 6, 12};  // the raster vertex list (obj_loader.h:143-160)
 // node_out needs room for 2n nodes (12 floats each); *nnodes = nodes written (dummy node 0 included).
-// ploc_r > 0: the tree above the LBVH leaves is rebuilt by PLOC with search radius ploc_r.
-int lbvh_build(LbvhWork& w, const float* tri, int n, int leaf_n, int ploc_r, float* tri_out, float* node_out,
-               int* nnodes, hipStream_t s);
+// ploc_r > 0: the tree above the LBVH leaves is rebuilt by PLOC with search radius ploc_r. tri_out (45-float
+// records only) may be null; order (may be null) receives the original index of each leaf-order position.
+int lbvh_build(LbvhWork& w, const float* tri, TriLayout lay, int n, int leaf_n, int ploc_r, float* tri_out,
+               float* node_out, int* order, int* nnodes, hipStream_t s);
 
 }  // namespace ptk
 #endif

@@ -248,3 +248,12 @@ class Rasterize_RenderPass(RenderPass):
             check(pt().pt_pass_add_color_attachment(h, t))
         v = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1)
         check(pt().pt_raster_pass_bind(h, fptr(v), v.size))
+
+    def rebind_vertices(self, vertices) -> None:
+        """A new vertex list for the bound pass (moved geometry): pt_raster_pass_bind again, attachments kept."""
+        v = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1)
+        check(pt().pt_raster_pass_bind(self._handle(), fptr(v), v.size))
+
+    def rebind_vertices_device(self, device_ptr: int, n_floats: int, ploc_radius: int = 16) -> None:
+        """pt_raster_pass_bind_device: the vertex list already in device memory, its tree built on the GPU."""
+        check(pt().pt_raster_pass_bind_device(self._handle(), C.c_void_p(device_ptr), n_floats, ploc_radius))

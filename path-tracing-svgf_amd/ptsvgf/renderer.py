@@ -749,9 +749,13 @@ class Renderer:
             gl.destroy_texture(src)
         for p, _ in self.pt_slots:
             p.set_uniform_int("nNodes", nodes)
-        if raster is not None:
+        if raster is not None:  # the G-buffer passes: their trees built on the GPU from one device copy
+            import torch
+
+            v = torch.from_numpy(np.ascontiguousarray(raster, np.float32).reshape(-1)).cuda()
+            torch.cuda.synchronize()
             for p in self.init_pass:
-                p.bindData(raster)
+                p.rebind_vertices_device(v.data_ptr(), v.numel(), ploc_radius)
         return nodes, ms
 
     def close(self) -> None:

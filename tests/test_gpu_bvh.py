@@ -132,3 +132,33 @@ def test_render_over_gpu_lbvh_matches_oracle(gpu, scene_small):
         for key in ("color", "emission", "albedo"):
             assert np.array_equal(got[key].view(np.uint32), want[key].view(np.uint32)), (step, key)
     r.close()
+
+
+@pytest.mark.parametrize("gbuffer_mode", [1, 0])
+def test_device_raster_bind_equals_host_bind(gpu, scene_small, gbuffer_mode):
+    """pt_raster_pass_bind_device (the G-buffer's tree built by the GPU builder from a device vertex list, records
+    decoded on the device) after a move of the whole scene: G-buffer planes bit-identical to a renderer bound on the
+    host to the moved vertex list — tile-binned rasterisation (mode 1) and the ray cast walking the tree (mode 0)."""
+    from ptsvgf.renderer import Renderer
+
+    W, H = 160, 96
+    raster = scene_small.raster.reshape(-1, 6).copy()
+    raster[:, 1] += np.float32(0.03)  # every vertex position up by 0.03 (pos3 + nrm3 per vertex)
+    tri = scene_small.tri_enc.copy()
+    tri[:, [1, 4, 7]] += np.float32(0.03)
+    planes = ("normal_depth", "velocity", "fwidth", "world")
+    out = []
+    for device in (False, True):
+        sc = dataclasses.replace(scene_small, raster=raster.reshape(-1)) if not device else scene_small
+        r = Renderer(sc, W, H, mode="fast", run_taa=False, run_output=False)
+        if device:
+            r.rebuild_bvh(tri_enc=tri, raster=raster, leaf_n=8, ploc_radius=16)
+        for p in r.init_pass:
+            p.set_uniform_int("gbuffer_mode", gbuffer_mode)
+        r.frame()
+        got = r.planes()
+        out.append({k: gpu.readback(got[k]) for k in planes})
+        r.close()
+    for k in planes:
+        assert np.array_equal(out[0][k].view(np.uint32), out[1][k].view(np.uint32)), k
+    assert 0.05 < float(np.mean(out[0]["normal_depth"][..., 3] != 1.0)) < 0.95
