@@ -749,13 +749,15 @@ class Renderer:
             gl.destroy_texture(src)
         for p, _ in self.pt_slots:
             p.set_uniform_int("nNodes", nodes)
-        if raster is not None:  # the G-buffer passes: their trees built on the GPU from one device copy
+        if raster is not None:
+            # the G-buffer passes: trees built on the GPU from one device copy; a plain LBVH, since the tile-binned
+            # rasteriser walks it only when a tile list overflows
             import torch
 
             v = torch.from_numpy(np.ascontiguousarray(raster, np.float32).reshape(-1)).cuda()
             torch.cuda.synchronize()
             for p in self.init_pass:
-                p.rebind_vertices_device(v.data_ptr(), v.numel(), ploc_radius)
+                p.rebind_vertices_device(v.data_ptr(), v.numel(), 0)
         return nodes, ms
 
     def close(self) -> None:
