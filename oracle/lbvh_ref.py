@@ -48,11 +48,14 @@ def keys(tri_enc: np.ndarray):
     t = np.asarray(tri_enc, np.float32).reshape(-1, 45)
     n = t.shape[0]
     c = ((t[:, 0:3] + t[:, 3:6]) + t[:, 6:9]) / np.float32(3.0)
-    lo, hi = c.min(axis=0), c.max(axis=0)
+    with np.errstate(invalid="ignore"), __import__("warnings").catch_warnings():
+        __import__("warnings").simplefilter("ignore", RuntimeWarning)
+        lo, hi = np.nanmin(c, axis=0), np.nanmax(c, axis=0)  # NaN centroids stay out of the bounds
     ext = (hi - lo).astype(np.float32)
     with np.errstate(divide="ignore", invalid="ignore"):
         q = np.where(ext > 0, (c - lo) / np.where(ext > 0, ext, np.float32(1)), np.float32(0)).astype(np.float32)
     v = np.floor(q * np.float32(1024.0))
+    v = np.where(np.isnan(v), np.float32(0), v)  # NaN -> cell 0
     cell = np.clip(v, 0, 1023).astype(np.uint64)
     m = (_spread10(cell[:, 0]) << np.uint64(2)) | (_spread10(cell[:, 1]) << np.uint64(1)) | _spread10(cell[:, 2])
     b = 1
@@ -157,18 +160,24 @@ def ploc_top(leaves, r: int) -> np.ndarray:
     while n > 1:
         idx = np.arange(n)
         best = np.full(n, np.inf, np.float32)
-        bj = idx.copy()
+        bj = np.full(n, -1, np.int64)
         for off in range(-r, r + 1):  # ascending j: the first minimum wins
             if off == 0:
                 continue
             j = idx + off
             valid = (j >= 0) & (j < n)
             jj = np.clip(j, 0, n - 1)
-            d = _gmax(ch, ch[jj]) - _gmin(cl, cl[jj])
-            a = (d[:, 0] * d[:, 1] + d[:, 1] * d[:, 2]) + d[:, 2] * d[:, 0]
-            better = valid & (a < best)
+            with np.errstate(invalid="ignore"):  # union in position order (lower position first)
+                if off < 0:
+                    d = _gmax(ch[jj], ch) - _gmin(cl[jj], cl)
+                else:
+                    d = _gmax(ch, ch[jj]) - _gmin(cl, cl[jj])
+                a = (d[:, 0] * d[:, 1] + d[:, 1] * d[:, 2]) + d[:, 2] * d[:, 0]
+            a = np.where(np.isnan(a), np.float32(np.inf), a)  # NaN boxes rank last
+            better = valid & ((bj < 0) | (a < best))
             best = np.where(better, a, best)
             bj = np.where(better, j, bj)
+        bj = np.where(bj < 0, idx, bj)
         mutual = (bj != idx) & (bj[bj] == idx)
         newf = mutual & (idx < bj)
         keepf = ~(mutual & (idx > bj))
@@ -234,12 +243,15 @@ def check_tree(tri_sorted: np.ndarray, nodes: np.ndarray, leaf_n: int) -> dict:
             seen[first:first + cnt] += 1
             leaves += 1
             lo, hi = tlo[first:first + cnt].min(0), thi[first:first + cnt].max(0)
+            if not np.isfinite(t[first:first + cnt, :9]).all():
+                lo = hi = None  # NaN vertices: the box depends on the union order (glm min/max), not checked
         else:
             a, c = int(f[0]), int(f[1])
             stack += [(a, d + 1), (c, d + 1)]
             lo = hi = None
         if lo is not None:
-            assert np.array_equal(f[6:9], lo) and np.array_equal(f[9:12], hi), f"leaf {i} box"
+            assert np.array_equal(f[6:9], lo, equal_nan=True) and np.array_equal(f[9:12], hi, equal_nan=True), \
+                f"leaf {i} box"
     assert visited[1:].all(), "nodes not reachable from the root"
     assert (seen == 1).all(), "a triangle is in no leaf or in several"
     # interior boxes: the union of their children's boxes
@@ -247,6 +259,7 @@ def check_tree(tri_sorted: np.ndarray, nodes: np.ndarray, leaf_n: int) -> dict:
         f = nodes[i]
         if int(f[3]) == 0:
             a, c = nodes[int(f[0])], nodes[int(f[1])]
-            assert np.array_equal(f[6:9], np.minimum(a[6:9], c[6:9])), f"node {i} AA"
-            assert np.array_equal(f[9:12], np.maximum(a[9:12], c[9:12])), f"node {i} BB"
+            if np.isfinite(f[6:12]).all() and np.isfinite(a[6:12]).all() and np.isfinite(c[6:12]).all():
+                assert np.array_equal(f[6:9], np.minimum(a[6:9], c[6:9])), f"node {i} AA"
+                assert np.array_equal(f[9:12], np.maximum(a[9:12], c[9:12])), f"node {i} BB"
     return {"leaves": leaves, "depth": depth}

@@ -66,9 +66,10 @@ __global__ void __launch_bounds__(256) lbvh_centroids(const float* __restrict__ 
   if (i < n) {
     const float3 c = centroid(tri + (size_t)i * lay.stride, lay.o2, lay.o3);
     cen[i] = float4{c.x, c.y, c.z, 0.0f};
-    lo[0] = hi[0] = ordered(c.x);
-    lo[1] = hi[1] = ordered(c.y);
-    lo[2] = hi[2] = ordered(c.z);
+    const float cc[3] = {c.x, c.y, c.z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a)  // NaN centroids (NaN vertices) stay out of the bounds
+      if (cc[a] == cc[a]) lo[a] = hi[a] = ordered(cc[a]);
   }
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
@@ -100,7 +101,7 @@ __device__ __forceinline__ uint32_t cell(float c, float lo, float hi) {
   const float ext = hi - lo;
   const float q = ext > 0.0f ? (c - lo) / ext : 0.0f;
   const float v = floorf(q * 1024.0f);
-  return v < 0.0f ? 0u : (v > 1023.0f ? 1023u : (uint32_t)v);
+  return !(v == v) || v < 0.0f ? 0u : (v > 1023.0f ? 1023u : (uint32_t)v);  // NaN -> cell 0
 }
 
 // 2. keys: Morton code (x in the highest of each bit triple) above b index bits
@@ -338,19 +339,23 @@ __global__ void __launch_bounds__(256) ploc_nn(const int* __restrict__ cnt, cons
   if (i >= n) return;
   const float4 lo = cbox[2 * i], hi = cbox[2 * i + 1];
   float best = __builtin_inff();
-  int bj = i;
+  int bj = -1;
   const int j0 = max(0, i - r), j1 = min(n - 1, i + r);
   for (int j = j0; j <= j1; ++j) {  // ascending j + strict <: ties go to the smallest j (the smaller pair)
     if (j == i) continue;
+    // the union in position order (lower position first), as ploc_compact merges: with NaN coordinates glm's
+    // min/max depend on the operand order, and the area must be the same seen from either end of the pair
     const float4 l2 = cbox[2 * j], h2 = cbox[2 * j + 1];
-    const float a = half_area(float4{gmin(lo.x, l2.x), gmin(lo.y, l2.y), gmin(lo.z, l2.z), 0.0f},
-                              float4{gmax(hi.x, h2.x), gmax(hi.y, h2.y), gmax(hi.z, h2.z), 0.0f});
-    if (a < best) {
+    const float4 la = j < i ? l2 : lo, lb = j < i ? lo : l2, ha = j < i ? h2 : hi, hb = j < i ? hi : h2;
+    float a = half_area(float4{gmin(la.x, lb.x), gmin(la.y, lb.y), gmin(la.z, lb.z), 0.0f},
+                        float4{gmax(ha.x, hb.x), gmax(ha.y, hb.y), gmax(ha.z, hb.z), 0.0f});
+    a = a == a ? a : __builtin_inff();  // NaN boxes rank last: (area, index) stays a total order, so PLOC ends
+    if (bj < 0 || a < best) {
       best = a;
       bj = j;
     }
   }
-  nn[i] = bj;
+  nn[i] = bj < 0 ? i : bj;
 }
 
 // f[i] = (merges here << 32) | survives, for i < N (zero past the live clusters)

@@ -69,6 +69,18 @@ def test_gpu_lbvh_equals_oracle_synthetic(gpu, n, flat, ploc):
     assert np.array_equal(nodes.view(np.uint32), want_nodes.view(np.uint32))
 
 
+@pytest.mark.parametrize("ploc", [0, 16])
+def test_gpu_lbvh_nan_vertices_equal_oracle(gpu, ploc):
+    """Garbage input (NaN vertex positions): the device tree still equals the restatement bit for bit (NaN centroids
+    out of the bounds, Morton cell 0; PLOC ranks NaN boxes last and terminates)."""
+    t = _random_tris(300, seed=9)
+    t[[5, 77, 150], 0] = np.nan
+    (tri, nodes), _ = _build(gpu, t, 4, ploc)
+    want_tri, want_nodes = L.lbvh(t, 4, ploc)
+    assert np.array_equal(tri.view(np.uint32), want_tri.view(np.uint32))
+    assert np.array_equal(nodes.view(np.uint32), want_nodes.view(np.uint32))
+
+
 def test_gpu_lbvh_is_deterministic(gpu, scene_cornell):
     a, _ = _build(gpu, scene_cornell.tri_enc, 8)
     b, _ = _build(gpu, scene_cornell.tri_enc, 8)

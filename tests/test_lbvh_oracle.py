@@ -65,3 +65,14 @@ def test_oracle_leaf_order_follows_morton_keys():
     tri, _ = L.lbvh(t, 8)
     k, b = L.keys(t)
     assert np.array_equal(tri[:, 42].astype(np.int64), (np.sort(k) & np.uint64((1 << b) - 1)).astype(np.int64))
+
+
+@pytest.mark.parametrize("ploc", [0, 16])
+def test_oracle_nan_vertices(ploc):
+    """NaN vertex positions (garbage input) still give a valid tree: NaN centroids stay out of the bounds and fall
+    in Morton cell 0, and PLOC ranks NaN boxes last, so it terminates."""
+    t = _random_tris(300, seed=9)
+    t[[5, 77, 150], 0] = np.nan
+    tri, nodes = L.lbvh(t, 4, ploc)
+    L.check_tree(tri, nodes, 4)
+    assert sorted(tri[:, 42].astype(int)) == list(range(300))
