@@ -261,6 +261,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(args.backend)
+        # every rank takes part in the first collective (batch_isend_irecv requires it when it comes first)
+        dist.barrier()
     else:
         torch.cuda.set_device(0)
 
