@@ -176,7 +176,7 @@ def config0(gl):
 
 def dynamic_bvh(scene, W, H, K, steps, warmup, host_ms):
     """SURVEY.md §8(f)2, dynamic scenes: the GPU builder (pt_bvh_build) rebuilding the path tracer's BVH in place —
-    a plain LBVH and with the PLOC-built top (radius 16) — median device and host-wall ms of 10 rebuilds against the
+    a plain LBVH (leaves of <= 8) and with the PLOC-built top (leaves of <= 3, radius 32) — median device and host-wall ms of 10 rebuilds against the
     host SAH build of the same triangles, a rebuild plus the frame that decodes it against a frame alone, and the
     frame rate of the headline configuration rendered over the GPU-built tree instead of the reference's SAH tree."""
     import numpy as np
@@ -185,14 +185,14 @@ def dynamic_bvh(scene, W, H, K, steps, warmup, host_ms):
     from ptsvgf.camera import parameter_config
     from ptsvgf.renderer import Renderer
 
-    out = {"triangles": scene.ntris, "leaf_n": 8, "host_sah_build_ms": round(host_ms, 1) if host_ms else None}
-    for name, radius in (("lbvh", 0), ("ploc16", 16)):
+    out = {"triangles": scene.ntris, "host_sah_build_ms": round(host_ms, 1) if host_ms else None}
+    for name, leaf_n, radius in (("lbvh", 8, 0), ("ploc", 3, 32)):
         r = Renderer(scene, W, H, parameter_config(), mode="fast", aspect_corrected=True, run_taa=False,
                      run_output=False, frames_in_flight=K)
         dev, wall, nodes, upd, plain = [], [], 0, [], []
         for _ in range(10):
             t0 = time.perf_counter()
-            nodes, ms = r.rebuild_bvh(leaf_n=8, ploc_radius=radius)
+            nodes, ms = r.rebuild_bvh(leaf_n=leaf_n, ploc_radius=radius)
             wall.append((time.perf_counter() - t0) * 1e3)
             dev.append(ms)
             r.frame()  # the first draw over the new buffers decodes them (capi get_scene)
@@ -214,12 +214,13 @@ def dynamic_bvh(scene, W, H, K, steps, warmup, host_ms):
         moved = []  # geometry moved: the path tracer's tree and the K + 1 G-buffer passes' trees, all on the GPU
         for _ in range(5):
             t0 = time.perf_counter()
-            r.rebuild_bvh(tri_enc=scene.tri_enc, raster=scene.raster, leaf_n=8, ploc_radius=radius)
+            r.rebuild_bvh(tri_enc=scene.tri_enc, raster=scene.raster, leaf_n=leaf_n, ploc_radius=radius)
             r.frame()
             torch.cuda.synchronize()
             moved.append((time.perf_counter() - t0) * 1e3)
         r.close()
-        out[name] = {"nodes": nodes, "gpu_build_ms": round(float(np.median(dev)), 4),
+        out[name] = {"leaf_n": leaf_n, "ploc_radius": radius, "nodes": nodes,
+                     "gpu_build_ms": round(float(np.median(dev)), 4),
                      "rebuild_all_trees_plus_frame_ms": round(float(np.median(moved)), 3),
                      "gpu_build_wall_ms": round(float(np.median(wall)), 3),
                      "rebuild_plus_frame_ms": round(float(np.median(upd)), 3),
