@@ -86,7 +86,7 @@ def parse():
                     help="path tracers of this many frames drawn as one batch (default 1)")
     ap.add_argument("--frames-in-flight", type=int, default=None,
                     help="K > 1: front ends (G-buffer + path tracer) of K frames overlap on K streams "
-                         "(default 4 on one GPU, 8 on bands: thinner bands have relatively longer launch tails)")
+                         "(default 4 up to 4 GPUs, 8 on 8 bands: thinner bands have relatively longer launch tails)")
     ap.add_argument("--pt-uniform", action="append", default=[], metavar="NAME=INT",
                     help="extra int uniform on the path-tracing pass (A/B switches, e.g. shadow_bvh4=0)")
     return ap.parse_args()
@@ -245,7 +245,9 @@ def main():
         world = args.gpus if world == 1 and args.gpus == 1 else world
     k1080 = args.frames_in_flight  # 1080p: 6 frames in flight by default on one GPU (4 / 6 / 8: 512 / 538 / 536 fps)
     if args.frames_in_flight is None:
-        args.frames_in_flight = 4 if world == 1 else 8
+        # simulated bands (tools/band_sim_sweep.sh): 2 bands K = 4 / 8: 303 / 289 fps, 4 bands 524 / 524, 8 bands: 8
+        # (thin bands' launch tails need more frames to overlap)
+        args.frames_in_flight = 4 if world <= 4 else 8
         k1080 = 6 if world == 1 else 8
     if args.trace_batch is None:
         args.trace_batch = 1

@@ -546,8 +546,9 @@ int lbvh_build(LbvhWork& w, const float* tri, TriLayout lay, int n, int leaf_n, 
   int2* nchild = (int2*)take(sizeof(int2) * n);
   int* cnt = (int*)take(64);
   void* scratch = (void*)(p);
-  const unsigned init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
-  if ((e = hipMemcpyAsync(bounds, init, sizeof(init), hipMemcpyHostToDevice, s)) != hipSuccess) return (int)e;
+  // bounds: ordered min words start at 0xffffffff, max words at 0 (no host buffer involved)
+  if ((e = hipMemsetAsync(bounds, 0xff, 3 * sizeof(unsigned), s)) != hipSuccess) return (int)e;
+  if ((e = hipMemsetAsync(bounds + 3, 0, 3 * sizeof(unsigned), s)) != hipSuccess) return (int)e;
   if ((e = hipMemsetAsync(flags, 0, sizeof(int) * n, s)) != hipSuccess) return (int)e;
   const int gb = (n + 255) / 256, ge = (2 * n - 1 + 255) / 256;
   hipLaunchKernelGGL(lbvh_centroids, dim3(gb), dim3(256), 0, s, tri, n, lay, cen, bounds);
