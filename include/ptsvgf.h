@@ -134,6 +134,10 @@ int pt_raster_pass_bind(uint32_t pass, const float* vertices, size_t n_floats); 
  * builder (LBVH, PLOC top with ploc_radius > 0) and its records decoded on the device; the G-buffer does not depend
  * on the tree (closest t, ties to the lower original index), so the planes equal the host bind's bit for bit. */
 int pt_raster_pass_bind_device(uint32_t pass, const void* device_vertices, size_t n_floats, int ploc_radius);
+/* A rasterize pass drawing another (bound) rasterize pass's triangles and tree: the reference has one G-buffer pass;
+ * a driver with several G-buffer targets (frames in flight) binds one and shares it. Rebinding `pass` ends the share;
+ * destroying `src_pass` first makes `pass`'s draws fail with PT_ERR_STATE. */
+int pt_raster_pass_share(uint32_t pass, uint32_t src_pass);
 int pt_pass_reset_texture_slot(uint32_t pass);
 int pt_pass_set_texture(uint32_t pass, uint32_t target, uint32_t tex, const char* name);
 int pt_pass_set_uniform_mat4(uint32_t pass, const char* name, const float* m16);

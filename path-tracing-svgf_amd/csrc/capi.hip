@@ -202,6 +202,7 @@ struct Pass {
   std::unordered_map<std::string, Uniform> uni;
   int y_begin = -1, y_end = -1;
   RasterScene raster;
+  uint32_t raster_src = 0;  // pt_raster_pass_share: draw this rasterize pass's triangles and tree instead
   RasterBins bins;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
@@ -1180,7 +1181,10 @@ int draw_pathtrace_batch(Pass** ps, int n) {
 }
 
 int draw_raster(Pass* p) {
-  if (!p->raster.geom && p->raster.ntris > 0) return err(PT_ERR_STATE, "raster pass not bound");
+  Pass* src = p->raster_src ? pass_of(p->raster_src) : p;
+  if (!src) return err(PT_ERR_STATE, "raster pass shares the triangles of a destroyed pass");
+  const RasterScene& rs = src->raster;
+  if (!rs.geom && rs.ntris > 0) return err(PT_ERR_STATE, "raster pass not bound");
   GBufParams k;
   memset(&k, 0, sizeof(k));
   k.W = p->W;
@@ -1193,11 +1197,11 @@ int draw_raster(Pass* p) {
   Texture* fwt = tex_of(p->att[3]);
   if (!fwt->aux) HIPCHK(hipMalloc((void**)&fwt->aux, (size_t)fwt->W * fwt->rows * 4));
   k.fwidth_aux = fwt->aux;
-  k.geom = p->raster.geom;
-  k.nrm = p->raster.nrm;
-  k.bvh = p->raster.bvh;
-  k.root_ref = p->raster.root_ref;
-  k.stack_need = p->raster.stack_need;
+  k.geom = rs.geom;
+  k.nrm = rs.nrm;
+  k.bvh = rs.bvh;
+  k.root_ref = rs.root_ref;
+  k.stack_need = rs.stack_need;
   float V[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1}, P[16], PV[16];
   memcpy(P, V, 64);
   memcpy(PV, V, 64);
@@ -1215,14 +1219,14 @@ int draw_raster(Pass* p) {
       k.M[c * 4 + r] = ((P[0 * 4 + r] * V[c * 4 + 0] + P[1 * 4 + r] * V[c * 4 + 1]) + P[2 * 4 + r] * V[c * 4 + 2]) +
                        P[3 * 4 + r] * V[c * 4 + 3];
   memcpy(k.PV, PV, 64);
-  if (p->raster.ntris == 0) k.root_ref = -1;  // empty leaf
+  if (rs.ntris == 0) k.root_ref = -1;  // empty leaf
   if (p->motion_max) {
     HIPCHK(hipMemsetAsync(p->motion_max, 0, sizeof(uint32_t), g.stream));
     k.motion_max = p->motion_max;
   }
   const int ntiles = ((k.W + 15) / 16) * ((std::max(0, k.y1 - k.y0) + 15) / 16);  // gbuffer_kernel's grid
   if (ui(p, "gbuffer_mode", 1) == 1) {  // tile-binned rasterisation (default); the ray cast on list overflow
-    TRY(bins_for(p->bins, p->raster.ntris, k.W, k.y0, k.y1, ui(p, "raster_pair_cap", 0), &k.bins));
+    TRY(bins_for(p->bins, rs.ntris, k.W, k.y0, k.y1, ui(p, "raster_pair_cap", 0), &k.bins));
     int rc = launch_gbuffer_raster(k, g.stream);
     if (rc) return hip_err((hipError_t)rc, "gbuffer raster launch");
   } else {  // A/B: the ray cast with cost-ordered tiles
@@ -1759,6 +1763,7 @@ int pt_raster_pass_bind(uint32_t pass, const float* verts, size_t n_floats) {
   if (n_floats % 18) return err(PT_ERR_ARG, "vertex list must be whole triangles of pos3+nrm3");
   int ntris = (int)(n_floats / 18);
   p->raster.ntris = ntris;
+  p->raster_src = 0;
   p->bound = true;
   if (ntris == 0) return PT_OK;
   // SAH tree over the raster triangles (sah_build: the walk's answer does not depend on the tree);
@@ -1818,6 +1823,7 @@ int pt_raster_pass_bind_device(uint32_t pass, const void* dverts, size_t n_float
   const int ntris = (int)(n_floats / 18);
   if (ntris > 0 && !dverts) return err(PT_ERR_ARG, "null device vertex list");
   p->raster.ntris = ntris;
+  p->raster_src = 0;
   p->bound = true;
   if (ntris == 0) return PT_OK;
   float* nbuf = nullptr;
@@ -1867,6 +1873,19 @@ int pt_raster_pass_bind_device(uint32_t pass, const void* dverts, size_t n_float
   const hipError_t e = hipStreamSynchronize(g.stream);
   release();
   if (e != hipSuccess) return hip_err(e, "pt_raster_pass_bind_device");
+  return PT_OK;
+}
+
+int pt_raster_pass_share(uint32_t pass, uint32_t src_pass) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  Pass *p = pass_of(pass), *s = pass_of(src_pass);
+  if (!p || !s) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
+  if (g.programs[p->program] != PK_RASTER || g.programs[s->program] != PK_RASTER)
+    return err(PT_ERR_ARG, "pt_raster_pass_share: both passes must be rasterize passes");
+  if (pass == src_pass || s->raster_src) return err(PT_ERR_ARG, "pt_raster_pass_share: share from an own-bound pass");
+  p->raster_src = src_pass;
+  p->bound = true;
   return PT_OK;
 }
 

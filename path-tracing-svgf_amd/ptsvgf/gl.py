@@ -257,3 +257,7 @@ class Rasterize_RenderPass(RenderPass):
     def rebind_vertices_device(self, device_ptr: int, n_floats: int, ploc_radius: int = 16) -> None:
         """pt_raster_pass_bind_device: the vertex list already in device memory, its tree built on the GPU."""
         check(pt().pt_raster_pass_bind_device(self._handle(), C.c_void_p(device_ptr), n_floats, ploc_radius))
+
+    def share_vertices(self, src: "Rasterize_RenderPass") -> None:
+        """pt_raster_pass_share: draw src's triangles and tree (src bound on its own)."""
+        check(pt().pt_raster_pass_share(self._handle(), src._handle()))

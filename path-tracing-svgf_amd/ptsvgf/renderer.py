@@ -757,8 +757,9 @@ class Renderer:
 
             v = torch.from_numpy(np.ascontiguousarray(raster, np.float32).reshape(-1)).cuda()
             torch.cuda.synchronize()
-            for p in self.init_pass:
-                p.rebind_vertices_device(v.data_ptr(), v.numel(), 0)
+            self.init_pass[0].rebind_vertices_device(v.data_ptr(), v.numel(), 0)
+            for p in self.init_pass[1:]:  # the other G-buffer sets draw the same triangles: one tree
+                p.share_vertices(self.init_pass[0])
         return nodes, ms
 
     def close(self) -> None:
