@@ -58,6 +58,10 @@ struct Texture {
   uint64_t version = 1;
   float* aux = nullptr;  // compact depth-fwidth side plane
   bool aux_valid = false;
+  unsigned char* tflags = nullptr;  // a-trous per-tile surface flags derived from aux (atrous_tile_flags)
+  size_t tflags_cap = 0;
+  uint64_t tflags_ver = 0;          // texture version / rows they were derived for
+  int tflags_y0 = 0, tflags_y1 = -1;
   bool lbvh = false;     // written by pt_bvh_build (the device copy is authoritative: get_scene decodes it there)
 };
 
@@ -1197,6 +1201,25 @@ int draw_raster(Pass* p) {
   Texture* fwt = tex_of(p->att[3]);
   if (!fwt->aux) HIPCHK(hipMalloc((void**)&fwt->aux, (size_t)fwt->W * fwt->rows * 4));
   k.fwidth_aux = fwt->aux;
+  // the a-trous per-tile surface flags of this G-buffer, marked by the G-buffer kernels as they write the pixels
+  if (ui(p, "atrous_tile_flags", 1) && k.y1 > k.y0) {
+    const size_t nb = ptk::atrous_flag_bytes(k.W, k.y0, k.y1);
+    if (fwt->tflags_cap < nb) {
+      if (fwt->tflags) (void)hipFree(fwt->tflags);
+      fwt->tflags = nullptr;
+      fwt->tflags_cap = 0;
+      HIPCHK(hipMalloc((void**)&fwt->tflags, nb));
+      fwt->tflags_cap = nb;
+    }
+    HIPCHK(hipMemsetAsync(fwt->tflags, 0, nb, g.stream));
+    k.tflags = fwt->tflags;
+    for (int si = 0; si < 5; ++si) k.tf_off[si] = (int)ptk::atrous_flag_offset(si, k.W, k.y0, k.y1);
+    fwt->tflags_ver = fwt->version;
+    fwt->tflags_y0 = k.y0;
+    fwt->tflags_y1 = k.y1;
+  } else {
+    fwt->tflags_ver = 0;
+  }
   k.geom = rs.geom;
   k.nrm = rs.nrm;
   k.bvh = rs.bvh;
@@ -1288,6 +1311,29 @@ int draw_svgf(Pass* p, int kind) {
     k.phi_color = uf(p, "gPhiColor", 0.0f);
     k.phi_normal = uf(p, "gPhiNormal", 0.0f);
     k.xcd_run = ui(p, "atrous_xcd_run", 0);
+    // production tiled kernel: per-tile surface flags, derived once per G-buffer from its depth-fwidth plane
+    const int si = k.step == 1 ? 0 : k.step == 2 ? 1 : k.step == 4 ? 2 : k.step == 8 ? 3 : k.step == 16 ? 4 : -1;
+    if (!ui(p, "exact", 0) && ui(p, "atrous_variant", 0) == 0 && ui(p, "atrous_tile_flags", 1) && k.fwidth.aux &&
+        si >= 0 && y1 > y0) {
+      Texture* ft = sampler(p, "gNormalDepthFwidth");
+      const size_t nb = ptk::atrous_flag_bytes(k.W, y0, y1);
+      if (ft->tflags_cap < nb) {
+        if (ft->tflags) (void)hipFree(ft->tflags);
+        ft->tflags = nullptr;
+        ft->tflags_cap = 0;
+        HIPCHK(hipMalloc((void**)&ft->tflags, nb));
+        ft->tflags_cap = nb;
+        ft->tflags_ver = 0;
+      }
+      if (ft->tflags_ver != ft->version || ft->tflags_y0 != y0 || ft->tflags_y1 != y1) {
+        const int frc = ptk::atrous_tile_flags(k.fwidth, k.W, y0, y1, ft->tflags, g.stream);
+        if (frc) return hip_err((hipError_t)frc, "a-trous tile flags");
+        ft->tflags_ver = ft->version;
+        ft->tflags_y0 = y0;
+        ft->tflags_y1 = y1;
+      }
+      k.tile_any = ft->tflags + ptk::atrous_flag_offset(si, k.W, y0, y1);
+    }
     if (ui(p, "exact", 0)) rc = launch_atrous_exact(k, g.stream);          // bit-exact form (tests)
     else if (ui(p, "atrous_variant", 0) == 1) rc = launch_atrous_simple(k, g.stream);  // A/B: generic
     else if (ui(p, "atrous_variant", 0) == 2) rc = launch_atrous_step(k, g.stream);    // A/B: step kernel
@@ -1398,6 +1444,7 @@ int pt_shutdown(void) {
     Texture* t = kv.second.get();
     if (t->owned && t->dev) (void)hipFree(t->dev);
     if (t->aux) (void)hipFree(t->aux);
+    if (t->tflags) (void)hipFree(t->tflags);
   }
   for (auto& kv : g.passes) {
     Pass* p = kv.second.get();
@@ -1709,6 +1756,7 @@ int pt_texture_destroy(uint32_t tex) {
   (void)hipStreamSynchronize(g.stream);
   if (it->second->owned && it->second->dev) (void)hipFree(it->second->dev);
   if (it->second->aux) (void)hipFree(it->second->aux);
+  if (it->second->tflags) (void)hipFree(it->second->tflags);
   g.textures.erase(it);
   // the device scenes decoded from this buffer (keyed by (triangles, nodes) handles) go with it
   for (auto sc = g.scenes.begin(); sc != g.scenes.end();) {

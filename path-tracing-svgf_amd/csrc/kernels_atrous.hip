@@ -236,7 +236,7 @@ __global__ void __launch_bounds__(256) atrous_step_kernel(AtrousParams p) {
 // NX: 64-column strips per tile (waves side by side). The halo costs 4S staged columns per tile, so the widest
 // step stages twice its output with NX = 1; S = 16 uses NX = 2 (128 columns, 1024 threads, 74 KB of LDS: measured
 // 100 -> 91.5 us on the 4K bench inputs, tools/exp_atrous_real.hip), the other steps are fastest with NX = 1.
-constexpr int kTileRows = 8;   // TJ
+constexpr int kTileRows = kAtrousTJ;   // TJ
 constexpr int kTileWaves = 8;  // per 64-column strip; one pixel per thread
 template <int S> constexpr int tile_nx() { return S >= 16 ? 2 : 1; }
 
@@ -278,7 +278,12 @@ __global__ void __launch_bounds__(64 * kTileWaves * tile_nx<S>()) atrous_tile_ke
   const size_t ci = (size_t)(y - row0) * W + x;
   bool bg = true;
   float fwz = 0.0f;
-  if (own) {
+  // Per-tile flags precomputed from the depth-fwidth plane once per G-buffer (atrous_tile_flags): a background tile
+  // copies without reading its pixels' flags or meeting at a barrier; the others read them for their taps.
+  const bool pre = AUX && p.tile_any != nullptr;
+  bool tile_any = true;
+  if (pre) tile_any = p.tile_any[(g * S + b) * gridDim.x + bx] != 0;
+  if (own && tile_any) {
     if (AUX) {
       const float a = p.fwidth.aux[ci];
       bg = aux_flag(a);
@@ -288,22 +293,17 @@ __global__ void __launch_bounds__(64 * kTileWaves * tile_nx<S>()) atrous_tile_ke
       fwz = p.fwidth.p[ci].y;
     }
   }
+  if (!pre) {
 // any surface pixel in the tile? One ballot per wave and ONE barrier (the flags have their own LDS words) instead
 // of __syncthreads_or's three (76.1 vs 79.8 us default view, 152.4 vs 158.5 surface view, tools/bench_atrous.py).
-#ifndef PT_ATROUS_BALLOT
-#define PT_ATROUS_BALLOT 1
-#endif
-#if PT_ATROUS_BALLOT
-  __shared__ int any_surface[NW];
-  const bool wave_any = __ballot(!bg) != 0ull;
-  if (lane == 0) any_surface[wv] = wave_any;
-  __syncthreads();
-  bool tile_any = false;
+    __shared__ int any_surface[NW];
+    const bool wave_any = __ballot(!bg) != 0ull;
+    if (lane == 0) any_surface[wv] = wave_any;
+    __syncthreads();
+    tile_any = false;
 #pragma unroll
-  for (int w = 0; w < NW; ++w) tile_any |= any_surface[w] != 0;
-#else
-  const bool tile_any = __syncthreads_or(!bg);
-#endif
+    for (int w = 0; w < NW; ++w) tile_any |= any_surface[w] != 0;
+  }
   if (!tile_any) {
     if (own) p.out.p[ci] = I[ci];
     return;
@@ -588,6 +588,39 @@ int launch_atrous_slide(const AtrousParams& p, int chunks, int nx, int xcd, hipS
     case 16: launch_slide_s<16>(p, aux, chunks, nx, xcd, s); break;
     default: return launch_atrous_step(p, s);
   }
+  return (int)hipGetLastError();
+}
+
+// Tile flags of the five step sizes (atrous_tile_kernel's tiles: S = 1 << si, NX = tile_nx<S>(), TJ rows of one
+// residue class): byte (g * S + b) * NXT + bx of step si is 1 iff an owned pixel of that tile is a surface pixel
+// (the depth-fwidth plane's sign bit clear). One wave per 64 columns of a row; a ballot, then one byte store per step.
+static int tiles_of(int S, int W, int y0, int y1) {
+  const int nx = S >= 16 ? 2 : 1, nxt = (W + 64 * nx - 1) / (64 * nx);
+  const int groups = (y1 - y0 + S * kTileRows - 1) / (S * kTileRows);
+  return nxt * groups * S;
+}
+size_t atrous_flag_offset(int si, int W, int y0, int y1) {
+  size_t o = 0;
+  for (int t = 0; t < si; ++t) o += (size_t)tiles_of(1 << t, W, y0, y1);
+  return o;
+}
+__global__ void __launch_bounds__(64) atrous_flags_kernel(const float* __restrict__ aux, int row0, int W, int y0,
+                                                         unsigned char* __restrict__ flags, int o1, int o2, int o3,
+                                                         int o4) {
+  const int x0 = blockIdx.x * 64, x = x0 + (int)threadIdx.x, y = y0 + (int)blockIdx.y;
+  const bool surf = x < W && !aux_flag(aux[(size_t)(y - row0) * W + x]);
+  if (__ballot(surf) == 0ull || threadIdx.x != 0) return;
+  const int off[5] = {0, o1, o2, o3, o4};
+  atrous_mark_tiles(flags, off, W, x0, y - y0);
+}
+size_t atrous_flag_bytes(int W, int y0, int y1) { return atrous_flag_offset(5, W, y0, y1); }
+int atrous_tile_flags(const Plane& fw, int W, int y0, int y1, unsigned char* flags, hipStream_t s) {
+  if (y1 <= y0 || !fw.aux) return 0;
+  hipError_t e = hipMemsetAsync(flags, 0, atrous_flag_bytes(W, y0, y1), s);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(atrous_flags_kernel, dim3((W + 63) / 64, y1 - y0), dim3(64), 0, s, fw.aux, fw.row0, W, y0, flags,
+                     (int)atrous_flag_offset(1, W, y0, y1), (int)atrous_flag_offset(2, W, y0, y1),
+                     (int)atrous_flag_offset(3, W, y0, y1), (int)atrous_flag_offset(4, W, y0, y1));
   return (int)hipGetLastError();
 }
 

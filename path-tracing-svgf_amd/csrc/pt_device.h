@@ -206,6 +206,8 @@ struct GBufParams {
   int W, H, y0, y1;
   Plane world, normal_depth, motion, fwidth;
   float* fwidth_aux;    // compact depth-fwidth plane (rows of fwidth), may be null
+  unsigned char* tflags;  // a-trous per-tile surface flags (atrous_mark_tiles) for rows from y0, may be null
+  int tf_off[5];          // their per-step offsets (atrous_flag_offset)
   const float4* geom;   // 4 x float4 per raster triangle (walk): (p1,idx)(e1,-)(e2,-)(Ng,-)
   const float4* nrm;    // 3 x float4 per raster triangle (closest hit only): n1, n2, n3
   const float4* bvh;
@@ -241,7 +243,24 @@ struct AtrousParams {
   int step;
   float phi_color, phi_normal;
   int xcd_run;  // tiled kernel: > 0 runs of this many consecutive tiles per XCD (L2 halo reuse), 0 = dispatch order
+  const unsigned char* tile_any;  // tiled kernel: per-tile "holds a surface pixel" flags of this step, or null
 };
+// Tiles of the tiled a-trous (kernels_atrous.hip): 64 * NX columns (NX = 2 for S >= 16) x kAtrousTJ rows of one
+// residue class mod S; tile (g, b, bx) of step S has byte (g * S + b) * NXT + bx in that step's flags.
+constexpr int kAtrousTJ = 8;
+__device__ __forceinline__ void atrous_mark_tiles(unsigned char* flags, const int* off, int W, int x, int r) {
+#pragma unroll
+  for (int si = 0; si < 5; ++si) {
+    const int S = 1 << si, nx = S >= 16 ? 2 : 1, nxt = (W + 64 * nx - 1) / (64 * nx);
+    const int g = r / (S * kAtrousTJ), b = r % S;
+    flags[off[si] + (size_t)(g * S + b) * nxt + x / (64 * nx)] = 1;
+  }
+}
+// per-tile surface flags of the tiled a-trous for the 5 steps (1, 2, 4, 8, 16) of rows [y0, y1), from the
+// depth-fwidth plane's sign bits: atrous_flag_bytes() bytes, step si's flags at atrous_flag_offset(si)
+size_t atrous_flag_bytes(int W, int y0, int y1);
+size_t atrous_flag_offset(int si, int W, int y0, int y1);
+int atrous_tile_flags(const Plane& fwidth, int W, int y0, int y1, unsigned char* flags, hipStream_t s);
 
 struct ModulateParams {
   int W, H, y0, y1;

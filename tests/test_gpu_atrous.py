@@ -118,7 +118,7 @@ def test_tile_kernel_equals_step_kernel(gpu, step, size):
     included."""
     illum, nd, fw = _planes(seed=5, W=size[0], H=size[1])
     b = _run(gpu, illum, nd, fw, step, 2)
-    cases = [(0, {}), (3, {})] + [(0, dict(atrous_xcd_run=r)) for r in (1, 3, 60)] + [(4, dict(atrous_chunks=c, atrous_nx=nx, atrous_xcd=xcd))
+    cases = [(0, {}), (0, dict(atrous_tile_flags=0)), (3, {})] + [(0, dict(atrous_xcd_run=r)) for r in (1, 3, 60)] + [(4, dict(atrous_chunks=c, atrous_nx=nx, atrous_xcd=xcd))
                                   for c in (1, 2, 3, 6) for nx in (1, 2) for xcd in (0, 1)]
     for v, kw in cases:
         a = _run(gpu, illum, nd, fw, step, v, **kw)

@@ -30,8 +30,8 @@ VARIANTS = sys.argv[1:] or ["0", "3"]
 def select(ap, spec):
     """Set atrous_variant and the spec's extra uniforms (reset to 0 first so variants do not leak into each other)."""
     v, *kv = spec.split(":")
-    for name in ("atrous_chunks", "atrous_nx", "atrous_xcd", "atrous_xcd_run"):
-        ap.set_uniform_int(name, 6 if name == "atrous_chunks" else 0)
+    for name in ("atrous_chunks", "atrous_nx", "atrous_xcd", "atrous_xcd_run", "atrous_tile_flags"):
+        ap.set_uniform_int(name, {"atrous_chunks": 6, "atrous_tile_flags": 1}.get(name, 0))
     ap.set_uniform_int("atrous_variant", int(v))
     for item in kv:
         name, val = item.split("=")
