@@ -172,3 +172,46 @@ def test_device_raster_bind_equals_host_bind(gpu, scene_small, gbuffer_mode):
     for k in planes:
         assert np.array_equal(out[0][k].view(np.uint32), out[1][k].view(np.uint32)), k
     assert 0.05 < float(np.mean(out[0]["normal_depth"][..., 3] != 1.0)) < 0.95
+
+
+def test_raster_pass_share_rules(gpu, scene_small):
+    """pt_raster_pass_share: both passes must be rasterize passes, the source bound on its own; a sharing pass draws
+    the source's triangles (same G-buffer bits), and fails loudly once the source is destroyed."""
+    from ptsvgf._lib import PtError
+    from ptsvgf.gl import Rasterize_RenderPass, RenderPass, getShaderProgram, getTextureRGB32F
+
+    W, H = 64, 48
+    prog = getShaderProgram("shaders/rasterize_frag.frag", "shaders/rasterize_vert.vert")
+    passes, outs = [], []
+    for _ in range(2):
+        p = Rasterize_RenderPass(prog, W, H)
+        tex = [getTextureRGB32F(W, H) for _ in range(4)]
+        p.colorAttachments += tex
+        passes.append(p)
+        outs.append(tex)
+    a, b = passes
+    a.bindData(scene_small.raster)
+    b.bindData(np.zeros(18, np.float32))  # one degenerate triangle: replaced by the share below
+    other = RenderPass(getShaderProgram("shaders/svgf_modulate.frag", "shaders/vert.vert"), W, H)
+    other.colorAttachments.append(getTextureRGB32F(W, H))
+    other.bindData(False)
+    with pytest.raises(PtError):
+        b.share_vertices(other)
+    b.share_vertices(a)
+    with pytest.raises(PtError):
+        a.share_vertices(b)  # b is not bound on its own
+    from ptsvgf.camera import Camera, mat_mul
+    cam = Camera(W, H)
+    cam.update()
+    for p in (a, b):
+        p.set_uniform_mat4("view", cam.cam_view_mat)
+        p.set_uniform_mat4("projection", cam.cam_proj_mat)
+        p.set_uniform_mat4("pre_viewproj", mat_mul(cam.cam_proj_mat, cam.cam_view_mat))
+        p.draw()
+    for ta, tb in zip(outs[0], outs[1]):
+        assert np.array_equal(gpu.readback(ta).view(np.uint32), gpu.readback(tb).view(np.uint32))
+    a.destroy()
+    with pytest.raises(PtError):
+        b.draw()
+    b.destroy()
+    other.destroy()
