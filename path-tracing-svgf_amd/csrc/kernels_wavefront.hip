@@ -573,8 +573,11 @@ constexpr int kRefillBlocks = 256 * 10;
 // Measured at 4K (tools/lib_ab.sh, R = 4, kRefillMin = 16): refill 0 / 50 / 75 / 85 % -> 147.7 / 156.0 / 159.3 /
 // 158.7 fps with 4 frames in flight, 117.1 / 116.0 / 110.0 / 108.1 fps serial: the refill waves raise the share of
 // busy lanes (shadow 0.42 -> 0.65) but lengthen the launch's tail, which other frames in flight fill.
+// The cap on R (end of round 2, same box, K = 4, tools/lib_ab.sh + lib_ab_views.sh): 4 / 8 / 12 / 16 -> 179.6 / 182.6 /
+// 183.1 / 182.6 fps at 4K, surface view 53.1 -> 57.2 fps with 12, 1080p unchanged (its lists give R < 4 anyway);
+// kRefillMin 8 / 16 / 32: 180.1 / 179.6 / 178.0.
 #ifndef PT_REFILL_ROUNDS
-#define PT_REFILL_ROUNDS 4
+#define PT_REFILL_ROUNDS 12
 #endif
 #ifndef PT_REFILL_MIN
 #define PT_REFILL_MIN 16

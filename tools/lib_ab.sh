@@ -9,7 +9,7 @@ mkdir -p "$R/gpurun_out/lib_ab"
 ARGS=""
 for kv in $(echo "$U" | tr ',' ' '); do ARGS="$ARGS --pt-uniform $kv"; done
 for L in "$@"; do
-  for K in 4 1; do
+  for K in ${KLIST:-4 1}; do
     N=$(echo "$L" | tr '/' '_')_k$K
     PTSVGF_LIB_DIR="$R/path-tracing-svgf_amd/$L" timeout -k 10 200 python3 "$R/bench.py" --no-cpu-baseline --no-1080p \
       --no-extras --frames-in-flight $K $ARGS > "$R/gpurun_out/lib_ab/$N.json" 2> "$R/gpurun_out/lib_ab/$N.err" || exit $?
