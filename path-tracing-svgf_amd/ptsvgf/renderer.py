@@ -281,7 +281,10 @@ class Renderer:
             p.set_uniform_int("aspect_corrected", int(self.aspect_corrected))
             p.set_uniform_int("prune", int(self._pt_prune))
             # lane-refill traversal waves: +8 % frames/s with frames in flight, -6 % serial (kernels_wavefront.hip)
-            p.set_uniform_int("trace_refill", 75 if self.K > 1 else 0)
+            # share of each bounce / shadow list traced by lane-refill waves (frames in flight only); with up to 12
+            # chunk rounds per wave 75 / 85 / 90 / 95 % measured 183.1 / 184.3 / 183.7 / 183.9 fps at 4K and 57.2 / 58.7 /
+            # 59.5 / 60.6 fps on the surface view, 1080p and 8 bands within noise (tools/refill_pct_sweep.sh)
+            p.set_uniform_int("trace_refill", 90 if self.K > 1 else 0)
             p.set_uniform_int("trace_batch", self.B)
             self.pt_slots.append((p, outs))
         self.pass_path_tracing = PassGroup([p for p, _ in self.pt_slots])  # settings apply to every slot
