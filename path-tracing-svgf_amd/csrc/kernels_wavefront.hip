@@ -589,8 +589,12 @@ constexpr int kRefillRounds = PT_REFILL_ROUNDS, kRefillMin = PT_REFILL_MIN;
 // Chunk rounds per big wave, from the list length: a big wave lasts about R one-ray waves, which pays only when the
 // launch spans several rounds of resident waves anyway (at 1080p the lists are too short: refill there measured
 // 367 -> 312 fps with R = 4 everywhere; with R from the length 380 fps at 1080p, 156.6 at 4K). kResidentWaves: 256 CUs
-// x 20 waves (86 VGPRs: 5 waves per SIMD).
-constexpr int kResidentWaves = 256 * 20;
+// x 20 waves (86 VGPRs: 5 waves per SIMD). Estimates of 16 / 12 / 8 waves per CU (more rounds per wave) measured
+// 182.8 / 181.2 / 177.5 fps against 183.7 at 4K, the surface view unchanged (end of round 2).
+#ifndef PT_RESIDENT_WAVES
+#define PT_RESIDENT_WAVES (256 * 20)
+#endif
+constexpr int kResidentWaves = PT_RESIDENT_WAVES;
 #ifndef PT_REFILL_DIV
 #define PT_REFILL_DIV 1
 #endif
