@@ -14,7 +14,7 @@ the line also carries the serial rate (one frame at a time: camera-to-display
 latency of one frame), 1080p (configs[1]), the path tracer's rays/s and BVH
 visits/s, a surface-dominated view, the a-trous roofline three ways (SURVEY.md's
 52 B/px convention, PMC traffic, background-weighted bytes), the CPU oracle on
-16 threads and on 1 core, configs[0] (Cornell box + teapot 512x512, SVGF off,
+every usable core and on 1 core, configs[0] (Cornell box + teapot 512x512, SVGF off,
 CPU reference traversal), and the dynamic-scene path (GPU LBVH rebuild time, frame
 rate over the LBVH).
 
@@ -43,22 +43,27 @@ ATROUS_BYTES_BG_PX = 36      # a background pixel: depth-fwidth/flag 4 + illum 1
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8 TB/s spec
 METRIC = "frames/sec @1spp+SVGF, 1080p & 4K; à-trous HBM GB/s vs peak"  # BASELINE.json "metric"
 ATROUS_KERNEL = "atrous_tile_kernel"
-# HBM bytes per a-trous launch measured with rocprofv3 PMC passes (tools/gpu_profile.sh), committed under profiles/
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "atrous_traffic.json")
+EXCHANGE_STAGES = ("reproject", "variance", "atrous0", "atrous1", "atrous2", "atrous3", "atrous4", "taa")
+# planes compared bitwise between the gathered bands and the one-GPU frame (--gpus N > 1)
+PARITY_PLANES = ("color", "albedo", "reproj_illum", "variance", "history_illum", "atrous", "modulate")
+# HBM bytes per a-trous launch measured with rocprofv3 PMC passes (tools/gpu_profile.sh), committed under profiles/,
+# one file per camera view (the surface view's bytes are its own, not the default view's)
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "atrous_traffic_{view}.json")
 # configs[2] on a surface-dominated camera (94 % geometry pixels: the plant, a corner of the clock; ~24 % on the
 # default view): orbit radius, elevation, azimuth and look-at point (Utils/camera.h:14-38 parameters)
 VIEWS = {"default": None, "surface": dict(r_dis=0.8, upAngle=70.0, rotatAngle=180.0, move_vec=(0.4, -0.25, 0.0))}
 
 
-def atrous_traffic(W, rows):
+def atrous_traffic(W, rows, view="default"):
     """PMC-measured HBM bytes per a-trous launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, in KB units as the
-    guide prescribes) from the committed profile, when it was taken for this kernel at this frame size."""
+    guide prescribes) from the committed profile, when it was taken for this kernel at this frame size on this
+    camera view; None otherwise."""
     try:
-        with open(TRAFFIC_FILE) as f:
+        with open(TRAFFIC_FILE.format(view=view)) as f:
             t = json.load(f)
     except (OSError, ValueError):
         return None
-    if t.get("kernel") != ATROUS_KERNEL or t.get("pixels") != W * rows:
+    if t.get("kernel") != ATROUS_KERNEL or t.get("pixels") != W * rows or t.get("view") != view:
         return None
     return t.get("bytes_per_launch")
 
@@ -74,11 +79,13 @@ def parse():
     ap.add_argument("--view", default="default", choices=sorted(VIEWS), help="camera of the headline run")
     ap.add_argument("--moving", action="store_true", help="orbit the camera 1 deg/frame (configs[4])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", default="960x540", help="oracle sample frame size for cpu_baseline (16 threads)")
+    ap.add_argument("--cpu-sample", default="960x540", help="oracle sample frame size for cpu_baseline (all cores)")
     ap.add_argument("--cpu-sample-1core", default="480x270", help="oracle sample frame size on 1 core")
     ap.add_argument("--no-1080p", action="store_true", help="skip the secondary 1080p measurement")
     ap.add_argument("--no-extras", action="store_true", help="skip the serial, surface-view and configs[0] runs")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for --gpus > 1 (nccl = RCCL)")
+    ap.add_argument("--no-band-parity", action="store_true",
+                    help="multi-GPU: skip the untimed bitwise check of the gathered bands against a one-GPU frame")
     ap.add_argument("--equal-bands", action="store_true", help="multi-GPU: equal band heights (no cost balancing)")
     ap.add_argument("--breakdown", action="store_true", help="print per-pass ms to stderr")
     ap.add_argument("--pt-kernel", type=int, default=0, help="0 wavefront (production), 1 megakernel (A/B)")
@@ -126,10 +133,41 @@ def oracle_fps(scene, W, H, threads, seconds, svgf=True):
     return n / (time.perf_counter() - t0), n
 
 
+def host_cpus() -> dict:
+    """The host's CPUs as this process sees them: nproc (affinity), the machine's count, the cgroup CPU quota and
+    lscpu's model line; `usable` = every core this process may run on at once (affinity, capped by the quota)."""
+    import subprocess
+
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            quota = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        model = next((ln.split(":", 1)[1].strip() for ln in out.splitlines() if ln.startswith("Model name")), None)
+    except (OSError, subprocess.SubprocessError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    # the GPU pool gives a one-GPU box a CPU share and exports it as OMP_NUM_THREADS (16): worker pools stay
+    # within it, so the baseline's "all cores" are the cores of that share
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        usable = min(usable, int(share))
+    return {"nproc": aff, "machine_cpus": os.cpu_count(), "cgroup_cpu_quota": quota, "omp_num_threads": share,
+            "lscpu_model": model, "usable": usable}
+
+
 def cpu_baseline(scene, W, H, sample: str, sample1: str):
-    """The CPU oracle on a bounded sample frame (16 threads, and 1 core), scaled to W x H by pixel count."""
+    """The CPU oracle on a bounded sample frame (every usable host core, and 1 core), scaled to W x H by pixel
+    count (all host cores, nproc / lscpu recorded)."""
     out = {}
-    for key, smp, threads in (("all", sample, min(16, os.cpu_count() or 1)), ("one", sample1, 1)):
+    hc = host_cpus()
+    for key, smp, threads in (("all", sample, hc["usable"]), ("one", sample1, 1)):
         sw, sh = (int(v) for v in smp.split("x"))
         fps, n = oracle_fps(scene, sw, sh, threads, 10.0)
         scale = (W * H) / (sw * sh)
@@ -138,12 +176,13 @@ def cpu_baseline(scene, W, H, sample: str, sample1: str):
                               f"{1e3 / fps:.1f} ms/frame, scaled by pixel count to {W}x{H}"}
     line = dict(out["all"])
     line["single_core"] = out["one"]
+    line["host"] = hc
     return line
 
 
 def config0(gl):
     """configs[0]: Cornell box + teapot stand-in, 512x512, 1 spp, SVGF off — the CPU reference traversal (oracle
-    path tracer, 16 threads and 1 core), with the GPU path tracer's rate on the same frame beside it."""
+    path tracer, all usable cores and 1 core), with the GPU path tracer's rate on the same frame beside it."""
     import torch
 
     from ptsvgf.camera import parameter_config
@@ -155,7 +194,7 @@ def config0(gl):
     check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
     scene = build_scene("cornell_teapot")
     res = {"workload": "cornell_teapot 512x512 1spp depth2, SVGF off", "triangles": scene.ntris}
-    for key, threads in (("cpu_fps_16t", min(16, os.cpu_count() or 1)), ("cpu_fps_1t", 1)):
+    for key, threads in (("cpu_fps_all_cores", host_cpus()["usable"]), ("cpu_fps_1t", 1)):
         fps, n = oracle_fps(scene, 512, 512, threads, 4.0, svgf=False)
         res[key] = round(fps, 3)
     r = Renderer(scene, 512, 512, parameter_config(), mode="fast", run_taa=False, run_output=False)
@@ -288,7 +327,7 @@ def main():
         dist.all_reduce(t)
         return t.tolist()
 
-    def run(W, H, K, view="default", probes=True):
+    def run(W, H, K, view="default", probes=True, parity=False):
         """Warm up, time exactly args.steps frames (barrier + sync on both sides, max over ranks); then, untimed:
         one frame with the traversal counters on, one profiled frame (per-pass HIP events), the a-trous launches
         replayed between HIP events, and the surface fraction of the frame."""
@@ -312,9 +351,12 @@ def main():
                 setattr(cam, k, np.array(v, np.float32) if isinstance(v, tuple) else np.float32(v))
             cam.dirty = True
 
+        moves = []  # per frame the band renderer drew: the orbit applied before it (band_parity replays them)
+
         def step():
             if args.moving:
                 r.camera.orbit(1.0, 0.0)
+            moves.append((1.0, 0.0) if args.moving else None)
             r.frame()
 
         for _ in range(max(args.warmup, K + 1)):
@@ -322,6 +364,8 @@ def main():
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
+        if world > 1:
+            r.time_exchanges(True)  # HIP events around each halo stage on the back-end stream
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
@@ -337,17 +381,32 @@ def main():
             dt = float(t.item())
         out = {"dt": dt, "rows": r.rows_rendered() if hasattr(r, "rows_rendered") else H}
         if world > 1:  # the band plan the calibration chose: (slowest band ms, bounds) per measured plan
+            ex = r.exchange_ms()
+            r.time_exchanges(False)
+            # per-stage exchange ms per frame, MAX over ranks (the slowest rank's wait sets the frame)
+            mx = torch.tensor([ex.get(k, 0.0) for k in EXCHANGE_STAGES], dtype=torch.float64, device="cuda")
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
             out["bands"] = {"bounds": list(r.plan.bounds), "back_lag": r.r.lag,
+                            "exchange_ms_per_frame": {k: round(v, 4) for k, v in zip(EXCHANGE_STAGES, mx.tolist())
+                                                      if k in ex or v > 0},
+                            "exchange_ms_rank0": ex,
                             "calibration": [[round(m, 3), list(b)] for m, b in getattr(r, "calibration", [])]}
         log(f"  {args.steps} frames in {dt:.3f} s = {args.steps / dt:.2f} frames/s")
         if probes:
             st = r.trace_stats()
+            moves.append(None)  # trace_stats drew one frame (no camera move)
             out["stats"] = dict(zip(st, allsum([float(v) for v in st.values()])))
             r.profile(True)
             step()
             torch.cuda.synchronize()
             out["per_pass"] = r.pass_times()
             r.profile(False)
+            if world > 1 and parity:
+                # the bands' rows before the a-trous replay below: a band's replay reads ghost rows the frame's later
+                # exchanges refilled, so it times the kernels but leaves band planes that are not the frame's
+                p = r.plan
+                pl = r.planes()
+                owned = {k: gl.readback(pl[k])[p.y0 - p.row0:p.y1 - p.row0] for k in PARITY_PLANES}
             # the roofline kernel alone: the last frame's 5 a-trous launches replayed back to back between two
             # HIP events on the library's stream (per-draw events above include launch gaps)
             out["per_pass"]["atrous_avg_ms"] = r.time_atrous(20)
@@ -359,10 +418,57 @@ def main():
             out["background_fraction"] = bg / px
             if hasattr(r, "motion_log") and r.motion_log:
                 out["max_history_rows"] = int(max(n for _, n in r.motion_log))
+        if world > 1 and parity and probes:
+            r.close()
+            out["band_parity"] = band_parity(owned, r.plan, W, H, view, moves)
+            return out
         r.close() if hasattr(r, "close") else None
         return out
 
-    def atrous_roofline(res, W, rows):
+    def band_parity(owned, p, W, H, view, moves):
+        """The bands' owned rows, gathered on rank 0 (P2P: RCCL over xGMI, or gloo), against a one-GPU Renderer
+        drawing the same camera path from frame 0: bitwise, per plane (svgf_Atrous.frag:92-97 and
+        svgf_reproject.frag:45-156 are what the halo rows carry). Untimed."""
+        from ptsvgf.dist import gather_bands
+        from ptsvgf.renderer import Renderer
+
+        torch.cuda.synchronize()
+        full = gather_bands(owned, p, dist)
+        res = None
+        if rank == 0:
+            log(f"band parity: one-GPU reference, {len(moves)} frames")
+            gl.set_band(W, H, 0, H, 0, H)  # the library's band state is process-global: back to the whole frame
+            check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
+            ref = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, run_taa=False, run_output=False)
+            ref.pass_path_tracing.set_uniform_int("pt_kernel", args.pt_kernel)
+            for kv in args.pt_uniform:
+                name, val = kv.split("=")
+                ref.pass_path_tracing.set_uniform_int(name, int(val))
+            if VIEWS[view]:
+                for k, v in VIEWS[view].items():
+                    setattr(ref.camera, k, np.array(v, np.float32) if isinstance(v, tuple) else np.float32(v))
+                ref.camera.dirty = True
+            for mv in moves:
+                if mv:
+                    ref.camera.orbit(*mv)
+                ref.frame()
+            want = {k: gl.readback(ref.planes()[k]) for k in PARITY_PLANES}
+            ref.close()
+            planes = {}
+            for k in PARITY_PLANES:
+                a, b = full[k].view(np.uint32), want[k].view(np.uint32)
+                diff = np.abs(full[k].astype(np.float64) - want[k].astype(np.float64))
+                planes[k] = {"bit_exact": bool(np.array_equal(a, b)),
+                             "differing_px": int(np.count_nonzero(np.any(a != b, axis=-1))),
+                             "max_abs": float(np.nanmax(diff)) if diff.size else 0.0}
+            res = {"bit_exact": all(v["bit_exact"] for v in planes.values()),
+                   "max_abs": max(v["max_abs"] for v in planes.values()), "frames": len(moves),
+                   "backend": dist.get_backend(), "planes": planes}
+            log(f"band parity: bit_exact={res['bit_exact']} max_abs={res['max_abs']}")
+        dist.barrier()
+        return res
+
+    def atrous_roofline(res, W, rows, view="default"):
         atrous_ms = res["per_pass"].get("atrous_avg_ms")
         if not atrous_ms:
             return None
@@ -371,7 +477,7 @@ def main():
         achieved = alg / t / 1e9
         bgf = res["background_fraction"]
         weighted = W * rows * (bgf * ATROUS_BYTES_BG_PX + (1.0 - bgf) * ATROUS_BYTES_PER_PX)
-        traffic = atrous_traffic(W, rows)
+        traffic = atrous_traffic(W, rows, view)
         return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": ATROUS_KERNEL, "avg_launch_ms": round(atrous_ms, 4), "algorithmic_bytes_per_launch": alg,
@@ -401,7 +507,7 @@ def main():
 
     W, H = args.width, args.height
     K = args.frames_in_flight
-    res = run(W, H, K, args.view)
+    res = run(W, H, K, args.view, parity=world > 1 and not args.no_band_parity)
     ms = res["dt"] / args.steps * 1e3
     fps = args.steps / res["dt"]  # whole frames per second (all ranks together render one frame)
     extra = {}
@@ -424,7 +530,7 @@ def main():
         extra["surface_view"] = {"camera": VIEWS["surface"], "fps": round(sfps, 3),
                                  "ms_per_step": round(sv["dt"] / args.steps * 1e3, 3),
                                  "surface_fraction": round(1.0 - sv["background_fraction"], 4),
-                                 "roofline": atrous_roofline(sv, W, sv["rows"]),
+                                 "roofline": atrous_roofline(sv, W, sv["rows"], "surface"),
                                  "path_tracer": pt_rates(sv, sfps),
                                  "passes_ms": {k: round(v, 4) for k, v in sv["per_pass"].items()}}
 
@@ -436,7 +542,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            log("cpu baseline (oracle, 16 threads and 1 core)")
+            log("cpu baseline (oracle, all usable cores and 1 core)")
             cpu = cpu_baseline(scene, W, H, args.cpu_sample, args.cpu_sample_1core)
         except Exception as e:  # the baseline is reported, never the target
             cpu = {"value": None, "error": str(e)}
@@ -459,13 +565,15 @@ def main():
                            "atrous_iterations": cfg.num_atrous_iterations, "triangles": scene.ntris,
                            "parallelism": f"bands{world}", "frames_in_flight": K,
                            "trace_batch": min(args.trace_batch, K)},
-                "roofline": atrous_roofline(res, W, res["rows"]), "cpu_baseline": cpu,
+                "roofline": atrous_roofline(res, W, res["rows"], args.view), "cpu_baseline": cpu,
                 "path_tracer": pt_rates(res, fps), **extra,
                 "passes_ms": {k: round(v, 4) for k, v in res["per_pass"].items()}}
         if "max_history_rows" in res:
             line["max_history_rows"] = res["max_history_rows"]
         if "bands" in res:
             line["bands"] = res["bands"]
+        if res.get("band_parity") is not None:
+            line["band_parity"] = res["band_parity"]
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(line) + "\n").encode())
     gl.shutdown()

@@ -101,10 +101,10 @@ struct WFBuffers {
   size_t spill_cols = 0;
 };
 
-// Spill columns for a reference tree needing `need` stack entries (> the LDS stack): (need - kStack + 1) entries per
+// Spill columns for a tree needing `need` stack entries (> the LDS stack): (need - kSpillKS + 1) entries per
 // pixel of the band, allocated on first use and kept while the depth fits.
 int wf_spill(WFBuffers& b, int need) {
-  const int levels = need - kStack + 1;
+  const int levels = need - kSpillKS + 1;
   const size_t m = b.n * (size_t)b.nb;  // columns of the batch's pixels (global pids)
   if (levels <= 0) {
     for (int f = 0; f < b.nb; ++f) {
@@ -446,6 +446,8 @@ struct SahNode {
   float lo[3], hi[3];
   int left = -1, right = -1;  // children (interior)
   int first = 0, n = 0;       // primitive range (leaf)
+  int ref = 0;                // leaf: its ref, when `direct` (a fine leaf of refine_leaves) instead of leaf_ref()
+  bool direct = false;
 };
 
 static float sah_area(const float* lo, const float* hi) {
@@ -515,7 +517,9 @@ static int ceil_log2(int n) {
 // depth: this node's level (root = 1). Once the SAH splits could take the tree past the LDS stack, the rest of the
 // range is halved by index (sorted along the widest centroid axis), so every tree fits the stack: interior levels
 // stay below kStack - 1 whatever the geometry (coincident centroids make SAH peel one primitive per level).
-static int sah_build(std::vector<SahPrim>& pr, int l, int r, int max_leaf, std::vector<SahNode>& nodes, int depth = 1) {
+// reserve: stack levels kept free below the leaves (the any-hit tree's fine subtrees, refine_leaves)
+static int sah_build(std::vector<SahPrim>& pr, int l, int r, int max_leaf, std::vector<SahNode>& nodes, int depth = 1,
+                     int reserve = 0) {
   const int id = (int)nodes.size();
   nodes.emplace_back();
   SahNode nd;
@@ -587,7 +591,7 @@ static int sah_build(std::vector<SahPrim>& pr, int l, int r, int max_leaf, std::
     return id;
   }
   int m;
-  if (depth + ceil_log2(n) >= kStack - 2) {  // depth cap: balanced halves from here on
+  if (depth + ceil_log2(n) + reserve >= kStack - 2) {  // depth cap: balanced halves from here on
     int ax = 0;
     for (int a = 1; a < 3; ++a)
       if (chi[a] - clo[a] > chi[ax] - clo[ax]) ax = a;
@@ -607,8 +611,8 @@ static int sah_build(std::vector<SahPrim>& pr, int l, int r, int max_leaf, std::
   } else {
     m = l + n / 2;  // coincident centroids: halve the range
   }
-  nd.left = sah_build(pr, l, m, max_leaf, nodes, depth + 1);
-  nd.right = sah_build(pr, m, r, max_leaf, nodes, depth + 1);
+  nd.left = sah_build(pr, l, m, max_leaf, nodes, depth + 1, reserve);
+  nd.right = sah_build(pr, m, r, max_leaf, nodes, depth + 1, reserve);
   nodes[id] = nd;
   return id;
 }
@@ -642,8 +646,8 @@ static int pack_sah(const std::vector<SahNode>& nodes, const std::function<int(i
     const SahNode& n = nodes[order[k]];
     const SahNode& L = nodes[n.left];
     const SahNode& R = nodes[n.right];
-    const int rl = L.n > 0 ? leaf_ref(L.first, L.n) : idx[n.left];
-    const int rr = R.n > 0 ? leaf_ref(R.first, R.n) : idx[n.right];
+    const int rl = L.n > 0 ? (L.direct ? L.ref : leaf_ref(L.first, L.n)) : idx[n.left];
+    const int rr = R.n > 0 ? (R.direct ? R.ref : leaf_ref(R.first, R.n)) : idx[n.right];
     float4* q = &out[4 * k];
     q[0] = float4{L.lo[0], L.lo[1], L.lo[2], L.hi[0]};
     q[1] = float4{L.hi[1], L.hi[2], R.lo[0], R.lo[1]};
@@ -657,9 +661,102 @@ static int pack_sah(const std::vector<SahNode>& nodes, const std::function<int(i
   return PT_OK;
 }
 
-// Any-hit tree over the leaves of the reference tree (see above).
-int build_anyhit_tree(const float* node_enc, int nnodes, int ntris, std::vector<float4>& out, int* root_ref,
-                      int* need) {
+static int ref_first_of(int ref) { return (-(ref + 1)) >> 4; }
+static int ref_count_of(int ref) { return (-(ref + 1)) & 15; }
+
+// Fine leaves under the reference leaves (PTSVGF_FINE_LEAVES = F, the largest fine leaf; 0 = off). A reference leaf
+// holds up to 8 triangles (BVH.h:77, main.cpp:96) in one box; every ray that passes that box tests all of them. Here
+// each reference leaf of more than F triangles becomes an interior node over contiguous sub-ranges of its triangles
+// (index order kept, so a fine leaf is a valid leaf ref), cut by SAH on their boxes, down to <= F triangles.
+// Result-preserving: the reference leaf's own box is still tested exactly (it is the box the parent stores for this
+// child), and a fine box is the min/max box of its triangles widened by `pad` (2^-12 of the largest coordinate
+// magnitude, ~500x the float rounding of hitTriangle's hit point and of the slab arithmetic), so a ray that
+// hitTriangle (:215-272) accepts for one of those triangles passes it: the fine boxes only cull triangles that cannot
+// be hit, and the candidate set (and with it every closest t and any-hit verdict) is the reference leaf's. Exact ties
+// are re-walked on the reference tree as before. Leaves with a non-finite vertex coordinate stay whole.
+static int fine_leaf_max() {
+  static const int f = [] {
+    const char* e = getenv("PTSVGF_FINE_LEAVES");
+    return e ? std::max(0, atoi(e)) : 4;
+  }();
+  return f;
+}
+
+static int fine_subtree(const float* tri_enc, const float* tlo, const float* thi, int a, int b, int F, float pad,
+                        std::vector<SahNode>& nodes, int forced_id = -1) {
+  const int id = forced_id >= 0 ? forced_id : (int)nodes.size();
+  if (forced_id < 0) nodes.emplace_back();
+  SahNode nd = forced_id >= 0 ? nodes[forced_id] : SahNode{};
+  auto box = [&](int u, int v, float* lo, float* hi) {
+    for (int k = 0; k < 3; ++k) { lo[k] = INFINITY; hi[k] = -INFINITY; }
+    for (int i = u; i < v; ++i)
+      for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], tlo[3 * i + k]); hi[k] = std::max(hi[k], thi[3 * i + k]); }
+    for (int k = 0; k < 3; ++k) { lo[k] -= pad; hi[k] += pad; }
+  };
+  if (forced_id < 0) box(a, b, nd.lo, nd.hi);  // the subtree root keeps the reference leaf's exact box
+  if (b - a <= F) {
+    nd.n = b - a;
+    nd.direct = true;
+    nd.ref = -(a * 16 + (b - a)) - 1;
+    nodes[id] = nd;
+    return id;
+  }
+  float best = INFINITY;
+  int m = a + (b - a) / 2;
+  for (int c = a + 1; c < b; ++c) {
+    float l0[3], l1[3], r0[3], r1[3];
+    box(a, c, l0, l1);
+    box(c, b, r0, r1);
+    const float cost = sah_area(l0, l1) * (c - a) + sah_area(r0, r1) * (b - c);
+    if (cost < best) { best = cost; m = c; }
+  }
+  nd.n = 0;
+  nd.direct = false;
+  nd.left = fine_subtree(tri_enc, tlo, thi, a, m, F, pad, nodes);
+  nd.right = fine_subtree(tri_enc, tlo, thi, m, b, F, pad, nodes);
+  nodes[id] = nd;
+  return id;
+}
+
+static void refine_leaves(std::vector<SahNode>& nodes, const std::vector<SahPrim>& pr, const float* tri_enc, int ntris,
+                          int F) {
+  if (F <= 0 || !tri_enc) return;
+  std::vector<float> tlo((size_t)ntris * 3), thi((size_t)ntris * 3);
+  std::vector<char> finite((size_t)ntris);
+  float mag = 0.0f;
+  for (int i = 0; i < ntris; ++i) {
+    const float* f = tri_enc + (size_t)i * 45;  // Triangle_encoded: p1 p2 p3 first (Triangle.h:12-24)
+    bool ok = true;
+    for (int k = 0; k < 3; ++k) {
+      const float v0 = f[k], v1 = f[3 + k], v2 = f[6 + k];
+      ok = ok && std::isfinite(v0) && std::isfinite(v1) && std::isfinite(v2);
+      tlo[3 * i + k] = std::min(v0, std::min(v1, v2));
+      thi[3 * i + k] = std::max(v0, std::max(v1, v2));
+    }
+    finite[i] = ok;
+    if (ok)
+      for (int k = 0; k < 9; ++k) mag = std::max(mag, std::fabs(f[k]));
+  }
+  const float pad = std::max(mag, 1.0f) * (1.0f / 4096.0f);
+  const size_t n0 = nodes.size();
+  for (size_t id = 0; id < n0; ++id) {
+    if (nodes[id].n <= 0) continue;
+    const int ref = pr[nodes[id].first].ref;
+    const int first = ref_first_of(ref), cnt = ref_count_of(ref);
+    if (cnt <= F) continue;
+    bool ok = true;
+    for (int i = first; i < first + cnt; ++i) ok = ok && finite[i];
+    if (!ok) continue;
+    SahNode root = nodes[id];  // exact reference-leaf box, stored by the parent for this child
+    root.n = 0;
+    nodes[id] = root;
+    fine_subtree(tri_enc, tlo.data(), thi.data(), first, first + cnt, F, pad, nodes, (int)id);
+  }
+}
+
+// Any-hit tree over the leaves of the reference tree (see above), with fine leaves under them (refine_leaves).
+int build_anyhit_tree(const float* node_enc, int nnodes, int ntris, const float* tri_enc, std::vector<float4>& out,
+                      int* root_ref, int* need) {
   std::vector<SahPrim> pr;
   for (int i = 1; i < nnodes; ++i) {
     const float* f = node_enc + (size_t)i * 12;
@@ -675,7 +772,9 @@ int build_anyhit_tree(const float* node_enc, int nnodes, int ntris, std::vector<
   if (pr.empty()) return err(PT_ERR_FORMAT, "BVH without leaves");
   std::vector<SahNode> nodes;
   nodes.reserve(2 * pr.size());
-  sah_build(pr, 0, (int)pr.size(), 1, nodes);
+  const int F = fine_leaf_max();
+  sah_build(pr, 0, (int)pr.size(), 1, nodes, 1, F > 0 ? ceil_log2(16) : 0);  // a fine subtree is <= 4 levels deep
+  refine_leaves(nodes, pr, tri_enc, ntris, F);
   return pack_sah(nodes, [&](int first, int) { return pr[first].ref; }, out, root_ref, need);
 }
 
@@ -783,7 +882,7 @@ int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU*
   sg.root4 = root4;
   {  // optional, like the 4-wide tree: without it shadow and closest-hit rays walk the reference tree
     std::vector<float4> any;
-    if (build_anyhit_tree((const float*)nodes->host.data(), (int)nnodes, (int)ntris, any, &sg.root_any,
+    if (build_anyhit_tree((const float*)nodes->host.data(), (int)nnodes, (int)ntris, te, any, &sg.root_any,
                           &sg.need_any) == PT_OK) {
       if (any.empty()) any.push_back(float4{0, 0, 0, 0});
       if ((rc = upload_vec(any, &sg.bvh_any)) != PT_OK) return rc;
@@ -1310,7 +1409,6 @@ int draw_svgf(Pass* p, int kind) {
     k.step = ui(p, "gStepSize", 1);
     k.phi_color = uf(p, "gPhiColor", 0.0f);
     k.phi_normal = uf(p, "gPhiNormal", 0.0f);
-    k.xcd_run = ui(p, "atrous_xcd_run", 0);
     // production tiled kernel: per-tile surface flags, derived once per G-buffer from its depth-fwidth plane
     const int si = k.step == 1 ? 0 : k.step == 2 ? 1 : k.step == 4 ? 2 : k.step == 8 ? 3 : k.step == 16 ? 4 : -1;
     if (!ui(p, "exact", 0) && ui(p, "atrous_variant", 0) == 0 && ui(p, "atrous_tile_flags", 1) && k.fwidth.aux &&
@@ -1337,9 +1435,6 @@ int draw_svgf(Pass* p, int kind) {
     if (ui(p, "exact", 0)) rc = launch_atrous_exact(k, g.stream);          // bit-exact form (tests)
     else if (ui(p, "atrous_variant", 0) == 1) rc = launch_atrous_simple(k, g.stream);  // A/B: generic
     else if (ui(p, "atrous_variant", 0) == 2) rc = launch_atrous_step(k, g.stream);    // A/B: step kernel
-    else if (ui(p, "atrous_variant", 0) == 3) rc = launch_atrous_pair(k, g.stream);    // A/B: packed pairs
-    else if (ui(p, "atrous_variant", 0) == 4)                                         // A/B: sliding LDS ring
-      rc = launch_atrous_slide(k, ui(p, "atrous_chunks", 6), ui(p, "atrous_nx", 0), ui(p, "atrous_xcd", 0), g.stream);
     else rc = launch_atrous_fast(k, g.stream);                             // LDS-tiled (production)
   } else if (kind == PK_MODULATE) {
     ModulateParams k;

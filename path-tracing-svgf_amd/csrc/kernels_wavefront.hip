@@ -24,7 +24,14 @@ using namespace glsl;
 namespace ptk {
 
 constexpr int kTB = 128;  // threads per traversal block (LDS stack: kStack*kTB*4 = 16 KiB)
-#ifdef PT_TRACE_WAVES_PER_EU
+// Resident waves per SIMD the traversal kernels are compiled for. Left to itself the compiler gives the lane-refill
+// kernels 98 VGPRs (4 waves/SIMD: 104-register allocation); asking for 5 fits them in 96 without spills: 4K 179.8 ->
+// 185.8 fps, surface view 59.9 -> 62.0 (same box, tools/env_ab_views.sh, profiles/r03/occupancy_ab.log); 6 spills
+// (36 / 98 VGPRs of the refill kernels to scratch) and measured 181 / 60.4.
+#ifndef PT_TRACE_WAVES_PER_EU
+#define PT_TRACE_WAVES_PER_EU 5
+#endif
+#if PT_TRACE_WAVES_PER_EU > 0
 #define PT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(PT_TRACE_WAVES_PER_EU)))
 #else
 #define PT_TRACE_ATTR
@@ -1295,14 +1302,14 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, hipStream_t aux,
 int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent_t ev_fork,
                                hipEvent_t ev_join) {
   // the LDS stack bounds resident waves: a tree that fits the small stack gets more of them
-  if (p.wf.spill) return launch_wavefront<kStack, true>(&p, 1, s, nullptr, nullptr, nullptr);  // deep tree, no fork
+  if (p.wf.spill) return launch_wavefront<kSpillKS, true>(&p, 1, s, nullptr, nullptr, nullptr);  // deep tree, no fork
   return p.stack_need <= kStackSmall ? launch_wavefront<kStackSmall, false>(&p, 1, s, aux, ev_fork, ev_join)
                                      : launch_wavefront<kStack, false>(&p, 1, s, aux, ev_fork, ev_join);
 }
 
 int launch_pathtrace_wavefront_batch(const PTParams* ps, int nb, hipStream_t s) {
   if (nb < 1 || nb > kMaxBatch) return (int)hipErrorInvalidValue;
-  if (ps[0].wf.spill) return launch_wavefront<kStack, true>(ps, nb, s, nullptr, nullptr, nullptr);
+  if (ps[0].wf.spill) return launch_wavefront<kSpillKS, true>(ps, nb, s, nullptr, nullptr, nullptr);
   return ps[0].stack_need <= kStackSmall ? launch_wavefront<kStackSmall, false>(ps, nb, s, nullptr, nullptr, nullptr)
                                          : launch_wavefront<kStack, false>(ps, nb, s, nullptr, nullptr, nullptr);
 }

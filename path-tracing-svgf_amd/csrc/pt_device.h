@@ -39,6 +39,13 @@ namespace ptk {
 #endif
 constexpr int kStack = PT_KSTACK;  // traversal stack depth (host checks BVH depth < kStack)
 constexpr int kStackSmall = 24;    // smaller LDS stack (more resident waves) for trees that fit it
+// LDS entries of the spilling traversal stack (SpillStack): a tree deeper than this walks kSpillKS entries in LDS and
+// the rest in global memory. Default kStack (spill only beyond the 32-entry stack); PT_SPILL_KS < kStackSmall trades
+// rare global spills for more resident waves (A/B).
+#ifndef PT_SPILL_KS
+#define PT_SPILL_KS PT_KSTACK
+#endif
+constexpr int kSpillKS = PT_SPILL_KS;
 constexpr int kBlock = 256;      // threads per block for per-pixel kernels
 constexpr int kNoneRef = (int)0x80000000;
 constexpr int kPointBins = 4;     // point-light shadow lists, one per light index mod 4 (coherent waves)
@@ -242,7 +249,6 @@ struct AtrousParams {
   Plane illum, nd, fwidth, out;
   int step;
   float phi_color, phi_normal;
-  int xcd_run;  // tiled kernel: > 0 runs of this many consecutive tiles per XCD (L2 halo reuse), 0 = dispatch order
   const unsigned char* tile_any;  // tiled kernel: per-tile "holds a surface pixel" flags of this step, or null
 };
 // Tiles of the tiled a-trous (kernels_atrous.hip): 64 * NX columns (NX = 2 for S >= 16) x kAtrousTJ rows of one
@@ -297,8 +303,6 @@ int launch_reproject(const ReprojParams& p, hipStream_t s);
 int launch_variance(const VarianceParams& p, hipStream_t s);
 int launch_atrous_exact(const AtrousParams& p, hipStream_t s);
 int launch_atrous_fast(const AtrousParams& p, hipStream_t s);   // LDS-tiled (production)
-int launch_atrous_pair(const AtrousParams& p, hipStream_t s);   // LDS-tiled, channel-planar, packed pixel pairs
-int launch_atrous_slide(const AtrousParams& p, int chunks, int nx, int xcd, hipStream_t s);  // LDS ring down a residue class
 int launch_atrous_step(const AtrousParams& p, hipStream_t s);   // step-specialised, texture-path taps
 int launch_atrous_simple(const AtrousParams& p, hipStream_t s);
 int launch_modulate(const ModulateParams& p, hipStream_t s);

@@ -236,6 +236,7 @@ class BandRenderer:
         self.plan = BandPlan(W, H, rank, world, ghost=ghost, bounds=bounds, iterations=iters)
         self.dist = dist
         self.exchange = True  # False only while calibrating (make_band_renderer): ranks time their bands alone
+        self.stage_events = None  # (stage, event, event) per exchange while time_exchanges(True)
         self._group = host_group(dist) if world > 1 else None
         self._tensors = {}
         gl.set_band(W, H, self.plan.y0, self.plan.y1, self.plan.row0, self.plan.rows)
@@ -300,7 +301,35 @@ class BandRenderer:
             return
         if stage == "reproject":
             self._motion()
-        run_stage(stage, {k: self._tensors[h] for k, h in handles.items()}, self.plan, self.dist)
+        planes = {k: self._tensors[h] for k, h in handles.items()}
+        if self.stage_events is None:
+            run_stage(stage, planes, self.plan, self.dist)
+            return
+        import torch
+
+        # exchange time on the stream the SVGF passes run on: the exchange's rows are waited for there (RCCL's own
+        # stream joins it at req.wait()), so the event pair spans the stage as the back end sees it
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        run_stage(stage, planes, self.plan, self.dist)
+        e1.record()
+        self.stage_events.append((stage, e0, e1))
+
+    def time_exchanges(self, on: bool) -> None:
+        """Record HIP events around every halo stage from now on (on) / stop (off); exchange_ms() reads them."""
+        self.stage_events = [] if on else None
+
+    def exchange_ms(self) -> dict:
+        """Per stage: mean ms per frame between the events around its exchanges (after the frames finished), and
+        the frames counted. Synchronises."""
+        import torch
+
+        torch.cuda.synchronize()
+        tot, n = {}, {}
+        for stage, e0, e1 in self.stage_events or []:
+            tot[stage] = tot.get(stage, 0.0) + e0.elapsed_time(e1)
+            n[stage] = n.get(stage, 0) + 1
+        return {s: round(tot[s] / n[s], 4) for s in tot}
 
     def frame(self) -> None:
         self.r.frame()
@@ -312,6 +341,9 @@ class BandRenderer:
         return self.r.pass_times()
 
     def time_atrous(self, reps: int = 20) -> float:
+        """The a-trous kernels' average launch time (Renderer.time_atrous). The replay runs without exchanges, so
+        iterations 1-4 read ghost rows that the frame's LATER exchanges refilled: the band planes it leaves are not
+        the frame's (read what a frame produced before calling this)."""
         return self.r.time_atrous(reps)
 
     def trace_stats(self) -> dict:
@@ -367,6 +399,36 @@ class BandRenderer:
         self.dist.all_reduce(per_rank)
         self.last_band_ms = per_rank.cpu().numpy()  # every rank's band time alone (ms per frame)
         return band_row_cost(visits.cpu().numpy(), p.bounds, self.last_band_ms)
+
+
+def gather_bands(owned: dict, plan: BandPlan, dist, dst: int = 0) -> dict | None:
+    """Assemble full frames on rank `dst` from every rank's owned rows: owned maps plane names to (y1 - y0, W, C)
+    float32 numpy arrays; returns {name: (H, W, C)} on dst, None elsewhere. Point-to-point sends of device tensors
+    (RCCL over xGMI) or host tensors (gloo); for checking and dumps, outside any timed region."""
+    import numpy as np
+    import torch
+
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() != "gloo" else torch.device("cpu")
+    names = sorted(owned)
+    if plan.rank != dst:
+        for k in names:
+            dist.send(torch.from_numpy(np.ascontiguousarray(owned[k])).to(dev), dst)
+        return None
+    full = {}
+    for k in names:
+        a = owned[k]
+        out = np.empty((plan.H,) + a.shape[1:], a.dtype)
+        out[plan.y0:plan.y1] = a
+        full[k] = out
+    for src in range(plan.world):
+        if src == dst:
+            continue
+        y0, y1 = plan.owned(src)
+        for k in names:
+            t = torch.empty((y1 - y0,) + full[k].shape[1:], dtype=torch.float32, device=dev)
+            dist.recv(t, src)
+            full[k][y0:y1] = t.cpu().numpy()
+    return full
 
 
 def band_row_cost(visits, bounds, ms):

@@ -226,3 +226,31 @@ def test_band_row_cost_matches_band_times():
     nb = balanced_bounds(c, 4)
     assert nb[1] < 100 and nb[3] < 300                   # the slow first band shrinks, the cheap last one grows
     assert abs(band_row_cost(np.zeros(400), bounds, ms)[350] - 0.5 / 100) < 1e-12
+
+
+def _gather_worker(rank, world, port, W, H, bounds):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "path-tracing-svgf_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ptsvgf.dist import BandPlan, gather_bands
+
+        plan = BandPlan(W, H, rank, world, bounds=bounds)
+        frame = np.arange(H * W * 4, dtype=np.float32).reshape(H, W, 4)
+        owned = {"a": frame[plan.y0:plan.y1].copy(), "b": -frame[plan.y0:plan.y1, :, :2].copy()}
+        full = gather_bands(owned, plan, dist)
+        if rank == 0:
+            assert np.array_equal(full["a"], frame)
+            assert np.array_equal(full["b"], -frame[..., :2])
+        else:
+            assert full is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,bounds", [(2, None), (3, (0, 10, 14, 40))])
+def test_gather_bands_assembles_full_frame(world, bounds):
+    """bench.py's band_parity gathers every rank's owned rows on rank 0 (ptsvgf.dist.gather_bands)."""
+    mp.spawn(_gather_worker, args=(world, _free_port(), 6, 40, bounds), nprocs=world, join=True)

@@ -117,6 +117,49 @@ def test_cornell_teapot_matches_oracle(gpu, scene_cornell):
         _cmp(key, got[key], want[key], rel=True)
 
 
+@pytest.mark.parametrize("K", [1, 4])
+def test_config0_cornell_teapot_512_matches_oracle(gpu, K):
+    """configs[0] at its stated size: the Cornell box + teapot stand-in at 512x512, 1 spp, depth 2, the path tracer
+    alone (SVGF plays no part in its planes). Production fast driver (G-buffer-bounded primaries, SAH trees, lane
+    refill with K = 4 frames in flight), then bench.py config0's unhinted _path_trace: color / emission / albedo
+    bit-exact against the oracle path tracer (path_tracing.frag:1056-1128) on frames 0-3."""
+    from ptsvgf.camera import Camera, parameter_config, rigid_inverse
+    from ptsvgf.scene import build_scene
+
+    gl = gpu
+    W = H = 512
+    scene = build_scene("cornell_teapot")
+    cfg = parameter_config()
+    r = _renderer(scene, W, H, config=cfg, mode="fast", run_taa=False, run_output=False, frames_in_flight=K)
+    osc = O.OracleScene(scene)
+    cam = Camera(W, H)
+
+    def want():
+        cam.update()
+        out = osc.path_trace(W, H, cam.frameCounter, cam.cam_position, rigid_inverse(cam.cam_view_mat),
+                             cfg.clamp_threshold, cfg.max_tracing_depth, aspect_corrected=False)
+        cam.frameCounter += 1
+        return dict(zip(("color", "emission", "albedo"), out))
+
+    for f in range(3):
+        r.frame()
+        exp = want()
+        got = _readback(gl, r)
+        assert r.camera.frameCounter == cam.frameCounter
+        for key in ("color", "emission", "albedo"):
+            ex = _cmp(f"K{K}/f{f}/{key}", got[key], exp[key])
+            assert ex == 1.0, f"path tracer output {key} is not bit-exact ({ex})"
+        assert np.count_nonzero(got["albedo"][..., :3].any(axis=-1)) > W * H // 2  # the box fills the frame
+    if K == 1:  # bench.py config0's timed call: the path tracer without the G-buffer hint
+        r._path_trace()
+        r.camera.frameCounter += 1
+        exp = want()
+        for key, plane in zip(("color", "emission", "albedo"), (r.curColor, r.Emission, r.Albedo)):
+            ex = _cmp(f"unhinted/{key}", gl.readback(plane), exp[key])
+            assert ex == 1.0, f"unhinted path tracer output {key} is not bit-exact ({ex})"
+    r.close()
+
+
 def test_nan_normals_match_oracle(gpu, scene_nan):
     """Degenerate faces -> NaN vertex normals: both sides propagate NaN identically."""
     gl = gpu

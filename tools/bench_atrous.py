@@ -3,8 +3,8 @@
 For each view: render 3 frames, then time every variant x step as 20 back-to-back launches between two HIP
 events on the library stream (no per-launch sync), interleaved over ROUNDS rounds; report the median per-launch
 time and the algorithmic (52 B/px) fraction of 8 TB/s. The variants' outputs are compared bit for bit.
-usage: python tools/bench_atrous.py [variant ...]   (variants: 0 tile, 2 step, 3 pair, 4 sliding ring; default 0 3)
-A variant may carry extra int uniforms: 4:atrous_chunks=8:atrous_xcd=1"""
+usage: python tools/bench_atrous.py [variant ...]   (variants: 0 tile, 1 generic, 2 step; default 0 2)
+A variant may carry extra int uniforms: 0:atrous_tile_flags=0"""
 import json
 import os
 import sys
@@ -24,14 +24,14 @@ from ptsvgf.renderer import Renderer, _prog
 from ptsvgf.scene import build_scene
 
 W, H = int(os.environ.get("W", 3840)), int(os.environ.get("H", 2160))
-VARIANTS = sys.argv[1:] or ["0", "3"]
+VARIANTS = sys.argv[1:] or ["0", "2"]
 
 
 def select(ap, spec):
     """Set atrous_variant and the spec's extra uniforms (reset to 0 first so variants do not leak into each other)."""
     v, *kv = spec.split(":")
-    for name in ("atrous_chunks", "atrous_nx", "atrous_xcd", "atrous_xcd_run", "atrous_tile_flags"):
-        ap.set_uniform_int(name, {"atrous_chunks": 6, "atrous_tile_flags": 1}.get(name, 0))
+    for name in ("atrous_tile_flags",):
+        ap.set_uniform_int(name, {"atrous_tile_flags": 1}.get(name, 0))
     ap.set_uniform_int("atrous_variant", int(v))
     for item in kv:
         name, val = item.split("=")

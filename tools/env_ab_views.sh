@@ -1,0 +1,26 @@
+#!/bin/bash
+# Same-box A/B of one environment switch over several values, 4K default and surface views (K = 4), alternating
+# values within each repetition; per run: fps, profiled path-tracer ms, visits per ray, lane efficiency.
+# usage: REPS=2 bash tools/env_ab_views.sh NAME V1 V2 ... [-- extra bench args]
+# (library builds: NAME = PTSVGF_LIB_DIR, values = $GRAFT_REPO_ROOT/path-tracing-svgf_amd/lib_exp/<name>)
+cd "$GRAFT_REPO_ROOT"
+N=$1; shift
+VALS=()
+while [ $# -gt 0 ] && [ "$1" != "--" ]; do VALS+=("$1"); shift; done
+[ "$1" == "--" ] && shift
+for rep in $(seq 1 ${REPS:-2}); do
+  for v in "${VALS[@]}"; do
+    for view in ${VIEWS_AB:-default surface}; do
+      f=gpurun_out/envab_$(echo "$v" | tr '/' '_')_$view.log
+      env "$N=$v" timeout -k 10 300 python bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-1080p --no-extras \
+        --view $view "$@" > $f 2>&1 || exit $?
+      python - "$N" "$v" "$view" "$f" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[4]) if l.startswith("{")][-1])
+pt = d["path_tracer"]
+print(f"{sys.argv[1]}={sys.argv[2]} {sys.argv[3]:8s} fps {d['value']:8.2f}  pt_ms {d['passes_ms'].get('pathtrace', 0):6.3f}"
+      f"  visits/ray {pt['visits_per_ray']}  lanes {pt['lane_efficiency']}", flush=True)
+PY
+    done
+  done
+done

@@ -2,11 +2,12 @@
 
 * kernel_stats.csv        — rocprofv3 --kernel-trace --stats summary (copied)
 * pmc_per_dispatch_avg.json — every PMC counter averaged per dispatch, per kernel
-* atrous_traffic.json     — HBM bytes per a-trous launch for bench.py's roofline.traffic:
-  FETCH_SIZE x 2 (gfx950 tallies 128-B streaming requests at 64 B; MI355X_MICROARCH.md
-  "HBM / rocprofv3") + WRITE_SIZE, both in KiB, averaged over the step kernel's dispatches.
+* atrous_traffic_<view>.json — HBM bytes per a-trous launch for bench.py's roofline.traffic on that camera
+  view: FETCH_SIZE x 2 (gfx950 tallies 128-B streaming requests at 64 B; MI355X_MICROARCH.md
+  "HBM / rocprofv3") + WRITE_SIZE, both in KiB, averaged over the tile kernel's dispatches.
+  bench.py reads profiles/atrous_traffic_<view>.json; copy the file there from the round's directory.
 
-usage: python tools/summarize_profile.py gpurun_out/prof_<tag> profiles/<tag> <pixels per launch>
+usage: python tools/summarize_profile.py gpurun_out/prof_<tag> profiles/<tag> <pixels per launch> [view]
 """
 import csv
 import json
@@ -23,7 +24,7 @@ def short(name: str) -> str:
     return name.split("(")[0]
 
 
-def main(src: str, dst: str, pixels: int) -> None:
+def main(src: str, dst: str, pixels: int, view: str = "default") -> None:
     os.makedirs(dst, exist_ok=True)
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
     if os.path.exists(stats):
@@ -48,14 +49,14 @@ def main(src: str, dst: str, pixels: int) -> None:
     if fetch and write:
         fb = 2.0 * sum(fetch) / len(fetch) * 1024.0
         wb = sum(write) / len(write) * 1024.0
-        out = {"kernel": ATROUS, "pixels": pixels, "bytes_per_launch": round(fb + wb),
+        out = {"kernel": ATROUS, "view": view, "pixels": pixels, "bytes_per_launch": round(fb + wb),
                "fetch_bytes": round(fb), "write_bytes": round(wb), "algorithmic_bytes": 52 * pixels,
                "dispatches": len(fetch), "source": os.path.basename(os.path.normpath(src)),
                "method": "FETCH_SIZE*2 + WRITE_SIZE (KiB), separate --pmc passes"}
-        with open(os.path.join(dst, "atrous_traffic.json"), "w") as f:
+        with open(os.path.join(dst, f"atrous_traffic_{view}.json"), "w") as f:
             json.dump(out, f, indent=1)
         print(json.dumps(out))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], int(sys.argv[3]))
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4] if len(sys.argv) > 4 else "default")
