@@ -23,6 +23,9 @@ using namespace glsl;
 
 namespace ptk {
 
+#ifndef PT_WIDE_SHADOW_SORT
+#define PT_WIDE_SHADOW_SORT 0  // shadow rays' 4-wide walk: 1 = nearest child first, 0 = slot order
+#endif
 constexpr int kTB = 128;  // threads per traversal block (LDS stack: kStack*kTB*4 = 16 KiB)
 // Resident waves per SIMD the traversal kernels are compiled for. Left to itself the compiler gives the lane-refill
 // kernels 98 VGPRs (4 waves/SIMD: 104-register allocation); asking for 5 fits them in 96 without spills: 4K 179.8 ->
@@ -641,7 +644,9 @@ __host__ __device__ constexpr int refill_blocks(int items_max) {
 // per ray unchanged); any-hit verdicts do not depend on which lane or when.
 // With a visit budget (PTParams::wf.shadow_budget) a ray still undecided past it is handed to the wave-cooperative
 // walk (wf_shadow_coop) and its lane takes the next item, as in wf_trace_shadow.
-template <int KS, bool DEEP>
+// WIDE: the walk runs on the 4-wide form of the any-hit tree (pack_wide: the same candidate triangles); a ray whose
+// pushes would overflow the LDS stack goes to the cooperative walk like a ray past the visit budget.
+template <int KS, bool DEEP, bool WIDE>
 __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTParams p, ListBatch lb, int cap,
                                                                              int* __restrict__ heads,
                                                                              int* __restrict__ strag_count) {
@@ -661,7 +666,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
   const SceneDev sc = anyhit_scene(p.scene);
   const unsigned long long below = (1ull << lane) - 1ull;
   auto st = ray_stack<kTB, KS, DEEP>(stk + threadIdx.x, p, 0);
-  bool have = false, point = false, spill = false;
+  bool have = false, point = false, spill = false, ovf = false;
   int pid = 0, sp = 0, node = kNone, leaf = kNone;
   v3 S = splat(0.0f), d = splat(0.0f), inv = splat(0.0f);
   float lim = 0.0f, maxd = 0.0f;
@@ -684,8 +689,9 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
         maxd = dir.w;
         lim = point ? maxd * 1.0002f + 2.0e-4f : __builtin_inff();
         sp = 0;
-        node = sc.root_ref;
+        node = WIDE ? p.scene.root4 : sc.root_ref;
         leaf = kNone;
+        ovf = false;
         if (node < 0) { leaf = node; node = kNone; }
         if constexpr (DEEP) st = ray_stack<kTB, KS, DEEP>(stk + threadIdx.x, p, pid);
         have = true;
@@ -695,8 +701,20 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
     }
     if (!__any(have)) break;
     while (node >= 0) {  // anyhit2's descent (only lanes holding a ray have node >= 0)
-      ++nvis;
+      nvis += PT_NODE_VISIT;
       ++rvis;
+      if constexpr (WIDE) {
+        if (!wide_step<KS, PT_WIDE_SHADOW_SORT>(p.scene.bvh4, node, st, sp, S, inv, lim)) {  // stack full: coop walk
+          ovf = true;
+          node = leaf = kNone;
+        }
+        if (node < 0 && node != kNone && leaf == kNone) {
+          leaf = node;
+          node = sp > 0 ? st.get(--sp) : kNone;
+        }
+        if (!__any(leaf == kNone)) break;
+        continue;
+      }
       const float4* nd = sc.bvh + 4 * node;
       const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
       float t0l, t0r;
@@ -738,13 +756,14 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
         node = sp > 0 ? st.get(--sp) : kNone;
       }
     }
-    if (have && (hit || (node == kNone && leaf == kNone))) {  // this lane's ray is decided
+    if (have && !ovf && (hit || (node == kNone && leaf == kNone))) {  // this lane's ray is decided
       (point ? p.wf.occ_p : p.wf.occ_h)[pid] = hit;
       have = false;
       node = leaf = kNone;
       spill = spill || st.spilled;
     }
-    const bool defer = have && budget && rvis > budget;  // past the budget: the cooperative walk decides it
+    // past the budget, or the 4-wide walk's stack full: the cooperative walk decides it
+    const bool defer = have && (ovf || (budget && rvis > budget));
     const unsigned long long m = __ballot(defer);
     if (m) {
       int base = 0;
@@ -770,7 +789,10 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
 // Production switches only (closest_tree = prune = 1); the host keeps wf_trace_closest otherwise.
 // With a visit budget (PTParams::wf.closest_budget) a ray still walking past it goes to the cooperative closest-hit
 // walk (wf_closest_coop) and its lane takes the next item.
-template <int KS, bool DEEP>
+// WIDE: the walk runs on the 4-wide form of the SAH tree (pack_wide: the same candidate triangles, so the same
+// minimum t); a ray whose best t was met exactly by a second triangle, or whose pushes would overflow the LDS stack,
+// goes to the cooperative walk (wf_closest_coop), which re-walks ties on the reference tree.
+template <int KS, bool DEEP, bool WIDE>
 __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTParams p, ListBatch lb, int cap,
                                                                               int* __restrict__ heads,
                                                                               int* __restrict__ strag_count) {
@@ -788,7 +810,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTP
   if (q.next >= q.end) return;
   const unsigned long long below = (1ull << lane) - 1ull;
   auto st = ray_stack<kTB, KS, DEEP>(stk + threadIdx.x, p, 0);
-  bool have = false, rewalk = false, tied = false, spill = false;
+  bool have = false, rewalk = false, tied = false, spill = false, ovf = false;
   int pid = 0, sp = 0, node = kNone, leaf = kNone, best = -1;
   const float4* tree = p.scene.bvh_any;  // this lane's tree: the SAH tree, or the reference tree for a re-walk
   v3 S = splat(0.0f), d = splat(0.0f), inv = splat(0.0f);
@@ -807,8 +829,9 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTP
         d = xyz(dd);
         inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
         tree = p.scene.bvh_any;
-        node = p.scene.root_any;
+        node = WIDE ? p.scene.root4 : p.scene.root_any;
         rewalk = false;
+        ovf = false;
         tbest = PT_INF;
         best = -1;
         tied = false;
@@ -824,8 +847,20 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTP
     }
     if (!__any(have)) break;
     while (node >= 0) {  // traverse<0>'s descent, pruned by the current best t
-      ++nvis;
+      nvis += PT_NODE_VISIT;
       ++rvis;
+      if constexpr (WIDE) {
+        if (!wide_step<KS, true>(p.scene.bvh4, node, st, sp, S, inv, tbest * 1.0002f + 2.0e-4f)) {
+          ovf = true;  // stack full: the cooperative walk
+          node = leaf = kNone;
+        }
+        if (node < 0 && node != kNone && leaf == kNone) {
+          leaf = node;
+          node = sp > 0 ? st.get(--sp) : kNone;
+        }
+        if (!__any(leaf == kNone)) break;
+        continue;
+      }
       const float4* nd = tree + 4 * node;
       const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
       float t0l, t0r;
@@ -871,8 +906,8 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTP
         node = sp > 0 ? st.get(--sp) : kNone;
       }
     }
-    if (have && node == kNone && leaf == kNone) {  // this lane's walk is complete
-      if (!rewalk && tied) {  // exact tie: walk the ray again on the reference tree, in the reference's order
+    if (have && !ovf && node == kNone && leaf == kNone && !(WIDE && tied)) {  // this lane's walk is complete
+      if (!WIDE && !rewalk && tied) {  // exact tie: walk the ray again on the reference tree, in the reference's order
         rewalk = true;
         ++nrewalk;
         tree = p.scene.bvh;
@@ -888,7 +923,9 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTP
         spill = spill || st.spilled;
       }
     }
-    const bool defer = have && budget && rvis > budget;  // past the budget: the cooperative walk finishes it
+    // past the budget, the 4-wide walk's stack full, or (4-wide) an exact tie met: the cooperative walk finishes it
+    const bool defer = have && (ovf || (budget && rvis > budget) ||
+                                (WIDE && tied && node == kNone && leaf == kNone));
     const unsigned long long m = __ballot(defer);
     if (m) {
       int base = 0;
@@ -1226,6 +1263,7 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, hipStream_t aux,
   const bool fork = aux && ev_fork && ev_join && nb == 1;
   auto lst = [&](const PTParams& f, int i) { return (i & 1) ? f.wf.list1 : f.wf.list0; };  // bounce i's live list
   const bool refill_closest = p.refill && p.closest_tree && p.prune && p.scene.bvh_any;
+  const bool wide = !DEEP && p.refill && p.scene.bvh4;  // the refill walks on the 4-wide any-hit tree
   auto closest = [&](int i, hipStream_t st) {
     if (refill_closest) {
       ListBatch lb{nb, N, {}, {}};
@@ -1234,9 +1272,15 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, hipStream_t aux,
         lb.counts[b] = ps[b].wf.counters + kWfCtr * (i - 1);
       }
       int* strag = p.wf.counters + kWfCtr * i + kCtrStragC;
-      hipLaunchKernelGGL((wf_trace_closest_refill<KS, DEEP>), dim3(refill_blocks(nb * N)), dim3(kTB), 0, st, p, lb,
-                         cap, p.wf.counters + kWfCtr * i + kCtrQClosest, strag);
-      if (p.wf.closest_budget)
+      if constexpr (!DEEP)
+        if (wide) {
+          hipLaunchKernelGGL((wf_trace_closest_refill<KS, false, true>), dim3(refill_blocks(nb * N)), dim3(kTB), 0, st,
+                             p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQClosest, strag);
+        }
+      if (!wide)
+        hipLaunchKernelGGL((wf_trace_closest_refill<KS, DEEP, false>), dim3(refill_blocks(nb * N)), dim3(kTB), 0, st,
+                           p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQClosest, strag);
+      if (p.wf.closest_budget || wide)  // (4-wide: ties and stack overflows go there too)
         hipLaunchKernelGGL(wf_closest_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, st, p, (const int*)strag);
     } else {
       for (int b = 0; b < nb; ++b)
@@ -1265,16 +1309,22 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, hipStream_t aux,
       closest(i + 1, aux);
       if ((e = hipEventRecord(ev_join, aux)) != hipSuccess) return (int)e;
     }
-    if (p.refill && !p.scene.bvh4) {
+    if (p.refill) {
       ListBatch lb{nb, N, {}, {}};
       for (int b = 0; b < nb; ++b) {
         lb.list[b] = ps[b].wf.shadow_list;
         lb.counts[b] = ps[b].wf.counters + kWfCtr * i + kCtrHdr;
       }
       int* strag = p.wf.counters + kWfCtr * i + kCtrStrag;  // shadow rays handed to the cooperative walk
-      hipLaunchKernelGGL((wf_trace_shadow_refill<KS, DEEP>), dim3(refill_blocks(2 * nb * N)), dim3(kTB), 0, s, p, lb,
-                         cap, p.wf.counters + kWfCtr * i + kCtrQShadow, strag);
-      if (p.wf.shadow_budget)
+      if constexpr (!DEEP)
+        if (wide) {
+          hipLaunchKernelGGL((wf_trace_shadow_refill<KS, false, true>), dim3(refill_blocks(2 * nb * N)), dim3(kTB), 0,
+                             s, p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQShadow, strag);
+        }
+      if (!wide)
+        hipLaunchKernelGGL((wf_trace_shadow_refill<KS, DEEP, false>), dim3(refill_blocks(2 * nb * N)), dim3(kTB), 0, s,
+                           p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQShadow, strag);
+      if (p.wf.shadow_budget || wide)
         hipLaunchKernelGGL(wf_shadow_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, s, p, (const int*)strag);
     } else {
       for (int b = 0; b < nb; ++b) {

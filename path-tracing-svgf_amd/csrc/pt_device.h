@@ -38,6 +38,10 @@ namespace ptk {
 #define PT_KSTACK 32
 #endif
 constexpr int kStack = PT_KSTACK;  // traversal stack depth (host checks BVH depth < kStack)
+// Traversal counters: a node visit counts PT_NODE_VISIT (1; a diagnostic build with 0 counts triangle tests only)
+#ifndef PT_NODE_VISIT
+#define PT_NODE_VISIT 1
+#endif
 constexpr int kStackSmall = 24;    // smaller LDS stack (more resident waves) for trees that fit it
 // LDS entries of the spilling traversal stack (SpillStack): a tree deeper than this walks kSpillKS entries in LDS and
 // the rest in global memory. Default kStack (spill only beyond the 32-entry stack); PT_SPILL_KS < kStackSmall trades

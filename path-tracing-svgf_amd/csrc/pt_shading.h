@@ -214,7 +214,7 @@ __device__ int traverse(const SceneDev& sc, Stk& stk, v3 S, v3 d, float maxd, in
   if (node < 0) { leaf = node; node = kNone; }
   while (node != kNone || leaf != kNone) {
     while (node >= 0) {  // interior nodes (kNone and leaf refs are negative)
-      ++nvis;
+      nvis += PT_NODE_VISIT;
       const float4* nd = sc.bvh + 4 * node;
       float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
       float t0l, t0r;
@@ -335,7 +335,7 @@ __device__ bool anyhit2(const SceneDev& sc, Stk& stk, v3 S, v3 d, bool point, fl
       return false;
     }
     while (node >= 0) {
-      ++nvis;
+      nvis += PT_NODE_VISIT;
       const float4* nd = sc.bvh + 4 * node;
       float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
       float t0l, t0r;
@@ -538,6 +538,74 @@ __device__ int closest_coop_walk(const SceneDev& sc, int* __restrict__ st, int c
   return __shfl(tri, 0);
 }
 
+// One node of a 4-wide walk (pack_wide's layout) for the lane-refill kernels: the four child boxes are slab-tested
+// (hitAABB, :275-288), a child counts as hit when hitAABB's distance is > 0 and its entry t0 is not beyond `lim` (the
+// pruning bound of the binary walks), the walk descends into the nearest hit child (hitAABB's distance, ties to the
+// lower slot) and pushes the others farthest first, so the next pop is the next nearest (SORT; without it, for
+// any-hit rays whose verdict does not depend on the order, the first hit slot is taken and the others pushed). With
+// no hit child it pops.
+// Returns false, leaving the stack as it was, when the pushes would overflow the KS-entry stack: the caller hands the
+// ray to the cooperative walk.
+template <int KS, bool SORT, class Stk>
+__device__ __forceinline__ bool wide_step(const float4* __restrict__ tree, int& node, Stk& st, int& sp, v3 S, v3 inv,
+                                          float lim) {
+  const float4* q = tree + 7 * node;
+  const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5], rf = q[6];
+  const float alx[4] = {lx.x, lx.y, lx.z, lx.w}, ahx[4] = {hx.x, hx.y, hx.z, hx.w};
+  const float aly[4] = {ly.x, ly.y, ly.z, ly.w}, ahy[4] = {hy.x, hy.y, hy.z, hy.w};
+  const float alz[4] = {lz.x, lz.y, lz.z, lz.w}, ahz[4] = {hz.x, hz.y, hz.z, hz.w};
+  int ref[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
+  float key[4];  // hitAABB's distance of a hit child, +inf otherwise
+  int nh = 0;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    float t0;
+    const float dist = slab(S, inv, alx[c], aly[c], alz[c], ahx[c], ahy[c], ahz[c], &t0);
+    const bool hit = ref[c] != kNone && dist > 0.0f && !(t0 > lim);
+    key[c] = hit ? dist : __builtin_inff();
+    ref[c] = hit ? ref[c] : kNone;
+    nh += hit ? 1 : 0;
+  }
+  if (nh == 0) {
+    node = sp > 0 ? st.get(--sp) : kNone;
+    return true;
+  }
+  if (sp + nh - 1 > KS) return false;
+  if constexpr (SORT) {
+    // sorting network on (key, slot): 5 compare-exchanges; stable for equal keys (slot order kept)
+    auto cx = [&](int a, int b) __attribute__((always_inline)) {
+      const bool sw = key[b] < key[a];
+      const float ka = key[a], kb = key[b];
+      const int ra = ref[a], rb = ref[b];
+      key[a] = sw ? kb : ka;
+      key[b] = sw ? ka : kb;
+      ref[a] = sw ? rb : ra;
+      ref[b] = sw ? ra : rb;
+    };
+    cx(0, 1);
+    cx(2, 3);
+    cx(0, 2);
+    cx(1, 3);
+    cx(1, 2);
+    // hit children now lead in near-to-far order: push slots nh-1 .. 1, take slot 0
+#pragma unroll
+    for (int r = 3; r >= 1; --r)
+      if (r < nh) st.put(sp++, ref[r]);
+    node = ref[0];
+  } else {
+    // any order (any-hit): take the first hit slot, push the others
+    int first = kNone;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (ref[c] == kNone) continue;
+      if (first == kNone) first = ref[c];
+      else st.put(sp++, ref[c]);
+    }
+    node = first;
+  }
+  return true;
+}
+
 // Returns 1 occluded, 0 visible, -1 when the stack would overflow (the caller
 // re-traces that ray on the binary tree, whose depth the host bounds by kStack).
 template <int STRIDE, int KS = kStack>
@@ -552,7 +620,7 @@ __device__ int anyhit4(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, bo
   if (node < 0) { leaf = node; node = kNone; }
   while (node != kNone || leaf != kNone) {
     while (node >= 0) {
-      ++nvis;
+      nvis += PT_NODE_VISIT;
       const float4* q = sc.bvh4 + 7 * node;
       const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5], rf = q[6];
       const float alx[4] = {lx.x, lx.y, lx.z, lx.w}, ahx[4] = {hx.x, hx.y, hx.z, hx.w};

@@ -527,6 +527,7 @@ def test_lane_refill_is_result_preserving(gpu, scene_name, request):
     for refill in (100, 75, 0):
         r = _renderer(scene, W, H, mode="fast", run_taa=False, run_output=False)
         r.pass_path_tracing.set_uniform_int("trace_refill", refill)
+        r.pass_path_tracing.set_uniform_int("wide_bvh", 0)  # visit counts compare on one tree shape
         r.frame()
         stats.append(r.trace_stats())
         outs.append({k: gl.readback(r.planes()[k]) for k in ("color", "emission", "albedo")})
@@ -538,3 +539,32 @@ def test_lane_refill_is_result_preserving(gpu, scene_name, request):
             assert st[k] == stats[2][k], (k, stats)
         for k in ("shadow_visits", "bounce_visits"):
             assert abs(st[k] - stats[2][k]) <= 0.01 * stats[2][k], (k, stats)
+
+
+@pytest.mark.parametrize("scene_name", ["scene_small", "scene_cornell", "scene_nan"])
+def test_wide_tree_is_result_preserving(gpu, scene_name, request):
+    """The 4-wide form of the any-hit tree (pack_wide; wide_bvh = 1, an A/B switch) gives the binary walks' bits: lane
+    refill with 4 frames in flight, a moving camera, a tiny LDS stack budget is not needed here (overflows and exact
+    ties go to the cooperative walk, which the deep-tree tests exercise). Fewer node visits than the binary tree."""
+    gl = gpu
+    scene = request.getfixturevalue(scene_name)
+    W, H = 96, 64
+    outs, stats = [], []
+    for wide in (1, 0):
+        r = _renderer(scene, W, H, mode="fast", run_taa=False, run_output=False, frames_in_flight=4)
+        r.pass_path_tracing.set_uniform_int("wide_bvh", wide)
+        frames = []
+        for f in range(5):
+            if f == 3:
+                r.camera.orbit(2.0, 1.0)
+            r.frame()
+            frames.append({k: gl.readback(r.planes()[k]) for k in ("color", "emission", "albedo", "modulate")})
+        stats.append(r.trace_stats())
+        outs.append(frames)
+        r.close()
+    for fw, fb in zip(*outs):
+        for k in fw:
+            assert np.array_equal(fw[k].view(np.uint32), fb[k].view(np.uint32)), k
+    for k in ("primary_rays", "bounce_rays", "shadow_rays"):
+        assert stats[0][k] == stats[1][k], (k, stats)
+    print("visits wide / binary:", {k: (stats[0][k], stats[1][k]) for k in ("bounce_visits", "shadow_visits")})

@@ -3,7 +3,8 @@
 For every rank r of N: build the BandRenderer of r with the halo exchanges replaced by a recorder, time its frame
 (GPU time of the band + host issue time) and probe its per-row BVH visit counts. Then fit the cost model of
 make_band_renderer (T = a*visits + b*rows over the ranks), derive the balanced bounds and simulate again.
-The predicted N-GPU frame time is the slowest rank plus the halo exchanges (not simulated: reported as bytes).
+The predicted N-GPU frame time is the slowest rank, its halo exchanges stood in for by spin kernels of the modelled
+RCCL time on the band's back-end stream (fake_exchange; XLAT_US=0 XGBS=0 turns them off).
 usage: python tools/band_sim.py [N] [W] [H]"""
 import os
 import sys
@@ -38,14 +39,47 @@ class FakeDist:
         return None
 
 
+# Exchange stand-in (XLAT_US / XGBS, default 20 us + 50 GB/s; XLAT_US=0 and XGBS=0: none, the round-2 simulation):
+# each batch_isend_irecv the real halo_exchange would issue becomes a spin kernel on the stream the exchange runs on
+# (the band's SVGF back-end stream), lasting latency + max(bytes sent, bytes received) / bandwidth — RCCL P2P over
+# one xGMI link per neighbour, the sends and receives of a batch overlapping. The SVGF pass behind it waits for it
+# exactly as it waits for the real exchange.
+XLAT_US = float(os.environ.get("XLAT_US", "20"))
+XGBS = float(os.environ.get("XGBS", "50"))
+_CYC_PER_US = None
+
+
+def _spin(us):
+    """torch.cuda._sleep spins on the shader clock: calibrated once against HIP events."""
+    global _CYC_PER_US
+    if us <= 0:
+        return
+    if _CYC_PER_US is None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(1000)
+        e0.record()
+        torch.cuda._sleep(2_000_000)
+        e1.record()
+        e1.synchronize()
+        _CYC_PER_US = 2_000_000 / (e0.elapsed_time(e1) * 1e3)
+        print(f"spin calibration: {_CYC_PER_US:.0f} cycles/us", flush=True)
+    torch.cuda._sleep(int(us * _CYC_PER_US))
+
+
 def fake_exchange(items, plan, dist, group=None):
-    """Record the bytes the real exchange would send (rows this rank sends to the others, ghost-bounded)."""
+    """Record the bytes the real exchange would send and receive (ghost-bounded) and stand in for its time."""
+    sent_b = recv_b = 0
     for t, n in items:
         if plan.world == 1 or n <= 0:
             continue
-        sent = sum(max(0, min(b, plan.y1) - max(a, plan.y0)) for k in range(plan.world) if k != plan.rank
-                   for a, b in plan.need(k, n))
-        LOG.append(sent * t.shape[1] * t.shape[2] * 4)
+        row = t.shape[1] * t.shape[2] * 4
+        sent_b += row * sum(max(0, min(b, plan.y1) - max(a, plan.y0)) for k in range(plan.world) if k != plan.rank
+                            for a, b in plan.need(k, n))
+        recv_b += row * sum(max(0, min(b, plan.owned(k)[1]) - max(a, plan.owned(k)[0])) for k in range(plan.world)
+                            if k != plan.rank for a, b in plan.need(plan.rank, n))
+    if sent_b or recv_b:
+        LOG.append(sent_b)
+        _spin(XLAT_US + (max(sent_b, recv_b) / (XGBS * 1e3) if XGBS > 0 else 0.0))
 
 
 D.halo_exchange = fake_exchange
@@ -116,7 +150,7 @@ def report(tag, res):
               f"svgf {s['gpu'] - s['pp'].get('gbuffer', 0) - s['pp'].get('pathtrace', 0):.3f}  halo {s['nex']:.0f}x "
               f"{s['xbytes'] / 1e6:.2f} MB")
     mx = max(s["wall"] for s in res)
-    print(f"predicted frame (slowest rank, no exchange time): {mx:.3f} ms = {1e3 / mx:.1f} fps; "
+    print(f"predicted frame (slowest rank, exchanges {XLAT_US:g} us + bytes / {XGBS:g} GB/s): {mx:.3f} ms = {1e3 / mx:.1f} fps; "
           f"sum of rank GPU times {sum(s['gpu'] for s in res):.3f} ms; sum of rank walls "
           f"{sum(s['wall'] for s in res):.3f} ms")
     return mx
