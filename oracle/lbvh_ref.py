@@ -148,7 +148,8 @@ def lbvh(tri_enc: np.ndarray, leaf_n: int = 8, ploc_radius: int = 0):
 def ploc_top(leaves, r: int) -> np.ndarray:
     """BVHNode_encoded nodes of the tree PLOC (Meister & Bittner 2018) builds over the given leaves, as the kernels
     ploc_nn / ploc_flags / ploc_compact / ploc_emit do: each cluster picks, among the clusters within r positions,
-    the one whose merged box has the least half area ((dx*dy + dy*dz) + dz*dx in float32; ties: the smaller index),
+    the one whose merged box has the least half area ((dx*dy + dy*dz) + dz*dx in float32; ties: the sibling i ^ 1
+    first, then the smaller pair),
     mutual pairs merge into a new node at the lower position (children in position order), the array is compacted.
     Node ids: PLOC node k (creation order) -> 1 + (M - 2 - k), leaf L -> M + L; node 0 the dummy."""
     M = len(leaves)
@@ -160,7 +161,9 @@ def ploc_top(leaves, r: int) -> np.ndarray:
     while n > 1:
         idx = np.arange(n)
         best = np.full(n, np.inf, np.float32)
+        bs = np.ones(n, np.int64)
         bj = np.full(n, -1, np.int64)
+        # pairs ranked by (area, j != i ^ 1, min(i, j), max(i, j)) (kernels_bvh.hip ploc_nn)
         for off in range(-r, r + 1):  # ascending j: the first minimum wins
             if off == 0:
                 continue
@@ -174,8 +177,10 @@ def ploc_top(leaves, r: int) -> np.ndarray:
                     d = _gmax(ch, ch[jj]) - _gmin(cl, cl[jj])
                 a = (d[:, 0] * d[:, 1] + d[:, 1] * d[:, 2]) + d[:, 2] * d[:, 0]
             a = np.where(np.isnan(a), np.float32(np.inf), a)  # NaN boxes rank last
-            better = valid & ((bj < 0) | (a < best))
+            sj = (j != (idx ^ 1)).astype(np.int64)
+            better = valid & ((bj < 0) | (a < best) | ((a == best) & (sj < bs)))
             best = np.where(better, a, best)
+            bs = np.where(better, sj, bs)
             bj = np.where(better, j, bj)
         bj = np.where(bj < 0, idx, bj)
         mutual = (bj != idx) & (bj[bj] == idx)

@@ -1271,9 +1271,14 @@ int draw_pathtrace_batch(Pass** ps, int n) {
     SceneGPU* sb = nullptr;
     TRY(pt_params(ps[b], k[b], sb));
     if (b == 0) sg = sb;
+    // the batched traversal launches take their lane-refill share and visit budgets from passes[0] (pt_wf_setup
+    // sets k[b].refill and the budgets from these uniforms later): every pass of the batch must agree on them
+    const char* same[] = {"trace_refill", "shadow_budget", "closest_budget", "wide_bvh"};
+    bool agree = true;
+    for (const char* u : same) agree = agree && ui(ps[b], u, 0) == ui(ps[0], u, 0);
     if (sb != sg || k[b].W != k[0].W || k[b].y0 != k[0].y0 || k[b].y1 != k[0].y1 || k[b].max_depth != k[0].max_depth ||
-        k[b].refill != k[0].refill)
-      return err(PT_ERR_ARG, "a path-tracing batch needs one scene, size, band and depth");
+        !agree)
+      return err(PT_ERR_ARG, "a path-tracing batch needs one scene, size, band, depth and traversal settings");
     if (ui(ps[b], "pt_kernel", 0) != 0 || k[b].tile_stride != 1 || k[b].accumulate)
       return err(PT_ERR_ARG, "a path-tracing batch needs the wavefront path tracer on whole frames, no accumulation");
   }
@@ -1290,6 +1295,8 @@ int draw_pathtrace_batch(Pass** ps, int n) {
 int draw_raster(Pass* p) {
   Pass* src = p->raster_src ? pass_of(p->raster_src) : p;
   if (!src) return err(PT_ERR_STATE, "raster pass shares the triangles of a destroyed pass");
+  if (src != p && src->raster_src)  // the source became a sharer itself: its own raster scene is stale
+    return err(PT_ERR_STATE, "raster pass shares the triangles of a pass that now shares another pass's");
   const RasterScene& rs = src->raster;
   if (!rs.geom && rs.ntris > 0) return err(PT_ERR_STATE, "raster pass not bound");
   GBufParams k;

@@ -339,9 +339,12 @@ __global__ void __launch_bounds__(256) ploc_nn(const int* __restrict__ cnt, cons
   if (i >= n) return;
   const float4 lo = cbox[2 * i], hi = cbox[2 * i + 1];
   float best = __builtin_inff();
-  int bj = -1;
+  int bj = -1, bs = 1;
   const int j0 = max(0, i - r), j1 = min(n - 1, i + r);
-  for (int j = j0; j <= j1; ++j) {  // ascending j + strict <: ties go to the smallest j (the smaller pair)
+  // Pairs are ranked by (area, j != (i ^ 1), min(i, j), max(i, j)): a total order on pairs, so the globally best pair
+  // is mutual and every iteration merges; on runs of equal areas (coincident points, NaN boxes) the sibling pairs
+  // (2k, 2k + 1) rank first and are all mutual, so such a run halves per iteration instead of losing one cluster.
+  for (int j = j0; j <= j1; ++j) {  // ascending j: for equal (area, sibling flag) the smaller pair comes first
     if (j == i) continue;
     // the union in position order (lower position first), as ploc_compact merges: with NaN coordinates glm's
     // min/max depend on the operand order, and the area must be the same seen from either end of the pair
@@ -349,10 +352,12 @@ __global__ void __launch_bounds__(256) ploc_nn(const int* __restrict__ cnt, cons
     const float4 la = j < i ? l2 : lo, lb = j < i ? lo : l2, ha = j < i ? h2 : hi, hb = j < i ? hi : h2;
     float a = half_area(float4{gmin(la.x, lb.x), gmin(la.y, lb.y), gmin(la.z, lb.z), 0.0f},
                         float4{gmax(ha.x, hb.x), gmax(ha.y, hb.y), gmax(ha.z, hb.z), 0.0f});
-    a = a == a ? a : __builtin_inff();  // NaN boxes rank last: (area, index) stays a total order, so PLOC ends
-    if (bj < 0 || a < best) {
+    a = a == a ? a : __builtin_inff();  // NaN boxes rank last: the pair order stays total, so PLOC ends
+    const int sj = j != (i ^ 1);
+    if (bj < 0 || a < best || (a == best && sj < bs)) {
       best = a;
       bj = j;
+      bs = sj;
     }
   }
   nn[i] = bj < 0 ? i : bj;
@@ -596,14 +601,18 @@ int lbvh_build(LbvhWork& w, const float* tri, TriLayout lay, int n, int leaf_n, 
       if ((e = hipStreamSynchronize(s)) != hipSuccess) return (int)e;
       converged = host_cnt[2 * (it & 1)] <= 1;
     }
-    if (!converged) return (int)hipErrorUnknown;  // every iteration merges at least one pair: unreachable
-    hipLaunchKernelGGL(ploc_emit, dim3(gb), dim3(256), 0, s, cnt, n, nchild, nbox, leaf, leafbox, node_out);
-    if (tri_out)
-      hipLaunchKernelGGL(lbvh_reorder, dim3((unsigned)(((size_t)n * kTriFloats + 255) / 256)), dim3(256), 0, s, tri,
-                         kout, n, ibits, tri_out);
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return (int)e;
-    *nnodes = 2 * host_cnt[4];  // dummy + (M - 1) PLOC nodes + M leaves
-    return (int)hipGetLastError();
+    if (converged) {
+      hipLaunchKernelGGL(ploc_emit, dim3(gb), dim3(256), 0, s, cnt, n, nchild, nbox, leaf, leafbox, node_out);
+      if (tri_out)
+        hipLaunchKernelGGL(lbvh_reorder, dim3((unsigned)(((size_t)n * kTriFloats + 255) / 256)), dim3(256), 0, s, tri,
+                           kout, n, ibits, tri_out);
+      if ((e = hipStreamSynchronize(s)) != hipSuccess) return (int)e;
+      *nnodes = 2 * host_cnt[4];  // dummy + (M - 1) PLOC nodes + M leaves
+      return (int)hipGetLastError();
+    }
+    // past the iteration cap (every iteration merges at least one pair, and runs of equal areas halve, so only a
+    // pathological input gets here): the plain LBVH top over the same leaves, whose buffers PLOC left untouched
+    hipLaunchKernelGGL(lbvh_emit, dim3(ge), dim3(256), 0, s, n, leaf_n, child, range, keep, id, box, node_out);
   }
   if (tri_out)
     hipLaunchKernelGGL(lbvh_reorder, dim3((unsigned)(((size_t)n * kTriFloats + 255) / 256)), dim3(256), 0, s, tri,

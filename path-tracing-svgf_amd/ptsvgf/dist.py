@@ -207,10 +207,14 @@ def host_group(dist):
     interleave with the RCCL halo traffic). Collective: every rank creates it at the same point."""
     if dist.get_backend() == "gloo":
         return None
-    key = id(dist.group.WORLD)
-    if key not in _HOST_GROUP:
-        _HOST_GROUP[key] = dist.new_group(backend="gloo")
-    return _HOST_GROUP[key]
+    world = dist.group.WORLD
+    key = (id(world), dist.get_rank(), dist.get_world_size())
+    hit = _HOST_GROUP.get(key)
+    # the cache holds the WORLD object it was made for, so its id cannot be reused while cached; a re-initialised
+    # default group is a new object and gets a new gloo group
+    if hit is None or hit[0] is not world:
+        _HOST_GROUP[key] = hit = (world, dist.new_group(backend="gloo"))
+    return hit[1]
 
 
 def allreduce_motion(m: float, dist, group=None) -> float:

@@ -215,3 +215,22 @@ def test_raster_pass_share_rules(gpu, scene_small):
         b.draw()
     b.destroy()
     other.destroy()
+
+
+@pytest.mark.parametrize("case", ["point", "nan_object"])
+def test_gpu_ploc_degenerate_runs_converge(gpu, case):
+    """Runs of clusters with equal merge areas: 20 000 triangles collapsed to one point (every union
+    area 0), or a whole object of NaN vertices (every area inf) beside a normal one. Pairs rank by (area, j != i ^ 1,
+    min, max), so the sibling pairs of such a run are all mutual and it halves per iteration: the build completes
+    (no iteration cap) and equals the restatement bit for bit, at Renderer.rebuild_bvh's defaults (3, 32)."""
+    t = _random_tris(20000, seed=3)
+    if case == "point":
+        t[:, :9] = np.tile(np.float32([0.25, -0.5, 0.75]), 3)
+    else:
+        t[:12000, :9] = np.nan
+    (tri, nodes), ms = _build(gpu, t, 3, 32)
+    want_tri, want_nodes = L.lbvh(t, 3, 32)
+    assert np.array_equal(tri.view(np.uint32), want_tri.view(np.uint32))
+    assert np.array_equal(nodes.view(np.uint32), want_nodes.view(np.uint32))
+    print(f"{case}: {len(nodes)} nodes, build {ms:.3f} ms")
+    assert ms < 50.0  # tens of PLOC iterations, not thousands
