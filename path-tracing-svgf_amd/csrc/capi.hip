@@ -1224,6 +1224,7 @@ int pt_wf_setup(Pass* p, PTParams& k, SceneGPU* sg, const WFState& st) {
     // percent of the bounce / shadow lists traced by lane-refill waves: 75 pays with frames in flight (the renderer
     // sets it then), 0 (default) keeps the shortest single-frame latency
     k.refill = std::min(100, std::max(0, ui(p, "trace_refill", 0)));
+    k.refill_waves = std::max(0, ui(p, "refill_waves", 0));
     const int ntiles = wf_subset_tiles(k.W, std::max(0, k.y1 - k.y0), k.tile_stride, k.tile_offset);  // wf_primary's grid
     TRY(tile_order_begin(p, ntiles, &k.tiles));
     // primary rays by tile-binned rasterisation of the reference leaves (default; 0 = the per-pixel walk)

@@ -608,17 +608,20 @@ constexpr int kResidentWaves = PT_RESIDENT_WAVES;
 #ifndef PT_REFILL_DIV
 #define PT_REFILL_DIV 1
 #endif
-__device__ __forceinline__ int refill_rounds(int total) {
-  const int r = total / (64 * kResidentWaves * PT_REFILL_DIV);
+// `waves`: the resident waves the launch may count on (0: the chip, kResidentWaves). A band renderer's launches are
+// small and share the chip with the other frames in flight: sized for the whole chip they get one round per wave
+// (no refill at all); sized for a share of it they keep refilling.
+__device__ __forceinline__ int refill_rounds(int total, int waves) {
+  const int r = total / (64 * (waves > 0 ? waves : kResidentWaves) * PT_REFILL_DIV);
   return r < 1 ? 1 : (r > kRefillRounds ? kRefillRounds : r);
 }
-__device__ __forceinline__ WaveQueue refill_queue(int* heads, int total, int big_pct) {
+__device__ __forceinline__ WaveQueue refill_queue(int* heads, int total, int big_pct, int waves) {
   WaveQueue q{heads, total, (int)(blockIdx.x & 7), 0u, 0, 0};
   if (PT_REFILL_QUEUE) {
     q.grab();
   } else {
     const int wave = blockIdx.x * (kTB / 64) + (threadIdx.x >> 6);
-    const int R = refill_rounds(total);
+    const int R = refill_rounds(total, waves);
     const int big = R > 1 ? (int)((long long)total * big_pct / 100) / (64 * R) : 0;  // waves with big chunks
     if (wave < big) {
       q.next = wave * 64 * R;
@@ -661,7 +664,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
     for (int c = 0; c < kPointBins; ++c) tot[b] += seg_total(lb.counts[b] + (1 + c) * kSeg);
     total += tot[b];
   }
-  WaveQueue q = refill_queue(heads, total, p.refill);
+  WaveQueue q = refill_queue(heads, total, p.refill, p.refill_waves);
   if (q.next >= q.end) return;
   const SceneDev sc = anyhit_scene(p.scene);
   const unsigned long long below = (1ull << lane) - 1ull;
@@ -806,7 +809,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTP
     for (int c = 0; c < kLiveBins * kSeg; ++c) tot[b] += lb.counts[b][c];
     total += tot[b];
   }
-  WaveQueue q = refill_queue(heads, total, p.refill);
+  WaveQueue q = refill_queue(heads, total, p.refill, p.refill_waves);
   if (q.next >= q.end) return;
   const unsigned long long below = (1ull << lane) - 1ull;
   auto st = ray_stack<kTB, KS, DEEP>(stk + threadIdx.x, p, 0);

@@ -194,6 +194,7 @@ struct PTParams {
   int closest_tree;     // closest-hit rays walk the SAH tree over the reference leaves (closest_hit, pt_shading.h)
   int stack_need;       // deepest interior level of the binary BVH (selects the LDS stack size)
   int refill;           // > 0: percent of each bounce/shadow list traced by lane-refill waves (kernels_wavefront.hip)
+  int refill_waves;     // resident waves a refill launch is sized for (0: the whole chip, kResidentWaves)
   float sobol_u[4], sobol_v[4];  // sobolVec2(frameCounter+1, b): uniform across pixels
   WFState wf;
   // optional bound for the primary rays from this frame's G-buffer (world position + normal/linearZ planes,

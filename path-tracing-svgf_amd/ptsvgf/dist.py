@@ -51,6 +51,7 @@ TAA_NEIGHBOURS = 2  # rows of the TAA 3x3 neighbourhood: +-1 texel, plus the LIN
 GHOST = 96        # default stored rows either side of a band (storage only); motion up to GHOST - 3 rows per frame
 MIN_BAND_ROWS = 16
 BAND_VISIT_BUDGET = 256  # shadow / closest-hit visits before a band's ray goes to the cooperative walk
+BAND_REFILL_WAVES = 1280  # resident waves a band's lane-refill launch is sized for (the chip: 5120)
 
 # stage -> ((plane, rows), ...) exchanged before that stage; rows: int, or "reproj" / "reproj_nd" (set from this
 # frame's motion bound) / "nd" (the widest a-trous halo of the configured iterations)
@@ -279,6 +280,10 @@ class BandRenderer:
             # launches are full, keeps them off)
             self.pass_path_tracing.set_uniform_int("shadow_budget", BAND_VISIT_BUDGET)
             self.pass_path_tracing.set_uniform_int("closest_budget", BAND_VISIT_BUDGET)
+            # a band's refill launches are small and share the chip with the other frames in flight: sized for the
+            # whole chip they get one chunk per wave (no refill); sized for a quarter of it they keep refilling
+            # (8 simulated bands, same box: slowest non-edge band 1.35 -> 1.27 ms, profiles/r03/band_sim_r03.log)
+            self.pass_path_tracing.set_uniform_int("refill_waves", BAND_REFILL_WAVES)
 
     def _after_gbuffer(self, b: int, stream) -> None:
         """The G-buffer of set b was issued on `stream`: fetch its motion bound behind it (no wait here)."""

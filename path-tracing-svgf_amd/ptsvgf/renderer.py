@@ -184,10 +184,16 @@ class Renderer:
             import torch  # streams and events are torch plumbing (the kernels are the library's)
 
             self._streams = [torch.cuda.Stream() for _ in range(self.K)]
-            self._gstreams = [torch.cuda.Stream() for _ in range(self.K)]  # G-buffer beside the path tracer
-            # A/B switch, off by default: with K frames in flight the extra streams measured slower
+            # A/B switch, off by default: with K frames in flight the extra streams measured slower.
+            # Its streams exist only when it is on: every stream beyond the process's hardware queues
+            # (GPU_MAX_HW_QUEUES) shares a queue, in order, with another stream.
             self._gfork = os.environ.get("PTSVGF_GBUFFER_FORK", "0") != "0"
-            self._back = torch.cuda.Stream()
+            self._gstreams = [torch.cuda.Stream() for _ in range(self.K)] if self._gfork else None
+            # the SVGF back end is a chain of short launches (and, on bands, exchanges) beside the front ends' long
+            # traversal launches: on a high-priority queue its kernels take CUs as soon as waves retire instead of
+            # queueing behind resident traversal waves (PTSVGF_BACK_PRIORITY=0: normal priority, A/B)
+            hi = os.environ.get("PTSVGF_BACK_PRIORITY", "1") != "0"
+            self._back = torch.cuda.Stream(priority=-1) if hi else torch.cuda.Stream()
             self._slot_free = [None] * self.K  # event: SVGF of the frame that last used the slot is done
             self._fe_prev = None
 

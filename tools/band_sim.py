@@ -110,12 +110,24 @@ def sim_rank(rk, bounds, probe=False, K=30):
     torch.cuda.synchronize()
     LOG.clear()
     torch.cuda.synchronize()
+    waits = []  # host time blocked on the G-buffer motion bound (BandRenderer._motion)
+    orig_motion = D.BandRenderer._motion
+
+    def timed_motion(self):
+        tw = time.perf_counter()
+        orig_motion(self)
+        waits.append(time.perf_counter() - tw)
+    D.BandRenderer._motion = timed_motion
     t0 = time.perf_counter()
+    c0 = time.process_time()
     for _ in range(K):
         r.frame()
     issue = (time.perf_counter() - t0) / K
+    cpu = (time.process_time() - c0) / K
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / K
+    D.BandRenderer._motion = orig_motion
+    wait = sum(waits) / K
     xbytes = sum(LOG) / K
     nex = len(LOG) / K
     counts = None
@@ -139,14 +151,14 @@ def sim_rank(rk, bounds, probe=False, K=30):
     y0, y1 = r.plan.y0, r.plan.y1
     r.close()
     return dict(y0=y0, y1=y1, wall=wall * 1e3, issue=issue * 1e3, gpu=pp["frame_sum_ms"], pp=pp, counts=counts,
-                xbytes=xbytes, nex=nex)
+                xbytes=xbytes, nex=nex, cpu=cpu * 1e3, wait=wait * 1e3)
 
 
 def report(tag, res):
     print(f"--- {tag}: N={N} {W}x{H}")
     for rk, s in enumerate(res):
         print(f"rank {rk}: rows {s['y0']}..{s['y1']} ({s['y1'] - s['y0']}) wall {s['wall']:.3f} ms gpu {s['gpu']:.3f} "
-              f"issue {s['issue']:.3f}  gbuf {s['pp'].get('gbuffer', 0):.3f} pt {s['pp'].get('pathtrace', 0):.3f} "
+              f"issue {s['issue']:.3f} (host cpu {s['cpu']:.3f}, motion wait {s['wait']:.3f})  gbuf {s['pp'].get('gbuffer', 0):.3f} pt {s['pp'].get('pathtrace', 0):.3f} "
               f"svgf {s['gpu'] - s['pp'].get('gbuffer', 0) - s['pp'].get('pathtrace', 0):.3f}  halo {s['nex']:.0f}x "
               f"{s['xbytes'] / 1e6:.2f} MB")
     mx = max(s["wall"] for s in res)
