@@ -124,6 +124,27 @@ class BandPlan:
     def owned(self, k: int) -> tuple:
         return self.bounds[k], self.bounds[k + 1]
 
+    def halo_parts(self, n: int) -> list:
+        """The point-to-point transfers of an n-row halo, in the order every rank issues them (so sends and
+        receives pair up): (send?, first row, end row, peer) per part, peers ascending, this rank's sends to a peer
+        before its receives from it. Pure function of the plan and n; cached (a frame issues it per SVGF stage)."""
+        cache = self.__dict__.setdefault("_halo_parts", {})
+        if n not in cache:
+            me, mine, parts = self.rank, self.owned(self.rank), []
+            for k in range(self.world):
+                if k == me:
+                    continue
+                for part in self.need(k, n):       # rows of my band that rank k reads
+                    a, b = _meet(mine, part)
+                    if b > a:
+                        parts.append((True, a, b, k))
+                for part in self.need(me, n):      # rows of rank k's band that I read
+                    a, b = _meet(self.owned(k), part)
+                    if b > a:
+                        parts.append((False, a, b, k))
+            cache[n] = parts
+        return cache[n]
+
     def need(self, k: int, n: int) -> tuple:
         """Rows rank k reads outside its band for a halo of n rows: ((above), (below)), clipped to the frame."""
         a, b = self.owned(k)
@@ -174,21 +195,10 @@ def halo_exchange(items, plan: BandPlan, dist, group=None) -> None:
         for (t, _), (h, _) in zip(items, host):
             t.copy_(h)
         return
-    me = plan.rank
-    mine = plan.owned(me)
     ops = []
     for t, n in items:
-        for k in range(plan.world):  # same (tensor, peer) order on every rank: sends and receives pair up in order
-            if k == me:
-                continue
-            for part in plan.need(k, n):       # rows of my band that rank k reads
-                a, b = _meet(mine, part)
-                if b > a:
-                    ops.append(dist.P2POp(dist.isend, t[a - plan.row0:b - plan.row0], k, group))
-            for part in plan.need(me, n):      # rows of rank k's band that I read
-                a, b = _meet(plan.owned(k), part)
-                if b > a:
-                    ops.append(dist.P2POp(dist.irecv, t[a - plan.row0:b - plan.row0], k, group))
+        for send, a, b, k in plan.halo_parts(n):
+            ops.append(dist.P2POp(dist.isend if send else dist.irecv, t[a - plan.row0:b - plan.row0], k, group))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()

@@ -73,10 +73,11 @@ def fake_exchange(items, plan, dist, group=None):
         if plan.world == 1 or n <= 0:
             continue
         row = t.shape[1] * t.shape[2] * 4
-        sent_b += row * sum(max(0, min(b, plan.y1) - max(a, plan.y0)) for k in range(plan.world) if k != plan.rank
-                            for a, b in plan.need(k, n))
-        recv_b += row * sum(max(0, min(b, plan.owned(k)[1]) - max(a, plan.owned(k)[0])) for k in range(plan.world)
-                            if k != plan.rank for a, b in plan.need(plan.rank, n))
+        for send, a, b, _ in plan.halo_parts(n):  # the transfers dist.halo_exchange would issue
+            if send:
+                sent_b += row * (b - a)
+            else:
+                recv_b += row * (b - a)
     if sent_b or recv_b:
         LOG.append(sent_b)
         _spin(XLAT_US + (max(sent_b, recv_b) / (XGBS * 1e3) if XGBS > 0 else 0.0))
