@@ -1423,7 +1423,8 @@ int draw_svgf(Pass* p, int kind) {
     k.phi_normal = uf(p, "gPhiNormal", 0.0f);
     // production tiled kernel: per-tile surface flags, derived once per G-buffer from its depth-fwidth plane
     const int si = k.step == 1 ? 0 : k.step == 2 ? 1 : k.step == 4 ? 2 : k.step == 8 ? 3 : k.step == 16 ? 4 : -1;
-    if (!ui(p, "exact", 0) && ui(p, "atrous_variant", 0) == 0 && ui(p, "atrous_tile_flags", 1) && k.fwidth.aux &&
+    const int av = ui(p, "atrous_variant", 0);
+    if (!ui(p, "exact", 0) && av == 0 && ui(p, "atrous_tile_flags", 1) && k.fwidth.aux &&
         si >= 0 && y1 > y0) {
       Texture* ft = sampler(p, "gNormalDepthFwidth");
       const size_t nb = ptk::atrous_flag_bytes(k.W, y0, y1);

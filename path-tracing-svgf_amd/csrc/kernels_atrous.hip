@@ -236,16 +236,88 @@ __global__ void __launch_bounds__(256) atrous_step_kernel(AtrousParams p) {
 // NX: 64-column strips per tile (waves side by side). The halo costs 4S staged columns per tile, so the widest
 // step stages twice its output with NX = 1; S = 16 uses NX = 2 (128 columns, 1024 threads, 74 KB of LDS: measured
 // 100 -> 91.5 us on the 4K bench inputs, tools/exp_atrous_real.hip), the other steps are fastest with NX = 1.
-constexpr int kTileRows = kAtrousTJ;   // TJ
-constexpr int kTileWaves = 8;  // per 64-column strip; one pixel per thread
-template <int S> constexpr int tile_nx() { return S >= 16 ? 2 : 1; }
+template <int S> constexpr int tile_nx() { return atrous_tile_nx(S); }
+template <int S> constexpr int tile_tj() { return atrous_tile_tj(S); }  // tile rows = waves per 64-column strip
 
 __device__ __forceinline__ bool aux_flag(float a) { return (__float_as_uint(a) >> 31) != 0; }
 
+// One output pixel of the tiled kernels: its constants and accumulators, and one tap (atrous_taps' arithmetic and tap
+// order, so every tiled form is bit-identical to the step kernel). FLAT: phiIllumination == 0 (see atrous_taps).
+struct TapPixel {
+  float4 nd;
+  float lc, wLr, wLg, wLb, cL, sumW;
+  float kDr[5];
+  f2v s01, s23;
+  bool flat;
+  __device__ __forceinline__ void init(float4 ic, float4 nd_, float fwz, float phi_color, int S) {
+    const float LOG2E = 1.4426950408889634f;
+    nd = nd_;
+    lc = (0.2125f * ic.x + 0.7154f * ic.y) + 0.0721f * ic.z;
+    const float phiL = phi_color * __builtin_sqrtf(fmaxf(0.0f, 1e-10f + ic.w));
+    flat = !(phiL > 0.0f);
+    const float kL = LOG2E / phiL;
+    const float kD = LOG2E / (fmaxf(fwz, 1e-8f) * (float)S);
+    kDr[0] = kD;
+    kDr[1] = kD * 0.70710678f;
+    kDr[2] = kD * 0.5f;
+    kDr[3] = kD * 0.44721360f;
+    kDr[4] = kD * 0.35355339f;
+    wLr = 0.2125f * kL;
+    wLg = 0.7154f * kL;
+    wLb = 0.0721f * kL;
+    cL = -(lc * kL);
+    sumW = 1.0f;
+    s01 = f2v{ic.x, ic.y};
+    s23 = f2v{ic.z, ic.w};
+  }
+  template <bool FLAT>
+  __device__ __forceinline__ void tap(float4 ip, float4 q, int xx, int yy, float phi_normal) {
+    const int r2 = xx * xx + yy * yy;
+    const float kDl = r2 == 1 ? kDr[0] : r2 == 2 ? kDr[1] : r2 == 4 ? kDr[2] : r2 == 5 ? kDr[3] : kDr[4];
+    const int ax = xx < 0 ? -xx : xx, ay = yy < 0 ? -yy : yy;
+    const float kern = (ax == 0 ? 1.0f : ax == 1 ? 2.0f / 3.0f : 1.0f / 6.0f) *
+                       (ay == 0 ? 1.0f : ay == 1 ? 2.0f / 3.0f : 1.0f / 6.0f);
+    const float dn = fminf(fmaxf(__builtin_fmaf(nd.z, q.z, __builtin_fmaf(nd.y, q.y, nd.x * q.x)), 0.0f), 1.0f);
+    float a;
+    if (FLAT) {
+      const float lp = (0.2125f * ip.x + 0.7154f * ip.y) + 0.0721f * ip.z;
+      a = lp == lc ? fabsf(nd.w - q.w) * kDl : __builtin_inff();
+    } else {
+      const float tl = __builtin_fmaf(ip.z, wLb, __builtin_fmaf(ip.y, wLg, __builtin_fmaf(ip.x, wLr, cL)));
+      a = __builtin_fmaf(fabsf(nd.w - q.w), kDl, fabsf(tl));
+    }
+    const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(phi_normal, __builtin_amdgcn_logf(dn), -a)) * kern;
+    sumW += w;
+    s01 = __builtin_elementwise_fma(f2v{w, w}, f2v{ip.x, ip.y}, s01);
+    s23 = __builtin_elementwise_fma(f2v{w, w * w}, f2v{ip.z, ip.w}, s23);
+  }
+  // the 24 taps of a window whose top-left texel is Li / Ln (row stride C, column step S); EDGE: skip taps outside
+  // the frame for the pixel at (x, y)
+  template <bool FLAT, bool EDGE, int S, int C>
+  __device__ __forceinline__ void window(const float4* Li, const float4* Ln, int x, int y, int W, int H,
+                                         float phi_normal) {
+#pragma unroll
+    for (int yy = -2; yy <= 2; ++yy) {
+      if (EDGE && (y + yy * S < 0 || y + yy * S >= H)) continue;
+#pragma unroll
+      for (int xx = -2; xx <= 2; ++xx) {
+        if (xx == 0 && yy == 0) continue;
+        if (EDGE && (x + xx * S < 0 || x + xx * S >= W)) continue;
+        const int o = (yy + 2) * C + (xx + 2) * S;
+        tap<FLAT>(Li[o], Ln[o], xx, yy, phi_normal);
+      }
+    }
+  }
+  __device__ __forceinline__ float4 result() const {
+    const float inv = 1.0f / sumW;
+    return float4{s01.x * inv, s01.y * inv, s23.x * inv, s23.y * (inv * inv)};
+  }
+};
+
 template <int S, bool AUX>
-__global__ void __launch_bounds__(64 * kTileWaves * tile_nx<S>()) atrous_tile_kernel(AtrousParams p) {
+__global__ void __launch_bounds__(64 * tile_tj<S>() * tile_nx<S>()) atrous_tile_kernel(AtrousParams p) {
   constexpr int NX = tile_nx<S>();
-  constexpr int TJ = kTileRows, NW = kTileWaves * NX, R = TJ + 4, C = 64 * NX + 4 * S, NT = 64 * NW;
+  constexpr int TJ = tile_tj<S>(), NW = TJ * NX, R = TJ + 4, C = 64 * NX + 4 * S, NT = 64 * NW;
   __shared__ float4 LI[R * C];
   __shared__ float4 LN[R * C];
   const int W = p.illum.W, row0 = p.illum.row0;
@@ -313,71 +385,28 @@ __global__ void __launch_bounds__(64 * kTileWaves * tile_nx<S>()) atrous_tile_ke
     *out = ic;
     return;
   }
-  const float4 nd = Ln[2 * C + 2 * S];
   const bool edge =
       x0 - 2 * S < 0 || x0 + 64 * NX - 1 + 2 * S >= p.W || ybase - 2 * S < 0 || ybase + S * (TJ + 1) >= p.H;
-  const float LOG2E = 1.4426950408889634f;
-  const float lc = (0.2125f * ic.x + 0.7154f * ic.y) + 0.0721f * ic.z;
-  const float phiL = p.phi_color * __builtin_sqrtf(fmaxf(0.0f, 1e-10f + ic.w));
-  const float kL = LOG2E / phiL;
-  const float kD = LOG2E / (fmaxf(fwz, 1e-8f) * (float)S);
-  const float kDr[5] = {kD, kD * 0.70710678f, kD * 0.5f, kD * 0.44721360f, kD * 0.35355339f};
-  float sumW = 1.0f;
-  f2v s01 = {ic.x, ic.y}, s23 = {ic.z, ic.w};
+  TapPixel px;
+  px.init(ic, Ln[2 * C + 2 * S], fwz, p.phi_color, S);
   // EDGE = false: the block's dilated footprint lies inside the frame, so the 24 taps are straight-line code the
   // compiler schedules freely (LDS reads of later taps issued ahead of earlier taps' arithmetic). A per-tap `edge`
   // test in that path compiles to an exec-masked branch per tap, each behind its own LDS wait (the r02 kernel).
-  auto taps = [&](auto flat_tag, auto edge_tag) __attribute__((always_inline)) {
-    constexpr bool FLAT = decltype(flat_tag)::value, EDGE = decltype(edge_tag)::value;
-    const float wLr = 0.2125f * kL, wLg = 0.7154f * kL, wLb = 0.0721f * kL, cL = -(lc * kL);
-#pragma unroll
-    for (int yy = -2; yy <= 2; ++yy) {
-      if (EDGE && edge && (y + yy * S < 0 || y + yy * S >= p.H)) continue;
-#pragma unroll
-      for (int xx = -2; xx <= 2; ++xx) {
-        if (xx == 0 && yy == 0) continue;
-        if (EDGE && edge && (x + xx * S < 0 || x + xx * S >= p.W)) continue;
-        const int r2 = xx * xx + yy * yy;
-        const float kDl = r2 == 1 ? kDr[0] : r2 == 2 ? kDr[1] : r2 == 4 ? kDr[2] : r2 == 5 ? kDr[3] : kDr[4];
-        const int ax = xx < 0 ? -xx : xx, ay = yy < 0 ? -yy : yy;
-        const float kern = (ax == 0 ? 1.0f : ax == 1 ? 2.0f / 3.0f : 1.0f / 6.0f) *
-                           (ay == 0 ? 1.0f : ay == 1 ? 2.0f / 3.0f : 1.0f / 6.0f);
-        const int o = (yy + 2) * C + (xx + 2) * S;
-        const float4 ip = Li[o];
-        const float4 q = Ln[o];
-        const float dn =
-            fminf(fmaxf(__builtin_fmaf(nd.z, q.z, __builtin_fmaf(nd.y, q.y, nd.x * q.x)), 0.0f), 1.0f);
-        float a;
-        if (FLAT) {
-          const float lp = (0.2125f * ip.x + 0.7154f * ip.y) + 0.0721f * ip.z;
-          a = lp == lc ? fabsf(nd.w - q.w) * kDl : __builtin_inff();
-        } else {
-          const float tl = __builtin_fmaf(ip.z, wLb, __builtin_fmaf(ip.y, wLg, __builtin_fmaf(ip.x, wLr, cL)));
-          a = __builtin_fmaf(fabsf(nd.w - q.w), kDl, fabsf(tl));
-        }
-        const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(p.phi_normal, __builtin_amdgcn_logf(dn), -a)) * kern;
-        sumW += w;
-        s01 = __builtin_elementwise_fma(f2v{w, w}, f2v{ip.x, ip.y}, s01);
-        s23 = __builtin_elementwise_fma(f2v{w, w * w}, f2v{ip.z, ip.w}, s23);
-      }
-    }
-  };
-  if (__builtin_expect(phiL > 0.0f, 1)) {
-    if (__builtin_expect(!edge, 1)) taps(std::false_type{}, std::false_type{});
-    else taps(std::false_type{}, std::true_type{});
+  if (__builtin_expect(!px.flat, 1)) {
+    if (__builtin_expect(!edge, 1)) px.window<false, false, S, C>(Li, Ln, x, y, p.W, p.H, p.phi_normal);
+    else px.window<false, true, S, C>(Li, Ln, x, y, p.W, p.H, p.phi_normal);
   } else {
-    taps(std::true_type{}, std::true_type{});  // FLAT (phiIllumination == 0): rare, edge tested per tap
+    px.window<true, true, S, C>(Li, Ln, x, y, p.W, p.H, p.phi_normal);  // FLAT: rare
   }
-  const float inv = 1.0f / sumW;
-  *out = float4{s01.x * inv, s01.y * inv, s23.x * inv, s23.y * (inv * inv)};
+  *out = px.result();
 }
 
-// Tile flags of the five step sizes (atrous_tile_kernel's tiles: S = 1 << si, NX = tile_nx<S>(), TJ rows of one
+// Tile flags of the five step sizes (atrous_tile_kernel's tiles: S = 1 << si, NX = tile_nx<S>(), TJ = tile_tj<S>() rows of one
 // residue class): byte (g * S + b) * NXT + bx of step si is 1 iff an owned pixel of that tile is a surface pixel
 // (the depth-fwidth plane's sign bit clear). One wave per 64 columns of a row; a ballot, then one byte store per step.
 static int tiles_of(int S, int W, int y0, int y1) {
-  const int nx = S >= 16 ? 2 : 1, nxt = (W + 64 * nx - 1) / (64 * nx);
-  const int groups = (y1 - y0 + S * kTileRows - 1) / (S * kTileRows);
+  const int nx = atrous_tile_nx(S), nxt = (W + 64 * nx - 1) / (64 * nx), tj = atrous_tile_tj(S);
+  const int groups = (y1 - y0 + S * tj - 1) / (S * tj);
   return nxt * groups * S;
 }
 size_t atrous_flag_offset(int si, int W, int y0, int y1) {
@@ -407,11 +436,11 @@ int atrous_tile_flags(const Plane& fw, int W, int y0, int y1, unsigned char* fla
 
 template <int S>
 static void launch_tile_s(const AtrousParams& p, bool aux, hipStream_t s) {
-  constexpr int NX = tile_nx<S>();
-  const int groups = (p.y1 - p.y0 + S * kTileRows - 1) / (S * kTileRows);
+  constexpr int NX = tile_nx<S>(), TJ = tile_tj<S>();
+  const int groups = (p.y1 - p.y0 + S * TJ - 1) / (S * TJ);
   dim3 grid((p.W + 64 * NX - 1) / (64 * NX), groups * S);
-  if (aux) hipLaunchKernelGGL((atrous_tile_kernel<S, true>), grid, dim3(64 * kTileWaves * NX), 0, s, p);
-  else hipLaunchKernelGGL((atrous_tile_kernel<S, false>), grid, dim3(64 * kTileWaves * NX), 0, s, p);
+  if (aux) hipLaunchKernelGGL((atrous_tile_kernel<S, true>), grid, dim3(64 * TJ * NX), 0, s, p);
+  else hipLaunchKernelGGL((atrous_tile_kernel<S, false>), grid, dim3(64 * TJ * NX), 0, s, p);
 }
 
 static bool same_geometry(const AtrousParams& p) {

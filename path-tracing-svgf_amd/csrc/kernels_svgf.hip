@@ -67,7 +67,15 @@ __device__ __forceinline__ float edge_weight(float zc, float zp, float phiDepth,
 }
 
 // ------------------------------------------------------------ reproject ---
-__global__ void __launch_bounds__(256) reproject_kernel(ReprojParams p) {
+#ifndef PT_REPROJ_WAVES
+#define PT_REPROJ_WAVES 0  // waves/SIMD reproject_kernel is compiled for (0: the compiler's choice, 94 VGPRs = 5 waves)
+#endif
+#if PT_REPROJ_WAVES > 0
+#define PT_REPROJ_ATTR __attribute__((amdgpu_waves_per_eu(PT_REPROJ_WAVES)))
+#else
+#define PT_REPROJ_ATTR
+#endif
+__global__ void __launch_bounds__(256) PT_REPROJ_ATTR reproject_kernel(ReprojParams p) {
   int x = blockIdx.x * 16 + (threadIdx.x & 15);
   int y = p.y0 + blockIdx.y * 16 + (threadIdx.x >> 4);
   if (x >= p.W || y >= p.y1) return;

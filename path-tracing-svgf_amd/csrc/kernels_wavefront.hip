@@ -1037,7 +1037,15 @@ __device__ __forceinline__ bool zero_bits(v3 a) {  // all three exactly +0.0f
 // sample the next direction and prepare both NEE contributions (:948-968).
 // Shadow rays whose verdict cannot change a bit of the result (a light below the
 // surface: zero BRDF) are not queued; the others go to one compacted list.
-__global__ void __launch_bounds__(256) wf_shade(PTParams p, int bounce, const int* __restrict__ list_in,
+#ifndef PT_SHADE_WAVES
+#define PT_SHADE_WAVES 0  // waves/SIMD wf_shade is compiled for (0: the compiler's choice, 93 VGPRs = 5 waves)
+#endif
+#if PT_SHADE_WAVES > 0
+#define PT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(PT_SHADE_WAVES)))
+#else
+#define PT_SHADE_ATTR
+#endif
+__global__ void __launch_bounds__(256) PT_SHADE_ATTR wf_shade(PTParams p, int bounce, const int* __restrict__ list_in,
                                                 const int* __restrict__ counts_in, int* __restrict__ list_out,
                                                 int* __restrict__ counts_out, int* __restrict__ shadow_out,
                                                 int* __restrict__ shadow_counts, int cap) {

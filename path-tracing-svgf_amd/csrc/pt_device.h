@@ -256,14 +256,27 @@ struct AtrousParams {
   float phi_color, phi_normal;
   const unsigned char* tile_any;  // tiled kernel: per-tile "holds a surface pixel" flags of this step, or null
 };
-// Tiles of the tiled a-trous (kernels_atrous.hip): 64 * NX columns (NX = 2 for S >= 16) x kAtrousTJ rows of one
-// residue class mod S; tile (g, b, bx) of step S has byte (g * S + b) * NXT + bx in that step's flags.
-constexpr int kAtrousTJ = 8;
+// Tiles of the tiled a-trous (kernels_atrous.hip): 64 * NX columns x TJ rows of one residue class mod S, one wave
+// per 64-column strip of a tile row (64 * TJ * NX <= 1024 threads); tile (g, b, bx) of step S has byte
+// (g * S + b) * NXT + bx in that step's flags. The staged footprint is (TJ + 4) x (64 NX + 4S) texels for TJ x 64 NX
+// pixels. PT_ATROUS_TJ (rows for S <= 8) / PT_ATROUS_TJ16, PT_ATROUS_NX16 (S = 16) choose the shape (A/B).
+#ifndef PT_ATROUS_TJ
+#define PT_ATROUS_TJ 8
+#endif
+#ifndef PT_ATROUS_TJ16
+#define PT_ATROUS_TJ16 8
+#endif
+#ifndef PT_ATROUS_NX16
+#define PT_ATROUS_NX16 2
+#endif
+__host__ __device__ constexpr int atrous_tile_tj(int S) { return S >= 16 ? PT_ATROUS_TJ16 : PT_ATROUS_TJ; }
+__host__ __device__ constexpr int atrous_tile_nx(int S) { return S >= 16 ? PT_ATROUS_NX16 : 1; }
+static_assert(64 * PT_ATROUS_TJ <= 1024 && 64 * PT_ATROUS_TJ16 * PT_ATROUS_NX16 <= 1024, "a-trous tile too large");
 __device__ __forceinline__ void atrous_mark_tiles(unsigned char* flags, const int* off, int W, int x, int r) {
 #pragma unroll
   for (int si = 0; si < 5; ++si) {
-    const int S = 1 << si, nx = S >= 16 ? 2 : 1, nxt = (W + 64 * nx - 1) / (64 * nx);
-    const int g = r / (S * kAtrousTJ), b = r % S;
+    const int S = 1 << si, nx = atrous_tile_nx(S), nxt = (W + 64 * nx - 1) / (64 * nx);
+    const int g = r / (S * atrous_tile_tj(S)), b = r % S;
     flags[off[si] + (size_t)(g * S + b) * nxt + x / (64 * nx)] = 1;
   }
 }

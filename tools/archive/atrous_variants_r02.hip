@@ -461,3 +461,152 @@ int launch_atrous_pair(const AtrousParams& p, hipStream_t s) {
   }
   return (int)hipGetLastError();
 }
+
+
+// ---------------------------------------------------------------------------------------------------------------
+// Round 3: atrous_rows2_kernel (atrous_variant = 3), two tile rows per thread sharing their windows' LDS reads
+// (30 texel reads for 48 taps). Bit-identical to the step kernel (tests/test_gpu_atrous.py at the time), but slower:
+// 4K default view 74.4 vs 69.2 us, surface view 150.0 vs 144.5 us (79 VGPRs: 6 waves/SIMD against 8; the kernel is
+// VALU/latency-bound there, not LDS-bound). Uses kernels_atrous.hip's TapPixel.
+// Two pixels per thread (atrous_variant = 3): the thread owns tile rows 2k and 2k + 1 of one column, whose 5 x 5
+// windows share 4 of their 5 rows, so each of the 6 x 5 staged texels under the pair is read from LDS once and
+// applied to both pixels (30 texel reads for 48 taps instead of 48): 37.5 % fewer LDS reads, the same VALU work.
+// Per pixel the taps are applied in the same order with the same arithmetic (TapPixel): bit-identical to the step
+// kernel. Border tiles and FLAT pixels take the per-pixel windows of atrous_tile_kernel. Same tile geometry and
+// staging as atrous_tile_kernel (half the threads), so the same per-tile surface flags.
+template <int S, bool AUX>
+__global__ void __launch_bounds__(32 * tile_tj<S>() * tile_nx<S>()) atrous_rows2_kernel(AtrousParams p) {
+  constexpr int NX = tile_nx<S>();
+  constexpr int TJ = tile_tj<S>(), NW = TJ / 2 * NX, R = TJ + 4, C = 64 * NX + 4 * S, NT = 64 * NW;
+  static_assert(TJ % 2 == 0, "row pairs");
+  __shared__ float4 LI[R * C];
+  __shared__ float4 LN[R * C];
+  const int W = p.illum.W, row0 = p.illum.row0;
+  const float4* __restrict__ I = p.illum.p;
+  const float4* __restrict__ ND = p.nd.p;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bx = blockIdx.x, g = blockIdx.y / S, b = blockIdx.y - g * S;
+  const int ybase = p.y0 + g * S * TJ + b;
+  const int jp = wv / NX, xl = (wv - jp * NX) * 64 + lane;
+  const int j0 = 2 * jp;  // tile rows j0, j0 + 1
+  const int x0 = bx * 64 * NX, x = x0 + xl, yA = ybase + S * j0, yB = yA + S;
+  const bool ownA = x < p.W && yA < p.y1, ownB = x < p.W && yB < p.y1;
+  const size_t ciA = (size_t)(yA - row0) * W + x, ciB = ciA + (size_t)S * W;
+  bool bgA = true, bgB = true;
+  float fwA = 0.0f, fwB = 0.0f;
+  const bool pre = AUX && p.tile_any != nullptr;
+  bool tile_any = true;
+  if (pre) tile_any = p.tile_any[(g * S + b) * gridDim.x + bx] != 0;
+  if (tile_any) {
+    if (ownA) {
+      if (AUX) {
+        const float a = p.fwidth.aux[ciA];
+        bgA = aux_flag(a);
+        fwA = fabsf(a);
+      } else {
+        bgA = ND[ciA].w == 1.0f;
+        fwA = p.fwidth.p[ciA].y;
+      }
+    }
+    if (ownB) {
+      if (AUX) {
+        const float a = p.fwidth.aux[ciB];
+        bgB = aux_flag(a);
+        fwB = fabsf(a);
+      } else {
+        bgB = ND[ciB].w == 1.0f;
+        fwB = p.fwidth.p[ciB].y;
+      }
+    }
+  }
+  if (!pre) {
+    __shared__ int any_surface[NW];
+    const bool wave_any = __ballot(!bgA || !bgB) != 0ull;
+    if (lane == 0) any_surface[wv] = wave_any;
+    __syncthreads();
+    tile_any = false;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) tile_any |= any_surface[w] != 0;
+  }
+  if (!tile_any) {
+    if (ownA) p.out.p[ciA] = I[ciA];
+    if (ownB) p.out.p[ciB] = I[ciB];
+    return;
+  }
+  const int lo = max(0, row0), hi = min(p.H, row0 + p.illum.rows) - 1;
+  for (int e = tid; e < R * C; e += NT) {
+    const int r = e / C, c = e - r * C;
+    int gy = ybase + S * (r - 2), gx = x0 - 2 * S + c;
+    gy = gy < lo ? lo : (gy > hi ? hi : gy);
+    gx = gx < 0 ? 0 : (gx >= p.W ? p.W - 1 : gx);
+    const size_t gi = (size_t)(gy - row0) * W + gx;
+    LI[e] = I[gi];
+    LN[e] = ND[gi];
+  }
+  __syncthreads();
+  if (!ownA) return;  // (ownB implies ownA)
+  const float4* Li = LI + j0 * C + xl;  // top-left tap of pixel A's window; pixel B's is one row lower
+  const float4* Ln = LN + j0 * C + xl;
+  const float4 icA = Li[2 * C + 2 * S], icB = Li[3 * C + 2 * S];
+  const bool cA = !bgA, cB = ownB && !bgB;  // pixels that compute taps
+  if (!cA && !cB) {
+    p.out.p[ciA] = icA;
+    if (ownB) p.out.p[ciB] = icB;
+    return;
+  }
+  const bool edge =
+      x0 - 2 * S < 0 || x0 + 64 * NX - 1 + 2 * S >= p.W || ybase - 2 * S < 0 || ybase + S * (TJ + 1) >= p.H;
+  TapPixel A, B;
+  A.init(icA, Ln[2 * C + 2 * S], fwA, p.phi_color, S);
+  B.init(icB, Ln[3 * C + 2 * S], fwB, p.phi_color, S);
+  if (__builtin_expect(!edge && !(cA && A.flat) && !(cB && B.flat), 1)) {
+    // the pair's 6 window rows: row r serves A as yy = r - 2 (r <= 4) and B as yy = r - 3 (r >= 1)
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+#pragma unroll
+      for (int xx = -2; xx <= 2; ++xx) {
+        const int o = r * C + (xx + 2) * S;
+        const float4 ip = Li[o], q = Ln[o];
+        if (r <= 4 && !(r == 2 && xx == 0)) A.tap<false>(ip, q, xx, r - 2, p.phi_normal);
+        if (r >= 1 && !(r == 3 && xx == 0)) B.tap<false>(ip, q, xx, r - 3, p.phi_normal);
+      }
+    }
+  } else {
+    if (cA) {
+      if (A.flat) A.window<true, true, S, C>(Li, Ln, x, yA, p.W, p.H, p.phi_normal);
+      else A.window<false, true, S, C>(Li, Ln, x, yA, p.W, p.H, p.phi_normal);
+    }
+    if (cB) {
+      if (B.flat) B.window<true, true, S, C>(Li + C, Ln + C, x, yB, p.W, p.H, p.phi_normal);
+      else B.window<false, true, S, C>(Li + C, Ln + C, x, yB, p.W, p.H, p.phi_normal);
+    }
+  }
+  p.out.p[ciA] = cA ? A.result() : icA;
+  if (ownB) p.out.p[ciB] = cB ? B.result() : icB;
+}
+
+template <int S>
+static void launch_rows2_s(const AtrousParams& p, bool aux, hipStream_t s) {
+  constexpr int NX = tile_nx<S>(), TJ = tile_tj<S>();
+  const int groups = (p.y1 - p.y0 + S * TJ - 1) / (S * TJ);
+  dim3 grid((p.W + 64 * NX - 1) / (64 * NX), groups * S);
+  if (aux) hipLaunchKernelGGL((atrous_rows2_kernel<S, true>), grid, dim3(32 * TJ * NX), 0, s, p);
+  else hipLaunchKernelGGL((atrous_rows2_kernel<S, false>), grid, dim3(32 * TJ * NX), 0, s, p);
+}
+
+int launch_atrous_rows2(const AtrousParams& p, hipStream_t s) {
+  if (p.y1 <= p.y0) return 0;
+  if (!same_geometry(p)) return launch_atrous_simple(p, s);
+  const bool aux = p.fwidth.aux != nullptr;
+  switch (p.step) {
+    case 1: launch_rows2_s<1>(p, aux, s); break;
+    case 2: launch_rows2_s<2>(p, aux, s); break;
+    case 4: launch_rows2_s<4>(p, aux, s); break;
+    case 8: launch_rows2_s<8>(p, aux, s); break;
+    case 16: launch_rows2_s<16>(p, aux, s); break;
+    default: return launch_atrous_step(p, s);
+  }
+  return (int)hipGetLastError();
+}
+
