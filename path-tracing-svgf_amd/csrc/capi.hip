@@ -1143,10 +1143,10 @@ int pt_params(Pass* p, PTParams& k, SceneGPU*& sg) {
     k.scene.root_any = sg->root_any;
     k.stack_need = std::max(k.stack_need, sg->need_any);
   }
-  // wide_bvh = 1: the traversal kernels walk the 4-wide form of the any-hit tree (28 % fewer node + triangle visits,
-  // same bits; measured no faster: 4K 185.2 / 185.7 vs 184.7 / 184.7 fps, surface view 61.9 / 61.6 vs 62.0 / 61.8,
-  // 8 simulated bands 681 vs 693 fps, profiles/r03/wide_ab.log), so the binary walk stays the default
-  k.scene.bvh4 = (k.scene.bvh_any && sg->has4 && ui(p, "wide_bvh", 0)) ? sg->bvh4 : nullptr;
+  // wide_bvh = 1 (default): the traversal kernels walk the 4-wide form of the any-hit tree: 28 % fewer node + triangle
+  // visits, same bits. With the library built without the SLP vectorizer: 4K 197.7 / 198.9 -> 203.9 / 203.3 fps,
+  // surface view 65.4 / 65.2 -> 67.3 / 67.1 (profiles/r03/wide_ab.log; with SLP it measured no faster)
+  k.scene.bvh4 = (k.scene.bvh_any && sg->has4 && ui(p, "wide_bvh", 1)) ? sg->bvh4 : nullptr;
   k.scene.root4 = sg->root4;
   k.scene.ntris = sg->ntris;
   k.scene.leaves = sg->leaves;

@@ -543,7 +543,7 @@ def test_lane_refill_is_result_preserving(gpu, scene_name, request):
 
 @pytest.mark.parametrize("scene_name", ["scene_small", "scene_cornell", "scene_nan"])
 def test_wide_tree_is_result_preserving(gpu, scene_name, request):
-    """The 4-wide form of the any-hit tree (pack_wide; wide_bvh = 1, an A/B switch) gives the binary walks' bits: lane
+    """The 4-wide form of the any-hit tree (pack_wide; wide_bvh = 1, the default) gives the binary walks' bits: lane
     refill with 4 frames in flight, a moving camera, a tiny LDS stack budget is not needed here (overflows and exact
     ties go to the cooperative walk, which the deep-tree tests exercise). Fewer node visits than the binary tree."""
     gl = gpu
