@@ -211,6 +211,7 @@ class Renderer:
         self.frame_index = 0
         self._profile = False
         self._times: dict = {}
+        self.back_events = None  # [start, end] HIP events per back end when set to a list (frames in flight only)
 
     # ------------------------------------------------------------ passes ---
     def _svgf_pass(self, frag: str, atts) -> RenderPass:
@@ -534,6 +535,12 @@ class Renderer:
                 done = done["ev"]
             self._back.wait_event(done)
             self._stream_to(self._back)
+            if self.back_events is not None:  # diagnostics: when each frame's SVGF chain starts and ends on its stream
+                import torch
+
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record(self._back)
+                self.back_events.append([e0, None])
         self._halo("reproject", {"prev_illum": self.hist_illum[pb], "prev_moments": self.moments[pb],
                                  "prev_nd": gp["normal_depth"]})
         rp = self.reproject[b]
@@ -737,6 +744,10 @@ class Renderer:
 
             ev = torch.cuda.Event()
             ev.record(self._back)
+            if self.back_events is not None and ctx is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record(self._back)
+                self.back_events[-1][1] = e1
             self._slot_free[f % self.K] = ev
 
     # --------------------------------------------------------- accessors ---

@@ -119,6 +119,7 @@ def sim_rank(rk, bounds, probe=False, K=30):
         orig_motion(self)
         waits.append(time.perf_counter() - tw)
     D.BandRenderer._motion = timed_motion
+    r.r.back_events = []
     t0 = time.perf_counter()
     c0 = time.process_time()
     for _ in range(K):
@@ -129,6 +130,15 @@ def sim_rank(rk, bounds, probe=False, K=30):
     wall = (time.perf_counter() - t0) / K
     D.BandRenderer._motion = orig_motion
     wait = sum(waits) / K
+    r.r.flush()
+    torch.cuda.synchronize()
+    ev = [(a, b) for a, b in r.r.back_events if b is not None]
+    r.r.back_events = None
+    # the SVGF stream: busy time per frame (start to end of each back end) and idle gaps between consecutive ones
+    busy = [a.elapsed_time(b) for a, b in ev]
+    gaps = [ev[i][1].elapsed_time(ev[i + 1][0]) for i in range(len(ev) - 1)]
+    back_ms = sum(busy) / max(len(busy), 1)
+    gap_ms = sum(max(0.0, g) for g in gaps) / max(len(gaps), 1)
     xbytes = sum(LOG) / K
     nex = len(LOG) / K
     counts = None
@@ -152,14 +162,15 @@ def sim_rank(rk, bounds, probe=False, K=30):
     y0, y1 = r.plan.y0, r.plan.y1
     r.close()
     return dict(y0=y0, y1=y1, wall=wall * 1e3, issue=issue * 1e3, gpu=pp["frame_sum_ms"], pp=pp, counts=counts,
-                xbytes=xbytes, nex=nex, cpu=cpu * 1e3, wait=wait * 1e3)
+                xbytes=xbytes, nex=nex, cpu=cpu * 1e3, wait=wait * 1e3, back=back_ms, gap=gap_ms)
 
 
 def report(tag, res):
     print(f"--- {tag}: N={N} {W}x{H}")
     for rk, s in enumerate(res):
         print(f"rank {rk}: rows {s['y0']}..{s['y1']} ({s['y1'] - s['y0']}) wall {s['wall']:.3f} ms gpu {s['gpu']:.3f} "
-              f"issue {s['issue']:.3f} (host cpu {s['cpu']:.3f}, motion wait {s['wait']:.3f})  gbuf {s['pp'].get('gbuffer', 0):.3f} pt {s['pp'].get('pathtrace', 0):.3f} "
+              f"issue {s['issue']:.3f} (host cpu {s['cpu']:.3f}, motion wait {s['wait']:.3f})  SVGF stream busy "
+              f"{s['back']:.3f} ms/frame, idle {s['gap']:.3f}  gbuf {s['pp'].get('gbuffer', 0):.3f} pt {s['pp'].get('pathtrace', 0):.3f} "
               f"svgf {s['gpu'] - s['pp'].get('gbuffer', 0) - s['pp'].get('pathtrace', 0):.3f}  halo {s['nex']:.0f}x "
               f"{s['xbytes'] / 1e6:.2f} MB")
     mx = max(s["wall"] for s in res)
