@@ -19,8 +19,12 @@ CPU reference traversal), and the dynamic-scene path (GPU LBVH rebuild time, fra
 rate over the LBVH).
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-each rank renders one horizontal band of the SAME 4K frame and exchanges SVGF
-halo rows with its neighbours over RCCL (ptsvgf.dist) — strong scaling.
+every rank owns one horizontal band of the frame for the SVGF chain and exchanges
+its halo rows with the other bands over RCCL (ptsvgf.dist); the G-buffer + path
+tracer of frame f run over the whole frame on rank f % N, which sends each band's
+rows of colour / emission / albedo to its owner (--shard frames, the default), or
+every rank traces its own band of every frame (--shard bands). Strong scaling:
+the frame sequence is fixed, N ranks render it together.
 """
 from __future__ import annotations
 
@@ -87,6 +91,11 @@ def parse():
     ap.add_argument("--no-band-parity", action="store_true",
                     help="multi-GPU: skip the untimed bitwise check of the gathered bands against a one-GPU frame")
     ap.add_argument("--equal-bands", action="store_true", help="multi-GPU: equal band heights (no cost balancing)")
+    ap.add_argument("--shard", default="frames", choices=("frames", "bands"),
+                    help="multi-GPU: 'frames' = rank f %% N traces frame f whole and scatters its rows to the band owners, "
+                         "the SVGF chain banded (dist.FrameShardRenderer); 'bands' = every pass banded (dist.BandRenderer)")
+    ap.add_argument("--own-slots", type=int, default=3,
+                    help="--shard frames: whole frames a rank traces at once (its path tracer's frames in flight)")
     ap.add_argument("--breakdown", action="store_true", help="print per-pass ms to stderr")
     ap.add_argument("--pt-kernel", type=int, default=0, help="0 wavefront (production), 1 megakernel (A/B)")
     ap.add_argument("--trace-batch", type=int, default=None,
@@ -288,6 +297,9 @@ def main():
         # (thin bands' launch tails need more frames to overlap)
         args.frames_in_flight = 4 if world <= 4 else 8
         k1080 = 6 if world == 1 else 8
+        if world > 1 and args.shard == "frames":
+            # band slots cover another rank's whole-frame path tracer: a band's SVGF of frame f starts when f arrives
+            args.frames_in_flight = k1080 = 4 * world + 2
     if args.trace_batch is None:
         args.trace_batch = 1
     # every frame slot must have run once before the timed region (a slot's first frame allocates its
@@ -333,7 +345,10 @@ def main():
         replayed between HIP events, and the surface fraction of the frame."""
         check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))  # a previous renderer's streams are gone
         log(f"run {W}x{H} K={K} view={view}")
-        if world > 1:
+        if world > 1 and args.shard == "frames":
+            from ptsvgf.dist import FrameShardRenderer
+            r = FrameShardRenderer(scene, W, H, cfg, rank, world, dist, own_slots=args.own_slots, frames_in_flight=K)
+        elif world > 1:
             from ptsvgf.dist import make_band_renderer
             r = make_band_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,
                                    frames_in_flight=K, trace_batch=min(args.trace_batch, K))
@@ -386,11 +401,14 @@ def main():
             # per-stage exchange ms per frame, MAX over ranks (the slowest rank's wait sets the frame)
             mx = torch.tensor([ex.get(k, 0.0) for k in EXCHANGE_STAGES], dtype=torch.float64, device="cuda")
             dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-            out["bands"] = {"bounds": list(r.plan.bounds), "back_lag": r.r.lag,
+            out["bands"] = {"shard": args.shard, "bounds": list(r.plan.bounds), "back_lag": r.r.lag,
+                            "frames_in_flight": r.r.K,
                             "exchange_ms_per_frame": {k: round(v, 4) for k, v in zip(EXCHANGE_STAGES, mx.tolist())
                                                       if k in ex or v > 0},
                             "exchange_ms_rank0": ex,
                             "calibration": [[round(m, 3), list(b)] for m, b in getattr(r, "calibration", [])]}
+            if getattr(r, "scatter_log", None):  # --shard frames: bytes a rank sends per frame it traces
+                out["bands"]["scatter_mb_per_traced_frame"] = round(sum(r.scatter_log) / len(r.scatter_log) / 1e6, 3)
         log(f"  {args.steps} frames in {dt:.3f} s = {args.steps / dt:.2f} frames/s")
         if probes:
             st = r.trace_stats()
@@ -563,7 +581,8 @@ def main():
                                        + (f" {args.view} view" if args.view != "default" else ""),
                            "resolution": [W, H], "spp": 1, "max_tracing_depth": cfg.max_tracing_depth,
                            "atrous_iterations": cfg.num_atrous_iterations, "triangles": scene.ntris,
-                           "parallelism": f"bands{world}", "frames_in_flight": K,
+                           "parallelism": (f"frames{world}+svgf_bands{world}" if world > 1 and args.shard == "frames"
+                                           else f"bands{world}"), "frames_in_flight": K,
                            "trace_batch": min(args.trace_batch, K)},
                 "roofline": atrous_roofline(res, W, res["rows"], args.view), "cpu_baseline": cpu,
                 "path_tracer": pt_rates(res, fps), **extra,

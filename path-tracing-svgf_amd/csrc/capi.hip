@@ -1313,8 +1313,14 @@ int draw_raster(Pass* p) {
   if (!fwt->aux) HIPCHK(hipMalloc((void**)&fwt->aux, (size_t)fwt->W * fwt->rows * 4));
   k.fwidth_aux = fwt->aux;
   // the a-trous per-tile surface flags of this G-buffer, marked by the G-buffer kernels as they write the pixels
-  if (ui(p, "atrous_tile_flags", 1) && k.y1 > k.y0) {
-    const size_t nb = ptk::atrous_flag_bytes(k.W, k.y0, k.y1);
+  // the rows the a-trous passes will draw ("atrous_rows_begin" / "_end", e.g. a band's ghost-zone margin): default the
+  // G-buffer's own rows; they must lie inside them (a tile's flag is marked by the G-buffer pixels it holds)
+  k.tf_y0 = ui(p, "atrous_rows_begin", -1) >= 0 ? ui(p, "atrous_rows_begin", -1) : k.y0;
+  k.tf_y1 = ui(p, "atrous_rows_end", -1) >= 0 ? ui(p, "atrous_rows_end", -1) : k.y1;
+  if (k.tf_y0 < k.y0 || k.tf_y1 > k.y1 || k.tf_y0 > k.tf_y1)
+    return err(PT_ERR_ARG, "atrous_rows_begin / _end outside the G-buffer's rows");
+  if (ui(p, "atrous_tile_flags", 1) && k.tf_y1 > k.tf_y0) {
+    const size_t nb = ptk::atrous_flag_bytes(k.W, k.tf_y0, k.tf_y1);
     if (fwt->tflags_cap < nb) {
       if (fwt->tflags) (void)hipFree(fwt->tflags);
       fwt->tflags = nullptr;
@@ -1324,10 +1330,10 @@ int draw_raster(Pass* p) {
     }
     HIPCHK(hipMemsetAsync(fwt->tflags, 0, nb, g.stream));
     k.tflags = fwt->tflags;
-    for (int si = 0; si < 5; ++si) k.tf_off[si] = (int)ptk::atrous_flag_offset(si, k.W, k.y0, k.y1);
+    for (int si = 0; si < 5; ++si) k.tf_off[si] = (int)ptk::atrous_flag_offset(si, k.W, k.tf_y0, k.tf_y1);
     fwt->tflags_ver = fwt->version;
-    fwt->tflags_y0 = k.y0;
-    fwt->tflags_y1 = k.y1;
+    fwt->tflags_y0 = k.tf_y0;
+    fwt->tflags_y1 = k.tf_y1;
   } else {
     fwt->tflags_ver = 0;
   }

@@ -261,7 +261,7 @@ __device__ __forceinline__ void gb_finish(const GBufParams& p, int x, int y, boo
     p.fwidth_aux[(size_t)prow(p.fwidth, y) * p.W + x] =
         __uint_as_float(__float_as_uint(fwz) | (lz == 1.0f ? 0x80000000u : 0u));
   // the a-trous tiles holding this surface pixel (their background-only peers copy without reading their flags)
-  if (p.tflags && lz != 1.0f) atrous_mark_tiles(p.tflags, p.tf_off, p.W, x, y - p.y0);
+  if (p.tflags && lz != 1.0f && y >= p.tf_y0 && y < p.tf_y1) atrous_mark_tiles(p.tflags, p.tf_off, p.W, x, y - p.tf_y0);
 }
 
 template <int KS>

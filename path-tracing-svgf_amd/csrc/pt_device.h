@@ -218,8 +218,9 @@ struct GBufParams {
   int W, H, y0, y1;
   Plane world, normal_depth, motion, fwidth;
   float* fwidth_aux;    // compact depth-fwidth plane (rows of fwidth), may be null
-  unsigned char* tflags;  // a-trous per-tile surface flags (atrous_mark_tiles) for rows from y0, may be null
+  unsigned char* tflags;  // a-trous per-tile surface flags (atrous_mark_tiles) of rows [tf_y0, tf_y1), may be null
   int tf_off[5];          // their per-step offsets (atrous_flag_offset)
+  int tf_y0, tf_y1;       // the rows the a-trous passes draw (default: the G-buffer's own rows)
   const float4* geom;   // 4 x float4 per raster triangle (walk): (p1,idx)(e1,-)(e2,-)(Ng,-)
   const float4* nrm;    // 3 x float4 per raster triangle (closest hit only): n1, n2, n3
   const float4* bvh;

@@ -49,6 +49,7 @@ VARIANCE_HALO = 3
 REPROJ_REACH = 3  # rows beyond |motion| the history taps reach: bilinear + 1-texel tap / 3x3 fallback + rounding
 TAA_NEIGHBOURS = 2  # rows of the TAA 3x3 neighbourhood: +-1 texel, plus the LINEAR sampler's zero-weight row
 GHOST = 96        # default stored rows either side of a band (storage only); motion up to GHOST - 3 rows per frame
+GHOST_ZONE_GHOST = 128  # ghost zone: 65 margin rows + 3 + up to 60 rows of motion per frame
 MIN_BAND_ROWS = 16
 BAND_VISIT_BUDGET = 256  # shadow / closest-hit visits before a band's ray goes to the cooperative walk
 BAND_REFILL_WAVES = 1280  # resident waves a band's lane-refill launch is sized for (the chip: 5120)
@@ -69,6 +70,18 @@ def nd_halo(iterations: int) -> int:
     return max([VARIANCE_HALO] + ATROUS_HALO[:max(0, int(iterations))])
 
 
+def svgf_margins(iterations: int, taa: bool) -> dict:
+    """Ghost zone (FrameShardRenderer): rows beyond a band each SVGF pass draws so that the band's rows need no halo
+    exchange but the history's. Going backwards from what must be right: modulate on the band (+ TAA's 2-row
+    neighbourhood), a-trous iteration i valid on its input's margin minus 2 * 2^i rows (svgf_Atrous.frag:92-97),
+    variance 3 rows inside reproject (svgf_variance.frag:68). The a-trous iterations all draw iteration 0's rows (one
+    per-tile flag set for all five; a later iteration's extra rows are never read)."""
+    m = TAA_NEIGHBOURS if taa else 0
+    v = m + sum(ATROUS_HALO[:max(0, int(iterations))])  # the variance output's margin
+    return {"taa": 0, "modulate": m, "atrous": v - ATROUS_HALO[0] if iterations > 0 else m, "variance": v,
+            "reproject": v + VARIANCE_HALO}
+
+
 def motion_rows(m: float, H: int) -> int:
     """Rows the history taps reach beyond a band for a largest |motion.y| of m (UV units) in an H-row frame."""
     if not math.isfinite(m):
@@ -85,6 +98,7 @@ class BandPlan:
     ghost: int = GHOST
     bounds: tuple | None = None  # world+1 row boundaries (balanced_bounds); None = equal bands
     iterations: int = 5          # a-trous iterations the bands serve (sizes the normal/depth halo)
+    margins: dict | None = None  # ghost zone (svgf_margins): per-pass rows drawn beyond the band; None = HALO_SCHEDULE
 
     def __post_init__(self):
         b = list(self.bounds) if self.bounds is not None else [(self.H * k) // self.world for k in range(self.world + 1)]
@@ -93,6 +107,8 @@ class BandPlan:
         self.bounds = tuple(b)
         self.y0, self.y1 = b[self.rank], b[self.rank + 1]
         self.nd_rows = nd_halo(self.iterations)
+        if self.margins is not None and self.margins["reproject"] + REPROJ_REACH > self.ghost:
+            raise ValueError(f"a ghost zone of {self.margins['reproject']} rows needs more than {self.ghost} ghost rows")
         if self.nd_rows > self.ghost:
             raise ValueError(f"{self.iterations} a-trous iterations read {self.nd_rows} rows beyond a band, more than "
                              f"its {self.ghost} ghost rows (BandPlan(ghost=...))")
@@ -106,11 +122,24 @@ class BandPlan:
     def set_motion(self, m: float) -> int:
         """This frame's all-reduced largest |motion.y| (UV) -> rows the history exchanges carry."""
         n = motion_rows(m, self.H)
-        if n > self.ghost:
+        # ghost zone: the reprojection's margin rows read the previous G-buffer's normal/depth n rows further out
+        reach = n + (self.margins["reproject"] if self.margins is not None else 0)
+        if reach > self.ghost:
             raise RuntimeError(f"the camera moved {n - REPROJ_REACH} rows in one frame; a band holds {self.ghost} "
-                               f"ghost rows (history reach {n}): build the band renderer with a larger ghost")
+                               f"ghost rows (history reach {reach}): build the band renderer with a larger ghost")
         self.motion = n
         return n
+
+    def stage_rows(self, stage: str) -> tuple:
+        """Ghost zone: the rows the SVGF pass `stage` draws (the band widened by its margin, clipped to the frame)."""
+        m = self.margins[stage]
+        return max(0, self.y0 - m), min(self.H, self.y1 + m)
+
+    def zone(self, k: int) -> tuple:
+        """Ghost zone: rows of rank k's band the path tracer's planes must hold (its reprojection's rows)."""
+        a, b = self.owned(k)
+        m = self.margins["reproject"] if self.margins is not None else 0
+        return max(0, a - m), min(self.H, b + m)
 
     def rows_for(self, spec) -> int:
         if spec == "reproj":
@@ -240,15 +269,22 @@ def allreduce_motion(m: float, dist, group=None) -> float:
 class BandRenderer:
     """One rank's share of a frame: the fast Renderer on band storage + HALO_SCHEDULE exchanges."""
 
-    def __init__(self, scene, W, H, cfg, rank, world, dist, bounds=None, ghost=None, **kw):
+    def __init__(self, scene, W, H, cfg, rank, world, dist, bounds=None, ghost=None, ghost_zone: bool = False, **kw):
+        """ghost_zone: every SVGF pass draws its margin beyond the band (svgf_margins) over inputs that hold those
+        rows — the G-buffer on every stored row, the path tracer's planes on the reprojection's rows (pt_source must
+        provide them: FrameShardRenderer) — so the only rows that cross ranks are the history's, once per frame,
+        before the reprojection (and the TAA history's before TAA)."""
         import torch
 
         from . import gl
         from .renderer import Renderer
 
         iters = cfg.num_atrous_iterations
-        ghost = max(GHOST, nd_halo(iters)) if ghost is None else int(ghost)
-        self.plan = BandPlan(W, H, rank, world, ghost=ghost, bounds=bounds, iterations=iters)
+        margins = svgf_margins(iters, kw.get("run_taa", False)) if ghost_zone else None
+        if ghost is None:
+            ghost = max(GHOST, nd_halo(iters)) if not ghost_zone else GHOST_ZONE_GHOST
+        self.plan = BandPlan(W, H, rank, world, ghost=int(ghost), bounds=bounds, iterations=iters, margins=margins)
+        self.ghost_zone = bool(ghost_zone)
         self.dist = dist
         self.exchange = True  # False only while calibrating (make_band_renderer): ranks time their bands alone
         self.stage_events = None  # (stage, event, event) per exchange while time_exchanges(True)
@@ -272,8 +308,16 @@ class BandRenderer:
         if kw.get("frames_in_flight", 1) == 1:  # exchanges run on torch's stream: the draws must too
             from ._lib import check, pt
             check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
+        if ghost_zone:
+            kw["gbuffer_rows"] = (self.plan.row0, self.plan.row1)
+            kw["stage_rows"] = self.plan.stage_rows
         self.r = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, tex_factory=factory,
                           halo=self._halo, after_gbuffer=self._after_gbuffer, **kw)
+        if ghost_zone:  # the G-buffer marks the a-trous tiles of the rows the a-trous passes draw
+            a0, a1 = self.plan.stage_rows("atrous")
+            for p in self.r.init_pass:
+                p.set_uniform_int("atrous_rows_begin", a0)
+                p.set_uniform_int("atrous_rows_end", a1)
         # per G-buffer set: the device motion bound the G-buffer kernel writes, its pinned host copy, an event
         ng = len(self.r.gbuf)
         self._mb_dev = torch.zeros(ng, dtype=torch.int32, device=dev)
@@ -321,8 +365,23 @@ class BandRenderer:
         if stage == "reproject":
             self._motion()
         planes = {k: self._tensors[h] for k, h in handles.items()}
+        if self.ghost_zone:  # only the histories cross ranks (BandRenderer ghost_zone)
+            p = self.plan
+            if stage == "reproject":
+                items = [(planes["prev_illum"], p.margins["reproject"] + p.motion),
+                         (planes["prev_moments"], p.margins["reproject"] + p.motion)]
+            elif stage == "taa":
+                items = [(planes["prev_taa"], p.motion)]
+            else:
+                return
+            self._exchange_items(stage, items)
+            return
+        items = [(planes[name], self.plan.rows_for(spec)) for name, spec in STAGES.get(stage, ()) if name in planes]
+        self._exchange_items(stage, items)
+
+    def _exchange_items(self, stage: str, items) -> None:
         if self.stage_events is None:
-            run_stage(stage, planes, self.plan, self.dist)
+            halo_exchange(items, self.plan, self.dist)
             return
         import torch
 
@@ -330,7 +389,7 @@ class BandRenderer:
         # stream joins it at req.wait()), so the event pair spans the stage as the back end sees it
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        run_stage(stage, planes, self.plan, self.dist)
+        halo_exchange(items, self.plan, self.dist)
         e1.record()
         self.stage_events.append((stage, e0, e1))
 
@@ -418,6 +477,244 @@ class BandRenderer:
         self.dist.all_reduce(per_rank)
         self.last_band_ms = per_rank.cpu().numpy()  # every rank's band time alone (ms per frame)
         return band_row_cost(visits.cpu().numpy(), p.bounds, self.last_band_ms)
+
+
+_SCATTER_GROUP = {}
+
+
+def scatter_group(dist):
+    """A second process group (same backend) for the frame-shard scatter: its RCCL communicator has its own stream,
+    so a receive waiting for another rank's path tracer never queues the band halo exchanges behind it.
+    Collective: every rank creates it at the same point."""
+    import torch
+
+    world = dist.group.WORLD
+    key = (id(world), dist.get_rank(), dist.get_world_size())
+    hit = _SCATTER_GROUP.get(key)
+    if hit is None or hit[0] is not world:
+        backend = dist.get_backend()
+        g = dist.new_group(backend=backend)
+        if backend == "gloo":
+            dist.barrier(group=g)
+        else:  # the first operation on a group involves every rank (batch_isend_irecv requires it when it comes first)
+            dist.barrier(group=g, device_ids=[torch.cuda.current_device()])
+        _SCATTER_GROUP[key] = hit = (world, g)
+    return hit[1]
+
+
+def exchange_window(window, plan: BandPlan, dist, group=None) -> int:
+    """The point-to-point transfers of one frame-shard window: consecutive frames, at most one per source rank (frame
+    f is traced by rank f % N). window = [(src, planes)]: for a frame this rank traced, planes are its whole-frame
+    (H, W, C) tensors and every other band's rows (plan.zone: the band, widened by the ghost zone's reprojection
+    margin) go to that band's owner; for a frame rank src traced, planes are this band's zone rows, received from src. Every rank builds the same window, so the batch is symmetric: an
+    all-to-all over the window's sources, every link busy at once, one communicator. RCCL: the current stream waits
+    for the batch; gloo (tests): blocking, device tensors staged through host memory. Returns the bytes sent."""
+    import torch
+
+    gloo = dist.get_backend(group) == "gloo"
+    ops, staged, nbytes = [], [], 0
+    for src, planes in window:
+        if src == plan.rank:
+            for k in range(plan.world):
+                if k == plan.rank:
+                    continue
+                y0, y1 = plan.zone(k)
+                for t in planes:
+                    rows = t[y0:y1]
+                    if gloo and rows.is_cuda:
+                        rows = rows.cpu()
+                    ops.append(dist.P2POp(dist.isend, rows, k, group))
+                    nbytes += rows.numel() * rows.element_size()
+        else:
+            for t in planes:
+                buf = t
+                if gloo and t.is_cuda:
+                    buf = torch.empty(t.shape, dtype=t.dtype)
+                    staged.append((t, buf))
+                ops.append(dist.P2POp(dist.irecv, buf, src, group))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    for t, h in staged:
+        t.copy_(h)
+    return nbytes
+
+
+class FrameShardRenderer(BandRenderer):
+    """Frames interleaved across ranks for the path tracer, bands for the SVGF chain.
+
+    The G-buffer + path tracer of frame f (the front end: camera in, colour / emission / albedo out, no history) are
+    traced over the WHOLE frame by rank f % N, so every traversal launch is a full frame's (a band's launches are an
+    N-th of that and end on the same longest rays: DESIGN.md "What limits strong scaling"). The SVGF chain is
+    sequential through its history, so it stays banded exactly as in BandRenderer: every rank draws its band's
+    G-buffer (per pixel, nothing to exchange), receives its rows of the path tracer's planes and runs reproject /
+    variance / a-trous / modulate with the HALO_SCHEDULE exchanges. Same kernels on the same inputs: the bands equal
+    a one-GPU frame bit for bit.
+
+    The SVGF passes draw a ghost zone (BandRenderer ghost_zone, svgf_margins): the G-buffer covers every stored row
+    and the path tracer's planes arrive with the reprojection's margin, so per frame only the history rows cross
+    ranks, once, before the reprojection (7 halo stages per frame become 1).
+
+    The path tracer's rows travel once per window of N consecutive frames (exchange_window on a group of their own, scatter_group:
+    RCCL over xGMI): each rank sends its traced frame's rows to every other band and receives its band's rows of the
+    other N - 1 frames, all links at once. A frame's back end waits for its window, so the back end runs back_lag = N
+    frames behind the front end, and frames_in_flight (band slots) must cover that plus a path tracer's latency.
+    Per rank and N frames: one full-frame front end + N band G-buffers and SVGF chains. own_slots = whole frames this
+    rank traces at once (the path tracer's streams)."""
+
+    def __init__(self, scene, W, H, cfg, rank, world, dist, own_slots: int = 2, **kw):
+        import torch
+
+        from . import gl
+        from .renderer import Renderer
+
+        K = kw.get("frames_in_flight", 1)
+        kw.setdefault("back_lag", world)  # a frame's back end is issued after its window's exchange
+        if K <= kw["back_lag"]:
+            raise ValueError(f"FrameShardRenderer needs frames_in_flight > back_lag = {kw['back_lag']}, got {K}")
+        self._full_tensors = {}
+        dev = torch.device("cuda", torch.cuda.current_device())
+
+        def full_factory(w, h):
+            t = torch.zeros((h, w, 4), dtype=torch.float32, device=dev)
+            handle = gl.wrap_device_texture(t.data_ptr(), w, h)
+            self._full_tensors[handle] = t
+            return handle
+
+        gl.set_band(W, H, 0, H, 0, H)  # the library's band state is process-global: the full renderer's planes are whole
+        self.full = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, tex_factory=full_factory,
+                             run_taa=False, run_output=False, frames_in_flight=max(2, int(own_slots)))
+        for p in self.full.init_pass:
+            p.set_rows(0, H)
+        for p, _ in self.full.pt_slots:
+            p.set_rows(0, H)
+        self.own_slots = self.full.K
+        self._own_free = [None] * self.own_slots  # event: the window exchange that sent the slot's last frame is done
+        self._win = []  # frames registered since the last window exchange
+        kw.setdefault("front_streams", 1)  # band front ends are a G-buffer each: one stream, in order
+        kw.setdefault("ghost_zone", True)
+        super().__init__(scene, W, H, cfg, rank, world, dist, pt_source=self._pt_source, pt_flush=self._exchange,
+                         **kw)
+        self.full.camera = self.r.camera  # one camera: the full front end draws the band renderer's frame
+        self.pass_path_tracing = self.full.pass_path_tracing
+        self._sgroup = scatter_group(dist) if world > 1 else None
+        self._recv_stream = torch.cuda.Stream()
+        self.scatter_log = []  # per exchange that carried a frame of this rank: bytes sent
+
+    def _band_rows(self, handle):
+        p = self.plan
+        a, b = p.zone(p.rank)
+        return self._tensors[handle][a - p.row0:b - p.row0]
+
+    def _pt_source(self, f: int, slot: int, stream):
+        """Renderer pt_source: register frame f in the current window (exchanging the previous window when it is
+        full); when f is this rank's, trace the whole frame and copy its own band's rows. Returns the holder whose
+        "ev" the back end of f waits for (set when f's window is exchanged)."""
+        import torch
+
+        r, p = self.r, self.plan
+        if len(self._win) == p.world:
+            self._exchange()
+        holder = {}
+        item = dict(src=f % p.world, outs=[self._band_rows(h) for h in r.pt_slots[slot][1]],
+                    free=r._slot_free[f % r.K], holder=holder)
+        if item["src"] == p.rank:
+            o, pt_done = self._render_own(f)
+            r._stream_to(stream)  # the library's stream is process-global: back to the band's front-end stream
+            full = [self._full_tensors[h] for h in self.full.pt_slots[o][1]]
+            rs = self._recv_stream
+            if item["free"] is not None:
+                rs.wait_event(item["free"])
+            rs.wait_event(pt_done)
+            z0, z1 = p.zone(p.rank)
+            with torch.cuda.stream(rs):
+                for a, b in zip(item["outs"], full):
+                    a.copy_(b[z0:z1])
+            ev = torch.cuda.Event()
+            ev.record(rs)
+            holder["ev"] = ev
+            item.update(o=o, full=full)
+        self._win.append(item)
+        return holder
+
+    def _exchange(self) -> None:
+        """Send / receive the rows of the registered window (every rank registers the same frames, so every rank
+        calls this at the same point: when a window is full, and on flush)."""
+        import torch
+
+        win, self._win = self._win, []
+        if not win:
+            return
+        p, rs = self.plan, self._recv_stream
+        for it in win:  # receives overwrite band slots: the SVGF chains that read them K frames ago are done
+            if it["src"] != p.rank and it["free"] is not None:
+                rs.wait_event(it["free"])
+        window = [(it["src"], it["full"] if it["src"] == p.rank else it["outs"]) for it in win]
+        with torch.cuda.stream(rs):
+            nbytes = exchange_window(window, p, self.dist, self._sgroup) if p.world > 1 else 0
+        ev = torch.cuda.Event()
+        ev.record(rs)
+        for it in win:
+            if it["src"] != p.rank:
+                it["holder"]["ev"] = ev
+            else:
+                self._own_free[it["o"]] = ev  # the slot's frame has been sent
+                self.scatter_log.append(nbytes)
+
+    def _render_own(self, f: int):
+        """G-buffer + path tracer of frame f over the whole frame on an own stream. Returns (own slot, event after
+        the path tracer)."""
+        import torch
+
+        fr, p = self.full, self.plan
+        o = (f // p.world) % self.own_slots
+        st = fr._streams[o]
+        if self._own_free[o] is not None:
+            st.wait_event(self._own_free[o])
+        fr._use_slot(o)
+        fr._stream_to(st)
+        fr.pre_viewproj = self.r.pre_viewproj
+        fr.frame_index = f
+        fr._gbuffer(o)
+        fr._path_trace(fr.gbuf[o])
+        done = torch.cuda.Event()
+        done.record(st)
+        return o, done
+
+    def trace_stats(self) -> dict:
+        """Traversal counters of one frame: the rank tracing it counts the whole frame, the others nothing (bench
+        sums over ranks)."""
+        import torch
+
+        buf = torch.zeros(len(self.r.STAT_KEYS), dtype=torch.int64, device="cuda")
+        self.r.flush()
+        torch.cuda.synchronize()
+        for p, _ in self.full.pt_slots:
+            p.set_trace_stats(buf.data_ptr())
+        try:
+            self.r.frame()
+            self.r.flush()
+            torch.cuda.synchronize()
+        finally:
+            for p, _ in self.full.pt_slots:
+                p.set_trace_stats(0)
+        return dict(zip(self.r.STAT_KEYS, (int(v) for v in buf.cpu().tolist())))
+
+    def profile(self, on: bool) -> None:
+        self.r.profile(on)
+        self.full.profile(on)
+
+    def pass_times(self) -> dict:
+        out = self.r.pass_times()
+        for k, v in self.full.pass_times().items():
+            if k in ("gbuffer", "pathtrace"):
+                out["full_" + k] = v
+        return out
+
+    def close(self) -> None:
+        super().close()
+        self.full.close()
+        self._full_tensors.clear()
 
 
 def gather_bands(owned: dict, plan: BandPlan, dist, dst: int = 0) -> dict | None:

@@ -58,7 +58,8 @@ class Renderer:
                  mode: str = "fast", aspect_corrected: bool | None = None, band=None, prune: bool = True,
                  atrous_exact: bool = False, run_taa: bool = True, run_output: bool = True, tex_factory=None,
                  halo=None, gbuffer_rows=None, frames_in_flight: int = 1, after_gbuffer=None, back_lag: int = 0,
-                 trace_batch: int = 1):
+                 trace_batch: int = 1, front_streams: int | None = None, pt_source=None, pt_flush=None,
+                 stage_rows=None):
         """band = (y0, y1, row0, rows) for screen-band sharding; tex_factory(w, h) -> handle allocates the
         frame-sized planes (ptsvgf.dist wraps torch tensors); halo(stage, {plane name: handle}) is called before
         the SVGF passes that read rows beyond the band (dist.HALO_SCHEDULE names the planes); after_gbuffer(set,
@@ -82,7 +83,15 @@ class Renderer:
         trace_batch = B (2..8, at most K, frames in flight only): the path tracer of B consecutive frames runs as
         one batched draw (pt_pass_draw_batch) issued with the last of them — its list-driven traversal launches
         trace all B frames' rays at once, so a thin band's launches carry B times the rays. The back lag is raised
-        to at least B - 1 (a frame's back end needs its batch). Same bits."""
+        to at least B - 1 (a frame's back end needs its batch). Same bits.
+
+        front_streams = S (frames in flight only, default K): the front ends of frame f run on stream f % S (the K
+        frame slots are unchanged). pt_source(f, slot, stream) (fast driver, frames in flight): instead of drawing
+        the path tracer, fill frame f's colour / emission / albedo planes of `slot` from elsewhere
+        (dist.FrameShardRenderer: some rank traced the whole frame) once the slot is free; it is called right after the
+        G-buffer of f is issued on `stream` and returns a holder dict whose "ev" (a torch event, set by the time the
+        back end of f is issued) the back end waits for; pt_flush() is called by flush() before the pending back
+        ends are issued."""
         if mode not in ("fast", "reference"):
             raise ValueError(mode)
         self.mode = mode
@@ -139,6 +148,15 @@ class Renderer:
         self.lag = max(int(back_lag), self.B - 1)
         if not 0 <= self.lag < self.K:
             raise ValueError(f"back_lag must be in [0, frames_in_flight) = [0, {self.K}), got {back_lag}")
+        self._nfs = self.K if front_streams is None else int(front_streams)
+        if not 1 <= self._nfs <= self.K:
+            raise ValueError(f"front_streams must be in [1, frames_in_flight], got {front_streams}")
+        if pt_source is not None and (mode != "fast" or self.K < 2 or self.B > 1):
+            raise ValueError("pt_source needs the fast driver with frames in flight and no trace batching")
+        self._pt_source = pt_source
+        self._pt_flush = pt_flush
+        self._stage_rows = stage_rows
+        self._ready = None  # pt_source's event for the front end being issued
         self._batch: list = []  # path-tracing passes of the open batch: (pass, G-buffer-done event, stream, holder)
         self._pending: list = []  # front ends whose back end is not issued yet (back_lag)
         # a serial renderer draws on torch's stream of its construction, whatever stream another renderer in the
@@ -183,7 +201,7 @@ class Renderer:
         if self.K > 1:
             import torch  # streams and events are torch plumbing (the kernels are the library's)
 
-            self._streams = [torch.cuda.Stream() for _ in range(self.K)]
+            self._streams = [torch.cuda.Stream() for _ in range(self._nfs)]
             # A/B switch, off by default: with K frames in flight the extra streams measured slower.
             # Its streams exist only when it is on: every stream beyond the process's hardware queues
             # (GPU_MAX_HW_QUEUES) shares a queue, in order, with another stream.
@@ -322,10 +340,14 @@ class Renderer:
 
     def _use_slot(self, s: int) -> None:
         """Path-tracing pass and outputs of frame slot s (frame f uses slot f % K)."""
+        self._slot = s
         self.pt_pass, (self.curColor, self.Emission, self.Albedo) = self.pt_slots[s]
 
     def _gbuffer_and_pt(self, b: int):
         self._gbuffer(b)
+        if self._pt_source is not None:
+            self._ready = self._pt_source(self.frame_index, self._slot, self._lib_stream)
+            return
         self._path_trace(self.gbuf[b] if self.mode == "fast" else None)
 
     def _gbuffer(self, b: int):
@@ -452,6 +474,7 @@ class Renderer:
         mp.set_texture_uniform(GL_TEXTURE_2D, self.Emission, "gEmission")
         mp.set_texture_uniform(GL_TEXTURE_2D, self.atrous_output, "gIllumination")
         mp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
+        self._rows(mp, "modulate")
         self._draw(mp, "modulate")
         if self.run_taa:                                       # main.cpp:537-544
             tp = self.pass_taa
@@ -482,14 +505,15 @@ class Renderer:
         if self.K > 1:                                         # front end on stream s, after SVGF(f - K)
             import torch
 
-            fe = self._streams[f % self.K]
+            fe = self._streams[f % self._nfs]
             if self._slot_free[f % self.K] is not None:
                 fe.wait_event(self._slot_free[f % self.K])
             if self.accumulate and self._fe_prev is not None:  # lastFrame = the previous front end's colour
                 fe.wait_event(self._fe_prev)
             # the G-buffer and the path tracer are independent (both need only the camera): the G-buffer runs on
             # a side stream beside the path tracer, so the two launches' tails overlap
-            if self._gfork:
+            self._ready = None
+            if self._gfork and self._pt_source is None:
                 gs = self._gstreams[f % self.K]
                 start = torch.cuda.Event()
                 start.record(fe)
@@ -515,7 +539,7 @@ class Renderer:
                     self._issue_batch()
         else:
             self._gbuffer_and_pt(f % ng)
-        return dict(f=f, slot=s, done=done, frame_counter=self.camera.frameCounter)
+        return dict(f=f, slot=s, done=done, ready=self._ready, frame_counter=self.camera.frameCounter)
 
     def _back_fast(self, ctx: dict):
         """The SVGF chain of the frame whose front end made ctx (back-end stream, sequential over frames)."""
@@ -534,6 +558,10 @@ class Renderer:
                     self._issue_batch()
                 done = done["ev"]
             self._back.wait_event(done)
+            if ctx.get("ready") is not None:  # pt_source: the colour / emission / albedo planes have arrived
+                if "ev" not in ctx["ready"]:
+                    raise RuntimeError(f"pt_source has not delivered frame {f} by its back end (back_lag too small)")
+                self._back.wait_event(ctx["ready"]["ev"])
             self._stream_to(self._back)
             if self.back_events is not None:  # diagnostics: when each frame's SVGF chain starts and ends on its stream
                 import torch
@@ -556,6 +584,7 @@ class Renderer:
         rp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
         rp.set_texture_uniform(GL_TEXTURE_2D, gp["normal_depth"], "gPrevNormalAndLinearZ")
         rp.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
+        self._rows(rp, "reproject")
         self._draw(rp, "reproject")
         self._halo("variance", {"illum": self.illum, "moments": self.moments[b], "nd": g["normal_depth"]})
         vp = self.variance_compute_pass
@@ -566,6 +595,7 @@ class Renderer:
         vp.set_texture_uniform(GL_TEXTURE_2D, self.moments[b], "gMoments_HistoryLength")
         vp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
         vp.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
+        self._rows(vp, "variance")
         self._draw(vp, "variance")
         # a-trous chain without copies: i0 var->ping, i1 ping->hist[b] (next frame's history),
         # then alternate through ping/pong
@@ -591,6 +621,7 @@ class Renderer:
             ap.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
             ap.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
             ap.set_texture_uniform(GL_TEXTURE_2D, src, "gIllumination")
+            self._rows(ap, "atrous")
             self._draw(ap, "atrous")
             src = self._atrous_tex(dests[i])
         self.atrous_final = src
@@ -600,6 +631,7 @@ class Renderer:
         mp.set_texture_uniform(GL_TEXTURE_2D, emission, "gEmission")
         mp.set_texture_uniform(GL_TEXTURE_2D, src, "gIllumination")
         mp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
+        self._rows(mp, "modulate")
         self._draw(mp, "modulate")
         if self.run_taa:
             self._halo("taa", {"modulate": self.modulate_color, "velocity": g["velocity"], "prev_taa": self.taa[pb]})
@@ -610,8 +642,15 @@ class Renderer:
             tp.set_texture_uniform(GL_TEXTURE_2D, g["velocity"], "velocityTexture")
             tp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "normal_depth")
             tp.set_uniform_uint("frameCounter", ctx["frame_counter"])
+            self._rows(tp, "taa")
             self._draw(tp, "taa")
         self.final = self.taa[b] if self.run_taa else self.modulate_color
+
+    def _rows(self, p: RenderPass, stage: str) -> None:
+        if self._stage_rows is not None:
+            rows = self._stage_rows(stage)
+            if rows is not None:
+                p.set_rows(*rows)
 
     def time_atrous(self, reps: int = 20) -> float:
         """Average duration (ms) of one a-trous launch: the last frame's iterations (same inputs, so the
@@ -725,6 +764,8 @@ class Renderer:
     def flush(self) -> None:
         """Issue the open path-tracing batch and the back ends still pending (back_lag)."""
         self._issue_batch()
+        if self._pt_flush is not None:
+            self._pt_flush()
         while self._pending:
             self._finish(self._pending.pop(0))
 

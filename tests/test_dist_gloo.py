@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, W, H, frames, moves, bounds=None, ghost=None):
+def _worker(rank, world, port, W, H, frames, moves, bounds=None, ghost=None, shard="bands"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, here)
@@ -35,11 +35,15 @@ def _worker(rank, world, port, W, H, frames, moves, bounds=None, ghost=None):
     try:
         import oracle_ref as O
         from ptsvgf.camera import rigid_inverse
-        from ptsvgf.dist import GHOST, BandPlan, allreduce_motion, run_stage
+        from ptsvgf.dist import (GHOST, GHOST_ZONE_GHOST, BandPlan, allreduce_motion, exchange_window, halo_exchange,
+                                 run_stage, svgf_margins)
         from ptsvgf.scene import build_scene
 
         scene = build_scene("table_clock_plant", hdr_size=(128, 64), plant_leaves=20)
-        plan = BandPlan(W, H, rank, world, ghost=ghost or GHOST, bounds=bounds)
+        gz = shard == "frames_gz"  # ghost zone: passes draw margins, only the histories cross ranks
+        plan = BandPlan(W, H, rank, world, ghost=ghost or (GHOST_ZONE_GHOST if gz else GHOST), bounds=bounds,
+                        margins=svgf_margins(5, taa=True) if gz else None)
+        rows = (lambda st: plan.stage_rows(st)) if gz else (lambda st: (plan.y0, plan.y1))
         full = O.OracleFrameLoop(scene, W, H, threads=2)
         band = O.OracleFrameLoop(scene, W, H, threads=2)  # same camera path, band-restricted execution
         log = []
@@ -50,6 +54,12 @@ def _worker(rank, world, port, W, H, frames, moves, bounds=None, ghost=None):
             return a
 
         def halo(stage, arrays):
+            if gz:  # the histories only (BandRenderer ghost_zone)
+                n = {"reproject": plan.margins["reproject"] + plan.motion, "taa": plan.motion}.get(stage)
+                if n is not None:
+                    halo_exchange([(torch.from_numpy(a)[plan.row0:plan.row1], n) for k, a in arrays.items()
+                                   if k in ("prev_illum", "prev_moments", "prev_taa")], plan, dist)
+                return
             run_stage(stage, {k: torch.from_numpy(a)[plan.row0:plan.row1] for k, a in arrays.items()}, plan, dist)
 
         nan = lambda: np.full((H, W, 4), np.nan, np.float32)  # noqa: E731
@@ -66,13 +76,24 @@ def _worker(rank, world, port, W, H, frames, moves, bounds=None, ghost=None):
             cam.update()
             view, proj = cam.cam_view_mat, cam.cam_proj_mat
             g = O.gbuffer(scene.raster, W, H, view, proj, band.pre_viewproj, 2)
-            for k in g:                      # the G-buffer computes the owned rows only
-                poison(g[k], plan.y0, plan.y1)
-            col, em, al = band.os.path_trace(W, H, cam.frameCounter, cam.cam_position, rigid_inverse(view),
-                                             cfg.clamp_threshold, cfg.max_tracing_depth, band.aspect_corrected,
-                                             rows=(plan.y0, plan.y1), threads=2)
+            for k in g:                      # the G-buffer computes the owned rows only (ghost zone: every stored row)
+                poison(g[k], *((plan.row0, plan.row1) if gz else (plan.y0, plan.y1)))
+            if shard == "bands":
+                col, em, al = band.os.path_trace(W, H, cam.frameCounter, cam.cam_position, rigid_inverse(view),
+                                                 cfg.clamp_threshold, cfg.max_tracing_depth, band.aspect_corrected,
+                                                 rows=(plan.y0, plan.y1), threads=2)
+            elif f % world == rank:  # frame shard: this rank traces frame f whole and sends the other bands' rows
+                col, em, al = band.os.path_trace(W, H, cam.frameCounter, cam.cam_position, rigid_inverse(view),
+                                                 cfg.clamp_threshold, cfg.max_tracing_depth, band.aspect_corrected,
+                                                 threads=2)
+                nbytes = exchange_window([(rank, [torch.from_numpy(a) for a in (col, em, al)])], plan, dist)
+                assert nbytes == 3 * sum(plan.zone(k)[1] - plan.zone(k)[0] for k in range(world) if k != rank) * W * 16
+            else:  # ... or receives its band's rows of the planes rank f % world traced
+                col, em, al = nan(), nan(), nan()
+                z0, z1 = plan.zone(rank)
+                exchange_window([(f % world, [torch.from_numpy(a)[z0:z1] for a in (col, em, al)])], plan, dist)
             for a in (col, em, al):
-                poison(a, plan.y0, plan.y1)
+                poison(a, *plan.zone(rank))
             # the motion bound the G-buffer kernel reduces (owned surface pixels), MAX over ranks
             own = g["velocity"][plan.y0:plan.y1]
             surf = g["normal_depth"][plan.y0:plan.y1, :, 3] != 1.0
@@ -82,18 +103,18 @@ def _worker(rank, world, port, W, H, frames, moves, bounds=None, ghost=None):
             halo("reproject", dict(prev_illum=prev_illum, prev_moments=prev_moments, prev_nd=prev_nd))
             ri, rm = O.reproject(g["velocity"], col, al, em, prev_illum, prev_moments, g["normal_depth"], prev_nd,
                                  g["fwidth"], np.float32(1.0 / W), np.float32(1.0 / H), 10.0, 16.0, 2)
-            poison(ri, plan.y0, plan.y1)
-            poison(rm, plan.y0, plan.y1)
+            poison(ri, *rows("reproject"))
+            poison(rm, *rows("reproject"))
             halo("variance", dict(illum=ri, moments=rm, nd=g["normal_depth"]))
-            a = poison(O.variance(ri, rm, g["normal_depth"], g["fwidth"], 4.0, 128.0, 2), plan.y0, plan.y1)
+            a = poison(O.variance(ri, rm, g["normal_depth"], g["fwidth"], 4.0, 128.0, 2), *rows("variance"))
             for i in range(cfg.num_atrous_iterations):
                 halo(f"atrous{i}", dict(atrous_in=a))
-                a = poison(O.atrous(a, g["normal_depth"], g["fwidth"], 1 << i, 4.0, 128.0, 2), plan.y0, plan.y1)
+                a = poison(O.atrous(a, g["normal_depth"], g["fwidth"], 1 << i, 4.0, 128.0, 2), *rows("atrous"))
                 if i == 1:
                     hist = a
-            m = poison(O.modulate(al, em, a, g["normal_depth"], 2), plan.y0, plan.y1)
+            m = poison(O.modulate(al, em, a, g["normal_depth"], 2), *rows("modulate"))
             halo("taa", dict(modulate=m, velocity=g["velocity"], prev_taa=prev_taa))
-            t = poison(O.taa(m, prev_taa, g["velocity"], g["normal_depth"], cam.frameCounter, 2), plan.y0, plan.y1)
+            t = poison(O.taa(m, prev_taa, g["velocity"], g["normal_depth"], cam.frameCounter, 2), *rows("taa"))
             prev_taa = t
             band.pre_viewproj = band._mat_mul(proj, view)
             cam.frameCounter += 1
@@ -130,6 +151,69 @@ BIG = [(0.0, 5.0), (2.0, -5.0), (-3.0, 6.0)]
 def test_band_halo_large_motion_gloo(world, bounds):
     W, H = 64, 256
     mp.spawn(_worker, args=(world, _free_port(), W, H, 4, [None] + BIG, bounds), nprocs=world, join=True)
+
+
+@pytest.mark.parametrize("world,moves,bounds", [(2, SMALL, None), (3, [None] + BIG, (0, 20, 140, 256))])
+def test_frame_shard_scatter_gloo(world, moves, bounds):
+    """Frame shard (dist.FrameShardRenderer's data path): rank f % N path-traces frame f whole and exchange_window()
+    sends each band's rows of colour / emission / albedo to its owner, the SVGF chain stays banded. The bands must
+    equal the single-process frame bit for bit (rows not received stay NaN and would leak)."""
+    W, H = (48, 108) if bounds is None else (64, 256)
+    mp.spawn(_worker, args=(world, _free_port(), W, H, 4, moves, bounds, None, "frames"), nprocs=world, join=True)
+
+
+def _window_worker(rank, world, port, bounds, windows):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "path-tracing-svgf_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ptsvgf.dist import BandPlan, exchange_window
+        W, H = 8, bounds[-1]
+        plan = BandPlan(W, H, rank, world, ghost=4, bounds=bounds, iterations=1)
+
+        def frame(f):  # plane c of frame f as rank f % world traces it
+            return [torch.arange(H * W * 4, dtype=torch.float32).reshape(H, W, 4) * (f + 1) + 1000 * c
+                    for c in range(3)]
+
+        f0 = 0
+        for n in windows:  # consecutive frames f0 .. f0 + n - 1, at most one per source rank
+            window, got = [], {}
+            for f in range(f0, f0 + n):
+                if f % world == rank:
+                    window.append((rank, frame(f)))
+                else:
+                    got[f] = [torch.full((plan.y1 - plan.y0, W, 4), float("nan")) for _ in range(3)]
+                    window.append((f % world, got[f]))
+            sent = exchange_window(window, plan, dist)
+            mine = sum(1 for f in range(f0, f0 + n) if f % world == rank)
+            assert sent == mine * 3 * (H - (plan.y1 - plan.y0)) * W * 16
+            for f, planes in got.items():
+                for a, b in zip(planes, frame(f)):
+                    assert torch.equal(a, b[plan.y0:plan.y1]), (rank, f)
+            f0 += n
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,bounds,windows", [(3, (0, 5, 9, 16), [3, 3, 1, 3, 2]), (4, (0, 2, 4, 10, 12), [4, 2, 4])])
+def test_exchange_window_gloo(world, bounds, windows):
+    """exchange_window: a window of consecutive frames (full and cut short, as flush() cuts them) delivers each band's
+    rows of every frame another rank traced, and each rank sends exactly its frames' other-band rows."""
+    mp.spawn(_window_worker, args=(world, _free_port(), bounds, windows), nprocs=world, join=True)
+
+
+@pytest.mark.parametrize("world,moves,bounds", [(2, SMALL, None), (3, [None] + BIG, (0, 20, 140, 256)),
+                                                (4, [None] + BIG, (0, 16, 32, 140, 256))])
+def test_frame_shard_ghost_zone_gloo(world, moves, bounds):
+    """Frame shard with the ghost zone (FrameShardRenderer's default): the path tracer's planes arrive with the
+    reprojection's margin, the G-buffer covers every stored row, each SVGF pass draws its svgf_margins rows (a-trous
+    at iteration 0's), and only the histories cross ranks (prev illumination / moments with margin + motion rows,
+    the TAA history with motion rows). Everything outside the rows a pass draws is NaN; the bands must equal the
+    single-process frame bit for bit, through 11-16-row motion and 16-row bands."""
+    W, H = (48, 108) if bounds is None else (64, 256)
+    mp.spawn(_worker, args=(world, _free_port(), W, H, 4, moves, bounds, None, "frames_gz"), nprocs=world, join=True)
 
 
 def test_band_motion_beyond_ghost_raises():

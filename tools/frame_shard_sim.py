@@ -1,0 +1,177 @@
+"""Single-GPU prediction of an N-GPU frame-shard run (ptsvgf.dist.FrameShardRenderer), ranks simulated one by one.
+
+Rank r of N traces every N-th frame whole (G-buffer + path tracer) and, every frame, draws its band's G-buffer and
+SVGF chain. Here one rank's share runs alone on the GPU with the communication stood in for by spin kernels of the
+modelled RCCL time (20 us + bytes / 50 GB/s by default, XLAT_US / XGBS to change):
+  * the exchange of a window of N frames (exchange_window: this rank's traced frame to the N - 1 other bands, the
+    other N - 1 frames' rows of this band from their ranks, all links at once): latency + the largest per-peer
+    volume / bandwidth, on the receive stream (the window's SVGF chains wait for it);
+  * the SVGF halo exchanges: as tools/band_sim.py.
+The arrival of another rank's frame is not delayed by that rank's path tracer: the run measures a rank's throughput
+(frames in flight cover the latency), not the latency itself. Prints each simulated rank's ms per frame; the
+predicted N-GPU frame is the slowest rank.
+usage: python tools/frame_shard_sim.py [N] [W] [H]   (RANKS=0,3 to simulate a subset; FRAMES, OWN, K)"""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("PTSVGF_HW_QUEUES", "16")  # as bench.py
+sys.path.insert(0, os.path.join(REPO, "path-tracing-svgf_amd"))
+import torch
+
+from ptsvgf import dist as D
+from ptsvgf import gl
+from ptsvgf.camera import parameter_config
+from ptsvgf.scene import build_scene
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+W = int(sys.argv[2]) if len(sys.argv) > 2 else 3840
+H = int(sys.argv[3]) if len(sys.argv) > 3 else 2160
+XLAT_US = float(os.environ.get("XLAT_US", "20"))
+XGBS = float(os.environ.get("XGBS", "50"))
+_CYC_PER_US = None
+LOG = {"halo": 0, "send": 0, "recv": 0}
+
+
+class FakeDist:
+    """Stands in for torch.distributed: this rank's own motion bound is the all-reduced one."""
+    class ReduceOp:
+        MAX = "max"
+
+    def get_backend(self, group=None):
+        return "gloo"
+
+    def all_reduce(self, t, op=None, group=None):
+        return None
+
+
+def _spin(us):
+    """torch.cuda._sleep spins on the shader clock: calibrated once against HIP events."""
+    global _CYC_PER_US
+    if us <= 0:
+        return
+    if _CYC_PER_US is None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(1000)
+        e0.record()
+        torch.cuda._sleep(2_000_000)
+        e1.record()
+        e1.synchronize()
+        _CYC_PER_US = 2_000_000 / (e0.elapsed_time(e1) * 1e3)
+    torch.cuda._sleep(int(us * _CYC_PER_US))
+
+
+def _xfer_us(nbytes):
+    return XLAT_US + (nbytes / (XGBS * 1e3) if XGBS > 0 else 0.0)
+
+
+def fake_exchange(items, plan, dist, group=None):
+    sent_b = recv_b = 0
+    for t, n in items:
+        if plan.world == 1 or n <= 0:
+            continue
+        row = t.shape[1] * t.shape[2] * 4
+        for send, a, b, _ in plan.halo_parts(n):
+            if send:
+                sent_b += row * (b - a)
+            else:
+                recv_b += row * (b - a)
+    if sent_b or recv_b:
+        LOG["halo"] += max(sent_b, recv_b)
+        _spin(_xfer_us(max(sent_b, recv_b)))
+
+
+def fake_window(window, plan, dist, group=None):
+    """exchange_window stand-in: the window's sends and receives run over all links at once, so the batch lasts
+    latency + the largest per-peer volume (sent to or received from one peer) / link bandwidth."""
+    per_peer, sent = {}, 0
+    for src, planes in window:
+        if src == plan.rank:
+            for k in range(plan.world):
+                if k != plan.rank:
+                    y0, y1 = plan.owned(k)
+                    nb = sum(t[y0:y1].numel() * 4 for t in planes)
+                    per_peer[("s", k)] = per_peer.get(("s", k), 0) + nb
+                    sent += nb
+        else:
+            nb = sum(t.numel() * 4 for t in planes)
+            per_peer[("r", src)] = per_peer.get(("r", src), 0) + nb
+            LOG["recv"] += nb
+    LOG["send"] += sent
+    if per_peer:
+        _spin(_xfer_us(max(per_peer.values())))
+    return sent
+
+
+D.halo_exchange = fake_exchange
+D.exchange_window = fake_window
+D.scatter_group = lambda dist: None
+torch.cuda.set_device(0)
+gl.init(0)
+from ptsvgf._lib import check, pt  # noqa: E402
+
+check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
+scene = build_scene("table_clock_plant")
+cfg = parameter_config()
+FRAMES = int(os.environ.get("FRAMES", str(max(96, 24 * N))))
+OWN = int(os.environ.get("OWN", "3"))
+K = int(os.environ.get("K", str(4 * N + 2)))
+
+
+def sim_rank(rk):
+    r = D.FrameShardRenderer(scene, W, H, cfg, rk, N, FakeDist(), own_slots=OWN, frames_in_flight=K)
+    for kv in filter(None, os.environ.get("PT_UNIFORMS", "").split(",")):  # name=value,... on the path tracer
+        name, val = kv.split("=")
+        r.pass_path_tracing.set_uniform_int(name, int(val))
+    for _ in range(2 * K + N):  # every band slot and own slot used before timing (first use allocates)
+        r.frame()
+    r.r.flush()
+    torch.cuda.synchronize()
+    for k in LOG:
+        LOG[k] = 0
+    r.r.back_events = []
+    waits = []  # host time blocked on the G-buffer motion bound (BandRenderer._motion): the GPU being full
+    orig_motion = D.BandRenderer._motion
+
+    def timed_motion(self):
+        tw = time.perf_counter()
+        orig_motion(self)
+        waits.append(time.perf_counter() - tw)
+    D.BandRenderer._motion = timed_motion
+    t0 = time.perf_counter()
+    c0 = time.process_time()
+    for _ in range(FRAMES):
+        r.frame()
+    issue = (time.perf_counter() - t0) / FRAMES
+    cpu = (time.process_time() - c0) / FRAMES
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / FRAMES
+    D.BandRenderer._motion = orig_motion
+    r.r.flush()
+    torch.cuda.synchronize()
+    ev = [(a, b) for a, b in r.r.back_events if b is not None]
+    r.r.back_events = None
+    busy = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
+    out = dict(rows=(r.plan.y0, r.plan.y1), wall=wall * 1e3, issue=issue * 1e3, cpu=cpu * 1e3, back=busy,
+               wait=sum(waits) / FRAMES * 1e3,
+               halo_mb=LOG["halo"] / FRAMES / 1e6, send_mb=LOG["send"] / FRAMES / 1e6,
+               recv_mb=LOG["recv"] / FRAMES / 1e6)
+    r.close()
+    return out
+
+
+if __name__ == "__main__":
+    ranks = [int(v) for v in os.environ["RANKS"].split(",")] if "RANKS" in os.environ else range(N)
+    print(f"--- frame shard: N={N} {W}x{H} K={K} own slots {OWN}, {FRAMES} frames per rank, "
+          f"links {XLAT_US:g} us + bytes / {XGBS:g} GB/s", flush=True)
+    res = []
+    for rk in ranks:
+        s = sim_rank(rk)
+        res.append(s)
+        print(f"rank {rk}: rows {s['rows'][0]}..{s['rows'][1]} wall {s['wall']:.3f} ms/frame ({1e3 / s['wall']:.1f} fps) "
+              f"issue {s['issue']:.3f} (host cpu {s['cpu']:.3f}, motion wait {s['wait']:.3f})  SVGF stream busy {s['back']:.3f} ms/frame  per frame: "
+              f"halo {s['halo_mb']:.2f} MB, sent {s['send_mb']:.1f} MB, received {s['recv_mb']:.1f} MB", flush=True)
+    mx = max(s["wall"] for s in res)
+    print(f"predicted frame (slowest simulated rank): {mx:.3f} ms = {1e3 / mx:.1f} fps")
+    gl.shutdown()
