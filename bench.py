@@ -47,7 +47,7 @@ ATROUS_BYTES_BG_PX = 36      # a background pixel: depth-fwidth/flag 4 + illum 1
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8 TB/s spec
 METRIC = "frames/sec @1spp+SVGF, 1080p & 4K; à-trous HBM GB/s vs peak"  # BASELINE.json "metric"
 ATROUS_KERNEL = "atrous_tile_kernel"
-EXCHANGE_STAGES = ("reproject", "variance", "atrous0", "atrous1", "atrous2", "atrous3", "atrous4", "taa")
+EXCHANGE_STAGES = ("history", "reproject", "variance", "atrous0", "atrous1", "atrous2", "atrous3", "atrous4", "taa")
 # planes compared bitwise between the gathered bands and the one-GPU frame (--gpus N > 1)
 PARITY_PLANES = ("color", "albedo", "reproj_illum", "variance", "history_illum", "atrous", "modulate")
 # HBM bytes per a-trous launch measured with rocprofv3 PMC passes (tools/gpu_profile.sh), committed under profiles/,

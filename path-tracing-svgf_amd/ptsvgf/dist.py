@@ -209,12 +209,13 @@ def _meet(a: tuple, b: tuple) -> tuple:
     return max(a[0], b[0]), min(a[1], b[1])
 
 
-def halo_exchange(items, plan: BandPlan, dist, group=None) -> None:
+def halo_exchange(items, plan: BandPlan, dist, group=None, wait: bool = True):
     """Fill the ghost rows each (tensor, n) item reads: every rank sends the rows of its band that another rank's
-    n-row halo covers. Tensors are (rows, W, C) holding global rows [row0, row1) of this rank."""
+    n-row halo covers. Tensors are (rows, W, C) holding global rows [row0, row1) of this rank. wait=False (RCCL):
+    return the works instead of making the current stream wait for them (gloo is host-blocking either way)."""
     items = [(t, int(n)) for t, n in items if int(n) > 0]
     if plan.world == 1 or not items:
-        return
+        return []
     if max(n for _, n in items) > plan.ghost:
         raise RuntimeError(f"halo of {max(n for _, n in items)} rows exceeds the {plan.ghost} ghost rows")
     if items[0][0].is_cuda and dist.get_backend(group) == "gloo":
@@ -223,14 +224,17 @@ def halo_exchange(items, plan: BandPlan, dist, group=None) -> None:
         halo_exchange(host, plan, dist, group)
         for (t, _), (h, _) in zip(items, host):
             t.copy_(h)
-        return
+        return []
     ops = []
     for t, n in items:
         for send, a, b, k in plan.halo_parts(n):
             ops.append(dist.P2POp(dist.isend if send else dist.irecv, t[a - plan.row0:b - plan.row0], k, group))
-    if ops:
-        for req in dist.batch_isend_irecv(ops):
+    works = dist.batch_isend_irecv(ops) if ops else []
+    if wait:
+        for req in works:
             req.wait()
+        return []
+    return works
 
 
 def run_stage(stage: str, planes: dict, plan: BandPlan, dist, group=None) -> None:
@@ -308,9 +312,11 @@ class BandRenderer:
         if kw.get("frames_in_flight", 1) == 1:  # exchanges run on torch's stream: the draws must too
             from ._lib import check, pt
             check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
+        self._hist_works = None  # ghost zone: the next frame's history exchange, started early
         if ghost_zone:
             kw["gbuffer_rows"] = (self.plan.row0, self.plan.row1)
             kw["stage_rows"] = self.plan.stage_rows
+            kw["early_history"] = self._early_history
         self.r = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, tex_factory=factory,
                           halo=self._halo, after_gbuffer=self._after_gbuffer, **kw)
         if ghost_zone:  # the G-buffer marks the a-trous tiles of the rows the a-trous passes draw
@@ -347,20 +353,56 @@ class BandRenderer:
             self._mb_host[b:b + 1].copy_(self._mb_dev[b:b + 1], non_blocking=True)
             self._mb_event[b].record(stream)
 
-    def _motion(self) -> None:
-        """History reach of the frame whose back end is being issued: wait for its G-buffer's bound (issued with
-        its front end, back_lag frames earlier), MAX over ranks on the host."""
+    def _motion(self, b: int | None = None) -> int:
+        """History reach of the frame whose back end is being issued (or of G-buffer set b): wait for its G-buffer's
+        bound (issued with its front end, back_lag frames earlier), MAX over ranks on the host."""
         import numpy as np
 
-        b = self.r.back_set
+        b = self.r.back_set if b is None else b
         self._mb_event[b].synchronize()
         m = float(self._mb_host[b:b + 1].numpy().view(np.float32)[0])
         m = allreduce_motion(m, self.dist, self._group)
         n = self.plan.set_motion(m)
         self.motion_log.append((m * self.plan.H, n))
+        return n
+
+    def _early_history(self, handles: dict, next_set) -> None:
+        """Ghost zone, Renderer early_history: the a-trous iteration that writes the next frame's history has been
+        issued (frame f); when the next frame's front end is issued too (G-buffer set next_set), size its history
+        exchange from that G-buffer's motion bound and start it now, so it overlaps the rest of frame f's chain.
+        Frame f + 1's reprojection waits for it."""
+        if not self.exchange or next_set is None or self._hist_works is not None:
+            return
+        import torch
+
+        cur = self.plan.motion
+        n = self._motion(next_set)
+        self.plan.motion = cur  # frame f's TAA stage still reads frame f's reach
+        planes = {k: self._tensors[h] for k, h in handles.items()}
+        rows = self.plan.margins["reproject"] + n
+        e0 = None
+        if self.stage_events is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        works = halo_exchange([(planes["prev_illum"], rows), (planes["prev_moments"], rows)], self.plan, self.dist,
+                              wait=False)
+        self._hist_works = (works, n, e0)
 
     def _halo(self, stage: str, handles: dict) -> None:
         if not self.exchange:
+            return
+        if stage == "reproject" and self._hist_works is not None:  # started early (_early_history): wait for it
+            import torch
+
+            works, n, e0 = self._hist_works
+            self._hist_works = None
+            self.plan.motion = n
+            for w in works:
+                w.wait()
+            if e0 is not None and self.stage_events is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                self.stage_events.append(("history", e0, e1))
             return
         if stage == "reproject":
             self._motion()

@@ -59,7 +59,7 @@ class Renderer:
                  atrous_exact: bool = False, run_taa: bool = True, run_output: bool = True, tex_factory=None,
                  halo=None, gbuffer_rows=None, frames_in_flight: int = 1, after_gbuffer=None, back_lag: int = 0,
                  trace_batch: int = 1, front_streams: int | None = None, pt_source=None, pt_flush=None,
-                 stage_rows=None):
+                 stage_rows=None, early_history=None):
         """band = (y0, y1, row0, rows) for screen-band sharding; tex_factory(w, h) -> handle allocates the
         frame-sized planes (ptsvgf.dist wraps torch tensors); halo(stage, {plane name: handle}) is called before
         the SVGF passes that read rows beyond the band (dist.HALO_SCHEDULE names the planes); after_gbuffer(set,
@@ -156,6 +156,7 @@ class Renderer:
         self._pt_source = pt_source
         self._pt_flush = pt_flush
         self._stage_rows = stage_rows
+        self._early_history = early_history
         self._ready = None  # pt_source's event for the front end being issued
         self._batch: list = []  # path-tracing passes of the open batch: (pass, G-buffer-done event, stream, holder)
         self._pending: list = []  # front ends whose back end is not issued yet (back_lag)
@@ -624,6 +625,11 @@ class Renderer:
             self._rows(ap, "atrous")
             self._draw(ap, "atrous")
             src = self._atrous_tex(dests[i])
+            if i == 1 and self._early_history is not None:  # the next frame's history is written
+                nxt = self._pending[0] if self._pending and self._pending[0]["f"] == f + 1 else None
+                with self._on_back():
+                    self._early_history({"prev_illum": self.hist_illum[b], "prev_moments": self.moments[b]},
+                                        None if nxt is None else (f + 1) % ng)
         self.atrous_final = src
         mp = self.svgf_modulate_pass
         mp.reset_texture_slot()
@@ -710,15 +716,20 @@ class Renderer:
         _set_stream(stream)
         self._lib_stream = stream
 
+    def _on_back(self):
+        """Context: torch's current stream = the back end's (exchanges issue on the current stream)."""
+        import contextlib
+
+        if self.K > 1:
+            import torch
+
+            return torch.cuda.stream(self._back)
+        return contextlib.nullcontext()
+
     def _halo(self, stage: str, handles: dict) -> None:
         if self._halo_cb is None:
             return
-        if self.K > 1:  # the exchange belongs to the back-end stream (torch.distributed uses the current one)
-            import torch
-
-            with torch.cuda.stream(self._back):
-                self._halo_cb(stage, handles)
-        else:
+        with self._on_back():
             self._halo_cb(stage, handles)
 
     def _draw(self, p: RenderPass, name: str) -> None:

@@ -48,4 +48,7 @@ def test_bench_band_parity_gloo(world, moving, balance, shard):
     if shard == "frames":
         assert line["bands"]["scatter_mb_per_traced_frame"] > 0
     ex = line["bands"]["exchange_ms_per_frame"]
-    assert {"reproject", "variance", "atrous0", "atrous4"} <= set(ex)
+    if shard == "bands":
+        assert {"reproject", "variance", "atrous0", "atrous4"} <= set(ex)
+    else:  # ghost zone: the history exchange only, started early (overlapping the previous frame's chain)
+        assert "history" in ex and not {"variance", "atrous0", "atrous4"} & set(ex), ex

@@ -66,7 +66,7 @@ def _spin(us):
     torch.cuda._sleep(int(us * _CYC_PER_US))
 
 
-def fake_exchange(items, plan, dist, group=None):
+def fake_exchange(items, plan, dist, group=None, wait=True):
     """Record the bytes the real exchange would send and receive (ghost-bounded) and stand in for its time."""
     sent_b = recv_b = 0
     for t, n in items:
@@ -114,10 +114,11 @@ def sim_rank(rk, bounds, probe=False, K=30):
     waits = []  # host time blocked on the G-buffer motion bound (BandRenderer._motion)
     orig_motion = D.BandRenderer._motion
 
-    def timed_motion(self):
+    def timed_motion(self, *a):
         tw = time.perf_counter()
-        orig_motion(self)
+        n = orig_motion(self, *a)
         waits.append(time.perf_counter() - tw)
+        return n
     D.BandRenderer._motion = timed_motion
     r.r.back_events = []
     t0 = time.perf_counter()

@@ -66,7 +66,7 @@ def _xfer_us(nbytes):
     return XLAT_US + (nbytes / (XGBS * 1e3) if XGBS > 0 else 0.0)
 
 
-def fake_exchange(items, plan, dist, group=None):
+def fake_exchange(items, plan, dist, group=None, wait=True):
     sent_b = recv_b = 0
     for t, n in items:
         if plan.world == 1 or n <= 0:
@@ -80,6 +80,7 @@ def fake_exchange(items, plan, dist, group=None):
     if sent_b or recv_b:
         LOG["halo"] += max(sent_b, recv_b)
         _spin(_xfer_us(max(sent_b, recv_b)))
+    return []
 
 
 def fake_window(window, plan, dist, group=None):
@@ -134,10 +135,11 @@ def sim_rank(rk):
     waits = []  # host time blocked on the G-buffer motion bound (BandRenderer._motion): the GPU being full
     orig_motion = D.BandRenderer._motion
 
-    def timed_motion(self):
+    def timed_motion(self, *a):
         tw = time.perf_counter()
-        orig_motion(self)
+        n = orig_motion(self, *a)
         waits.append(time.perf_counter() - tw)
+        return n
     D.BandRenderer._motion = timed_motion
     t0 = time.perf_counter()
     c0 = time.process_time()
