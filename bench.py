@@ -94,7 +94,7 @@ def parse():
     ap.add_argument("--shard", default="frames", choices=("frames", "bands"),
                     help="multi-GPU: 'frames' = rank f %% N traces frame f whole and scatters its rows to the band owners, "
                          "the SVGF chain banded (dist.FrameShardRenderer); 'bands' = every pass banded (dist.BandRenderer)")
-    ap.add_argument("--own-slots", type=int, default=3,
+    ap.add_argument("--own-slots", type=int, default=4,
                     help="--shard frames: whole frames a rank traces at once (its path tracer's frames in flight)")
     ap.add_argument("--breakdown", action="store_true", help="print per-pass ms to stderr")
     ap.add_argument("--pt-kernel", type=int, default=0, help="0 wavefront (production), 1 megakernel (A/B)")
@@ -298,8 +298,10 @@ def main():
         args.frames_in_flight = 4 if world <= 4 else 8
         k1080 = 6 if world == 1 else 8
         if world > 1 and args.shard == "frames":
-            # band slots cover another rank's whole-frame path tracer: a band's SVGF of frame f starts when f arrives
-            args.frames_in_flight = k1080 = 4 * world + 2
+            # band slots cover another rank's whole-frame path tracer: a band's SVGF of frame f starts when f's window
+            # has arrived (simulated, tools/frame_shard_sim.py: N = 2 K = 10 / 16 / 24: 294 / 333 / 321 fps; N = 8
+            # K = 34 / 50 within noise)
+            args.frames_in_flight = k1080 = max(16, 4 * world + 2)
     if args.trace_batch is None:
         args.trace_batch = 1
     # every frame slot must have run once before the timed region (a slot's first frame allocates its

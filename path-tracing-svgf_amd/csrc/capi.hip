@@ -196,8 +196,6 @@ struct Pass {
   uint32_t program = 0;
   WFBuffers wf;
   TileOrder order;
-  hipStream_t aux = nullptr;                   // path tracer: stream for the concurrent closest-hit trace
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int W = 0, H = 0;
   std::vector<uint32_t> att;
   bool bound = false, final_pass = false;
@@ -1250,13 +1248,7 @@ int draw_pathtrace(Pass* p) {
     TRY(wf_alloc(p->wf, k.W, std::max(0, k.y1 - k.y0)));
     if (wf_spill(p->wf, k.stack_need) != PT_OK) return err(PT_ERR_HIP, "spill stack allocation failed");
     TRY(pt_wf_setup(p, k, sg, p->wf.st));
-    if (ui(p, "trace_fork", 0) && !p->aux) {  // A/B switch (off: measured slower with frames in flight)
-      HIPCHK(hipStreamCreateWithFlags(&p->aux, hipStreamNonBlocking));
-      HIPCHK(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
-      HIPCHK(hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
-    }
-    const bool fork = ui(p, "trace_fork", 0) && !g.profiling;  // profiling times each draw on one stream
-    rc = launch_pathtrace_wavefront(k, g.stream, fork ? p->aux : nullptr, p->ev_fork, p->ev_join);
+    rc = launch_pathtrace_wavefront(k, g.stream);
     if (!rc && k.tiles.cost) p->order.ordered = true;
   }
   return rc ? hip_err((hipError_t)rc, "pathtrace launch") : PT_OK;
@@ -1570,9 +1562,6 @@ int pt_shutdown(void) {
     if (p->wf.spill) (void)hipFree(p->wf.spill);
     if (p->order.cost) (void)hipFree(p->order.cost);
     if (p->order.perm) (void)hipFree(p->order.perm);
-    if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
-    if (p->ev_join) (void)hipEventDestroy(p->ev_join);
-    if (p->aux) (void)hipStreamDestroy(p->aux);
     if (p->ev0) (void)hipEventDestroy(p->ev0);
     if (p->ev1) (void)hipEventDestroy(p->ev1);
   }
@@ -2225,9 +2214,6 @@ int pt_pass_destroy(uint32_t pass) {
   if (p->wf.spill) (void)hipFree(p->wf.spill);
   if (p->order.cost) (void)hipFree(p->order.cost);
   if (p->order.perm) (void)hipFree(p->order.perm);
-  if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
-  if (p->ev_join) (void)hipEventDestroy(p->ev_join);
-  if (p->aux) (void)hipStreamDestroy(p->aux);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
   g.passes.erase(it);

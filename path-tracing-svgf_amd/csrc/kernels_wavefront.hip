@@ -1115,8 +1115,7 @@ __global__ void __launch_bounds__(256) PT_SHADE_ATTR wf_shade(PTParams p, int bo
       v3 L = sample_brdf(xi1, xi2, xi3, V, h.normal, h.m);
       if (dot(h.normal, L) > 0.0f) {
         push = true;
-        lbin = ((L.x < 0.0f) | ((L.y < 0.0f) << 1) | ((L.z < 0.0f) << 2)) & (kLiveBins - 1);
-        v3 brdf = brdf_eval(V, h.normal, L, h.m);
+                v3 brdf = brdf_eval(V, h.normal, L, h.m);
         float bpdf = brdf_pdf(V, h.normal, L, h.m);
         // hdriLight, evaluated as if unoccluded (:922-946)
         float r1 = u32_to_unit(wang_hash(&seed));
@@ -1237,8 +1236,7 @@ int wf_subset_tiles(int W, int rows, int stride, int offset) {
 // kernels run per frame). Frame b's wavefront state lies at pid offset b * N of ps[0]'s, its counters at
 // ps[0].wf.counters + b * kWfCounters; the batched launches use frame 0's work-queue heads and straggler lists.
 template <int KS, bool DEEP>
-int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, hipStream_t aux, hipEvent_t ev_fork,
-                     hipEvent_t ev_join) {
+int launch_wavefront(const PTParams* ps, int nb, hipStream_t s) {
   const PTParams& p = ps[0];
   const int rows = p.y1 - p.y0;
   if (rows <= 0) return 0;
@@ -1271,11 +1269,11 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, hipStream_t aux,
   }
   const int gN = (N + 255) / 256, gT = (N + kTB - 1) / kTB, gT2 = (2 * N + kTB - 1) / kTB;
   const int gS0 = ntiles;  // bounce-0 shade: one block per primary tile
-  const bool fork = aux && ev_fork && ev_join && nb == 1;
   auto lst = [&](const PTParams& f, int i) { return (i & 1) ? f.wf.list1 : f.wf.list0; };  // bounce i's live list
   const bool refill_closest = p.refill && p.closest_tree && p.prune && p.scene.bvh_any;
   const bool wide = !DEEP && p.refill && p.scene.bvh4;  // the refill walks on the 4-wide any-hit tree
-  auto closest = [&](int i, hipStream_t st) {
+  auto closest = [&](int i) {
+    hipStream_t st = s;
     if (refill_closest) {
       ListBatch lb{nb, N, {}, {}};
       for (int b = 0; b < nb; ++b) {
@@ -1300,25 +1298,13 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, hipStream_t aux,
     }
   };
   for (int i = 0; i < p.max_depth; ++i) {
-    if (i > 0) {
-      if (fork) {
-        if ((e = hipStreamWaitEvent(s, ev_join, 0)) != hipSuccess) return (int)e;  // closest(i) done
-      } else {
-        closest(i, s);
-      }
-    }
+    if (i > 0) closest(i);
     for (int b = 0; b < nb; ++b) {
       const PTParams& f = ps[b];
       const int* live_in = f.wf.counters + kWfCtr * (i > 0 ? i - 1 : 0);
       hipLaunchKernelGGL(wf_shade, dim3(i == 0 ? gS0 : gN), dim3(256), 0, s, f, i, (const int*)lst(f, i + 1), live_in,
                          lst(f, i), f.wf.counters + kWfCtr * i, f.wf.shadow_list, f.wf.counters + kWfCtr * i + kCtrHdr,
                          cap);
-    }
-    if (fork && i + 1 < p.max_depth) {  // closest(i+1) on aux, beside shadow(i) + finish(i)
-      if ((e = hipEventRecord(ev_fork, s)) != hipSuccess) return (int)e;
-      if ((e = hipStreamWaitEvent(aux, ev_fork, 0)) != hipSuccess) return (int)e;
-      closest(i + 1, aux);
-      if ((e = hipEventRecord(ev_join, aux)) != hipSuccess) return (int)e;
     }
     if (p.refill) {
       ListBatch lb{nb, N, {}, {}};
@@ -1360,19 +1346,18 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, hipStream_t aux,
   return (int)hipGetLastError();
 }
 
-int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux, hipEvent_t ev_fork,
-                               hipEvent_t ev_join) {
+int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s) {
   // the LDS stack bounds resident waves: a tree that fits the small stack gets more of them
-  if (p.wf.spill) return launch_wavefront<kSpillKS, true>(&p, 1, s, nullptr, nullptr, nullptr);  // deep tree, no fork
-  return p.stack_need <= kStackSmall ? launch_wavefront<kStackSmall, false>(&p, 1, s, aux, ev_fork, ev_join)
-                                     : launch_wavefront<kStack, false>(&p, 1, s, aux, ev_fork, ev_join);
+  if (p.wf.spill) return launch_wavefront<kSpillKS, true>(&p, 1, s);  // deep tree
+  return p.stack_need <= kStackSmall ? launch_wavefront<kStackSmall, false>(&p, 1, s)
+                                     : launch_wavefront<kStack, false>(&p, 1, s);
 }
 
 int launch_pathtrace_wavefront_batch(const PTParams* ps, int nb, hipStream_t s) {
   if (nb < 1 || nb > kMaxBatch) return (int)hipErrorInvalidValue;
-  if (ps[0].wf.spill) return launch_wavefront<kSpillKS, true>(ps, nb, s, nullptr, nullptr, nullptr);
-  return ps[0].stack_need <= kStackSmall ? launch_wavefront<kStackSmall, false>(ps, nb, s, nullptr, nullptr, nullptr)
-                                         : launch_wavefront<kStack, false>(ps, nb, s, nullptr, nullptr, nullptr);
+  if (ps[0].wf.spill) return launch_wavefront<kSpillKS, true>(ps, nb, s);
+  return ps[0].stack_need <= kStackSmall ? launch_wavefront<kStackSmall, false>(ps, nb, s)
+                                         : launch_wavefront<kStack, false>(ps, nb, s);
 }
 
 }  // namespace ptk

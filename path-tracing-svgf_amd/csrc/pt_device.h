@@ -53,10 +53,7 @@ constexpr int kSpillKS = PT_SPILL_KS;
 constexpr int kBlock = 256;      // threads per block for per-pixel kernels
 constexpr int kNoneRef = (int)0x80000000;
 constexpr int kPointBins = 4;     // point-light shadow lists, one per light index mod 4 (coherent waves)
-#ifndef PT_LIVE_BINS
-#define PT_LIVE_BINS 1
-#endif
-constexpr int kLiveBins = PT_LIVE_BINS;  // live-ray lists by direction octant: 8 measured 4 % slower than 1
+constexpr int kLiveBins = 1;  // live-ray lists (by direction octant, 8 of them, measured 4 % slower: one list)
 // wavefront list counters per bounce (8 segments each): live bins, HDR shadow, point bins, straggler count
 constexpr int kCtrHdr = 8 * kLiveBins, kCtrPoint = kCtrHdr + 8, kCtrStrag = kCtrPoint + 8 * kPointBins;
 // per-XCD work-queue heads of the refill traversal kernels launched in bounce i: shadow rays, closest-hit rays
@@ -309,8 +306,7 @@ struct TAAParams {
 namespace ptk {
 // Launchers (kernels_*.hip). Return hipError_t as int.
 int launch_pathtrace(const PTParams& p, hipStream_t s);
-int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s, hipStream_t aux = nullptr,
-                               hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr);
+int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s);
 int wf_list_capacity(int W, int rows);  // per-segment capacity of the compacted ray lists (8 segments)
 int wf_subset_tiles(int W, int rows, int stride, int offset);  // tiles of a PTParams tile subset (< 0: invalid)
 int launch_gbuffer(const GBufParams& p, hipStream_t s);

@@ -203,11 +203,6 @@ class Renderer:
             import torch  # streams and events are torch plumbing (the kernels are the library's)
 
             self._streams = [torch.cuda.Stream() for _ in range(self._nfs)]
-            # A/B switch, off by default: with K frames in flight the extra streams measured slower.
-            # Its streams exist only when it is on: every stream beyond the process's hardware queues
-            # (GPU_MAX_HW_QUEUES) shares a queue, in order, with another stream.
-            self._gfork = os.environ.get("PTSVGF_GBUFFER_FORK", "0") != "0"
-            self._gstreams = [torch.cuda.Stream() for _ in range(self.K)] if self._gfork else None
             # the SVGF back end is a chain of short launches (and, on bands, exchanges) beside the front ends' long
             # traversal launches: on a high-priority queue its kernels take CUs as soon as waves retire instead of
             # queueing behind resident traversal waves (PTSVGF_BACK_PRIORITY=0: normal priority, A/B)
@@ -511,24 +506,9 @@ class Renderer:
                 fe.wait_event(self._slot_free[f % self.K])
             if self.accumulate and self._fe_prev is not None:  # lastFrame = the previous front end's colour
                 fe.wait_event(self._fe_prev)
-            # the G-buffer and the path tracer are independent (both need only the camera): the G-buffer runs on
-            # a side stream beside the path tracer, so the two launches' tails overlap
             self._ready = None
-            if self._gfork and self._pt_source is None:
-                gs = self._gstreams[f % self.K]
-                start = torch.cuda.Event()
-                start.record(fe)
-                gs.wait_event(start)
-                self._stream_to(gs)
-                self._gbuffer(f % ng)
-                gdone = torch.cuda.Event()
-                gdone.record(gs)
-                self._stream_to(fe)
-                self._path_trace()
-                fe.wait_event(gdone)
-            else:
-                self._stream_to(fe)
-                self._gbuffer_and_pt(f % ng)
+            self._stream_to(fe)
+            self._gbuffer_and_pt(f % ng)
             done = torch.cuda.Event()
             done.record(fe)
             self._fe_prev = done

@@ -100,7 +100,6 @@ def sim_rank(rk, bounds, probe=False, K=30):
     r = D.BandRenderer(scene, W, H, cfg, rk, N, FakeDist(), bounds=bounds,
                        frames_in_flight=int(os.environ.get("FIF", "1")), trace_batch=int(os.environ.get("BATCH", "1")))
     r.pass_path_tracing.set_uniform_int("pt_kernel", int(os.environ.get("PTK", "0")))
-    r.pass_path_tracing.set_uniform_int("trace_fork", int(os.environ.get("PTSVGF_TRACE_FORK", "0")))
     if "SHADOW_BUDGET" in os.environ:
         r.pass_path_tracing.set_uniform_int("shadow_budget", int(os.environ["SHADOW_BUDGET"]))
     for kv in filter(None, os.environ.get("PT_UNIFORMS", "").split(",")):  # name=value,... on the path tracer

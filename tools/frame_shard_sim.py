@@ -66,21 +66,48 @@ def _xfer_us(nbytes):
     return XLAT_US + (nbytes / (XGBS * 1e3) if XGBS > 0 else 0.0)
 
 
+class FakeWork:
+    """A stood-in transfer running on the comm stream: wait() makes the current stream wait for it (as RCCL's)."""
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
+_COMM = None
+
+
 def fake_exchange(items, plan, dist, group=None, wait=True):
-    sent_b = recv_b = 0
+    """halo_exchange stand-in: the transfers to / from each peer run over that peer's link at once, so a batch lasts
+    latency + the largest per-peer volume / bandwidth. wait=True: on the current stream (it waits anyway);
+    wait=False (the ghost zone's early history exchange): on a comm stream after the current stream's work, the
+    caller's later wait() joins it, as RCCL's stream does."""
+    global _COMM
+    per_peer = {}
     for t, n in items:
         if plan.world == 1 or n <= 0:
             continue
         row = t.shape[1] * t.shape[2] * 4
-        for send, a, b, _ in plan.halo_parts(n):
-            if send:
-                sent_b += row * (b - a)
-            else:
-                recv_b += row * (b - a)
-    if sent_b or recv_b:
-        LOG["halo"] += max(sent_b, recv_b)
-        _spin(_xfer_us(max(sent_b, recv_b)))
-    return []
+        for send, a, b, k in plan.halo_parts(n):
+            per_peer[(send, k)] = per_peer.get((send, k), 0) + row * (b - a)
+    if not per_peer:
+        return []
+    LOG["halo"] += sum(v for (snd, _), v in per_peer.items() if snd)
+    us = _xfer_us(max(per_peer.values()))
+    if wait:
+        _spin(us)
+        return []
+    if _COMM is None:
+        _COMM = torch.cuda.Stream()
+    start = torch.cuda.Event()
+    start.record()
+    _COMM.wait_event(start)
+    with torch.cuda.stream(_COMM):
+        _spin(us)
+    done = torch.cuda.Event()
+    done.record(_COMM)
+    return [FakeWork(done)]
 
 
 def fake_window(window, plan, dist, group=None):
@@ -116,8 +143,8 @@ check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
 scene = build_scene("table_clock_plant")
 cfg = parameter_config()
 FRAMES = int(os.environ.get("FRAMES", str(max(96, 24 * N))))
-OWN = int(os.environ.get("OWN", "3"))
-K = int(os.environ.get("K", str(4 * N + 2)))
+OWN = int(os.environ.get("OWN", "4"))
+K = int(os.environ.get("K", str(max(16, 4 * N + 2))))  # bench.py's defaults
 
 
 def sim_rank(rk):
@@ -155,8 +182,15 @@ def sim_rank(rk):
     ev = [(a, b) for a, b in r.r.back_events if b is not None]
     r.r.back_events = None
     busy = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
+    r.profile(True)  # the band's passes alone (a draw at a time, synchronised): the floor of its SVGF stream
+    for _ in range(N):
+        r.frame()
+    r.r.flush()
+    torch.cuda.synchronize()
+    pp = r.pass_times()
+    r.profile(False)
     out = dict(rows=(r.plan.y0, r.plan.y1), wall=wall * 1e3, issue=issue * 1e3, cpu=cpu * 1e3, back=busy,
-               wait=sum(waits) / FRAMES * 1e3,
+               wait=sum(waits) / FRAMES * 1e3, pp={k: v / N for k, v in pp.items()},
                halo_mb=LOG["halo"] / FRAMES / 1e6, send_mb=LOG["send"] / FRAMES / 1e6,
                recv_mb=LOG["recv"] / FRAMES / 1e6)
     r.close()
@@ -174,6 +208,8 @@ if __name__ == "__main__":
         print(f"rank {rk}: rows {s['rows'][0]}..{s['rows'][1]} wall {s['wall']:.3f} ms/frame ({1e3 / s['wall']:.1f} fps) "
               f"issue {s['issue']:.3f} (host cpu {s['cpu']:.3f}, motion wait {s['wait']:.3f})  SVGF stream busy {s['back']:.3f} ms/frame  per frame: "
               f"halo {s['halo_mb']:.2f} MB, sent {s['send_mb']:.1f} MB, received {s['recv_mb']:.1f} MB", flush=True)
+        print("   passes alone, ms per frame: " + " ".join(f"{k} {v:.3f}" for k, v in sorted(s["pp"].items())),
+              flush=True)
     mx = max(s["wall"] for s in res)
     print(f"predicted frame (slowest simulated rank): {mx:.3f} ms = {1e3 / mx:.1f} fps")
     gl.shutdown()
