@@ -49,7 +49,7 @@ VARIANCE_HALO = 3
 REPROJ_REACH = 3  # rows beyond |motion| the history taps reach: bilinear + 1-texel tap / 3x3 fallback + rounding
 TAA_NEIGHBOURS = 2  # rows of the TAA 3x3 neighbourhood: +-1 texel, plus the LINEAR sampler's zero-weight row
 GHOST = 96        # default stored rows either side of a band (storage only); motion up to GHOST - 3 rows per frame
-GHOST_ZONE_GHOST = 128  # ghost zone: 65 margin rows + 3 + up to 60 rows of motion per frame
+GHOST_ZONE_GHOST = 128  # ghost zone: storage for 65 margin rows + up to 63 rows of history reach per frame
 MIN_BAND_ROWS = 16
 BAND_VISIT_BUDGET = 256  # shadow / closest-hit visits before a band's ray goes to the cooperative walk
 BAND_REFILL_WAVES = 1280  # resident waves a band's lane-refill launch is sized for (the chip: 5120)
@@ -134,6 +134,23 @@ class BandPlan:
         """Ghost zone: the rows the SVGF pass `stage` draws (the band widened by its margin, clipped to the frame)."""
         m = self.margins[stage]
         return max(0, self.y0 - m), min(self.H, self.y1 + m)
+
+    def gbuffer_rows(self) -> tuple:
+        """Ghost zone: the rows the band's G-buffer draws — the reprojection's rows and the reach of its taps into the
+        previous normal/depth at rest (REPROJ_REACH); a moving camera's further rows arrive with the history
+        (history_items)."""
+        r = self.margins["reproject"] + REPROJ_REACH
+        return max(0, self.y0 - r), min(self.H, self.y1 + r)
+
+    def history_items(self, planes: dict, n: int) -> list:
+        """Ghost zone: the exchanges before the reprojection for a motion reach of n rows (motion_rows): the previous
+        a-trous iteration-1 output and moments over the reprojection's margin + n rows, and the previous normal/depth
+        over as many when n reaches past the G-buffer's own rows."""
+        rows = self.margins["reproject"] + n
+        items = [(planes["prev_illum"], rows), (planes["prev_moments"], rows)]
+        if n > REPROJ_REACH and "prev_nd" in planes:
+            items.append((planes["prev_nd"], rows))
+        return items
 
     def zone(self, k: int) -> tuple:
         """Ghost zone: rows of rank k's band the path tracer's planes must hold (its reprojection's rows)."""
@@ -314,7 +331,7 @@ class BandRenderer:
             check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
         self._hist_works = None  # ghost zone: the next frame's history exchange, started early
         if ghost_zone:
-            kw["gbuffer_rows"] = (self.plan.row0, self.plan.row1)
+            kw["gbuffer_rows"] = self.plan.gbuffer_rows()
             kw["stage_rows"] = self.plan.stage_rows
             kw["early_history"] = self._early_history
         self.r = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, tex_factory=factory,
@@ -379,13 +396,11 @@ class BandRenderer:
         n = self._motion(next_set)
         self.plan.motion = cur  # frame f's TAA stage still reads frame f's reach
         planes = {k: self._tensors[h] for k, h in handles.items()}
-        rows = self.plan.margins["reproject"] + n
         e0 = None
         if self.stage_events is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
-        works = halo_exchange([(planes["prev_illum"], rows), (planes["prev_moments"], rows)], self.plan, self.dist,
-                              wait=False)
+        works = halo_exchange(self.plan.history_items(planes, n), self.plan, self.dist, wait=False)
         self._hist_works = (works, n, e0)
 
     def _halo(self, stage: str, handles: dict) -> None:
@@ -410,8 +425,7 @@ class BandRenderer:
         if self.ghost_zone:  # only the histories cross ranks (BandRenderer ghost_zone)
             p = self.plan
             if stage == "reproject":
-                items = [(planes["prev_illum"], p.margins["reproject"] + p.motion),
-                         (planes["prev_moments"], p.margins["reproject"] + p.motion)]
+                items = p.history_items(planes, p.motion)
             elif stage == "taa":
                 items = [(planes["prev_taa"], p.motion)]
             else:

@@ -608,8 +608,8 @@ class Renderer:
             if i == 1 and self._early_history is not None:  # the next frame's history is written
                 nxt = self._pending[0] if self._pending and self._pending[0]["f"] == f + 1 else None
                 with self._on_back():
-                    self._early_history({"prev_illum": self.hist_illum[b], "prev_moments": self.moments[b]},
-                                        None if nxt is None else (f + 1) % ng)
+                    self._early_history({"prev_illum": self.hist_illum[b], "prev_moments": self.moments[b],
+                                         "prev_nd": g["normal_depth"]}, None if nxt is None else (f + 1) % ng)
         self.atrous_final = src
         mp = self.svgf_modulate_pass
         mp.reset_texture_slot()

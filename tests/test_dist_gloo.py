@@ -55,10 +55,11 @@ def _worker(rank, world, port, W, H, frames, moves, bounds=None, ghost=None, sha
 
         def halo(stage, arrays):
             if gz:  # the histories only (BandRenderer ghost_zone)
-                n = {"reproject": plan.margins["reproject"] + plan.motion, "taa": plan.motion}.get(stage)
-                if n is not None:
-                    halo_exchange([(torch.from_numpy(a)[plan.row0:plan.row1], n) for k, a in arrays.items()
-                                   if k in ("prev_illum", "prev_moments", "prev_taa")], plan, dist)
+                t = {k: torch.from_numpy(a)[plan.row0:plan.row1] for k, a in arrays.items()}
+                if stage == "reproject":
+                    halo_exchange(plan.history_items(t, plan.motion), plan, dist)
+                elif stage == "taa":
+                    halo_exchange([(t["prev_taa"], plan.motion)], plan, dist)
                 return
             run_stage(stage, {k: torch.from_numpy(a)[plan.row0:plan.row1] for k, a in arrays.items()}, plan, dist)
 
@@ -76,8 +77,8 @@ def _worker(rank, world, port, W, H, frames, moves, bounds=None, ghost=None, sha
             cam.update()
             view, proj = cam.cam_view_mat, cam.cam_proj_mat
             g = O.gbuffer(scene.raster, W, H, view, proj, band.pre_viewproj, 2)
-            for k in g:                      # the G-buffer computes the owned rows only (ghost zone: every stored row)
-                poison(g[k], *((plan.row0, plan.row1) if gz else (plan.y0, plan.y1)))
+            for k in g:                      # the G-buffer computes the owned rows only (ghost zone: gbuffer_rows)
+                poison(g[k], *(plan.gbuffer_rows() if gz else (plan.y0, plan.y1)))
             if shard == "bands":
                 col, em, al = band.os.path_trace(W, H, cam.frameCounter, cam.cam_position, rigid_inverse(view),
                                                  cfg.clamp_threshold, cfg.max_tracing_depth, band.aspect_corrected,

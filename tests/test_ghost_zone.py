@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import oracle_ref as O
-from ptsvgf.dist import GHOST_ZONE_GHOST, REPROJ_REACH, motion_rows, svgf_margins
+from ptsvgf.dist import REPROJ_REACH, motion_rows, svgf_margins
 
 W, H = 24, 280
 Y0, Y1 = 130, 150
@@ -37,7 +37,7 @@ def _inputs(seed, max_motion_rows):
     vel[..., 1] = rng.choice([-max_motion_rows, max_motion_rows], (H, W)) / H  # the largest motion, both ways
     vel[..., 3] = 1.0
     pm = plane(0.0, 1.0)
-    pm[..., 2] = 0.0  # history length 0: every pixel young (7x7 variance), every reprojection blends
+    pm[..., 2] = 1.0  # history length 1 -> 2: young (7x7 variance), and a valid reprojection blends half history
     prev_nd = nd + rng.normal(scale=1e-3, size=nd.shape).astype(np.float32)  # reprojection valid almost everywhere
     prev_nd[..., 3] = nd[..., 3]
     return dict(nd=nd, fwidth=fw, velocity=vel, prev_nd=prev_nd, color=plane(0.0, 2.0), albedo=plane(0.1, 1.0),
@@ -70,16 +70,23 @@ def _chain(inp, rows, taa=True, frame_counter=3):
     return dict(atrous=a, modulate=m, taa=t)
 
 
-def _band_inputs(inp, margins, mrows, history_rows=None, zone=None):
-    """What a band holds: the G-buffer (this frame's and the previous) on every stored row, the path tracer's planes on
-    the reprojection's rows (finite garbage elsewhere), the histories on margin + motion rows (TAA: motion rows)."""
+def _band_inputs(inp, margins, mrows, history_rows=None, zone=None, prev_nd_rows=None):
+    """What a band holds: the G-buffer on the reprojection's rows + REPROJ_REACH (BandPlan.gbuffer_rows), the previous
+    one on as many or, with the history exchange, margin + motion rows; the path tracer's planes on the reprojection's
+    rows (finite garbage elsewhere); the histories on margin + motion rows (TAA: motion rows)."""
     rng = np.random.default_rng(99)
     out = dict(inp)
-    lo, hi = max(0, Y0 - GHOST_ZONE_GHOST), min(H, Y1 + GHOST_ZONE_GHOST)
-    for k in ("nd", "fwidth", "velocity", "prev_nd"):
+    g = margins["reproject"] + REPROJ_REACH  # BandPlan.gbuffer_rows
+    nd_rows = max(g, margins["reproject"] + mrows) if prev_nd_rows is None else prev_nd_rows
+    for k, rr in (("nd", g), ("fwidth", g), ("velocity", g), ("prev_nd", nd_rows)):
         a = inp[k].copy()
-        a[:lo] = np.nan
-        a[hi:] = np.nan
+        lo, hi = max(0, Y0 - rr), min(H, Y1 + rr)
+        if k == "prev_nd":  # NaN would pass the reprojection's validity tests (NaN > threshold is false): a
+            a[:lo] *= np.float32([-1, -1, -1, 1.5])  # surface that fails them (svgf_reproject.frag:26-40)
+            a[hi:] *= np.float32([-1, -1, -1, 1.5])
+        else:
+            a[:lo] = np.nan
+            a[hi:] = np.nan
         out[k] = a
     z = margins["reproject"] if zone is None else zone
     for k in ("color", "albedo", "emission"):  # garbage of the same distribution (edge-stopping weights stay > 0)
@@ -123,7 +130,7 @@ def test_ghost_zone_band_equals_whole_frame(case, taa):
 
 
 @pytest.mark.parametrize("what,taa", [("reproject", False), ("variance", False), ("atrous", False), ("zone", False),
-                                      ("history", False), ("taa_history", True)])
+                                      ("history", False), ("prev_nd", False), ("taa_history", True)])
 def test_ghost_zone_each_margin_is_needed(case, what, taa):
     """One row less anywhere and the band's rows change (or turn NaN). The path tracer's outermost zone row reaches
     the band only through the variance channel of the a-trous output (svgf_Atrous.frag:109-118), which modulate
@@ -133,17 +140,19 @@ def test_ghost_zone_each_margin_is_needed(case, what, taa):
     inp, mrows, full = case
     margins = svgf_margins(ITERS, taa=taa)
     m = dict(margins)
-    zone, hist, taa_rows = None, None, mrows
+    zone, hist, taa_rows, nd_rows = None, None, mrows, None
     if what in m:
         m[what] -= 1
     elif what == "zone":
         zone = margins["reproject"] - 1
     elif what == "history":  # REPROJ_REACH is the taps' reach with rounding slack: cut into the motion itself
         hist = margins["reproject"] + mrows - REPROJ_REACH - 1
+    elif what == "prev_nd":  # the previous normal/depth exchanged with the history, one row short of the motion
+        nd_rows = margins["reproject"] + mrows - REPROJ_REACH - 1
     else:
         taa_rows = mrows - REPROJ_REACH - 1
     band = _band_inputs(inp, margins, taa_rows, history_rows=hist if hist is not None else margins["reproject"] + mrows,
-                        zone=zone)
+                        zone=zone, prev_nd_rows=nd_rows)
     got = _chain(band, _rows_of(m), taa)
     same = [np.array_equal(np.nan_to_num(got[k][Y0:Y1], nan=-1.0).view(np.uint32), full[taa][k][Y0:Y1].view(np.uint32))
             for k in got]
