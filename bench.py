@@ -90,7 +90,8 @@ def parse():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for --gpus > 1 (nccl = RCCL)")
     ap.add_argument("--no-band-parity", action="store_true",
                     help="multi-GPU: skip the untimed bitwise check of the gathered bands against a one-GPU frame")
-    ap.add_argument("--equal-bands", action="store_true", help="multi-GPU: equal band heights (no cost balancing)")
+    ap.add_argument("--equal-bands", action="store_true",
+                    help="multi-GPU: equal band heights (no balancing of the measured band work)")
     ap.add_argument("--shard", default="frames", choices=("frames", "bands"),
                     help="multi-GPU: 'frames' = rank f %% N traces frame f whole and scatters its rows to the band owners, "
                          "the SVGF chain banded (dist.FrameShardRenderer); 'bands' = every pass banded (dist.BandRenderer)")
@@ -348,8 +349,9 @@ def main():
         check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))  # a previous renderer's streams are gone
         log(f"run {W}x{H} K={K} view={view}")
         if world > 1 and args.shard == "frames":
-            from ptsvgf.dist import FrameShardRenderer
-            r = FrameShardRenderer(scene, W, H, cfg, rank, world, dist, own_slots=args.own_slots, frames_in_flight=K)
+            from ptsvgf.dist import make_frame_shard_renderer
+            r = make_frame_shard_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,
+                                          own_slots=args.own_slots, frames_in_flight=K)
         elif world > 1:
             from ptsvgf.dist import make_band_renderer
             r = make_band_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,

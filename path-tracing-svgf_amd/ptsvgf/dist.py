@@ -760,6 +760,28 @@ class FrameShardRenderer(BandRenderer):
         self.r.profile(on)
         self.full.profile(on)
 
+    def band_ms(self, frames: int | None = None) -> float:
+        """This rank's band work per frame (its G-buffer and SVGF passes, each draw timed alone with HIP events;
+        the whole-frame path tracer, the same on every rank, is not counted). Collective: every rank draws the same
+        frames. Calibration only (make_frame_shard_renderer)."""
+        import torch
+
+        frames = frames or 2 * self.plan.world
+        for _ in range(self.r.K + self.plan.world):  # every slot once: first use allocates
+            self.frame()
+        self.r.flush()
+        torch.cuda.synchronize()
+        self.profile(True)
+        try:
+            for _ in range(frames):
+                self.frame()
+            self.r.flush()
+            torch.cuda.synchronize()
+            ms = self.r.pass_times().get("frame_sum_ms", 0.0) / frames
+        finally:
+            self.profile(False)
+        return ms
+
     def pass_times(self) -> dict:
         out = self.r.pass_times()
         for k, v in self.full.pass_times().items():
@@ -840,6 +862,42 @@ def fit_row_cost(visits, rows, ms):
     if A[:, 0].sum() > 0:
         return float(t.sum() / A[:, 0].sum()), 0.0
     return 0.0, float(t.sum() / max(A[:, 1].sum(), 1.0))
+
+
+def make_frame_shard_renderer(scene, W, H, cfg, rank, world, dist, balance: bool = True, rounds: int = 2, **kw):
+    """FrameShardRenderer whose bands equalise the band work (G-buffer + SVGF chain: the plant's rows cost several
+    times a sky row; every rank's whole-frame path tracer is the same). Each round measures every rank's band work
+    (band_ms), spreads it evenly over the band's rows and cuts new bands at equal quantiles of the mean of the rounds'
+    per-row estimates; the measured plan with the smallest slowest band wins and the renderer is rebuilt on it
+    (calibration frames are discarded). Every rank derives the same bounds from all-reduced times."""
+    import numpy as np
+    import torch
+
+    r = FrameShardRenderer(scene, W, H, cfg, rank, world, dist, **kw)
+    if not balance or world == 1:
+        return r
+    est, tried = [], []
+    for i in range(max(rounds, 1) + 1):
+        t = torch.zeros(world, dtype=torch.float64)
+        t[rank] = r.band_ms()
+        dist.all_reduce(t, group=r._group)  # host values: the gloo group (the default group under gloo)
+        times = t.numpy()
+        tried.append((float(times.max()), r.plan.bounds))
+        if i == max(rounds, 1):
+            break
+        b = r.plan.bounds
+        cost = np.empty(H)
+        for k in range(world):
+            cost[b[k]:b[k + 1]] = times[k] / (b[k + 1] - b[k])
+        est.append(cost)
+        bounds = balanced_bounds(np.mean(est, axis=0), world)
+        r.close()
+        r = FrameShardRenderer(scene, W, H, cfg, rank, world, dist, bounds=bounds, **kw)
+    best = min(tried, key=lambda x: x[0])[1]
+    r.close()
+    r = FrameShardRenderer(scene, W, H, cfg, rank, world, dist, bounds=best, **kw)
+    r.calibration = tried  # (slowest band's work ms per frame, bounds) per measured plan
+    return r
 
 
 def make_band_renderer(scene, W, H, cfg, rank, world, dist, balance: bool = True, rounds: int = 3, **kw):

@@ -26,7 +26,7 @@ def _port():
 
 
 @pytest.mark.parametrize("world,moving,balance,shard", [(2, True, True, "bands"), (4, False, False, "bands"),
-                                                        (2, True, False, "frames"), (3, True, False, "frames"),
+                                                        (2, True, False, "frames"), (3, True, True, "frames"),
                                                         (4, True, False, "frames")])
 def test_bench_band_parity_gloo(world, moving, balance, shard):
     """shard = "bands": every rank traces its band; "frames": rank f % N traces frame f whole and scatters the

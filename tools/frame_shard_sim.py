@@ -147,8 +147,9 @@ OWN = int(os.environ.get("OWN", "4"))
 K = int(os.environ.get("K", str(max(16, 4 * N + 2))))  # bench.py's defaults
 
 
-def sim_rank(rk):
-    r = D.FrameShardRenderer(scene, W, H, cfg, rk, N, FakeDist(), own_slots=OWN, frames_in_flight=K)
+def sim_rank(rk, bounds=None):
+    r = D.FrameShardRenderer(scene, W, H, cfg, rk, N, FakeDist(), own_slots=OWN, frames_in_flight=K, bounds=bounds)
+    r.camera.frameCounter += int(os.environ.get("FC_OFFSET", "0"))  # experiment: which frames a rank traces
     for kv in filter(None, os.environ.get("PT_UNIFORMS", "").split(",")):  # name=value,... on the path tracer
         name, val = kv.split("=")
         r.pass_path_tracing.set_uniform_int(name, int(val))
@@ -197,13 +198,12 @@ def sim_rank(rk):
     return out
 
 
-if __name__ == "__main__":
-    ranks = [int(v) for v in os.environ["RANKS"].split(",")] if "RANKS" in os.environ else range(N)
-    print(f"--- frame shard: N={N} {W}x{H} K={K} own slots {OWN}, {FRAMES} frames per rank, "
+def report(tag, ranks, bounds):
+    print(f"--- frame shard ({tag}): N={N} {W}x{H} K={K} own slots {OWN}, {FRAMES} frames per rank, "
           f"links {XLAT_US:g} us + bytes / {XGBS:g} GB/s", flush=True)
     res = []
     for rk in ranks:
-        s = sim_rank(rk)
+        s = sim_rank(rk, bounds)
         res.append(s)
         print(f"rank {rk}: rows {s['rows'][0]}..{s['rows'][1]} wall {s['wall']:.3f} ms/frame ({1e3 / s['wall']:.1f} fps) "
               f"issue {s['issue']:.3f} (host cpu {s['cpu']:.3f}, motion wait {s['wait']:.3f})  SVGF stream busy {s['back']:.3f} ms/frame  per frame: "
@@ -211,5 +211,25 @@ if __name__ == "__main__":
         print("   passes alone, ms per frame: " + " ".join(f"{k} {v:.3f}" for k, v in sorted(s["pp"].items())),
               flush=True)
     mx = max(s["wall"] for s in res)
-    print(f"predicted frame (slowest simulated rank): {mx:.3f} ms = {1e3 / mx:.1f} fps")
+    print(f"predicted frame (slowest simulated rank): {mx:.3f} ms = {1e3 / mx:.1f} fps", flush=True)
+    return res
+
+
+if __name__ == "__main__":
+    import numpy as np
+
+    ranks = [int(v) for v in os.environ["RANKS"].split(",")] if "RANKS" in os.environ else list(range(N))
+    given = tuple(int(v) for v in os.environ["BOUNDS"].split(",")) if "BOUNDS" in os.environ else None
+    res = report("given bands" if given else "equal bands", ranks, given)
+    if os.environ.get("BALANCE", "1") != "0" and len(ranks) == N and N > 1 and given is None:
+        # make_frame_shard_renderer's calibration, one round: each band's work (its own passes, timed alone) spread
+        # evenly over its rows, new bounds at equal quantiles
+        b = D.BandPlan(W, H, 0, N).bounds
+        cost = np.empty(H)
+        for k, s in enumerate(res):
+            work = s["pp"].get("frame_sum_ms", 0.0)  # the band renderer's own draws (full_* are the whole frame's)
+            cost[b[k]:b[k + 1]] = work / (b[k + 1] - b[k])
+        bounds = D.balanced_bounds(cost, N)
+        print(f"balanced bounds {bounds}", flush=True)
+        report("balanced bands", ranks, bounds)
     gl.shutdown()
