@@ -95,6 +95,8 @@ def parse():
     ap.add_argument("--shard", default="frames", choices=("frames", "bands"),
                     help="multi-GPU: 'frames' = rank f %% N traces frame f whole and scatters its rows to the band owners, "
                          "the SVGF chain banded (dist.FrameShardRenderer); 'bands' = every pass banded (dist.BandRenderer)")
+    ap.add_argument("--ship-gbuffer", type=int, default=0, choices=(0, 1),
+                    help="--shard frames: the tracing rank also sends the bands their G-buffer rows (they draw none)")
     ap.add_argument("--own-slots", type=int, default=4,
                     help="--shard frames: whole frames a rank traces at once (its path tracer's frames in flight)")
     ap.add_argument("--breakdown", action="store_true", help="print per-pass ms to stderr")
@@ -351,7 +353,8 @@ def main():
         if world > 1 and args.shard == "frames":
             from ptsvgf.dist import make_frame_shard_renderer
             r = make_frame_shard_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,
-                                          own_slots=args.own_slots, frames_in_flight=K)
+                                          own_slots=args.own_slots, frames_in_flight=K,
+                                          ship_gbuffer=bool(args.ship_gbuffer))
         elif world > 1:
             from ptsvgf.dist import make_band_renderer
             r = make_band_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,
@@ -405,7 +408,8 @@ def main():
             # per-stage exchange ms per frame, MAX over ranks (the slowest rank's wait sets the frame)
             mx = torch.tensor([ex.get(k, 0.0) for k in EXCHANGE_STAGES], dtype=torch.float64, device="cuda")
             dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-            out["bands"] = {"shard": args.shard, "bounds": list(r.plan.bounds), "back_lag": r.r.lag,
+            out["bands"] = {"shard": args.shard, "ship_gbuffer": bool(getattr(r, "ship_gbuffer", False)),
+                            "bounds": list(r.plan.bounds), "back_lag": r.r.lag,
                             "frames_in_flight": r.r.K,
                             "exchange_ms_per_frame": {k: round(v, 4) for k, v in zip(EXCHANGE_STAGES, mx.tolist())
                                                       if k in ex or v > 0},

@@ -138,6 +138,11 @@ int pt_raster_pass_bind_device(uint32_t pass, const void* device_vertices, size_
  * a driver with several G-buffer targets (frames in flight) binds one and shares it. Rebinding `pass` ends the share;
  * destroying `src_pass` first makes `pass`'s draws fail with PT_ERR_STATE. */
 int pt_raster_pass_share(uint32_t pass, uint32_t src_pass);
+/* The G-buffer planes of a rasterize pass's attachments were written elsewhere for rows [y_begin, y_end) (multi-GPU:
+ * another rank drew these rows of the same frame and sent them; the G-buffer is per pixel, so they equal a draw's):
+ * derive what a draw makes beside its planes (the a-trous's compact depth-fwidth plane and per-tile surface flags,
+ * "atrous_rows_begin" / "_end" as for a draw) on the current stream. No reference counterpart. */
+int pt_raster_pass_adopt(uint32_t pass, int y_begin, int y_end);
 int pt_pass_reset_texture_slot(uint32_t pass);
 int pt_pass_set_texture(uint32_t pass, uint32_t target, uint32_t tex, const char* name);
 int pt_pass_set_uniform_mat4(uint32_t pass, const char* name, const float* m16);

@@ -1285,28 +1285,10 @@ int draw_pathtrace_batch(Pass** ps, int n) {
   return rc ? hip_err((hipError_t)rc, "pathtrace batch launch") : PT_OK;
 }
 
-int draw_raster(Pass* p) {
-  Pass* src = p->raster_src ? pass_of(p->raster_src) : p;
-  if (!src) return err(PT_ERR_STATE, "raster pass shares the triangles of a destroyed pass");
-  if (src != p && src->raster_src)  // the source became a sharer itself: its own raster scene is stale
-    return err(PT_ERR_STATE, "raster pass shares the triangles of a pass that now shares another pass's");
-  const RasterScene& rs = src->raster;
-  if (!rs.geom && rs.ntris > 0) return err(PT_ERR_STATE, "raster pass not bound");
-  GBufParams k;
-  memset(&k, 0, sizeof(k));
-  k.W = p->W;
-  k.H = p->H;
-  rows_of(p, &k.y0, &k.y1);
-  TRY(att_plane(p, 0, &k.world));
-  TRY(att_plane(p, 1, &k.normal_depth));
-  TRY(att_plane(p, 2, &k.motion));
-  TRY(att_plane(p, 3, &k.fwidth));
-  Texture* fwt = tex_of(p->att[3]);
-  if (!fwt->aux) HIPCHK(hipMalloc((void**)&fwt->aux, (size_t)fwt->W * fwt->rows * 4));
-  k.fwidth_aux = fwt->aux;
-  // the a-trous per-tile surface flags of this G-buffer, marked by the G-buffer kernels as they write the pixels
-  // the rows the a-trous passes will draw ("atrous_rows_begin" / "_end", e.g. a band's ghost-zone margin): default the
-  // G-buffer's own rows; they must lie inside them (a tile's flag is marked by the G-buffer pixels it holds)
+// The tile flags of a draw of p over rows [k.y0, k.y1): the rows the a-trous passes draw ("atrous_rows_begin" /
+// "_end", e.g. a band's ghost-zone margin), default the G-buffer's own rows; they must lie inside them (a tile's flag is
+// marked by the G-buffer pixels it holds). Allocates and zeroes them on the fwidth texture; k.tflags null when off.
+static int gbuf_flags(Pass* p, Texture* fwt, GBufParams& k) {
   k.tf_y0 = ui(p, "atrous_rows_begin", -1) >= 0 ? ui(p, "atrous_rows_begin", -1) : k.y0;
   k.tf_y1 = ui(p, "atrous_rows_end", -1) >= 0 ? ui(p, "atrous_rows_end", -1) : k.y1;
   if (k.tf_y0 < k.y0 || k.tf_y1 > k.y1 || k.tf_y0 > k.tf_y1)
@@ -1329,6 +1311,30 @@ int draw_raster(Pass* p) {
   } else {
     fwt->tflags_ver = 0;
   }
+  return PT_OK;
+}
+
+int draw_raster(Pass* p) {
+  Pass* src = p->raster_src ? pass_of(p->raster_src) : p;
+  if (!src) return err(PT_ERR_STATE, "raster pass shares the triangles of a destroyed pass");
+  if (src != p && src->raster_src)  // the source became a sharer itself: its own raster scene is stale
+    return err(PT_ERR_STATE, "raster pass shares the triangles of a pass that now shares another pass's");
+  const RasterScene& rs = src->raster;
+  if (!rs.geom && rs.ntris > 0) return err(PT_ERR_STATE, "raster pass not bound");
+  GBufParams k;
+  memset(&k, 0, sizeof(k));
+  k.W = p->W;
+  k.H = p->H;
+  rows_of(p, &k.y0, &k.y1);
+  TRY(att_plane(p, 0, &k.world));
+  TRY(att_plane(p, 1, &k.normal_depth));
+  TRY(att_plane(p, 2, &k.motion));
+  TRY(att_plane(p, 3, &k.fwidth));
+  Texture* fwt = tex_of(p->att[3]);
+  if (!fwt->aux) HIPCHK(hipMalloc((void**)&fwt->aux, (size_t)fwt->W * fwt->rows * 4));
+  k.fwidth_aux = fwt->aux;
+  // the a-trous per-tile surface flags of this G-buffer, marked by the G-buffer kernels as they write the pixels
+  TRY(gbuf_flags(p, fwt, k));
   k.geom = rs.geom;
   k.nrm = rs.nrm;
   k.bvh = rs.bvh;
@@ -2037,6 +2043,39 @@ int pt_raster_pass_share(uint32_t pass, uint32_t src_pass) {
   if (pass == src_pass || s->raster_src) return err(PT_ERR_ARG, "pt_raster_pass_share: share from an own-bound pass");
   p->raster_src = src_pass;
   p->bound = true;
+  return PT_OK;
+}
+
+int pt_raster_pass_adopt(uint32_t pass, int y_begin, int y_end) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  Pass* p = pass_of(pass);
+  if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
+  if (g.programs[p->program] != PK_RASTER) return err(PT_ERR_ARG, "pt_raster_pass_adopt: not a rasterize pass");
+  if (p->att.size() < 4) return err(PT_ERR_STATE, "pt_raster_pass_adopt: the pass has no G-buffer attachments");
+  GBufParams k;
+  memset(&k, 0, sizeof(k));
+  k.W = p->W;
+  k.H = p->H;
+  if (y_begin < 0 || y_end > p->H || y_begin > y_end) return err(PT_ERR_ARG, "pt_raster_pass_adopt: bad rows");
+  k.y0 = y_begin;
+  k.y1 = y_end;
+  for (int i = 0; i < 4; ++i) {  // the attachments now hold new texels (their versions move on, as after a draw)
+    Plane* dst[4] = {&k.world, &k.normal_depth, &k.motion, &k.fwidth};
+    TRY(att_plane(p, i, dst[i]));
+  }
+  Texture* fwt = tex_of(p->att[3]);
+  for (int i : {1, 3}) {
+    const Texture* t = tex_of(p->att[i]);
+    if (y_begin < t->row0 || y_end > t->row0 + t->rows)
+      return err(PT_ERR_ARG, "pt_raster_pass_adopt: rows outside the attachments' stored rows");
+  }
+  if (!fwt->aux) HIPCHK(hipMalloc((void**)&fwt->aux, (size_t)fwt->W * fwt->rows * 4));
+  k.fwidth_aux = fwt->aux;
+  TRY(gbuf_flags(p, fwt, k));
+  const int rc = ptk::launch_gbuffer_adopt(k, g.stream);
+  if (rc) return hip_err((hipError_t)rc, "pt_raster_pass_adopt");
+  fwt->aux_valid = true;
   return PT_OK;
 }
 

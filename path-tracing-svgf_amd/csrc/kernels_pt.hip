@@ -534,6 +534,27 @@ __global__ void __launch_bounds__(kBlock) gbuffer_raster_kernel(GBufParams p) {
   gb_finish(p, x, y, valid, ln, o, d, best, bests, bu, bv);
 }
 
+// A G-buffer whose planes another process wrote (multi-GPU frame shard: the rank tracing the frame drew these rows of
+// it and sent them): the side data a draw makes beside its planes, from the planes — the compact depth-fwidth plane
+// (fwidth.y with the sign bit = linearZ == 1, exactly as gb_finish writes it) and the a-trous tile flags of rows
+// [tf_y0, tf_y1). One thread per pixel of rows [y0, y1).
+__global__ void __launch_bounds__(256) gbuffer_adopt_kernel(GBufParams p) {
+  const int x = blockIdx.x * 64 + (int)(threadIdx.x & 63);
+  const int y = p.y0 + (int)blockIdx.y * 4 + (int)(threadIdx.x >> 6);
+  if (x >= p.W || y >= p.y1) return;
+  const float lz = pld(p.normal_depth, x, y).w;
+  const float fwz = pld(p.fwidth, x, y).y;
+  if (p.fwidth_aux)
+    p.fwidth_aux[(size_t)prow(p.fwidth, y) * p.W + x] = __uint_as_float(__float_as_uint(fwz) | (lz == 1.0f ? 0x80000000u : 0u));
+  if (p.tflags && lz != 1.0f && y >= p.tf_y0 && y < p.tf_y1) atrous_mark_tiles(p.tflags, p.tf_off, p.W, x, y - p.tf_y0);
+}
+
+int launch_gbuffer_adopt(const GBufParams& p, hipStream_t s) {
+  if (p.y1 <= p.y0) return 0;
+  hipLaunchKernelGGL(gbuffer_adopt_kernel, dim3((p.W + 63) / 64, (p.y1 - p.y0 + 3) / 4), dim3(256), 0, s, p);
+  return (int)hipGetLastError();
+}
+
 int launch_gbuffer_raster(const GBufParams& p, hipStream_t s) {
   if (p.y1 <= p.y0) return 0;
   const int ntx = (p.W + kRTile - 1) / kRTile, nty = (p.y1 - p.y0 + kRTile - 1) / kRTile;

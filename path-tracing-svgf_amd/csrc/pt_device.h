@@ -310,7 +310,8 @@ int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s);
 int wf_list_capacity(int W, int rows);  // per-segment capacity of the compacted ray lists (8 segments)
 int wf_subset_tiles(int W, int rows, int stride, int offset);  // tiles of a PTParams tile subset (< 0: invalid)
 int launch_gbuffer(const GBufParams& p, hipStream_t s);
-int launch_gbuffer_raster(const GBufParams& p, hipStream_t s);  // bins, resolves, and the ray cast on overflow
+int launch_gbuffer_raster(const GBufParams& p, hipStream_t s);
+int launch_gbuffer_adopt(const GBufParams& p, hipStream_t s);  // side data of G-buffer planes written elsewhere  // bins, resolves, and the ray cast on overflow
 int launch_bins(const Bins& b, hipStream_t s);  // after the item setup kernel: large items, scan, scatter
 // nb frames' path tracing with batched traversal launches (ps[b]: frame b, its wavefront state at pid offset b * n)
 int launch_pathtrace_wavefront_batch(const PTParams* ps, int nb, hipStream_t s);

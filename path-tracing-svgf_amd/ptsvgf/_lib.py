@@ -97,6 +97,7 @@ _PT_SIGS = [
     ("pt_raster_pass_bind", C.c_int, [_u32, _fp, C.c_size_t]),
     ("pt_raster_pass_bind_device", C.c_int, [_u32, _vp, C.c_size_t, C.c_int]),
     ("pt_raster_pass_share", C.c_int, [_u32, _u32]),
+    ("pt_raster_pass_adopt", C.c_int, [_u32, C.c_int, C.c_int]),
     ("pt_pass_reset_texture_slot", C.c_int, [_u32]),
     ("pt_pass_set_texture", C.c_int, [_u32, _u32, _u32, C.c_char_p]),
     ("pt_pass_set_uniform_mat4", C.c_int, [_u32, C.c_char_p, _fp]),

@@ -135,12 +135,13 @@ class BandPlan:
         m = self.margins[stage]
         return max(0, self.y0 - m), min(self.H, self.y1 + m)
 
-    def gbuffer_rows(self) -> tuple:
-        """Ghost zone: the rows the band's G-buffer draws — the reprojection's rows and the reach of its taps into the
-        previous normal/depth at rest (REPROJ_REACH); a moving camera's further rows arrive with the history
-        (history_items)."""
+    def gbuffer_rows(self, k: int | None = None) -> tuple:
+        """Ghost zone: the rows band k's G-buffer draws (default this rank's) — the reprojection's rows and the reach
+        of its taps into the previous normal/depth at rest (REPROJ_REACH); a moving camera's further rows arrive with
+        the history (history_items)."""
+        a, b = self.owned(self.rank if k is None else k)
         r = self.margins["reproject"] + REPROJ_REACH
-        return max(0, self.y0 - r), min(self.H, self.y1 + r)
+        return max(0, a - r), min(self.H, b + r)
 
     def history_items(self, planes: dict, n: int) -> list:
         """Ghost zone: the exchanges before the reprojection for a motion reach of n rows (motion_rows): the previous
@@ -558,13 +559,14 @@ def scatter_group(dist):
     return hit[1]
 
 
-def exchange_window(window, plan: BandPlan, dist, group=None) -> int:
+def exchange_window(window, plan: BandPlan, dist, group=None, rows=None) -> int:
     """The point-to-point transfers of one frame-shard window: consecutive frames, at most one per source rank (frame
     f is traced by rank f % N). window = [(src, planes)]: for a frame this rank traced, planes are its whole-frame
     (H, W, C) tensors and every other band's rows (plan.zone: the band, widened by the ghost zone's reprojection
     margin) go to that band's owner; for a frame rank src traced, planes are this band's zone rows, received from src. Every rank builds the same window, so the batch is symmetric: an
-    all-to-all over the window's sources, every link busy at once, one communicator. RCCL: the current stream waits
-    for the batch; gloo (tests): blocking, device tensors staged through host memory. Returns the bytes sent."""
+    all-to-all over the window's sources, every link busy at once, one communicator. rows[j](k) (default plan.zone):
+    the rows of band k plane j carries. RCCL: the current stream waits for the batch; gloo (tests): blocking, device
+    tensors staged through host memory. Returns the bytes sent."""
     import torch
 
     gloo = dist.get_backend(group) == "gloo"
@@ -574,13 +576,13 @@ def exchange_window(window, plan: BandPlan, dist, group=None) -> int:
             for k in range(plan.world):
                 if k == plan.rank:
                     continue
-                y0, y1 = plan.zone(k)
-                for t in planes:
-                    rows = t[y0:y1]
-                    if gloo and rows.is_cuda:
-                        rows = rows.cpu()
-                    ops.append(dist.P2POp(dist.isend, rows, k, group))
-                    nbytes += rows.numel() * rows.element_size()
+                for j, t in enumerate(planes):
+                    y0, y1 = (rows[j] if rows else plan.zone)(k)
+                    part = t[y0:y1]
+                    if gloo and part.is_cuda:
+                        part = part.cpu()
+                    ops.append(dist.P2POp(dist.isend, part, k, group))
+                    nbytes += part.numel() * part.element_size()
         else:
             for t in planes:
                 buf = t
@@ -618,7 +620,16 @@ class FrameShardRenderer(BandRenderer):
     Per rank and N frames: one full-frame front end + N band G-buffers and SVGF chains. own_slots = whole frames this
     rank traces at once (the path tracer's streams)."""
 
-    def __init__(self, scene, W, H, cfg, rank, world, dist, own_slots: int = 2, **kw):
+    GBUF_PLANES = (1, 2, 3)  # G-buffer attachments the SVGF chain reads: normal/depth, motion, depth-fwidth
+
+    def __init__(self, scene, W, H, cfg, rank, world, dist, own_slots: int = 2, ship_gbuffer: bool | None = None,
+                 **kw):
+        """ship_gbuffer (default off): the frame's tracing rank also sends each band the rows of its G-buffer
+        (normal/depth, motion, depth-fwidth on the band's G-buffer rows), which the band adopts (pt_raster_pass_adopt)
+        instead of drawing its own. A band's G-buffer draw costs 0.06-0.25 ms per frame (the plant's rows dominate)
+        against 0.01 for the adoption, for twice the window's bytes (≈ 150 MB per window and link at 8 ranks); the
+        8-rank simulation measured it within noise (0.93-1.11 vs 0.90-0.99 ms per frame,
+        profiles/r03/frame_shard/fs_ship*.log), so it stays an option."""
         import torch
 
         from . import gl
@@ -649,6 +660,20 @@ class FrameShardRenderer(BandRenderer):
         self._win = []  # frames registered since the last window exchange
         kw.setdefault("front_streams", 1)  # band front ends are a G-buffer each: one stream, in order
         kw.setdefault("ghost_zone", True)
+        self.ship_gbuffer = bool(ship_gbuffer)
+        if self.ship_gbuffer and not kw["ghost_zone"]:
+            raise ValueError("ship_gbuffer needs the ghost zone")
+        if self.ship_gbuffer:
+            kw["draw_gbuffer"] = False
+            # the tracing rank's whole-frame G-buffer reduces the frame's motion bound (the bands draw none)
+            nb = len(self.full.init_pass)
+            self._fmb_dev = torch.zeros(nb, dtype=torch.int32, device=dev)
+            self._fmb_host = torch.zeros(nb, dtype=torch.int32).pin_memory()
+            self._fmb_event = [torch.cuda.Event() for _ in range(nb)]
+            for b, p in enumerate(self.full.init_pass):
+                p.set_motion_bound(self._fmb_dev[b:b + 1].data_ptr())
+        self._set_frame = {}  # band G-buffer set -> the frame that last used it
+        self._own_mb = {}     # own frame -> its full G-buffer set (motion bound)
         super().__init__(scene, W, H, cfg, rank, world, dist, pt_source=self._pt_source, pt_flush=self._exchange,
                          **kw)
         self.full.camera = self.r.camera  # one camera: the full front end draws the band renderer's frame
@@ -672,26 +697,69 @@ class FrameShardRenderer(BandRenderer):
         if len(self._win) == p.world:
             self._exchange()
         holder = {}
+        gset = f % len(r.gbuf)
+        self._set_frame[gset] = f
         item = dict(src=f % p.world, outs=[self._band_rows(h) for h in r.pt_slots[slot][1]],
-                    free=r._slot_free[f % r.K], holder=holder)
+                    free=r._slot_free[f % r.K], holder=holder, gset=gset)
+        if self.ship_gbuffer:
+            g0, g1 = p.gbuffer_rows()
+            ip = r.init_pass[gset]
+            item["outs"] += [self._tensors[ip.colorAttachments[j]][g0 - p.row0:g1 - p.row0] for j in self.GBUF_PLANES]
         if item["src"] == p.rank:
             o, pt_done = self._render_own(f)
             r._stream_to(stream)  # the library's stream is process-global: back to the band's front-end stream
             full = [self._full_tensors[h] for h in self.full.pt_slots[o][1]]
+            if self.ship_gbuffer:
+                full += [self._full_tensors[self.full.init_pass[o].colorAttachments[j]] for j in self.GBUF_PLANES]
             rs = self._recv_stream
             if item["free"] is not None:
                 rs.wait_event(item["free"])
             rs.wait_event(pt_done)
-            z0, z1 = p.zone(p.rank)
+            rows = self._plane_rows()
             with torch.cuda.stream(rs):
-                for a, b in zip(item["outs"], full):
+                for j, (a, b) in enumerate(zip(item["outs"], full)):
+                    z0, z1 = rows[j](p.rank)
                     a.copy_(b[z0:z1])
+            if self.ship_gbuffer:
+                self._adopt(gset, rs)
+                r._stream_to(stream)
             ev = torch.cuda.Event()
             ev.record(rs)
             holder["ev"] = ev
             item.update(o=o, full=full)
         self._win.append(item)
         return holder
+
+    def _plane_rows(self):
+        """Per window plane, the rows of band k it carries: the path tracer's planes on the band's zone, the
+        G-buffer's on the band's G-buffer rows."""
+        p = self.plan
+        return [p.zone] * 3 + ([p.gbuffer_rows] * len(self.GBUF_PLANES) if self.ship_gbuffer else [])
+
+    def _adopt(self, gset: int, stream) -> None:
+        """The band's G-buffer set holds its rows of a frame drawn by the tracing rank: make the a-trous side data
+        (pt_raster_pass_adopt) on `stream`, behind the rows' arrival."""
+        r = self.r
+        r._stream_to(stream)
+        r.init_pass[gset].adopt(*self.plan.gbuffer_rows())
+
+    def _motion(self, b: int | None = None) -> int:
+        """Shipped G-buffer: the frame's motion bound comes from its tracing rank's whole-frame G-buffer (the bands
+        draw none): MAX over ranks of (that rank's bound, 0 elsewhere)."""
+        if not self.ship_gbuffer:
+            return super()._motion(b)
+        import numpy as np
+
+        f = self._set_frame[self.r.back_set if b is None else b]
+        m = 0.0
+        if f % self.plan.world == self.plan.rank:
+            o = self._own_mb.pop(f)
+            self._fmb_event[o].synchronize()
+            m = float(self._fmb_host[o:o + 1].numpy().view(np.float32)[0])
+        m = allreduce_motion(m, self.dist, self._group)
+        n = self.plan.set_motion(m)
+        self.motion_log.append((m * self.plan.H, n))
+        return n
 
     def _exchange(self) -> None:
         """Send / receive the rows of the registered window (every rank registers the same frames, so every rank
@@ -707,7 +775,14 @@ class FrameShardRenderer(BandRenderer):
                 rs.wait_event(it["free"])
         window = [(it["src"], it["full"] if it["src"] == p.rank else it["outs"]) for it in win]
         with torch.cuda.stream(rs):
-            nbytes = exchange_window(window, p, self.dist, self._sgroup) if p.world > 1 else 0
+            nbytes = exchange_window(window, p, self.dist, self._sgroup, rows=self._plane_rows()) if p.world > 1 else 0
+        if self.ship_gbuffer:
+            cur = self.r._lib_stream
+            for it in win:
+                if it["src"] != p.rank:
+                    self._adopt(it["gset"], rs)
+            if cur is not None:
+                self.r._stream_to(cur)
         ev = torch.cuda.Event()
         ev.record(rs)
         for it in win:
@@ -732,6 +807,11 @@ class FrameShardRenderer(BandRenderer):
         fr.pre_viewproj = self.r.pre_viewproj
         fr.frame_index = f
         fr._gbuffer(o)
+        if self.ship_gbuffer:  # the frame's motion bound, read by every rank's _motion through the all-reduce
+            with torch.cuda.stream(st):
+                self._fmb_host[o:o + 1].copy_(self._fmb_dev[o:o + 1], non_blocking=True)
+                self._fmb_event[o].record(st)
+            self._own_mb[f] = o
         fr._path_trace(fr.gbuf[o])
         done = torch.cuda.Event()
         done.record(st)

@@ -258,6 +258,11 @@ class Rasterize_RenderPass(RenderPass):
         """pt_raster_pass_bind_device: the vertex list already in device memory, its tree built on the GPU."""
         check(pt().pt_raster_pass_bind_device(self._handle(), C.c_void_p(device_ptr), n_floats, ploc_radius))
 
+    def adopt(self, y0: int, y1: int) -> None:
+        """pt_raster_pass_adopt: the attachments' rows [y0, y1) were written elsewhere (another rank's draw of the same
+        frame); derive the a-trous side data a draw makes, on the current library stream."""
+        check(pt().pt_raster_pass_adopt(self._handle(), y0, y1))
+
     def share_vertices(self, src: "Rasterize_RenderPass") -> None:
         """pt_raster_pass_share: draw src's triangles and tree (src bound on its own)."""
         check(pt().pt_raster_pass_share(self._handle(), src._handle()))

@@ -59,7 +59,7 @@ class Renderer:
                  atrous_exact: bool = False, run_taa: bool = True, run_output: bool = True, tex_factory=None,
                  halo=None, gbuffer_rows=None, frames_in_flight: int = 1, after_gbuffer=None, back_lag: int = 0,
                  trace_batch: int = 1, front_streams: int | None = None, pt_source=None, pt_flush=None,
-                 stage_rows=None, early_history=None):
+                 stage_rows=None, early_history=None, draw_gbuffer: bool = True):
         """band = (y0, y1, row0, rows) for screen-band sharding; tex_factory(w, h) -> handle allocates the
         frame-sized planes (ptsvgf.dist wraps torch tensors); halo(stage, {plane name: handle}) is called before
         the SVGF passes that read rows beyond the band (dist.HALO_SCHEDULE names the planes); after_gbuffer(set,
@@ -156,6 +156,9 @@ class Renderer:
         self._pt_source = pt_source
         self._pt_flush = pt_flush
         self._stage_rows = stage_rows
+        self._draw_gbuffer = bool(draw_gbuffer)
+        if not draw_gbuffer and pt_source is None:
+            raise ValueError("draw_gbuffer=False needs a pt_source that provides the G-buffer planes")
         self._early_history = early_history
         self._ready = None  # pt_source's event for the front end being issued
         self._batch: list = []  # path-tracing passes of the open batch: (pass, G-buffer-done event, stream, holder)
@@ -354,6 +357,8 @@ class Renderer:
         ip.set_uniform_mat4("projection", proj)
         ip.set_uniform_mat4("pre_viewproj", self.pre_viewproj)
         ip.set_uniform_uint("frameCounter", cam.frameCounter)
+        if not self._draw_gbuffer:  # its planes come with the path tracer's (pt_source)
+            return
         self._draw(ip, "gbuffer")
         if self._after_gbuffer is not None:
             import torch

@@ -27,14 +27,18 @@ def _port():
 
 @pytest.mark.parametrize("world,moving,balance,shard", [(2, True, True, "bands"), (4, False, False, "bands"),
                                                         (2, True, False, "frames"), (3, True, True, "frames"),
-                                                        (4, True, False, "frames")])
+                                                        (4, True, False, "frames"), (3, True, False, "frames+gbuffer")])
 def test_bench_band_parity_gloo(world, moving, balance, shard):
     """shard = "bands": every rank traces its band; "frames": rank f % N traces frame f whole and scatters the
-    path tracer's rows to the band owners (dist.FrameShardRenderer)."""
+    path tracer's rows to the band owners (dist.FrameShardRenderer); "frames+gbuffer": and its G-buffer rows, which
+    the bands adopt instead of drawing (ship_gbuffer, an option)."""
+    ship = shard == "frames+gbuffer"
+    shard = "frames" if ship else shard
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "bench.py"),
            "--gpus", str(world), "--backend", "gloo", "--width", "320", "--height", "256", "--steps", "4",
-           "--warmup", "2", "--no-extras", "--no-1080p", "--no-cpu-baseline", "--shard", shard]
+           "--warmup", "2", "--no-extras", "--no-1080p", "--no-cpu-baseline", "--shard", shard,
+           "--ship-gbuffer", "1" if ship else "0"]
     cmd += ["--moving"] if moving else []
     cmd += [] if balance else ["--equal-bands"]
     p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=600)
@@ -45,7 +49,7 @@ def test_bench_band_parity_gloo(world, moving, balance, shard):
     assert line["n_gpus"] == world
     assert bp["backend"] == "gloo" and bp["frames"] >= 4
     assert bp["bit_exact"], bp
-    assert line["bands"]["shard"] == shard
+    assert line["bands"]["shard"] == shard and line["bands"].get("ship_gbuffer", False) == ship
     if shard == "frames":
         assert line["bands"]["scatter_mb_per_traced_frame"] > 0
     ex = line["bands"]["exchange_ms_per_frame"]

@@ -110,7 +110,7 @@ def fake_exchange(items, plan, dist, group=None, wait=True):
     return [FakeWork(done)]
 
 
-def fake_window(window, plan, dist, group=None):
+def fake_window(window, plan, dist, group=None, rows=None):
     """exchange_window stand-in: the window's sends and receives run over all links at once, so the batch lasts
     latency + the largest per-peer volume (sent to or received from one peer) / link bandwidth."""
     per_peer, sent = {}, 0
@@ -118,8 +118,7 @@ def fake_window(window, plan, dist, group=None):
         if src == plan.rank:
             for k in range(plan.world):
                 if k != plan.rank:
-                    y0, y1 = plan.owned(k)
-                    nb = sum(t[y0:y1].numel() * 4 for t in planes)
+                    nb = sum(t[slice(*(rows[j] if rows else plan.zone)(k))].numel() * 4 for j, t in enumerate(planes))
                     per_peer[("s", k)] = per_peer.get(("s", k), 0) + nb
                     sent += nb
         else:
@@ -148,7 +147,8 @@ K = int(os.environ.get("K", str(max(16, 4 * N + 2))))  # bench.py's defaults
 
 
 def sim_rank(rk, bounds=None):
-    r = D.FrameShardRenderer(scene, W, H, cfg, rk, N, FakeDist(), own_slots=OWN, frames_in_flight=K, bounds=bounds)
+    r = D.FrameShardRenderer(scene, W, H, cfg, rk, N, FakeDist(), own_slots=OWN, frames_in_flight=K, bounds=bounds,
+                             ship_gbuffer=os.environ.get("SHIP", "0") == "1")
     r.camera.frameCounter += int(os.environ.get("FC_OFFSET", "0"))  # experiment: which frames a rank traces
     for kv in filter(None, os.environ.get("PT_UNIFORMS", "").split(",")):  # name=value,... on the path tracer
         name, val = kv.split("=")
