@@ -288,6 +288,17 @@ def allreduce_motion(m: float, dist, group=None) -> float:
     return float(t.item())
 
 
+class _StageFilter:
+    """A halo callback with the set of stages it acts on (Renderer._halo skips the rest)."""
+
+    def __init__(self, fn, stages):
+        self.fn = fn
+        self.stages = frozenset(stages)
+
+    def __call__(self, stage, handles):
+        return self.fn(stage, handles)
+
+
 class BandRenderer:
     """One rank's share of a frame: the fast Renderer on band storage + HALO_SCHEDULE exchanges."""
 
@@ -335,8 +346,11 @@ class BandRenderer:
             kw["gbuffer_rows"] = self.plan.gbuffer_rows()
             kw["stage_rows"] = self.plan.stage_rows
             kw["early_history"] = self._early_history
+        halo = self._halo
+        if ghost_zone:  # only these stages exchange (the Renderer skips the others without a stream context)
+            halo = _StageFilter(self._halo, ("reproject", "taa"))
         self.r = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, tex_factory=factory,
-                          halo=self._halo, after_gbuffer=self._after_gbuffer, **kw)
+                          halo=halo, after_gbuffer=self._after_gbuffer, **kw)
         if ghost_zone:  # the G-buffer marks the a-trous tiles of the rows the a-trous passes draw
             a0, a1 = self.plan.stage_rows("atrous")
             for p in self.r.init_pass:

@@ -714,6 +714,9 @@ class Renderer:
     def _halo(self, stage: str, handles: dict) -> None:
         if self._halo_cb is None:
             return
+        stages = getattr(self._halo_cb, "stages", None)  # the stages the callback acts on (None: all)
+        if stages is not None and stage not in stages:
+            return  # (a stream context per stage costs host time on every frame)
         with self._on_back():
             self._halo_cb(stage, handles)
 
