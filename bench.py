@@ -106,6 +106,8 @@ def parse():
     ap.add_argument("--frames-in-flight", type=int, default=None,
                     help="K > 1: front ends (G-buffer + path tracer) of K frames overlap on K streams "
                          "(default 4 up to 4 GPUs, 8 on 8 bands: thinner bands have relatively longer launch tails)")
+    ap.add_argument("--svgf-uniform", action="append", default=[], metavar="NAME=INT",
+                    help="extra int uniform on the SVGF passes (A/B switches, e.g. reproj_block=0)")
     ap.add_argument("--pt-uniform", action="append", default=[], metavar="NAME=INT",
                     help="extra int uniform on the path-tracing pass (A/B switches, e.g. shadow_bvh4=0)")
     return ap.parse_args()
@@ -367,6 +369,11 @@ def main():
         for kv in args.pt_uniform:
             name, val = kv.split("=")
             r.pass_path_tracing.set_uniform_int(name, int(val))
+        rr = getattr(r, "r", r)  # the band renderer's Renderer
+        for kv in args.svgf_uniform:
+            name, val = kv.split("=")
+            for sp in [*rr.reproject, rr.variance_compute_pass, *rr.atrous_to.values(), rr.svgf_modulate_pass]:
+                sp.set_uniform_int(name, int(val))
         if VIEWS[view]:
             cam = r.camera
             for k, v in VIEWS[view].items():

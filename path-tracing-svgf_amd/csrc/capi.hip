@@ -1400,6 +1400,7 @@ int draw_svgf(Pass* p, int kind) {
     k.inv_h = uf(p, "inv_screen_height", 0.0f);
     k.depth_thr = uf(p, "depth_threshold", 0.0f);
     k.normal_thr = uf(p, "normal_threshold", 0.0f);
+    k.block = ui(p, "reproj_block", 1);  // A/B (0: lin per tap): the same texels either way
     rc = launch_reproject(k, g.stream);
   } else if (kind == PK_VARIANCE) {
     VarianceParams k;

@@ -75,6 +75,29 @@ __device__ __forceinline__ float edge_weight(float zc, float zp, float phiDepth,
 #else
 #define PT_REPROJ_ATTR
 #endif
+// The bilinear fetch of tap (OX, OY) from a 3x3 texel block B whose top-left texel is the tap (0, 0)'s (x0, y0):
+// the texels lin() reads, mixed with the tap's own weights.
+template <int OX, int OY>
+__device__ __forceinline__ float4 lin_blk(const float4 (&B)[3][3], const Bilin& b) {
+  const float4 c00 = B[OY][OX], c10 = B[OY][OX + 1], c01 = B[OY + 1][OX], c11 = B[OY + 1][OX + 1];
+  float4 r;
+  r.x = bilin_mix(b, c00.x, c10.x, c01.x, c11.x);
+  r.y = bilin_mix(b, c00.y, c10.y, c01.y, c11.y);
+  r.z = bilin_mix(b, c00.z, c10.z, c01.z, c11.z);
+  r.w = bilin_mix(b, c00.w, c10.w, c01.w, c11.w);
+  return r;
+}
+__device__ __forceinline__ void load_blk(const Plane& P, int X, int Y, float4 (&B)[3][3]) {
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) B[j][i] = ldp(P, X + i, Y + j);
+}
+template <int K>
+__device__ __forceinline__ float4 lin_tap(const float4 (&B)[3][3], const Bilin& b) {
+  return lin_blk<(K & 1), (K >> 1)>(B, b);
+}
+
 __global__ void __launch_bounds__(256) PT_REPROJ_ATTR reproject_kernel(ReprojParams p) {
   int x = blockIdx.x * 16 + (threadIdx.x & 15);
   int y = p.y0 + blockIdx.y * 16 + (threadIdx.x >> 4);
@@ -99,33 +122,91 @@ __global__ void __launch_bounds__(256) PT_REPROJ_ATTR reproject_kernel(ReprojPar
   float pI[4] = {0.f, 0.f, 0.f, 0.f}, pM[2] = {0.f, 0.f};
   const float ox[4] = {0.0f, p.inv_w, 0.0f, p.inv_w};
   const float oy[4] = {0.0f, 0.0f, p.inv_h, p.inv_h};
+  // the four history taps (+0/+1 texel in x and y, svgf_reproject.frag:99-125): lin()'s setups, once
+  Bilin bt[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) bt[k] = bilin_setup(ipx + ox[k], ipy + oy[k], W, H);
+  // when they tile one 3x3 block (no clamping, each tap one texel on from tap 0), every plane's 16 texel reads are
+  // its 9 block texels: load them once (same texels, same weights, same bits as lin per tap)
+  const int X = bt[0].x0, Y = bt[0].y0;
+  const bool blk = p.block && bt[0].x1 == X + 1 && bt[0].y1 == Y + 1 && X + 2 < W && Y + 2 < H &&
+                   bt[1].x0 == X + 1 && bt[1].y0 == Y && bt[2].x0 == X && bt[2].y0 == Y + 1 &&
+                   bt[3].x0 == X + 1 && bt[3].y0 == Y + 1;
   bool v[4];
   bool valid = false;
+  float4 hq;  // the history length tap (lin(prev_moments, ipx, ipy)), from the moments block when it is loaded
+  bool have_hq = false;
+  if (blk) {
+    {
+      float4 B[3][3];
+      load_blk(p.prev_nd, X, Y, B);
+      const float4 q[4] = {lin_tap<0>(B, bt[0]), lin_tap<1>(B, bt[1]), lin_tap<2>(B, bt[2]), lin_tap<3>(B, bt[3])};
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    float lx = ipx + ox[k], ly = ipy + oy[k];
-    float4 q = lin(p.prev_nd, W, H, lx, ly);
-    v[k] = reprj_valid(lx, ly, z, q.w, fw.y, n, mk(q.x, q.y, q.z), fw.x, p.depth_thr, p.normal_thr);
-    valid = valid || v[k];
-  }
-  if (valid) {
-    float sumw = 0.0f;
-    float bx = ipx - (float)f2i(ipx / p.inv_w) * p.inv_w;
-    float by = ipy - (float)f2i(ipy / p.inv_h) * p.inv_h;
-    const float w[4] = {(1.0f - bx) * (1.0f - by), bx * (1.0f - by), (1.0f - bx) * by, bx * by};
+      for (int k = 0; k < 4; ++k) {
+        v[k] = reprj_valid(ipx + ox[k], ipy + oy[k], z, q[k].w, fw.y, n, mk(q[k].x, q[k].y, q[k].z), fw.x,
+                           p.depth_thr, p.normal_thr);
+        valid = valid || v[k];
+      }
+    }
+    if (valid) {
+      float sumw = 0.0f;
+      float bx = ipx - (float)f2i(ipx / p.inv_w) * p.inv_w;
+      float by = ipy - (float)f2i(ipy / p.inv_h) * p.inv_h;
+      const float w[4] = {(1.0f - bx) * (1.0f - by), bx * (1.0f - by), (1.0f - bx) * by, bx * by};
+      {
+        float4 B[3][3];
+        load_blk(p.prev_illum, X, Y, B);
+        const float4 q[4] = {lin_tap<0>(B, bt[0]), lin_tap<1>(B, bt[1]), lin_tap<2>(B, bt[2]), lin_tap<3>(B, bt[3])};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!v[k]) continue;
+          pI[0] += w[k] * q[k].x; pI[1] += w[k] * q[k].y; pI[2] += w[k] * q[k].z; pI[3] += w[k] * q[k].w;
+        }
+      }
+      {
+        float4 B[3][3];
+        load_blk(p.prev_moments, X, Y, B);
+        const float4 q[4] = {lin_tap<0>(B, bt[0]), lin_tap<1>(B, bt[1]), lin_tap<2>(B, bt[2]), lin_tap<3>(B, bt[3])};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!v[k]) continue;
+          pM[0] += w[k] * q[k].x; pM[1] += w[k] * q[k].y;
+          sumw += w[k];
+        }
+        hq = q[0];
+        have_hq = true;
+      }
+      valid = (sumw >= 0.01f);
+      for (int q = 0; q < 4; ++q) pI[q] = valid ? pI[q] / sumw : 0.0f;
+      for (int q = 0; q < 2; ++q) pM[q] = valid ? pM[q] / sumw : 0.0f;
+    }
+  } else {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if (!v[k]) continue;
       float lx = ipx + ox[k], ly = ipy + oy[k];
-      float4 qi = lin(p.prev_illum, W, H, lx, ly);
-      float4 qm = lin(p.prev_moments, W, H, lx, ly);
-      pI[0] += w[k] * qi.x; pI[1] += w[k] * qi.y; pI[2] += w[k] * qi.z; pI[3] += w[k] * qi.w;
-      pM[0] += w[k] * qm.x; pM[1] += w[k] * qm.y;
-      sumw += w[k];
+      float4 q = lin(p.prev_nd, W, H, lx, ly);
+      v[k] = reprj_valid(lx, ly, z, q.w, fw.y, n, mk(q.x, q.y, q.z), fw.x, p.depth_thr, p.normal_thr);
+      valid = valid || v[k];
     }
-    valid = (sumw >= 0.01f);
-    for (int q = 0; q < 4; ++q) pI[q] = valid ? pI[q] / sumw : 0.0f;
-    for (int q = 0; q < 2; ++q) pM[q] = valid ? pM[q] / sumw : 0.0f;
+    if (valid) {
+      float sumw = 0.0f;
+      float bx = ipx - (float)f2i(ipx / p.inv_w) * p.inv_w;
+      float by = ipy - (float)f2i(ipy / p.inv_h) * p.inv_h;
+      const float w[4] = {(1.0f - bx) * (1.0f - by), bx * (1.0f - by), (1.0f - bx) * by, bx * by};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!v[k]) continue;
+        float lx = ipx + ox[k], ly = ipy + oy[k];
+        float4 qi = lin(p.prev_illum, W, H, lx, ly);
+        float4 qm = lin(p.prev_moments, W, H, lx, ly);
+        pI[0] += w[k] * qi.x; pI[1] += w[k] * qi.y; pI[2] += w[k] * qi.z; pI[3] += w[k] * qi.w;
+        pM[0] += w[k] * qm.x; pM[1] += w[k] * qm.y;
+        sumw += w[k];
+      }
+      valid = (sumw >= 0.01f);
+      for (int q = 0; q < 4; ++q) pI[q] = valid ? pI[q] / sumw : 0.0f;
+      for (int q = 0; q < 2; ++q) pM[q] = valid ? pM[q] / sumw : 0.0f;
+    }
   }
   if (!valid) {
     float nValid = 0.0f;
@@ -149,7 +230,7 @@ __global__ void __launch_bounds__(256) PT_REPROJ_ATTR reproject_kernel(ReprojPar
   }
   float hist;
   if (valid) {
-    hist = lin(p.prev_moments, W, H, ipx, ipy).z;
+    hist = (have_hq ? hq : lin(p.prev_moments, W, H, ipx, ipy)).z;  // tap 0's fetch: the same setup, the same texels
   } else {
     for (int q = 0; q < 4; ++q) pI[q] = 0.0f;
     pM[0] = pM[1] = 0.0f;

@@ -239,6 +239,7 @@ struct ReprojParams {
   Plane motion, color, albedo, emission, prev_illum, prev_moments, nd, prev_nd, fwidth;
   Plane out_illum, out_moments;
   float inv_w, inv_h, depth_thr, normal_thr;
+  int block;  // 1: the four history taps from one 3x3 texel block per plane when they tile it (same texels, same bits)
 };
 
 struct VarianceParams {

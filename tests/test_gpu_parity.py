@@ -568,3 +568,28 @@ def test_wide_tree_is_result_preserving(gpu, scene_name, request):
     for k in ("primary_rays", "bounce_rays", "shadow_rays"):
         assert stats[0][k] == stats[1][k], (k, stats)
     print("visits wide / binary:", {k: (stats[0][k], stats[1][k]) for k in ("bounce_visits", "shadow_visits")})
+
+
+@pytest.mark.parametrize("W,H,moves", [(96, 64, [(2.0, 0.5), (-3.0, 1.0), (4.0, -2.0)]), (200, 120, [(1.0, 0.0)] * 3)])
+def test_reproject_block_fetch_equals_per_tap(gpu, scene_small, W, H, moves):
+    """The reprojection's 3x3 block fetch (reproj_block = 1, the default: the four history taps' texels loaded once per
+    plane) against lin() per tap (reproj_block = 0): the same texels with the same weights, so the same bits, through
+    camera moves (non-zero motion, disocclusions, the 3x3 fallback) and the frame edges."""
+    gl = gpu
+    out = []
+    for block in (0, 1):
+        r = _renderer(scene_small, W, H, mode="fast", run_taa=False, run_output=False)
+        for p in r.reproject:
+            p.set_uniform_int("reproj_block", block)
+        planes = []
+        for mv in [None] + moves:
+            if mv:
+                r.camera.orbit(*mv)
+            r.frame()
+            pl = r.planes()
+            planes.append({k: gl.readback(pl[k]) for k in ("reproj_illum", "reproj_moments", "modulate")})
+        r.close()
+        out.append(planes)
+    for f, (a, b) in enumerate(zip(*out)):
+        for k in a:
+            assert np.array_equal(a[k].view(np.uint32), b[k].view(np.uint32)), (f, k)
