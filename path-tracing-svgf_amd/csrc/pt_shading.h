@@ -134,10 +134,7 @@ __device__ __forceinline__ bool tri_hit(const float4* __restrict__ g, int i, v3 
 // scan (any-hit rays). The loop keeps the shape of a chunked fetch (kLeafChunk triangles' geometry loaded before they
 // are tested): with a chunk of 1 it compiles to faster code than the plain loop (same box, 4K: 207.5 vs 190.4 fps),
 // and chunks of 2 / 4 / 8 measured slower (8.4 -> 10.2 / 13.1 / 23.7 ms: registers).
-#ifndef PT_LEAF_CHUNK
-#define PT_LEAF_CHUNK 1
-#endif
-constexpr int kLeafChunk = PT_LEAF_CHUNK;
+constexpr int kLeafChunk = 1;
 template <class F>
 __device__ __forceinline__ bool leaf_scan(const float4* __restrict__ g, int first, int cnt, v3 S, v3 d,
                                           F&& on_hit) {

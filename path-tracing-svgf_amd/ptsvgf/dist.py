@@ -647,7 +647,7 @@ class FrameShardRenderer(BandRenderer):
         import torch
 
         from . import gl
-        from .renderer import Renderer
+        from .renderer import Renderer, acquire_stream
 
         K = kw.get("frames_in_flight", 1)
         kw.setdefault("back_lag", world)  # a frame's back end is issued after its window's exchange
@@ -693,7 +693,7 @@ class FrameShardRenderer(BandRenderer):
         self.full.camera = self.r.camera  # one camera: the full front end draws the band renderer's frame
         self.pass_path_tracing = self.full.pass_path_tracing
         self._sgroup = scatter_group(dist) if world > 1 else None
-        self._recv_stream = torch.cuda.Stream()
+        self._recv_stream = acquire_stream()
         self.scatter_log = []  # per exchange that carried a frame of this rank: bytes sent
 
     def _band_rows(self, handle):
@@ -884,9 +884,13 @@ class FrameShardRenderer(BandRenderer):
         return out
 
     def close(self) -> None:
+        from .renderer import release_stream
+
         super().close()
         self.full.close()
         self._full_tensors.clear()
+        release_stream(self._recv_stream)
+        self._recv_stream = None
 
 
 def gather_bands(owned: dict, plan: BandPlan, dist, dst: int = 0) -> dict | None:

@@ -53,6 +53,25 @@ def _set_stream(stream) -> None:
     check(pt().pt_set_stream(stream.cuda_stream))
 
 
+_FREE_STREAMS: dict = {}  # (device, priority) -> streams a closed renderer gave back
+
+
+def acquire_stream(priority: int = 0):
+    """A stream no live renderer holds. torch.cuda.Stream() hands out its fixed per-priority pool (32 streams)
+    round-robin, so after 32 of them two live objects share one queue: a renderer's streams, or a renderer's and a
+    process group's communication stream (taken from the same pool). Recycling what closed renderers held keeps
+    the allocations far below the pool's size over a run of many renderers (bench calibration, several views)."""
+    import torch
+
+    pool = _FREE_STREAMS.setdefault((torch.cuda.current_device(), priority), [])
+    return pool.pop() if pool else torch.cuda.Stream(priority=priority)
+
+
+def release_stream(stream) -> None:
+    if stream is not None:
+        _FREE_STREAMS.setdefault((stream.device.index, stream.priority), []).append(stream)
+
+
 class Renderer:
     def __init__(self, scene: Scene, width: int, height: int, config: parameter_config | None = None,
                  mode: str = "fast", aspect_corrected: bool | None = None, band=None, prune: bool = True,
@@ -205,12 +224,12 @@ class Renderer:
         if self.K > 1:
             import torch  # streams and events are torch plumbing (the kernels are the library's)
 
-            self._streams = [torch.cuda.Stream() for _ in range(self._nfs)]
+            self._streams = [acquire_stream() for _ in range(self._nfs)]
             # the SVGF back end is a chain of short launches (and, on bands, exchanges) beside the front ends' long
             # traversal launches: on a high-priority queue its kernels take CUs as soon as waves retire instead of
             # queueing behind resident traversal waves (PTSVGF_BACK_PRIORITY=0: normal priority, A/B)
             hi = os.environ.get("PTSVGF_BACK_PRIORITY", "1") != "0"
-            self._back = torch.cuda.Stream(priority=-1) if hi else torch.cuda.Stream()
+            self._back = acquire_stream(-1 if hi else 0)
             self._slot_free = [None] * self.K  # event: SVGF of the frame that last used the slot is done
             self._fe_prev = None
 
@@ -828,6 +847,10 @@ class Renderer:
             import torch
 
             torch.cuda.synchronize()  # frames may still be in flight on the renderer's streams
+            for st in self._streams + [self._back]:
+                release_stream(st)
+            self._streams = []
+            self._back = None
         for v in list(vars(self).values()):
             if isinstance(v, PassGroup):
                 continue  # its passes are the pt_slots' (destroyed below)

@@ -593,3 +593,21 @@ def test_reproject_block_fetch_equals_per_tap(gpu, scene_small, W, H, moves):
     for f, (a, b) in enumerate(zip(*out)):
         for k in a:
             assert np.array_equal(a[k].view(np.uint32), b[k].view(np.uint32)), (f, k)
+
+
+def test_renderer_streams_distinct_and_recycled(gpu, scene_small):
+    """Frames in flight run on the renderer's own queues: distinct within a renderer (torch's stream pool hands its 32
+    streams out round-robin, so plain torch.cuda.Stream() would alias after 32), given back on close and reused by
+    the next renderer (renderer.acquire_stream)."""
+    r = _renderer(scene_small, 32, 24, frames_in_flight=4)
+    mine = [s.cuda_stream for s in r._streams] + [r._back.cuda_stream]
+    assert len(set(mine)) == len(mine)
+    r.frame()
+    r.flush()
+    r.close()
+    r2 = _renderer(scene_small, 32, 24, frames_in_flight=4)
+    again = [s.cuda_stream for s in r2._streams] + [r2._back.cuda_stream]
+    assert set(again) == set(mine)
+    r2.frame()
+    r2.flush()
+    r2.close()
