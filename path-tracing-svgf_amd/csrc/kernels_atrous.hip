@@ -308,93 +308,9 @@ struct TapPixel {
       }
     }
   }
-  // the same 24 taps from a footprint staged as eight planes of PL floats (atrous_soa_kernel): illumination x y z w,
-  // then normal x y z and depth; Lb = this pixel's top-left tap in plane 0 (row stride C)
-  template <bool FLAT, int S, int C, int PL>
-  __device__ __forceinline__ void window_soa(const float* Lb, int x, int y, int W, int H, float phi_normal) {
-#pragma unroll
-    for (int yy = -2; yy <= 2; ++yy) {
-      if (y + yy * S < 0 || y + yy * S >= H) continue;
-#pragma unroll
-      for (int xx = -2; xx <= 2; ++xx) {
-        if (xx == 0 && yy == 0) continue;
-        if (x + xx * S < 0 || x + xx * S >= W) continue;
-        const float* t = Lb + (yy + 2) * C + (xx + 2) * S;
-        tap<FLAT>(float4{t[0], t[PL], t[2 * PL], t[3 * PL]}, float4{t[4 * PL], t[5 * PL], t[6 * PL], t[7 * PL]}, xx,
-                  yy, phi_normal);
-      }
-    }
-  }
   __device__ __forceinline__ float4 result() const {
     const float inv = 1.0f / sumW;
     return float4{s01.x * inv, s01.y * inv, s23.x * inv, s23.y * (inv * inv)};
-  }
-};
-
-// Two horizontally adjacent pixels (A, B) in one lane, element 0 = A, 1 = B: TapPixel::tap's operations, element for
-// element, as packed-f32 instructions (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 give each element the IEEE result of
-// the scalar instruction); the clamp, the absolute values and the transcendentals stay scalar. Same operations in the
-// same order on every element, so the bits are TapPixel's.
-struct TapPair {
-  f2v nx, ny, nz, nw, wLr, wLg, wLb, cL, sumW, sx, sy, sz, sw;
-  f2v kD[5];
-  __device__ __forceinline__ void init(const TapPixel& a, const TapPixel& b) {
-    nx = f2v{a.nd.x, b.nd.x};
-    ny = f2v{a.nd.y, b.nd.y};
-    nz = f2v{a.nd.z, b.nd.z};
-    nw = f2v{a.nd.w, b.nd.w};
-    wLr = f2v{a.wLr, b.wLr};
-    wLg = f2v{a.wLg, b.wLg};
-    wLb = f2v{a.wLb, b.wLb};
-    cL = f2v{a.cL, b.cL};
-#pragma unroll
-    for (int k = 0; k < 5; ++k) kD[k] = f2v{a.kDr[k], b.kDr[k]};
-    sumW = f2v{a.sumW, b.sumW};
-    sx = f2v{a.s01.x, b.s01.x};
-    sy = f2v{a.s01.y, b.s01.y};
-    sz = f2v{a.s23.x, b.s23.x};
-    sw = f2v{a.s23.y, b.s23.y};
-  }
-  __device__ __forceinline__ void tap(f2v ix, f2v iy, f2v iz, f2v iw, f2v qx, f2v qy, f2v qz, f2v qw, int xx, int yy,
-                                      float phi_normal) {
-    const int r2 = xx * xx + yy * yy;
-    const f2v kDl = r2 == 1 ? kD[0] : r2 == 2 ? kD[1] : r2 == 4 ? kD[2] : r2 == 5 ? kD[3] : kD[4];
-    const int ax = xx < 0 ? -xx : xx, ay = yy < 0 ? -yy : yy;
-    const float kern = (ax == 0 ? 1.0f : ax == 1 ? 2.0f / 3.0f : 1.0f / 6.0f) *
-                       (ay == 0 ? 1.0f : ay == 1 ? 2.0f / 3.0f : 1.0f / 6.0f);
-    const f2v t = __builtin_elementwise_fma(ny, qy, nx * qx);
-    const float dA = fminf(fmaxf(__builtin_fmaf(nz.x, qz.x, t.x), 0.0f), 1.0f);
-    const float dB = fminf(fmaxf(__builtin_fmaf(nz.y, qz.y, t.y), 0.0f), 1.0f);
-    const f2v tl = __builtin_elementwise_fma(iz, wLb, __builtin_elementwise_fma(iy, wLg, __builtin_elementwise_fma(ix, wLr, cL)));
-    const f2v dz = nw - qw;
-    const f2v a = f2v{__builtin_fmaf(fabsf(dz.x), kDl.x, fabsf(tl.x)), __builtin_fmaf(fabsf(dz.y), kDl.y, fabsf(tl.y))};
-    const f2v l = f2v{__builtin_amdgcn_logf(dA), __builtin_amdgcn_logf(dB)};
-    const f2v xa = __builtin_elementwise_fma(f2v{phi_normal, phi_normal}, l, -a);
-    const f2v w = f2v{__builtin_amdgcn_exp2f(xa.x), __builtin_amdgcn_exp2f(xa.y)} * f2v{kern, kern};
-    sumW += w;
-    sx = __builtin_elementwise_fma(w, ix, sx);
-    sy = __builtin_elementwise_fma(w, iy, sy);
-    sz = __builtin_elementwise_fma(w, iz, sz);
-    sw = __builtin_elementwise_fma(w * w, iw, sw);
-  }
-  // the 24 taps of both pixels: Lw = pixel A's top-left tap in plane 0 (B's is Lw + 1)
-  template <int S, int C, int PL>
-  __device__ __forceinline__ void window(const float* Lw, float phi_normal) {
-#pragma unroll
-    for (int yy = -2; yy <= 2; ++yy) {
-#pragma unroll
-      for (int xx = -2; xx <= 2; ++xx) {
-        if (xx == 0 && yy == 0) continue;
-        const float* t = Lw + (yy + 2) * C + (xx + 2) * S;
-        tap(f2v{t[0], t[1]}, f2v{t[PL], t[PL + 1]}, f2v{t[2 * PL], t[2 * PL + 1]}, f2v{t[3 * PL], t[3 * PL + 1]},
-            f2v{t[4 * PL], t[4 * PL + 1]}, f2v{t[5 * PL], t[5 * PL + 1]}, f2v{t[6 * PL], t[6 * PL + 1]},
-            f2v{t[7 * PL], t[7 * PL + 1]}, xx, yy, phi_normal);
-      }
-    }
-  }
-  __device__ __forceinline__ float4 result(int h) const {
-    const float inv = 1.0f / sumW[h];
-    return float4{sx[h] * inv, sy[h] * inv, sz[h] * inv, sw[h] * (inv * inv)};
   }
 };
 
@@ -485,125 +401,6 @@ __global__ void __launch_bounds__(64 * tile_tj<S>() * tile_nx<S>()) atrous_tile_
   *out = px.result();
 }
 
-// SoA-staged form: a tile of 128 columns x 8 rows of one residue class (one wave per tile row, each lane two
-// horizontally adjacent pixels), its footprint staged as eight float planes, so both pixels' operands of a tap are
-// adjacent floats (8-B LDS reads) and the tap arithmetic runs packed on the pair (TapPair). Edge tiles, and pairs with a
-// flat pixel (phiIllumination == 0), take TapPixel's checked path per pixel from the same planes. Bit-identical to
-// atrous_tile_kernel and the step kernel; tile flags as atrous_tile_kernel's with NX = 2 (atrous_tile_nx).
-template <int S, bool AUX>
-__global__ void __launch_bounds__(512) atrous_soa_kernel(AtrousParams p) {
-  constexpr int TJ = 8, R = TJ + 4, C = 128 + 4 * S, PL = R * C, NT = 64 * TJ;
-  static_assert(atrous_tile_tj(S) == TJ && atrous_tile_nx(S) == 2, "tile flags assume this kernel's tiles");
-  __shared__ __attribute__((aligned(16))) float L[8 * PL];
-  const int W = p.illum.W, row0 = p.illum.row0;
-  const float4* __restrict__ I = p.illum.p;
-  const float4* __restrict__ ND = p.nd.p;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int j = __builtin_amdgcn_readfirstlane(tid >> 6);  // tile row
-  const int bx = blockIdx.x, g = blockIdx.y / S, b = blockIdx.y - g * S;
-  const int ybase = p.y0 + g * S * TJ + b;
-  const int xl = 2 * lane, x0 = bx * 128, x = x0 + xl, y = ybase + S * j;
-  const bool ownA = x < p.W && y < p.y1, ownB = ownA && x + 1 < p.W;
-  const size_t ci = (size_t)(y - row0) * W + x;
-  bool bgA = true, bgB = true;
-  float fwA = 0.0f, fwB = 0.0f;
-  const bool pre = AUX && p.tile_any != nullptr;
-  bool tile_any = true;
-  if (pre) tile_any = p.tile_any[(g * S + b) * gridDim.x + bx] != 0;
-  if (ownA && tile_any) {
-    if (AUX) {
-      const float a = p.fwidth.aux[ci];
-      bgA = aux_flag(a);
-      fwA = fabsf(a);
-      if (ownB) {
-        const float c = p.fwidth.aux[ci + 1];
-        bgB = aux_flag(c);
-        fwB = fabsf(c);
-      }
-    } else {
-      bgA = ND[ci].w == 1.0f;
-      fwA = p.fwidth.p[ci].y;
-      if (ownB) {
-        bgB = ND[ci + 1].w == 1.0f;
-        fwB = p.fwidth.p[ci + 1].y;
-      }
-    }
-  }
-  if (!pre) {
-    __shared__ int any_surface[TJ];
-    const bool wave_any = __ballot(!(bgA && bgB)) != 0ull;
-    if (lane == 0) any_surface[j] = wave_any;
-    __syncthreads();
-    tile_any = false;
-#pragma unroll
-    for (int w = 0; w < TJ; ++w) tile_any |= any_surface[w] != 0;
-  }
-  if (!tile_any) {
-    if (ownA) p.out.p[ci] = I[ci];
-    if (ownB) p.out.p[ci + 1] = I[ci + 1];
-    return;
-  }
-  // stage: tile row r <-> frame row ybase + S*(r-2), column c <-> x0 - 2S + c, clamped as atrous_tile_kernel's
-  const int lo = max(0, row0), hi = min(p.H, row0 + p.illum.rows) - 1;
-  for (int e = tid; e < PL; e += NT) {
-    const int r = e / C, c = e - r * C;
-    int gy = ybase + S * (r - 2), gx = x0 - 2 * S + c;
-    gy = gy < lo ? lo : (gy > hi ? hi : gy);
-    gx = gx < 0 ? 0 : (gx >= p.W ? p.W - 1 : gx);
-    const size_t gi = (size_t)(gy - row0) * W + gx;
-    const float4 a = I[gi], n = ND[gi];
-    L[e] = a.x;
-    L[PL + e] = a.y;
-    L[2 * PL + e] = a.z;
-    L[3 * PL + e] = a.w;
-    L[4 * PL + e] = n.x;
-    L[5 * PL + e] = n.y;
-    L[6 * PL + e] = n.z;
-    L[7 * PL + e] = n.w;
-  }
-  __syncthreads();
-  if (!ownA) return;
-  const float* Lw = L + j * C + xl;  // pixel A's top-left tap
-  constexpr int CO = 2 * C + 2 * S;  // its centre
-  const float* c0 = Lw + CO;
-  const float4 icA{c0[0], c0[PL], c0[2 * PL], c0[3 * PL]}, icB{c0[1], c0[PL + 1], c0[2 * PL + 1], c0[3 * PL + 1]};
-  const float4 ndA{c0[4 * PL], c0[5 * PL], c0[6 * PL], c0[7 * PL]};
-  const float4 ndB{c0[4 * PL + 1], c0[5 * PL + 1], c0[6 * PL + 1], c0[7 * PL + 1]};
-  float4* out = p.out.p + ci;
-  if (bgA && bgB) {
-    out[0] = icA;
-    if (ownB) out[1] = icB;
-    return;
-  }
-  const bool edge =
-      x0 - 2 * S < 0 || x0 + 127 + 2 * S >= p.W || ybase - 2 * S < 0 || ybase + S * (TJ + 1) >= p.H;
-  TapPixel pa, pb;
-  pa.init(icA, ndA, fwA, p.phi_color, S);
-  pb.init(icB, ndB, fwB, p.phi_color, S);
-  const bool flat = (!bgA && pa.flat) || (ownB && !bgB && pb.flat);
-  float4 rA, rB;
-  if (__builtin_expect(!edge && !flat, 1)) {
-    TapPair q;
-    q.init(pa, pb);
-    q.window<S, C, PL>(Lw, p.phi_normal);
-    rA = q.result(0);
-    rB = q.result(1);
-  } else {  // rare: per pixel, checked
-    if (!bgA) {
-      if (pa.flat) pa.window_soa<true, S, C, PL>(Lw, x, y, p.W, p.H, p.phi_normal);
-      else pa.window_soa<false, S, C, PL>(Lw, x, y, p.W, p.H, p.phi_normal);
-    }
-    if (ownB && !bgB) {
-      if (pb.flat) pb.window_soa<true, S, C, PL>(Lw + 1, x + 1, y, p.W, p.H, p.phi_normal);
-      else pb.window_soa<false, S, C, PL>(Lw + 1, x + 1, y, p.W, p.H, p.phi_normal);
-    }
-    rA = pa.result();
-    rB = pb.result();
-  }
-  out[0] = bgA ? icA : rA;
-  if (ownB) out[1] = bgB ? icB : rB;
-}
-
 // Tile flags of the five step sizes (atrous_tile_kernel's tiles: S = 1 << si, NX = tile_nx<S>(), TJ = tile_tj<S>() rows of one
 // residue class): byte (g * S + b) * NXT + bx of step si is 1 iff an owned pixel of that tile is a surface pixel
 // (the depth-fwidth plane's sign bit clear). One wave per 64 columns of a row; a ballot, then one byte store per step.
@@ -642,11 +439,6 @@ static void launch_tile_s(const AtrousParams& p, bool aux, hipStream_t s) {
   constexpr int NX = tile_nx<S>(), TJ = tile_tj<S>();
   const int groups = (p.y1 - p.y0 + S * TJ - 1) / (S * TJ);
   dim3 grid((p.W + 64 * NX - 1) / (64 * NX), groups * S);
-  if constexpr (PT_ATROUS_SOA != 0) {
-    if (aux) hipLaunchKernelGGL((atrous_soa_kernel<S, true>), grid, dim3(512), 0, s, p);
-    else hipLaunchKernelGGL((atrous_soa_kernel<S, false>), grid, dim3(512), 0, s, p);
-    return;
-  }
   if (aux) hipLaunchKernelGGL((atrous_tile_kernel<S, true>), grid, dim3(64 * TJ * NX), 0, s, p);
   else hipLaunchKernelGGL((atrous_tile_kernel<S, false>), grid, dim3(64 * TJ * NX), 0, s, p);
 }

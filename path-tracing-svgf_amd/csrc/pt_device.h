@@ -268,13 +268,8 @@ struct AtrousParams {
 #ifndef PT_ATROUS_NX16
 #define PT_ATROUS_NX16 2
 #endif
-// PT_ATROUS_SOA: the SoA-staged pair kernel (atrous_soa_kernel: 128 x 8 tiles for every step) instead of
-// atrous_tile_kernel
-#ifndef PT_ATROUS_SOA
-#define PT_ATROUS_SOA 0
-#endif
-__host__ __device__ constexpr int atrous_tile_tj(int S) { return PT_ATROUS_SOA ? 8 : S >= 16 ? PT_ATROUS_TJ16 : PT_ATROUS_TJ; }
-__host__ __device__ constexpr int atrous_tile_nx(int S) { return PT_ATROUS_SOA ? 2 : S >= 16 ? PT_ATROUS_NX16 : 1; }
+__host__ __device__ constexpr int atrous_tile_tj(int S) { return S >= 16 ? PT_ATROUS_TJ16 : PT_ATROUS_TJ; }
+__host__ __device__ constexpr int atrous_tile_nx(int S) { return S >= 16 ? PT_ATROUS_NX16 : 1; }
 static_assert(64 * PT_ATROUS_TJ <= 1024 && 64 * PT_ATROUS_TJ16 * PT_ATROUS_NX16 <= 1024, "a-trous tile too large");
 __device__ __forceinline__ void atrous_mark_tiles(unsigned char* flags, const int* off, int W, int x, int r) {
 #pragma unroll
