@@ -108,6 +108,9 @@ def parse():
                          "(default 4 up to 4 GPUs, 8 on 8 bands: thinner bands have relatively longer launch tails)")
     ap.add_argument("--svgf-uniform", action="append", default=[], metavar="NAME=INT",
                     help="extra int uniform on the SVGF passes (A/B switches, e.g. reproj_block=0)")
+    ap.add_argument("--fuse-modulate", type=int, choices=(0, 1), default=1,
+                    help="1: the last a-trous iteration writes the modulated colour too (Renderer.fuse_modulate); "
+                         "0: the separate modulate pass (A/B)")
     ap.add_argument("--pt-uniform", action="append", default=[], metavar="NAME=INT",
                     help="extra int uniform on the path-tracing pass (A/B switches, e.g. shadow_bvh4=0)")
     return ap.parse_args()
@@ -370,6 +373,7 @@ def main():
             name, val = kv.split("=")
             r.pass_path_tracing.set_uniform_int(name, int(val))
         rr = getattr(r, "r", r)  # the band renderer's Renderer
+        rr.fuse_modulate = bool(args.fuse_modulate)
         for kv in args.svgf_uniform:
             name, val = kv.split("=")
             for sp in [*rr.reproject, rr.variance_compute_pass, *rr.atrous_to.values(), rr.svgf_modulate_pass]:

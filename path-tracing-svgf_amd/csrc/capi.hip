@@ -1450,10 +1450,24 @@ int draw_svgf(Pass* p, int kind) {
       }
       k.tile_any = ft->tflags + ptk::atrous_flag_offset(si, k.W, y0, y1);
     }
+    // fused modulate (fast driver, last iteration): "fuse_modulate" = 1, colour attachment 1 = the modulate target,
+    // gAlbedo / gEmission bound; the production kernel writes it from its epilogue, the others launch modulate after
+    if (ui(p, "fuse_modulate", 0)) {
+      TRY(plane_of(sampler(p, "gAlbedo"), p, &k.albedo, "gAlbedo"));
+      TRY(plane_of(sampler(p, "gEmission"), p, &k.emission, "gEmission"));
+      TRY(att_plane(p, 1, &k.mod));
+      const Plane* mp[3] = {&k.albedo, &k.emission, &k.mod};
+      for (const Plane* q : mp)
+        if (y0 < std::max(0, q->row0) || y1 > std::min(p->H, q->row0 + q->rows))
+          return err(PT_ERR_ARG, "fused modulate: a plane does not store the draw's rows");
+      if (k.mod.p == k.illum.p || k.mod.p == k.out.p) return err(PT_ERR_ARG, "fused modulate target aliases the a-trous planes");
+    }
     if (ui(p, "exact", 0)) rc = launch_atrous_exact(k, g.stream);          // bit-exact form (tests)
     else if (ui(p, "atrous_variant", 0) == 1) rc = launch_atrous_simple(k, g.stream);  // A/B: generic
     else if (ui(p, "atrous_variant", 0) == 2) rc = launch_atrous_step(k, g.stream);    // A/B: step kernel
     else rc = launch_atrous_fast(k, g.stream);                             // LDS-tiled (production)
+    if (rc == PT_OK && k.mod.p && (ui(p, "exact", 0) || ui(p, "atrous_variant", 0) != 0))
+      rc = launch_modulate_after(k, g.stream);
   } else if (kind == PK_MODULATE) {
     ModulateParams k;
     memset(&k, 0, sizeof(k));

@@ -314,6 +314,26 @@ struct TapPixel {
   }
 };
 
+// The fused modulate (svgf_modulate.frag; kernels_svgf.hip::modulate_kernel's arithmetic, also built with
+// -ffp-contract=off): c * albedo + emission on surface pixels, c passed through on background pixels (zCenter == 1,
+// the a-trous kernel's own background test), alpha 1.
+__device__ __forceinline__ void modulate_store(const AtrousParams& p, int x, int y, float4 c, bool bg) {
+  float4 o;
+  if (bg) {
+    o.x = c.x;
+    o.y = c.y;
+    o.z = c.z;
+  } else {
+    const float4 a = p.albedo.p[(size_t)(y - p.albedo.row0) * p.albedo.W + x];
+    const float4 e = p.emission.p[(size_t)(y - p.emission.row0) * p.emission.W + x];
+    o.x = c.x * a.x + e.x;
+    o.y = c.y * a.y + e.y;
+    o.z = c.z * a.z + e.z;
+  }
+  o.w = 1.0f;
+  p.mod.p[(size_t)(y - p.mod.row0) * p.mod.W + x] = o;
+}
+
 template <int S, bool AUX>
 __global__ void __launch_bounds__(64 * tile_tj<S>() * tile_nx<S>()) atrous_tile_kernel(AtrousParams p) {
   constexpr int NX = tile_nx<S>();
@@ -360,7 +380,11 @@ __global__ void __launch_bounds__(64 * tile_tj<S>() * tile_nx<S>()) atrous_tile_
     for (int w = 0; w < NW; ++w) tile_any |= any_surface[w] != 0;
   }
   if (!tile_any) {
-    if (own) p.out.p[ci] = I[ci];
+    if (own) {
+      const float4 v = I[ci];
+      p.out.p[ci] = v;
+      if (p.mod.p) modulate_store(p, x, y, v, true);
+    }
     return;
   }
   // stage: tile row r <-> frame row ybase + S*(r-2), column c <-> x0 - 2S + c; rows outside the frame and
@@ -383,6 +407,7 @@ __global__ void __launch_bounds__(64 * tile_tj<S>() * tile_nx<S>()) atrous_tile_
   float4* out = p.out.p + ci;
   if (bg) {
     *out = ic;
+    if (p.mod.p) modulate_store(p, x, y, ic, true);
     return;
   }
   const bool edge =
@@ -398,7 +423,9 @@ __global__ void __launch_bounds__(64 * tile_tj<S>() * tile_nx<S>()) atrous_tile_
   } else {
     px.window<true, true, S, C>(Li, Ln, x, y, p.W, p.H, p.phi_normal);  // FLAT: rare
   }
-  *out = px.result();
+  const float4 r = px.result();
+  *out = r;
+  if (p.mod.p) modulate_store(p, x, y, r, false);
 }
 
 // Tile flags of the five step sizes (atrous_tile_kernel's tiles: S = 1 << si, NX = tile_nx<S>(), TJ = tile_tj<S>() rows of one
@@ -450,9 +477,28 @@ static bool same_geometry(const AtrousParams& p) {
   return p.illum.W == p.W;
 }
 
+// the fused modulate of a draw whose kernel does not fuse it: modulate_kernel over the same rows, after the a-trous
+int launch_modulate_after(const AtrousParams& p, hipStream_t s) {
+  if (!p.mod.p || p.y1 <= p.y0) return 0;
+  ModulateParams m;
+  m.W = p.W;
+  m.H = p.H;
+  m.y0 = p.y0;
+  m.y1 = p.y1;
+  m.albedo = p.albedo;
+  m.emission = p.emission;
+  m.illum = p.out;
+  m.nd = p.nd;
+  m.out = p.mod;
+  return launch_modulate(m, s);
+}
+
 int launch_atrous_fast(const AtrousParams& p, hipStream_t s) {
   if (p.y1 <= p.y0) return 0;
-  if (!same_geometry(p)) return launch_atrous_simple(p, s);
+  if (!same_geometry(p)) {
+    const int rc = launch_atrous_simple(p, s);
+    return rc ? rc : launch_modulate_after(p, s);
+  }
   const bool aux = p.fwidth.aux != nullptr;
   switch (p.step) {
     case 1: launch_tile_s<1>(p, aux, s); break;
@@ -460,7 +506,10 @@ int launch_atrous_fast(const AtrousParams& p, hipStream_t s) {
     case 4: launch_tile_s<4>(p, aux, s); break;
     case 8: launch_tile_s<8>(p, aux, s); break;
     case 16: launch_tile_s<16>(p, aux, s); break;
-    default: return launch_atrous_step(p, s);
+    default: {
+      const int rc = launch_atrous_step(p, s);
+      return rc ? rc : launch_modulate_after(p, s);
+    }
   }
   return (int)hipGetLastError();
 }

@@ -254,6 +254,9 @@ struct AtrousParams {
   int step;
   float phi_color, phi_normal;
   const unsigned char* tile_any;  // tiled kernel: per-tile "holds a surface pixel" flags of this step, or null
+  // fused modulate (the last iteration of a frame, fast driver): mod.p != null writes modulate_kernel's output of
+  // this draw's rows from `out`'s values, albedo and emission (every plane must store the draw's rows)
+  Plane albedo, emission, mod;
 };
 // Tiles of the tiled a-trous (kernels_atrous.hip): 64 * NX columns x TJ rows of one residue class mod S, one wave
 // per 64-column strip of a tile row (64 * TJ * NX <= 1024 threads); tile (g, b, bx) of step S has byte
@@ -323,6 +326,8 @@ int launch_atrous_fast(const AtrousParams& p, hipStream_t s);   // LDS-tiled (pr
 int launch_atrous_step(const AtrousParams& p, hipStream_t s);   // step-specialised, texture-path taps
 int launch_atrous_simple(const AtrousParams& p, hipStream_t s);
 int launch_modulate(const ModulateParams& p, hipStream_t s);
+// the modulate an a-trous draw with AtrousParams::mod set asks for, as its own launch (kernels that do not fuse it)
+int launch_modulate_after(const AtrousParams& p, hipStream_t s);
 int launch_output(const OutputParams& p, hipStream_t s);
 int launch_taa(const TAAParams& p, hipStream_t s);
 int launch_tile_sort(uint32_t* cost, int* perm, int ntiles, hipStream_t s);  // cost -> perm, clears cost

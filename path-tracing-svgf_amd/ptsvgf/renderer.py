@@ -78,7 +78,7 @@ class Renderer:
                  atrous_exact: bool = False, run_taa: bool = True, run_output: bool = True, tex_factory=None,
                  halo=None, gbuffer_rows=None, frames_in_flight: int = 1, after_gbuffer=None, back_lag: int = 0,
                  trace_batch: int = 1, front_streams: int | None = None, pt_source=None, pt_flush=None,
-                 stage_rows=None, early_history=None, draw_gbuffer: bool = True):
+                 stage_rows=None, early_history=None, draw_gbuffer: bool = True, fuse_modulate: bool = True):
         """band = (y0, y1, row0, rows) for screen-band sharding; tex_factory(w, h) -> handle allocates the
         frame-sized planes (ptsvgf.dist wraps torch tensors); halo(stage, {plane name: handle}) is called before
         the SVGF passes that read rows beyond the band (dist.HALO_SCHEDULE names the planes); after_gbuffer(set,
@@ -179,6 +179,10 @@ class Renderer:
         if not draw_gbuffer and pt_source is None:
             raise ValueError("draw_gbuffer=False needs a pt_source that provides the G-buffer planes")
         self._early_history = early_history
+        # fast driver: the last a-trous iteration also writes the modulated colour (svgf_modulate.frag) from its
+        # epilogue, saving the modulate pass's launch and its re-read of the a-trous output and normal/depth
+        # (same arithmetic, same bits: tests/test_gpu_parity.py::test_fused_modulate_equals_modulate_pass)
+        self.fuse_modulate = bool(fuse_modulate) and mode == "fast"
         self._ready = None  # pt_source's event for the front end being issued
         self._batch: list = []  # path-tracing passes of the open batch: (pass, G-buffer-done event, stream, holder)
         self._pending: list = []  # front ends whose back end is not issued yet (back_lag)
@@ -299,11 +303,16 @@ class Renderer:
                           "hist0": self._svgf_pass("svgf_Atrous.frag", [self.hist_illum[0]]),
                           "hist1": self._svgf_pass("svgf_Atrous.frag", [self.hist_illum[1]])}
         self.svgf_modulate_pass = self._svgf_pass("svgf_modulate.frag", [self.modulate_color])
+        # the last iteration with the modulate fused (colour attachment 1, "fuse_modulate"), per destination
+        self.atrous_mod_to = {k: self._svgf_pass("svgf_Atrous.frag", [self._atrous_tex(k), self.modulate_color])
+                              for k in self.atrous_to}
+        for p in self.atrous_mod_to.values():
+            p.set_uniform_int("fuse_modulate", 1)
         self.pass_taa = [self._svgf_pass("taa.frag", [self.taa[b]]) for b in (0, 1)]
         for p in self.pass_taa:
             p.set_uniform_int("screen_width", W)
             p.set_uniform_int("screen_height", H)
-        for p in self.reproject + [self.variance_compute_pass, *self.atrous_to.values()]:
+        for p in self.reproject + [self.variance_compute_pass, *self.atrous_to.values(), *self.atrous_mod_to.values()]:
             p.set_uniform_float("inv_screen_width", 1.0 / W)
             p.set_uniform_float("inv_screen_height", 1.0 / H)
 
@@ -615,10 +624,15 @@ class Renderer:
                 prev_tex = None if not dests else self._atrous_tex(dests[-1])
                 dests.append("pong" if prev_tex == self.ping else "ping")
         self._atrous_last = (g, [(dests[i], 1 << i) for i in range(n)], src)
+        fused = self.fuse_modulate and n > 0
         for i in range(n):
             self._halo(f"atrous{i}", {"atrous_in": src})
-            ap = self.atrous_to[dests[i]]
+            last = fused and i == n - 1
+            ap = (self.atrous_mod_to if last else self.atrous_to)[dests[i]]
             ap.reset_texture_slot()
+            if last:
+                ap.set_texture_uniform(GL_TEXTURE_2D, albedo, "gAlbedo")
+                ap.set_texture_uniform(GL_TEXTURE_2D, emission, "gEmission")
             ap.set_uniform_float("gPhiColor", cfg.sigma_l)
             ap.set_uniform_float("gPhiNormal", cfg.sigma_n)
             ap.set_uniform_int("gStepSize", 1 << i)
@@ -627,7 +641,7 @@ class Renderer:
             ap.set_texture_uniform(GL_TEXTURE_2D, g["fwidth"], "gNormalDepthFwidth")
             ap.set_texture_uniform(GL_TEXTURE_2D, src, "gIllumination")
             self._rows(ap, "atrous")
-            self._draw(ap, "atrous")
+            self._draw(ap, "atrous_modulate" if last else "atrous")
             src = self._atrous_tex(dests[i])
             if i == 1 and self._early_history is not None:  # the next frame's history is written
                 nxt = self._pending[0] if self._pending and self._pending[0]["f"] == f + 1 else None
@@ -635,14 +649,15 @@ class Renderer:
                     self._early_history({"prev_illum": self.hist_illum[b], "prev_moments": self.moments[b],
                                          "prev_nd": g["normal_depth"]}, None if nxt is None else (f + 1) % ng)
         self.atrous_final = src
-        mp = self.svgf_modulate_pass
-        mp.reset_texture_slot()
-        mp.set_texture_uniform(GL_TEXTURE_2D, albedo, "gAlbedo")
-        mp.set_texture_uniform(GL_TEXTURE_2D, emission, "gEmission")
-        mp.set_texture_uniform(GL_TEXTURE_2D, src, "gIllumination")
-        mp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
-        self._rows(mp, "modulate")
-        self._draw(mp, "modulate")
+        if not fused:
+            mp = self.svgf_modulate_pass
+            mp.reset_texture_slot()
+            mp.set_texture_uniform(GL_TEXTURE_2D, albedo, "gAlbedo")
+            mp.set_texture_uniform(GL_TEXTURE_2D, emission, "gEmission")
+            mp.set_texture_uniform(GL_TEXTURE_2D, src, "gIllumination")
+            mp.set_texture_uniform(GL_TEXTURE_2D, g["normal_depth"], "gNormalAndLinearZ")
+            self._rows(mp, "modulate")
+            self._draw(mp, "modulate")
         if self.run_taa:
             self._halo("taa", {"modulate": self.modulate_color, "velocity": g["velocity"], "prev_taa": self.taa[pb]})
             tp = self.pass_taa[b]

@@ -611,3 +611,28 @@ def test_renderer_streams_distinct_and_recycled(gpu, scene_small):
     r2.frame()
     r2.flush()
     r2.close()
+
+
+@pytest.mark.parametrize("K", [1, 3])
+def test_fused_modulate_equals_modulate_pass(gpu, scene_small, K):
+    """The last a-trous iteration with the modulate fused into its epilogue (Renderer(fuse_modulate=True), the
+    default) against the separate modulate pass: every plane identical, bit for bit, over frames with motion."""
+    from ptsvgf.camera import parameter_config
+
+    W, H = 96, 64
+    out = {}
+    for fuse in (False, True):
+        r = _renderer(scene_small, W, H, config=parameter_config(), mode="fast", run_taa=True, run_output=True,
+                      frames_in_flight=K, fuse_modulate=fuse)
+        frames = []
+        for i in range(4):
+            r.camera.orbit(2.0, 0.5)
+            r.frame()
+            r.flush()
+            frames.append(_readback(gpu, r))
+        r.close()
+        out[fuse] = frames
+    for a, b in zip(out[False], out[True]):
+        assert a.keys() == b.keys()
+        for k in a:
+            assert np.array_equal(a[k].view(np.uint32), b[k].view(np.uint32)), k
