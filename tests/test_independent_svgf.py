@@ -1,5 +1,5 @@
 """A second, independent restatement of the SVGF passes, in numpy float64 straight from the shaders' text
-(svgf_Atrous.frag, svgf_variance.frag, svgf_modulate.frag), against the CPU oracle (oracle/, C, fp32).
+(svgf_Atrous.frag, svgf_variance.frag, svgf_modulate.frag, output_pass.frag), against the CPU oracle (oracle/, C, fp32).
 
 The oracle and the HIP kernels share glsl_builtins.h, so a wrong built-in there would pass every kernel-vs-oracle
 parity test. This restatement shares nothing with them: numpy's pow / exp / sqrt in float64, the shaders' own
@@ -147,3 +147,18 @@ def test_modulate_oracle_matches_shader_restatement():
     p = _planes(5)
     _close(O.modulate(p["albedo"], p["emission"], p["illum"], p["nd"]),
            modulate_ref(p["albedo"], p["emission"], p["illum"], p["nd"]))
+
+
+def output_ref(color):
+    """output_pass.frag:12-24: tonrMapping(c, 1.5), then pow(c, 1 / 2.2); alpha 1."""
+    c = color[..., :3].astype(np.float64)
+    lum = 0.3 * c[..., 0] + 0.6 * c[..., 1] + 0.1 * c[..., 2]
+    c = c * 1.0 / (1.0 + lum / 1.5)[..., None]
+    with np.errstate(invalid="ignore"):
+        c = c ** (1.0 / 2.2)
+    return np.concatenate([c, np.ones(c.shape[:2] + (1,))], -1)
+
+
+def test_output_oracle_matches_shader_restatement():
+    c = _planes(6)["illum"] * 3.0  # non-negative colours (pow of a negative base is undefined in GLSL)
+    _close(O.output(c), output_ref(c))
