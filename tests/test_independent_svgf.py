@@ -1,5 +1,6 @@
 """A second, independent restatement of the SVGF passes, in numpy float64 straight from the shaders' text
-(svgf_Atrous.frag, svgf_variance.frag, svgf_modulate.frag, output_pass.frag), against the CPU oracle (oracle/, C, fp32).
+(svgf_reproject.frag, svgf_variance.frag, svgf_Atrous.frag, svgf_modulate.frag, output_pass.frag), against the
+CPU oracle (oracle/, C, fp32).
 
 The oracle and the HIP kernels share glsl_builtins.h, so a wrong built-in there would pass every kernel-vs-oracle
 parity test. This restatement shares nothing with them: numpy's pow / exp / sqrt in float64, the shaders' own
@@ -162,3 +163,118 @@ def output_ref(color):
 def test_output_oracle_matches_shader_restatement():
     c = _planes(6)["illum"] * 3.0  # non-negative colours (pow of a negative base is undefined in GLSL)
     _close(O.output(c), output_ref(c))
+
+
+def reproject_ref(motion, color, albedo, emission, prev_illum, prev_moments, nd, prev_nd, fw, depth_thr=10.0,
+                  normal_thr=16.0):
+    """svgf_reproject.frag:26-204 for motions of whole texels, so every tap (uv - motion + 0 / 1 texel, the 3x3
+    fallback) sits on a texel centre and the sampler's filter and wrap modes cannot matter; the history-length tap at
+    uv - motion is kept inside the frame by the inputs."""
+    f = lambda a: a.astype(np.float64)  # noqa: E731
+    motion, color, albedo, emission, prev_illum, prev_moments, nd, prev_nd, fw = map(
+        f, (motion, color, albedo, emission, prev_illum, prev_moments, nd, prev_nd, fw))
+    H, W = color.shape[:2]
+    iw, ih = 1.0 / W, 1.0 / H
+    oi, om = np.zeros((H, W, 4)), np.zeros((H, W, 4))
+    for y in range(H):
+        for x in range(W):
+            uv = np.array([(x + 0.5) * iw, (y + 0.5) * ih])
+            zc = nd[y, x, 3]
+            if zc == 1.0:
+                oi[y, x], om[y, x] = color[y, x], prev_moments[y, x]
+                continue
+            with np.errstate(divide="ignore", invalid="ignore"):
+                ill = (color[y, x, :3] - emission[y, x, :3]) / np.maximum(albedo[y, x, :3], 0.001)
+            if np.isnan(ill).any():
+                ill = np.zeros(3)
+            prev = uv - motion[y, x, :2]
+            fwn, fwz = fw[y, x, 0], fw[y, x, 1]
+            ncur = nd[y, x, :3]
+
+            def texel(loc):
+                return int(np.floor(loc[1] * H)), int(np.floor(loc[0] * W))
+
+            def valid_at(loc):
+                if loc[0] < 0.0 or loc[0] > 1.0 or loc[1] < 0.0 or loc[1] > 1.0:
+                    return False
+                ty, tx = texel(loc)
+                pz, pn = prev_nd[ty, tx, 3], prev_nd[ty, tx, :3]
+                if abs(pz - zc) / (fwz + 1e-2) > depth_thr:
+                    return False
+                return not (np.linalg.norm(ncur - pn) / (fwn + 1e-2) > normal_thr)
+
+            offs = [(0.0, 0.0), (iw, 0.0), (0.0, ih), (iw, ih)]
+            v = [valid_at(prev + np.array(o)) for o in offs]
+            pi, pm, ok = np.zeros(4), np.zeros(2), any(v)
+            if ok:
+                fx = prev[0] - int(prev[0] / iw) * iw
+                fy = prev[1] - int(prev[1] / ih) * ih
+                wts = [(1 - fx) * (1 - fy), fx * (1 - fy), (1 - fx) * fy, fx * fy]
+                sw = 0.0
+                for k, o in enumerate(offs):
+                    if v[k]:
+                        ty, tx = texel(prev + np.array(o))
+                        pi += wts[k] * prev_illum[ty, tx]
+                        pm += wts[k] * prev_moments[ty, tx, :2]
+                        sw += wts[k]
+                ok = sw >= 0.01
+                pi, pm = (pi / sw, pm / sw) if ok else (np.zeros(4), np.zeros(2))
+            if not ok:
+                n = 0.0
+                for yy in (-1, 0, 1):
+                    for xx in (-1, 0, 1):
+                        loc = prev + np.array([xx * iw, yy * ih])
+                        if valid_at(loc):
+                            ty, tx = texel(loc)
+                            pi += prev_illum[ty, tx]
+                            pm += prev_moments[ty, tx, :2]
+                            n += 1.0
+                if n > 0:
+                    ok = True
+                    pi, pm = pi / n, pm / n
+            if ok:
+                ty, tx = texel(prev)
+                hl = prev_moments[ty, tx, 2]
+            else:
+                pi, pm, hl = np.zeros(4), np.zeros(2), 0.0
+            hl = min(32.0, hl + 1.0 if ok else 1.0)
+            a = max(0.2, 1.0 / hl) if ok else 1.0
+            m1 = _lum(ill)
+            mom = (1.0 - a) * pm + a * np.array([m1, m1 * m1])
+            oi[y, x, :3] = (1.0 - a) * pi[:3] + a * ill
+            oi[y, x, 3] = max(0.0, mom[1] - mom[0] * mom[0])
+            om[y, x, :2], om[y, x, 2] = mom, hl
+    return oi, om
+
+
+def test_reproject_oracle_matches_shader_restatement():
+    H, W = 20, 24
+    rng = np.random.default_rng(8)
+    p = _planes(9, W, H)
+    n = np.zeros((H, W, 3))
+    n[..., 2] = 1.0
+    n[..., :2] = rng.normal(0.0, 0.01, (H, W, 2))
+    n /= np.linalg.norm(n, axis=-1, keepdims=True)
+    nd = np.concatenate([n, np.full((H, W, 1), 0.5)], -1)
+    nd[rng.uniform(size=(H, W)) < 0.08] = (0.2, 0.3, 0.3, 1.0)
+    prev_nd = nd + np.concatenate([rng.normal(0, 0.005, (H, W, 3)), rng.normal(0, 1e-4, (H, W, 1))], -1)
+    bad = rng.uniform(size=(H, W)) < 0.3  # clearly invalid history texels: flipped normals or a depth jump
+    prev_nd[bad & (rng.uniform(size=(H, W)) < 0.5), :3] *= -1.0
+    prev_nd[bad, 3] += np.where(rng.uniform(size=bad.sum()) < 0.5, 1.0, 0.0)
+    prev_nd[:6, :6] *= (-1.0, -1.0, -1.0, 1.0)  # a corner where only the 3x3 fallback, or nothing, is valid
+    fw = np.zeros((H, W, 4))
+    fw[..., 0], fw[..., 1] = 0.05, 0.001
+    yy, xx = np.mgrid[0:H, 0:W]
+    mx = np.clip(rng.integers(-2, 3, (H, W)), xx - (W - 1), xx)  # uv - motion stays on a texel of the frame
+    my = np.clip(rng.integers(-2, 3, (H, W)), yy - (H - 1), yy)
+    motion = np.zeros((H, W, 4))
+    motion[..., 0], motion[..., 1] = mx / W, my / H
+    color = p["illum"].astype(np.float64) * 2.0
+    color[2, 3, :3] = np.nan  # a NaN path-tracer sample: illumination 0 (svgf_reproject.frag:176-178)
+    moments = p["moments"].astype(np.float64)
+    ins = [a.astype(np.float32) for a in (motion, color, p["albedo"], p["emission"], p["illum"], moments, nd,
+                                          prev_nd, fw)]
+    gi, gm = O.reproject(*ins, np.float32(1.0 / W), np.float32(1.0 / H))
+    wi, wm = reproject_ref(*ins)
+    _close(gi, wi)
+    _close(gm, wm)
