@@ -63,13 +63,19 @@ def acquire_stream(priority: int = 0):
     the allocations far below the pool's size over a run of many renderers (bench calibration, several views)."""
     import torch
 
-    pool = _FREE_STREAMS.setdefault((torch.cuda.current_device(), priority), [])
-    return pool.pop() if pool else torch.cuda.Stream(priority=priority)
+    key = (torch.cuda.current_device(), priority)
+    pool = _FREE_STREAMS.setdefault(key, [])
+    if pool:
+        return pool.pop()
+    stream = torch.cuda.Stream(priority=priority)
+    stream._ptsvgf_key = key  # the bucket it returns to (the priority torch reports may be clamped)
+    return stream
 
 
 def release_stream(stream) -> None:
-    if stream is not None:
-        _FREE_STREAMS.setdefault((stream.device.index, stream.priority), []).append(stream)
+    key = getattr(stream, "_ptsvgf_key", None)
+    if key is not None:
+        _FREE_STREAMS.setdefault(key, []).append(stream)
 
 
 class Renderer:
