@@ -61,15 +61,27 @@ VIEWS = {"default": None, "surface": dict(r_dis=0.8, upAngle=70.0, rotatAngle=18
 def atrous_traffic(W, rows, view="default"):
     """PMC-measured HBM bytes per a-trous launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, in KB units as the
     guide prescribes) from the committed profile, when it was taken for this kernel at this frame size on this
-    camera view; None otherwise."""
+    camera view AND of the machine code this process loaded (tools/kernel_hash.py: the a-trous tile kernel's
+    instruction bytes in the library, stable across rebuilds); (bytes or None, provenance)."""
     try:
         with open(TRAFFIC_FILE.format(view=view)) as f:
             t = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, {"profile": None}
+    prov = {"profile": t.get("source"), "profile_code_sha256": t.get("code_sha256")}
     if t.get("kernel") != ATROUS_KERNEL or t.get("pixels") != W * rows or t.get("view") != view:
-        return None
-    return t.get("bytes_per_launch")
+        return None, dict(prov, reason="profile of another kernel, frame size or view")
+    try:
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        from kernel_hash import kernel_code_hash
+        from ptsvgf._lib import LIB_DIR
+        lib = os.path.join(os.environ.get("PTSVGF_LIB_DIR", LIB_DIR), "libptsvgf.so")
+        prov["loaded_code_sha256"] = kernel_code_hash(lib, ATROUS_KERNEL)
+    except Exception as e:  # noqa: BLE001 - a failed identity check reports no traffic, never a stale one
+        return None, dict(prov, reason=f"code hash failed: {e}")
+    if not t.get("code_sha256") or t["code_sha256"] != prov["loaded_code_sha256"]:
+        return None, dict(prov, reason="stale: the profile measured other a-trous machine code")
+    return t.get("bytes_per_launch"), prov
 
 
 def parse():
@@ -376,7 +388,9 @@ def main():
         rr.fuse_modulate = bool(args.fuse_modulate)
         for kv in args.svgf_uniform:
             name, val = kv.split("=")
-            for sp in [*rr.reproject, rr.variance_compute_pass, *rr.atrous_to.values(), rr.svgf_modulate_pass]:
+            # every a-trous draw: the plain iterations and the last one with the fused modulate (atrous_mod_to)
+            for sp in [*rr.reproject, rr.variance_compute_pass, *rr.atrous_to.values(), *rr.atrous_mod_to.values(),
+                       rr.svgf_modulate_pass]:
                 sp.set_uniform_int(name, int(val))
         if VIEWS[view]:
             cam = r.camera
@@ -514,9 +528,9 @@ def main():
         achieved = alg / t / 1e9
         bgf = res["background_fraction"]
         weighted = W * rows * (bgf * ATROUS_BYTES_BG_PX + (1.0 - bgf) * ATROUS_BYTES_PER_PX)
-        traffic = atrous_traffic(W, rows, view)
+        traffic, prov = atrous_traffic(W, rows, view)
         return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_provenance": prov,
                 "kernel": ATROUS_KERNEL, "avg_launch_ms": round(atrous_ms, 4), "algorithmic_bytes_per_launch": alg,
                 "frac_pmc_traffic": round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
                 "frac_background_weighted": round(weighted / t / 1e9 / HBM_PEAK_GBS, 4),

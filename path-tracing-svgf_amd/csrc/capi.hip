@@ -224,6 +224,9 @@ struct SceneGPU {
   int root_any = 0, need_any = 0;
   bool has4 = false;  // bvh4: the 4-wide form of bvh_any (pack_wide)
   int root4 = 0, need4 = 0;
+  // refine_leaves' fine boxes are padded for rays whose origin lies within kFineEyeReach x the scene's largest vertex
+  // coordinate; an eye further out (pt_params) walks the reference tree instead
+  float fine_eye_limit = INFINITY;
   int stack_need = 0;
   int root_ref = 0;
   int ntris = 0;
@@ -665,6 +668,11 @@ static int pack_wide(const std::vector<SahNode>& nodes, const std::function<int(
 // hitTriangle (:215-272) accepts for one of those triangles passes it: the fine boxes only cull triangles that cannot
 // be hit, and the candidate set (and with it every closest t and any-hit verdict) is the reference leaf's. Exact ties
 // are re-walked on the reference tree as before. Leaves with a non-finite vertex coordinate stay whole.
+// The rounding of the hit point grows with the ray origin's magnitude and the hit distance, not with the vertices:
+// bounce and shadow rays start on the scene (|origin| <= mag), primary rays at the eye. The pad covers eyes within
+// kFineEyeReach x max(mag, 1) per coordinate (the rounding then stays >= 32x below the pad); pt_params walks the
+// reference tree (no fine boxes) for an eye beyond that.
+constexpr float kFineEyeReach = 64.0f;
 static int fine_leaf_max() {
   static const int f = [] {
     const char* e = getenv("PTSVGF_FINE_LEAVES");
@@ -709,9 +717,10 @@ static int fine_subtree(const float* tri_enc, const float* tlo, const float* thi
   return id;
 }
 
-static void refine_leaves(std::vector<SahNode>& nodes, const std::vector<SahPrim>& pr, const float* tri_enc, int ntris,
-                          int F) {
-  if (F <= 0 || !tri_enc) return;
+// Returns the coordinate magnitude the pad was sized for (0: no fine leaves).
+static float refine_leaves(std::vector<SahNode>& nodes, const std::vector<SahPrim>& pr, const float* tri_enc,
+                           int ntris, int F) {
+  if (F <= 0 || !tri_enc) return 0.0f;
   std::vector<float> tlo((size_t)ntris * 3), thi((size_t)ntris * 3);
   std::vector<char> finite((size_t)ntris);
   float mag = 0.0f;
@@ -730,6 +739,7 @@ static void refine_leaves(std::vector<SahNode>& nodes, const std::vector<SahPrim
   }
   const float pad = std::max(mag, 1.0f) * (1.0f / 4096.0f);
   const size_t n0 = nodes.size();
+  bool any = false;
   for (size_t id = 0; id < n0; ++id) {
     if (nodes[id].n <= 0) continue;
     const int ref = pr[nodes[id].first].ref;
@@ -743,13 +753,15 @@ static void refine_leaves(std::vector<SahNode>& nodes, const std::vector<SahPrim
     root.keep = true;
     nodes[id] = root;
     fine_subtree(tri_enc, tlo.data(), thi.data(), first, first + cnt, F, pad, nodes, (int)id);
+    any = true;
   }
+  return any ? std::max(mag, 1.0f) : 0.0f;
 }
 
 // Any-hit tree over the leaves of the reference tree (see above), with fine leaves under them (refine_leaves).
 int build_anyhit_tree(const float* node_enc, int nnodes, int ntris, const float* tri_enc, std::vector<float4>& out,
                       int* root_ref, int* need, std::vector<float4>* wide = nullptr, int* root_wide = nullptr,
-                      int* need_wide = nullptr) {
+                      int* need_wide = nullptr, float* fine_mag = nullptr) {
   std::vector<SahPrim> pr;
   for (int i = 1; i < nnodes; ++i) {
     const float* f = node_enc + (size_t)i * 12;
@@ -767,7 +779,8 @@ int build_anyhit_tree(const float* node_enc, int nnodes, int ntris, const float*
   nodes.reserve(2 * pr.size());
   const int F = fine_leaf_max();
   sah_build(pr, 0, (int)pr.size(), 1, nodes, 1, F > 0 ? ceil_log2(16) : 0);  // a fine subtree is <= 4 levels deep
-  refine_leaves(nodes, pr, tri_enc, ntris, F);
+  const float mag = refine_leaves(nodes, pr, tri_enc, ntris, F);
+  if (fine_mag) *fine_mag = mag;
   auto leaf_ref = [&](int first, int) { return pr[first].ref; };
   const int rc = pack_sah(nodes, leaf_ref, out, root_ref, need);
   if (rc != PT_OK || !wide) return rc;
@@ -875,8 +888,11 @@ int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU*
   {  // optional: without it shadow and closest-hit rays walk the reference tree (binary, or its 4-wide form)
     std::vector<float4> any;
     sg.has4 = false;
+    float fine_mag = 0.0f;
+    sg.fine_eye_limit = INFINITY;
     if (build_anyhit_tree((const float*)nodes->host.data(), (int)nnodes, (int)ntris, te, any, &sg.root_any,
-                          &sg.need_any, &bvh4, &root4, &need4) == PT_OK) {
+                          &sg.need_any, &bvh4, &root4, &need4, &fine_mag) == PT_OK) {
+      if (fine_mag > 0.0f) sg.fine_eye_limit = kFineEyeReach * fine_mag;
       if (any.empty()) any.push_back(float4{0, 0, 0, 0});
       if ((rc = upload_vec(any, &sg.bvh_any)) != PT_OK) return rc;
       if (bvh4.empty()) bvh4.push_back(float4{0, 0, 0, 0});
@@ -1136,7 +1152,13 @@ int pt_params(Pass* p, PTParams& k, SceneGPU*& sg) {
   k.scene.bvh = sg->bvh;
   k.scene.root_ref = sg->root_ref;
   k.stack_need = sg->stack_need;
-  if (ui(p, "shadow_tree", 1)) {  // A/B switch: 0 = shadow rays walk the reference tree
+  const Uniform* e = U(p, "eye", 5);
+  if (e) memcpy(k.eye, e->f, 12);
+  // the any-hit / closest-hit SAH trees hold fine boxes padded for eyes within sg->fine_eye_limit (refine_leaves): an
+  // eye further out walks the reference tree, whose boxes are the reference's own
+  const bool eye_near = fabsf(k.eye[0]) <= sg->fine_eye_limit && fabsf(k.eye[1]) <= sg->fine_eye_limit &&
+                        fabsf(k.eye[2]) <= sg->fine_eye_limit;
+  if (ui(p, "shadow_tree", 1) && eye_near) {  // A/B switch: 0 = shadow rays walk the reference tree
     k.scene.bvh_any = sg->bvh_any;
     k.scene.root_any = sg->root_any;
     k.stack_need = std::max(k.stack_need, sg->need_any);
@@ -1170,8 +1192,6 @@ int pt_params(Pass* p, PTParams& k, SceneGPU*& sg) {
   k.hdrResolution = ui(p, "hdrResolution", hm->W);
   k.pointLightSize = ui(p, "pointLightSize", 0);
   k.frameCounter = uu(p, "frameCounter", 0);
-  const Uniform* e = U(p, "eye", 5);
-  if (e) memcpy(k.eye, e->f, 12);
   const Uniform* cr = U(p, "cameraRotate", 6);
   if (cr) memcpy(k.camRot, cr->f, 64);
   else { k.camRot[0] = k.camRot[5] = k.camRot[10] = k.camRot[15] = 1.0f; }
@@ -1265,12 +1285,15 @@ int draw_pathtrace_batch(Pass** ps, int n) {
     TRY(pt_params(ps[b], k[b], sb));
     if (b == 0) sg = sb;
     // the batched traversal launches take their lane-refill share and visit budgets from passes[0] (pt_wf_setup
-    // sets k[b].refill and the budgets from these uniforms later): every pass of the batch must agree on them
-    const char* same[] = {"trace_refill", "shadow_budget", "closest_budget", "wide_bvh"};
+    // sets k[b].refill and the budgets from these uniforms later): every pass of the batch must agree on them, each
+    // compared at its effective value (the default pt_params / pt_wf_setup apply when a pass never set it)
+    struct Same { const char* name; int dflt; };
+    const Same same[] = {{"trace_refill", 0}, {"shadow_budget", 0}, {"closest_budget", 0}, {"wide_bvh", 1},
+                         {"refill_waves", 0}};
     bool agree = true;
-    for (const char* u : same) agree = agree && ui(ps[b], u, 0) == ui(ps[0], u, 0);
+    for (const Same& u : same) agree = agree && ui(ps[b], u.name, u.dflt) == ui(ps[0], u.name, u.dflt);
     if (sb != sg || k[b].W != k[0].W || k[b].y0 != k[0].y0 || k[b].y1 != k[0].y1 || k[b].max_depth != k[0].max_depth ||
-        !agree)
+        k[b].scene.bvh_any != k[0].scene.bvh_any || !agree)
       return err(PT_ERR_ARG, "a path-tracing batch needs one scene, size, band, depth and traversal settings");
     if (ui(ps[b], "pt_kernel", 0) != 0 || k[b].tile_stride != 1 || k[b].accumulate)
       return err(PT_ERR_ARG, "a path-tracing batch needs the wavefront path tracer on whole frames, no accumulation");

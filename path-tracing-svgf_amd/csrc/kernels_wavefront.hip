@@ -214,9 +214,6 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
   }
   uint32_t steps = 0;
   bool rewalk = false, retry = false, spill = false;
-#ifdef PT_WAVE_TIMES
-  const uint32_t t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();
-#endif
   if (valid) {
     v3 S = mk(p.eye[0], p.eye[1], p.eye[2]);
     v3 d = primary_dir(p, x, y);
@@ -253,18 +250,8 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
   stat_add(p, kStatTieRewalks, rewalk ? 1u : 0u);
   stat_add(p, kStatPrimRetries, retry ? 1u : 0u);
   stat_add(p, kStatSpills, spill ? 1u : 0u);
-#ifdef PT_WAVE_TIMES  // investigation build: per wave (start, end, max steps) in the row-cost buffer
-  uint32_t ms = steps;
-  for (int o = 32; o > 0; o >>= 1) ms = max(ms, (uint32_t)__shfl_xor((int)ms, o));
-  const uint32_t t_end = (uint32_t)__builtin_amdgcn_s_memrealtime();
-  if (p.wf.row_cost && ln == 0) {
-    uint32_t* q = p.wf.row_cost + 4 * (tile * 4 + wv);
-    q[0] = t_start; q[1] = t_end; q[2] = ms; q[3] = 1;
-  }
-#else
   sched_cost(p.tiles, tile, steps);
   if (valid) add_row_cost(p, y - p.y0, pid, steps);
-#endif
 }
 
 // ------------------------------------------------ primaries by tile binning ---

@@ -78,8 +78,35 @@ def svgf_margins(iterations: int, taa: bool) -> dict:
     per-tile flag set for all five; a later iteration's extra rows are never read)."""
     m = TAA_NEIGHBOURS if taa else 0
     v = m + sum(ATROUS_HALO[:max(0, int(iterations))])  # the variance output's margin
-    return {"taa": 0, "modulate": m, "atrous": v - ATROUS_HALO[0] if iterations > 0 else m, "variance": v,
-            "reproject": v + VARIANCE_HALO}
+    out = {"taa": 0, "modulate": m, "atrous": v - ATROUS_HALO[0] if iterations > 0 else m, "variance": v,
+           "reproject": v + VARIANCE_HALO}
+    _check_early_history(out, int(iterations))
+    return out
+
+
+def _check_early_history(margins: dict, iterations: int) -> None:
+    """The invariant the early history exchange (BandRenderer._early_history, issued on the RCCL stream while the back
+    end still runs a-trous iterations 2..n-1) relies on. The exchange overwrites the rows of the iteration-1 output
+    (hist_illum) and of this frame's normal/depth (prev_nd) outside the band with the owners' bits. Those rows may
+    change under a running iteration only where nothing the band's final rows depend on reads them, or where the
+    local bits equal the owner's:
+      * iteration i >= 2 is exact on margin_i = v - sum(ATROUS_HALO[:i+1]) rows and reads its input (iteration i-1's
+        output) ATROUS_HALO[i] rows further out, i.e. within margin_{i-1}: for i = 2 that is the iteration-1 output's
+        own exact rows, whose local bits equal the owner's (same kernels, same inputs);
+      * every iteration reads normal/depth at most ATROUS_HALO[i] rows beyond its exact rows, within the variance
+        margin v, which the G-buffer draws (reproject margin + REPROJ_REACH > v): again the owner's bits.
+    Raises if a change to the margins breaks either."""
+    if iterations < 2:
+        return
+    v = margins["variance"]
+    exact = [v - sum(ATROUS_HALO[:i + 1]) for i in range(iterations)]
+    if exact[-1] < margins["modulate"]:
+        raise AssertionError(f"a-trous margins {exact} leave the band's modulated rows inexact")
+    for i in range(2, iterations):
+        if exact[i] + ATROUS_HALO[i] > exact[i - 1]:
+            raise AssertionError(f"a-trous iteration {i} reads beyond its input's exact rows: early history unsafe")
+    if max(exact[i] + ATROUS_HALO[i] for i in range(iterations)) > margins["reproject"] + REPROJ_REACH:
+        raise AssertionError("a-trous iterations read normal/depth rows the G-buffer does not draw")
 
 
 def motion_rows(m: float, H: int) -> int:
@@ -312,6 +339,11 @@ class BandRenderer:
         from . import gl
         from .renderer import Renderer
 
+        if ghost_zone and kw.get("pt_source") is None:
+            # the margin rows the SVGF passes draw read colour / emission / albedo the band's own path tracer never
+            # draws (it covers the band only): without a source of those rows the band silently differs from a frame
+            raise ValueError("ghost_zone needs a pt_source that provides the path tracer's planes on plan.zone() rows "
+                             "(FrameShardRenderer)")
         iters = cfg.num_atrous_iterations
         margins = svgf_margins(iters, kw.get("run_taa", False)) if ghost_zone else None
         if ghost is None:

@@ -157,3 +157,31 @@ def test_ghost_zone_each_margin_is_needed(case, what, taa):
     same = [np.array_equal(np.nan_to_num(got[k][Y0:Y1], nan=-1.0).view(np.uint32), full[taa][k][Y0:Y1].view(np.uint32))
             for k in got]
     assert not all(same), what
+
+
+@pytest.mark.parametrize("iters", range(0, 9))
+@pytest.mark.parametrize("taa", [False, True])
+def test_margins_keep_early_history_safe(iters, taa):
+    """the early history exchange overwrites the iteration-1 output's and the normal/depth rows outside the
+    band while iterations 2.. still run; svgf_margins asserts that nothing the band's rows depend on reads a row whose
+    local bits can differ from the owner's (dist._check_early_history). A margin cut by one row must trip it."""
+    from ptsvgf.dist import ATROUS_HALO, _check_early_history
+
+    m = svgf_margins(iters, taa)  # does not raise
+    if iters >= 2:
+        bad = dict(m, variance=m["variance"] - 1)
+        with pytest.raises(AssertionError):
+            _check_early_history(bad, iters)
+        # reading normal/depth beyond the G-buffer's rows
+        bad = dict(m, reproject=sum(ATROUS_HALO[:iters]) - REPROJ_REACH - 1)
+        with pytest.raises(AssertionError):
+            _check_early_history(bad, iters)
+
+
+def test_ghost_zone_band_needs_pt_source():
+    """a ghost-zone band draws SVGF margin rows that its own path tracer never draws; without a pt_source
+    providing them (FrameShardRenderer) BandRenderer refuses instead of silently differing from a frame."""
+    from ptsvgf.dist import BandRenderer
+
+    with pytest.raises(ValueError, match="pt_source"):
+        BandRenderer(None, 64, 64, None, 0, 2, None, ghost_zone=True)

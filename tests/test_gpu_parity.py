@@ -570,6 +570,30 @@ def test_wide_tree_is_result_preserving(gpu, scene_name, request):
     print("visits wide / binary:", {k: (stats[0][k], stats[1][k]) for k in ("bounce_visits", "shadow_visits")})
 
 
+def test_far_eye_walks_reference_tree(gpu, scene_small):
+    """the fine leaf boxes (capi.hip refine_leaves) are padded for ray origins within kFineEyeReach = 64 x
+    the scene's largest vertex coordinate. An eye beyond that (here 200 units from a unit-sized scene) makes pt_params
+    walk the reference tree: the default settings then give exactly the bits of the reference-tree walk
+    (closest_tree = 0, shadow_tree = 0), for a camera both inside and far outside the reach."""
+    gl = gpu
+    W, H = 96, 64
+    for r_dis in (2.0, 200.0):
+        outs = []
+        for ref_tree in (0, 1):
+            r = _renderer(scene_small, W, H, mode="fast", run_taa=False, run_output=False)
+            r.camera.r_dis = np.float32(r_dis)
+            r.camera.dirty = True
+            if ref_tree:
+                r.pass_path_tracing.set_uniform_int("closest_tree", 0)
+                r.pass_path_tracing.set_uniform_int("shadow_tree", 0)
+            for _ in range(2):
+                r.frame()
+            outs.append({k: gl.readback(r.planes()[k]) for k in ("color", "emission", "albedo")})
+            r.close()
+        for k in outs[0]:
+            assert np.array_equal(outs[0][k].view(np.uint32), outs[1][k].view(np.uint32)), (r_dis, k)
+
+
 @pytest.mark.parametrize("W,H,moves", [(96, 64, [(2.0, 0.5), (-3.0, 1.0), (4.0, -2.0)]), (200, 120, [(1.0, 0.0)] * 3)])
 def test_reproject_block_fetch_equals_per_tap(gpu, scene_small, W, H, moves):
     """The reprojection's 3x3 block fetch (reproj_block = 1, the default: the four history taps' texels loaded once per

@@ -1,7 +1,9 @@
 """Per-wave timeline of wf_primary (investigation build -DPT_WAVE_TIMES): each wave's start/end (s_memrealtime,
 100 MHz) and its largest traversal step count, for the full 4K frame and for a thin band. Shows how long the
 launch's tail is and the latency per traversal step of the slowest waves.
-usage: PTSVGF_LIB_DIR=.../lib_exp/wavetimes python tools/wave_times.py"""
+usage: PTSVGF_LIB_DIR=.../lib_exp/wavetimes python tools/archive/wave_times.py
+Archived in round 4: the PT_WAVE_TIMES blocks left kernels_wavefront.hip (they are at commit d4ff747); rebuild that
+revision's library with -DPT_WAVE_TIMES to use this script."""
 import os
 import sys
 

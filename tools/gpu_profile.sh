@@ -18,6 +18,8 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 B="$R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-1080p --no-extras --frames-in-flight $FIF --view $VIEW $*"
 echo "$FIF $VIEW $B" > "$OUT/config.txt"
+# the a-trous machine code this profile measures (bench.py compares it with the library it loads)
+python3 "$R/tools/kernel_hash.py" "${PTSVGF_LIB_DIR:-$R/path-tracing-svgf_amd/lib}/libptsvgf.so" > "$OUT/atrous_code_sha256.txt"
 for p in $PASSES; do
   case $p in
     trace) A="--kernel-trace --stats" ;;
