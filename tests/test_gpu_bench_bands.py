@@ -57,3 +57,31 @@ def test_bench_band_parity_gloo(world, moving, balance, shard):
         assert {"reproject", "variance", "atrous0", "atrous4"} <= set(ex)
     else:  # ghost zone: the history exchange only, started early (overlapping the previous frame's chain)
         assert "history" in ex and not {"variance", "atrous0", "atrous4"} & set(ex), ex
+
+
+@pytest.mark.timeout(900)
+def test_bench_frame_shard_8_ranks_1080p_gloo():
+    """the default multi-GPU mode (--shard frames: rank f % 8 traces frame f whole, the SVGF chain
+    banded with the ghost zone and the early history exchange) at a BASELINE size and rank count — 8 ranks, 1920 x
+    1080 (configs[1]), a moving camera, frames_in_flight at its 8-rank default (34 band slots, back_lag 8) — rehearsed
+    with gloo on the one GPU. 16 timed frames = 2 full windows of 8 after the warm-up's windows; the gathered bands must
+    equal a one-GPU render of the same camera path bit for bit (reference: main.cpp:436-535 per frame,
+    svgf_Atrous.frag:92-97 and svgf_reproject.frag:45-156 for what crosses bands). Equal bands: the calibration only
+    moves the bounds, which the 3-rank balanced case above covers."""
+    world = 8
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "bench.py"),
+           "--gpus", str(world), "--backend", "gloo", "--width", "1920", "--height", "1080", "--steps", "16",
+           "--warmup", "2", "--no-extras", "--no-1080p", "--no-cpu-baseline", "--shard", "frames", "--moving",
+           "--equal-bands"]
+    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=850)
+    assert p.returncode == 0, p.stderr[-4000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    bp, bands = line["band_parity"], line["bands"]
+    print(json.dumps(bp), json.dumps(bands["exchange_ms_per_frame"]), bands["frames_in_flight"], bands["back_lag"],
+          line.get("max_history_rows"))
+    assert line["n_gpus"] == world and bands["shard"] == "frames"
+    assert bands["back_lag"] == world and bands["frames_in_flight"] == 4 * world + 2
+    assert bp["backend"] == "gloo" and bp["frames"] >= 2 * world + 16  # warm-up windows + 2 timed windows + probes
+    assert bp["bit_exact"], bp
+    assert line.get("max_history_rows", 0) > 3  # the orbit moved the history (reprojection reach beyond the taps)

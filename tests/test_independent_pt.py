@@ -1,0 +1,514 @@
+"""A second, independent restatement of the path tracer (path_tracing.frag main(), :1056-1128, with everything it
+calls), in numpy float64 straight from the shader's text, against the CPU oracle (oracle/oracle_pt.cpp, C, fp32).
+
+The oracle and the HIP kernels share glsl_builtins.h (Cephes sin / cos / atan / asin / log / exp / pow restated in
+fp32), so a wrong built-in, or a constant both sides copied wrong, would pass every kernel-vs-oracle parity test.
+This restatement shares nothing with them: numpy's float64 transcendentals, the shader's own order of operations,
+brute-force closest hits over every triangle instead of a BVH walk (hitBVH's result is the nearest hitTriangle over
+the triangles whose leaf boxes the ray passes, and a ray passes the box of every triangle it hits), and texture
+fetches written out from the GL LINEAR + CLAMP_TO_EDGE rule. What it takes from GL rather than from the shader:
+float(uint) rounds to fp32 (GLSL's float is 32-bit; rand() and sobol() convert integers that way) and the sampler's
+sub-texel weights are 8-bit fixed point (the texture-unit precision GL leaves to the implementation; SURVEY.md §7
+hard part 3, DESIGN.md "Parity").
+
+Agreement: per channel within 1e-3 relative (abs floor 1e-4) on all but a few pixels, and the colour's median
+relative difference at fp32 rounding (<= 1e-6; measured 1.4e-7). The few exceptions are branch flips: a comparison (xi_3 against p_diffuse,
+NdotL <= 0, an edge test, a shadow ray grazing a silhouette) that float64 and fp32 decide differently changes that
+pixel by O(1); they are counted, not hidden. A changed constant (PI, the clearcoat weight, the point-light pdf,
+the HDR pdf's texel factor, the lobe mix) moves the whole frame and must fail the comparison. CPU only."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import oracle_ref as O
+
+INF = 114514.0                      # path_tracing.frag:53
+U32 = np.uint32
+
+
+def _f32u(x):
+    """float(uint) in GLSL: round the integer to the nearest fp32 (then computed on in float64)."""
+    return np.asarray(x, np.uint32).astype(np.float32).astype(np.float64)
+
+
+def _dot(a, b):
+    return np.sum(a * b, -1)
+
+
+def _norm(v):
+    return v / np.sqrt(_dot(v, v))[..., None]
+
+
+def _cross(a, b):
+    return np.cross(a, b)
+
+
+def _mix(a, b, t):
+    return a * (1.0 - t) + b * t
+
+
+class Restatement:
+    """path_tracing.frag's live code for one frame. Constants are attributes so the mutation test can change one."""
+
+    PI = 3.1415926            # :52
+    CLEARCOAT_W = 0.25        # BRDF_Evaluate :666, r_clearcoat :759 / :859
+    POINT_PDF = 2.0           # calculatePointLight :890 (2 PI / n)
+    HDR_HALF = 2              # hdrPdf :829 (hdrResolution^2 / 2, integer)
+    GGX_CC = 0.25             # clearcoat smithG alpha :659
+
+    def __init__(self, scene):
+        te = np.asarray(scene.tri_enc, np.float64).reshape(-1, 15, 3)  # 15 RGB32F texels (getTriangle :139-162)
+        self.p1, self.p2, self.p3 = te[:, 0], te[:, 1], te[:, 2]
+        self.n1, self.n2, self.n3 = te[:, 3], te[:, 4], te[:, 5]
+        self.emissive, self.baseColor = te[:, 6], te[:, 7]                  # getMaterial :165-190
+        self.param = te[:, 8:12].reshape(-1, 12)  # subsurface metallic specular | tint rough aniso | sheen tint cc | gloss IOR trans
+        self.Nf = _norm(_cross(self.p2 - self.p1, self.p3 - self.p1))       # hitTriangle :227
+        self.NP1 = _dot(self.Nf, self.p1)
+        self.lights = np.asarray(scene.lights, np.float64).reshape(-1, 6)
+        self.hdr = np.asarray(scene.hdr, np.float64)
+        self.cache = np.asarray(scene.cache, np.float64)
+        self.hdrResolution = int(scene.hdr.shape[1])
+
+    # ------------------------------------------------------------ scene queries ---
+    def closest(self, S, d, chunk=96):
+        """hitBVH (:372-424) as the nearest hitTriangle (:215-272) over every triangle: (tri index or -1, t, P)."""
+        R = S.shape[0]
+        best = np.full(R, -1)
+        tbest = np.full(R, INF)
+        for a in range(0, R, chunk):
+            s, dd = S[a:a + chunk], d[a:a + chunk]
+            dN = dd @ self.Nf.T                                              # dot(N, d) before the flip
+            inside = dN > 0.0
+            dNf = np.where(inside, -dN, dN)                                  # after N = -N
+            ok = ~(np.abs(dNf) < 0.00001)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                t = (self.NP1[None, :] - s @ self.Nf.T) / dN               # (dot(N,p1) - dot(S,N)) / dot(d,N): sign-free
+            ok &= t >= 0.0005
+            P = s[:, None, :] + dd[:, None, :] * t[..., None]
+            Nn = np.where(inside[..., None], -self.Nf[None], self.Nf[None])
+            c1 = _dot(_cross(self.p2 - self.p1, P - self.p1), Nn)
+            c2 = _dot(_cross(self.p3 - self.p2, P - self.p2), Nn)
+            c3 = _dot(_cross(self.p1 - self.p3, P - self.p3), Nn)
+            hit = ok & (((c1 > 0) & (c2 > 0) & (c3 > 0)) | ((c1 < 0) & (c2 < 0) & (c3 < 0)))
+            th = np.where(hit, t, np.inf)
+            k = np.argmin(th, 1)
+            tk = th[np.arange(th.shape[0]), k]
+            found = tk < INF                                                 # r.distance < res.distance (INF start)
+            best[a:a + chunk] = np.where(found, k, -1)
+            tbest[a:a + chunk] = np.where(found, tk, INF)
+        P = S + d * tbest[:, None]
+        return best, tbest, P
+
+    def hit_record(self, S, d, tri, t):
+        """The HitResult of the closest hit: hit point, smooth normal (xy-plane barycentrics :261-268), material."""
+        i = np.maximum(tri, 0)
+        P = S + d * t[:, None]
+        p1, p2, p3 = self.p1[i], self.p2[i], self.p3[i]
+        inside = _dot(self.Nf[i], d) > 0.0
+        alpha = ((-(P[:, 0] - p2[:, 0]) * (p3[:, 1] - p2[:, 1]) + (P[:, 1] - p2[:, 1]) * (p3[:, 0] - p2[:, 0]))
+                 / (-(p1[:, 0] - p2[:, 0]) * (p3[:, 1] - p2[:, 1]) + (p1[:, 1] - p2[:, 1]) * (p3[:, 0] - p2[:, 0]) + 1e-7))
+        beta = ((-(P[:, 0] - p3[:, 0]) * (p1[:, 1] - p3[:, 1]) + (P[:, 1] - p3[:, 1]) * (p1[:, 0] - p3[:, 0]))
+                / (-(p2[:, 0] - p3[:, 0]) * (p1[:, 1] - p3[:, 1]) + (p2[:, 1] - p3[:, 1]) * (p1[:, 0] - p3[:, 0]) + 1e-7))
+        gama = 1.0 - alpha - beta
+        Ns = _norm(alpha[:, None] * self.n1[i] + beta[:, None] * self.n2[i] + gama[:, None] * self.n3[i])
+        N = np.where(inside[:, None], -Ns, Ns)
+        return P, N, self.emissive[i], self.baseColor[i], self.param[i]
+
+    # ---------------------------------------------------------------- textures ---
+    @staticmethod
+    def tex_linear(img, u, v):
+        """texture2D with GL_LINEAR + GL_CLAMP_TO_EDGE, texel (i, j) centred at ((i+0.5)/W, (j+0.5)/H), 8-bit
+        sub-texel weights (rounded to nearest). img rows = t (GL row 0 = image row 0)."""
+        H, W = img.shape[:2]
+        qx = np.floor(np.clip(u * W - 0.5, -4e6, 4e6) * 256.0 + 0.5)
+        qy = np.floor(np.clip(v * H - 0.5, -4e6, 4e6) * 256.0 + 0.5)
+        x0, y0 = np.floor_divide(qx, 256).astype(np.int64), np.floor_divide(qy, 256).astype(np.int64)
+        ax, ay = (qx - 256.0 * x0)[:, None] / 256.0, (qy - 256.0 * y0)[:, None] / 256.0
+        xa, xb = np.clip(x0, 0, W - 1), np.clip(x0 + 1, 0, W - 1)
+        ya, yb = np.clip(y0, 0, H - 1), np.clip(y0 + 1, 0, H - 1)
+        top = img[ya, xa] * (1.0 - ax) + img[ya, xb] * ax
+        bot = img[yb, xa] * (1.0 - ax) + img[yb, xb] * ax
+        return top * (1.0 - ay) + bot * ay
+
+    def to_spherical(self, v):                                               # :804-810
+        u = np.arctan2(v[:, 2], v[:, 0]) / (2.0 * self.PI) + 0.5
+        w = np.arcsin(v[:, 1]) / self.PI + 0.5
+        return u, 1.0 - w
+
+    def hdr_color(self, L):                                                  # :813-817
+        u, v = self.to_spherical(_norm(L))
+        return self.tex_linear(self.hdr, u, v)
+
+    def hdr_pdf(self, L):                                                    # :821-832
+        u, v = self.to_spherical(_norm(L))
+        pdf = self.tex_linear(self.cache, u, v)[:, 2]
+        theta = self.PI * (0.5 - v)
+        sin_t = np.maximum(np.sin(theta), 1e-10)
+        return pdf * float(self.hdrResolution * self.hdrResolution // self.HDR_HALF) / (2.0 * self.PI * self.PI * sin_t)
+
+    def sample_hdr(self, xi1, xi2):                                          # :787-799
+        xy = self.tex_linear(self.cache, xi1, xi2)
+        x, y = xy[:, 0], 1.0 - xy[:, 1]
+        phi = 2.0 * self.PI * (x - 0.5)
+        theta = self.PI * (y - 0.5)
+        return np.stack([np.cos(theta) * np.cos(phi), np.sin(theta), np.cos(theta) * np.sin(phi)], -1)
+
+    # -------------------------------------------------------------------- BRDF ---
+    def gtr1(self, NdotH, a):                                                # :530-535
+        a2 = a * a
+        t = 1.0 + (a2 - 1.0) * NdotH * NdotH
+        with np.errstate(divide="ignore", invalid="ignore"):
+            return np.where(a >= 1.0, 1.0 / self.PI, (a2 - 1.0) / (self.PI * np.log(a2) * t))
+
+    def gtr2(self, NdotH, a):                                                # :537-541
+        a2 = a * a
+        t = 1.0 + (a2 - 1.0) * NdotH * NdotH
+        return a2 / (self.PI * t * t)
+
+    @staticmethod
+    def smith_ggx(NdotV, alphaG):                                            # :547-551
+        a, b = alphaG * alphaG, NdotV * NdotV
+        return 1.0 / (NdotV + np.sqrt(a + b - a * b))
+
+    @staticmethod
+    def schlick(u):                                                          # :524-528
+        m = np.clip(1.0 - u, 0.0, 1.0)
+        m2 = m * m
+        return m2 * m2 * m
+
+    def brdf(self, V, N, L, base, prm):                                      # BRDF_Evaluate :620-669
+        subsurface, metallic, specular = prm[:, 0], prm[:, 1], prm[:, 2]
+        specularTint, roughness = prm[:, 3], prm[:, 4]
+        sheen, sheenTint, clearcoat, clearcoatGloss = prm[:, 6], prm[:, 7], prm[:, 8], prm[:, 9]
+        NdotL, NdotV = _dot(N, L), _dot(N, V)
+        H = _norm(L + V)
+        NdotH, LdotH = _dot(N, H), _dot(L, H)
+        Cdlum = 0.3 * base[:, 0] + 0.6 * base[:, 1] + 0.1 * base[:, 2]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            Ctint = np.where((Cdlum > 0)[:, None], base / Cdlum[:, None], 1.0)
+        Cspec = specular[:, None] * _mix(1.0, Ctint, specularTint[:, None])
+        Cspec0 = _mix(0.08 * Cspec, base, metallic[:, None])
+        Csheen = _mix(1.0, Ctint, sheenTint[:, None])
+        Fd90 = 0.5 + 2.0 * LdotH * LdotH * roughness
+        FL, FV = self.schlick(NdotL), self.schlick(NdotV)
+        Fd = _mix(1.0, Fd90, FL) * _mix(1.0, Fd90, FV)
+        Fss90 = LdotH * LdotH * roughness
+        Fss = _mix(1.0, Fss90, FL) * _mix(1.0, Fss90, FV)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            ss = 1.25 * (Fss * (1.0 / (NdotL + NdotV) - 0.5) + 0.5)
+        alpha = np.maximum(0.001, roughness * roughness)
+        Ds = self.gtr2(NdotH, alpha)
+        FH = self.schlick(LdotH)
+        Fs = _mix(Cspec0, 1.0, FH[:, None])
+        Gs = self.smith_ggx(NdotL, roughness) * self.smith_ggx(NdotV, roughness)
+        Dr = self.gtr1(NdotH, _mix(0.1, 0.001, clearcoatGloss))
+        Fr = _mix(0.04, 1.0, FH)
+        Gr = self.smith_ggx(NdotL, self.GGX_CC) * self.smith_ggx(NdotV, self.GGX_CC)
+        Fsheen = (FH * sheen)[:, None] * Csheen
+        diffuse = (1.0 / self.PI) * _mix(Fd, ss, subsurface)[:, None] * base + Fsheen
+        spec = (Gs * Ds)[:, None] * Fs
+        cc = (self.CLEARCOAT_W * Gr * Fr * Dr * clearcoat)[:, None]
+        out = diffuse * (1.0 - metallic)[:, None] + spec + cc
+        return np.where(((NdotL < 0) | (NdotV < 0))[:, None], 0.0, out)
+
+    def lobe_probs(self, prm):                                               # :757-766 = :856-865
+        r_d, r_s, r_c = 1.0 - prm[:, 1], 1.0, self.CLEARCOAT_W * prm[:, 8]
+        r_sum = r_d + r_s + r_c
+        return r_d / r_sum, r_s / r_sum, r_c / r_sum
+
+    def brdf_pdf(self, V, N, L, prm):                                        # BRDF_Pdf :837-874
+        NdotL, NdotV = _dot(N, L), _dot(N, V)
+        H = _norm(L + V)
+        NdotH, LdotH = _dot(N, H), _dot(L, H)
+        alpha = np.maximum(0.001, prm[:, 4] ** 2)
+        Ds = self.gtr2(NdotH, alpha)
+        Dr = self.gtr1(NdotH, _mix(0.1, 0.001, prm[:, 9]))
+        pd, ps, pc = self.lobe_probs(prm)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            pdf = pd * (NdotL / self.PI) + ps * (Ds * NdotH / (4.0 * LdotH)) + pc * (Dr * NdotH / (4.0 * LdotH))
+        pdf = np.maximum(1e-10, pdf)
+        return np.where((NdotL < 0) | (NdotV < 0), 0.0, pdf)
+
+    @staticmethod
+    def to_hemisphere(v, N):                                                 # :681-687
+        helper = np.where((np.abs(N[:, 0]) > 0.999)[:, None], np.array([0.0, 0.0, 1.0]), np.array([1.0, 0.0, 0.0]))
+        tangent = _norm(_cross(N, helper))
+        bitangent = _norm(_cross(N, tangent))
+        return v[:, :1] * tangent + v[:, 1:2] * bitangent + v[:, 2:3] * N
+
+    def sample_brdf(self, xi1, xi2, xi3, V, N, prm):                         # SampleBRDF :753-784
+        pd, ps, _ = self.lobe_probs(prm)
+        # diffuse: SampleCosineHemisphere :699-710
+        r, th = np.sqrt(xi1), xi2 * 2.0 * self.PI
+        x, y = r * np.cos(th), r * np.sin(th)
+        Ld = self.to_hemisphere(np.stack([x, y, np.sqrt(1.0 - x * x - y * y)], -1), N)
+
+        def gtr_h(cos_h):
+            phi = 2.0 * self.PI * xi1
+            sin_h = np.sqrt(np.maximum(0.0, 1.0 - cos_h * cos_h))
+            Hh = self.to_hemisphere(np.stack([sin_h * np.cos(phi), sin_h * np.sin(phi), cos_h], -1), N)
+            I = -V
+            return I - 2.0 * _dot(Hh, I)[:, None] * Hh                     # reflect(-V, H)
+        a2 = np.maximum(0.001, prm[:, 4] ** 2)
+        Ls = gtr_h(np.sqrt((1.0 - xi2) / (1.0 + (a2 * a2 - 1.0) * xi2)))    # SampleGTR2 :713-730
+        a1 = _mix(0.1, 0.001, prm[:, 9])
+        Lc = gtr_h(np.sqrt((1.0 - (a1 * a1) ** (1.0 - xi2)) / (1.0 - a1 * a1)))  # SampleGTR1 :733-750
+        return np.where((xi3 <= pd)[:, None], Ld, np.where((xi3 <= pd + ps)[:, None], Ls, Lc))
+
+    # ---------------------------------------------------------------- the frame ---
+    def frame(self, W, H, frameCounter, eye, camRot, clamp_threshold=10.0, max_depth=2):
+        ys, xs = np.mgrid[0:H, 0:W]
+        x, y = xs.reshape(-1).astype(np.uint64), ys.reshape(-1).astype(np.uint64)
+        R = x.size
+        M = np.asarray(camRot, np.float64).reshape(4, 4)                   # column-major: M[col][row]
+        pix = np.stack([(2.0 * x + 1.0) / W - 1.0, (2.0 * y + 1.0) / H - 1.0], -1)
+        d = _norm(pix[:, :1] * M[0, :3] + pix[:, 1:] * M[1, :3] + (-1.0) * M[2, :3])  # cameraRotate * (pix, -1, 0)
+        S = np.tile(np.asarray(eye, np.float64), (R, 1))
+        seed = ((x * 1973 + y * 9277 + np.uint64(frameCounter) * 26699) & 0xFFFFFFFF) | 1   # :433-436
+
+        def wang(s):                                                          # :438-445, uint32 arithmetic
+            s = s & 0xFFFFFFFF
+            s = ((s ^ 61) ^ (s >> 16)) & 0xFFFFFFFF
+            s = (s * 9) & 0xFFFFFFFF
+            s = s ^ (s >> 4)
+            s = (s * 0x27d4eb2d) & 0xFFFFFFFF
+            return s ^ (s >> 15)
+
+        state = {"seed": seed.copy()}
+
+        def rand():                                                           # :447-449
+            state["seed"] = wang(state["seed"])
+            return _f32u(state["seed"]) / 4294967296.0
+
+        rand(), rand()                                                        # AA jitter, never applied (:1060)
+        pseed = (x * 1973 + y * 9277 + (114514 // 1919) * 26699) & 0xFFFFFFFF | 1  # CranleyPattersonRotation :498-501
+        h1 = wang(pseed)
+        cp_u, cp_v = _f32u(h1) / 4294967296.0, _f32u(wang(h1)) / 4294967296.0
+        light = np.zeros((R, 3))
+        reduction = np.ones((R, 3))
+        alive = np.ones(R, bool)
+        emis0, base0 = np.zeros((R, 3)), np.zeros((R, 3))
+        Vsob = SOBOL_V
+        gi = (frameCounter + 1) ^ ((frameCounter + 1) >> 1)                  # grayCode (:475-477)
+
+        def sobol(dim):                                                       # :480-488
+            r, j, i = 0, 0, gi
+            while i:
+                if i & 1:
+                    r ^= int(Vsob[dim * 32 + j])
+                i >>= 1
+                j += 1
+            return float(np.float32(r)) * (1.0 / 4294967296.0)               # 1/float(0xFFFFFFFF) = 2^-32 in fp32
+
+        for i in range(max_depth):
+            idx = np.nonzero(alive)[0]
+            if idx.size == 0:
+                break
+            tri, t, _ = self.closest(S[idx], d[idx])
+            hit = tri >= 0
+            miss = idx[~hit]
+            light[miss] += self.hdr_color(d[miss]) * reduction[miss]         # :1084-1087
+            alive[miss] = False
+            idx, tri, t = idx[hit], tri[hit], t[hit]
+            P, N, emis, base, prm = self.hit_record(S[idx], d[idx], tri, t)
+            if i == 0:
+                emis0[idx], base0[idx] = emis, base
+            u = sobol(2 * i) + cp_u[idx]                                      # sobolVec2 + CP rotation :1089-1092
+            u = np.where(u > 1, u - 1, u)
+            u = np.where(u < 0, u + 1, u)
+            v = sobol(2 * i + 1) + cp_v[idx]
+            v = np.where(v > 1, v - 1, v)
+            v = np.where(v < 0, v + 1, v)
+            full = rand()                                                     # every pixel's seed advances...
+            xi3 = full[idx]                                                   # ...only the live ones are used
+            V = -d[idx]
+            L = self.sample_brdf(u, v, xi3, V, N, prm)
+            cont = _dot(N, L) > 0.0                                          # NdotL <= 0: break (:1097-1098)
+            stop = idx[~cont]
+            alive[stop] = False
+            keep = np.nonzero(cont)[0]
+            idx, P, N, emis, base, prm, V, L = (a[keep] for a in (idx, P, N, emis, base, prm, V, L))
+            # shade() :948-968 — hdriLight :922-946 (r1, r2), calculatePointLight :884-919 (light pick)
+            brdf_L = self.brdf(V, N, L, base, prm)
+            pdf_L = self.brdf_pdf(V, N, L, prm)
+            r1, r2 = rand()[idx], rand()[idx]
+            Lh = self.sample_hdr(r1, r2)
+            occ_h, _, _ = self.closest(P, Lh)
+            hdr_ok = occ_h < 0
+            with np.errstate(divide="ignore", invalid="ignore"):
+                pdf_h = np.where(hdr_ok, self.hdr_pdf(Lh), 0.0)
+                val_h = np.where(hdr_ok[:, None], self.brdf(V, N, Lh, base, prm) * np.abs(_dot(Lh, N))[:, None]
+                                 * self.hdr_color(Lh) / pdf_h[:, None], 0.0)
+            n_l = self.lights.shape[0]
+            pdf_p = np.full(idx.size, (self.POINT_PDF * self.PI) / float(n_l))
+            li = (rand()[idx] * n_l).astype(np.int64)
+            lpos, lrad = self.lights[li, :3], self.lights[li, 3:]
+            Lp = _norm(lpos - P)
+            dist = np.sqrt(_dot(lpos - P, lpos - P))
+            occ_p, t_p, P_p = self.closest(P, Lp)
+            shadowed = (occ_p >= 0) & (np.sqrt(_dot(P_p - P, P_p - P)) < dist)
+            val_p = np.where(shadowed[:, None], 0.0, (lrad / (dist * dist)[:, None]) * self.brdf(V, N, Lp, base, prm)
+                             * np.abs(_dot(Lp, N))[:, None] / pdf_p[:, None])
+            cosL = np.abs(_dot(L, N))[:, None]
+            with np.errstate(divide="ignore", invalid="ignore"):
+                val_b = emis * (brdf_L * cosL) / pdf_L[:, None]
+            sw = pdf_h + pdf_p + pdf_L + 1e-6
+            hit_light = reduction[idx] * ((pdf_h / sw)[:, None] * val_h + (pdf_p / sw)[:, None] * val_p
+                                          + (pdf_L / sw)[:, None] * val_b)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                reduction[idx] *= brdf_L * cosL / pdf_L[:, None]
+            light[idx] += hit_light
+            S[idx], d[idx] = P, L
+            gone = np.setdiff1d(np.nonzero(alive)[0], idx)
+            alive[gone] = False
+        light = np.clip(light, 0.0, clamp_threshold)                          # :1110-1113
+        color = np.where(np.isnan(light).any(-1, keepdims=True), 0.0, light)
+        one = np.ones((R, 1))
+        shape = (H, W, 4)
+        return (np.concatenate([color, one], -1).reshape(shape), np.concatenate([emis0, one], -1).reshape(shape),
+                np.concatenate([base0, one], -1).reshape(shape))
+
+
+def _sobol_table():
+    """V[8*32] (path_tracing.frag:463-472) as the product lists it (csrc/sobol_v.inc, a data table). Its content is
+    pinned independently by test_sobol_table_is_joe_kuo: dimension 0 is van der Corput and five of the other seven
+    follow the Joe-Kuo direction-number recurrence; the rest is data read from the shader's listing."""
+    import os
+    import re
+
+    path = os.path.join(os.path.dirname(O.__file__), "..", "path-tracing-svgf_amd", "csrc", "sobol_v.inc")
+    with open(path) as f:
+        v = [int(x) for x in re.findall(r"(\d+)u", f.read())]
+    assert len(v) == 256
+    return np.array(v, np.uint64)
+
+
+def _joe_kuo(s, a, m):
+    """Sobol direction numbers V_1..V_32 of one dimension from its primitive polynomial (degree s, coefficients a)
+    and initial m_1..m_s (Bratley & Fox / Joe & Kuo recurrence), as 32-bit integers."""
+    V = [0] * 33
+    for k in range(1, s + 1):
+        V[k] = m[k - 1] << (32 - k)
+    for k in range(s + 1, 33):
+        v = V[k - s] ^ (V[k - s] >> s)
+        for j in range(1, s):
+            if (a >> (s - 1 - j)) & 1:
+                v ^= V[k - j]
+        V[k] = v & 0xFFFFFFFF
+    return V[1:]
+
+
+SOBOL_V = _sobol_table()
+
+
+# -------------------------------------------------------------------------------------------------- fixtures ---
+@pytest.fixture(scope="module")
+def zoo():
+    return zoo_scene()
+
+
+def zoo_scene():
+    """A small scene whose materials exercise every lobe and branch: a Cornell box (diffuse + subsurface + sheen), a
+    low-poly teapot (clearcoat, partly metallic, tinted specular), a few plant leaves (sheen, rough), an emissive
+    patch (the brdf-sampled emission term of shade, :958), the four point lights and a small HDR environment."""
+    from ptsvgf.scene import POINT_LIGHTS, Scene, SceneBuilder, env_map, gen_cornell, gen_plant, gen_teapot, \
+        hdr_cache, material, transform
+
+    b = SceneBuilder()
+    cpos, cidx = gen_cornell()
+    b.add_mesh(cpos, cidx, material(baseColor=(0.73, 0.70, 0.65), roughness=0.8, subsurface=0.4, sheen=0.3,
+                                    sheenTint=0.7), transform(), False, 0)
+    tpos, tidx = gen_teapot(12)
+    b.add_mesh(tpos, tidx, material(baseColor=(0.85, 0.55, 0.30), metallic=0.35, specularTint=0.6, roughness=0.3,
+                                    clearcoat=1.0, clearcoatGloss=0.7), transform(trans=(0.0, -1.0, 0.0),
+                                                                                  scale=(0.9, 0.9, 0.9)), True, 1)
+    ppos, pidx = gen_plant(0, 4)
+    b.add_mesh(ppos, pidx, material(baseColor=(0.16, 0.42, 0.12), roughness=0.7, sheen=0.5, specular=0.2),
+               transform(trans=(0.55, -1.0, 0.3), scale=(0.8, 0.8, 0.8)), True, 2)
+    quad = np.array([[-0.3, 0.99, -0.3], [0.3, 0.99, -0.3], [0.3, 0.99, 0.3], [-0.3, 0.99, 0.3]], np.float32)
+    b.add_mesh(quad, np.array([[0, 2, 1], [0, 3, 2]], np.int32),
+               material(baseColor=(0.9, 0.9, 0.9), emissive=(4.0, 3.5, 3.0), roughness=0.5), transform(), False, 3)
+    b.build(8)
+    tri, node, raster = b.encode()
+    hdr = env_map(64, 32)
+    return Scene("zoo", tri, node, raster, POINT_LIGHTS.copy(), hdr, hdr_cache(hdr), b.counts())
+
+
+def _camera(W, H):
+    from ptsvgf.camera import Camera, rigid_inverse
+
+    cam = Camera(W, H)
+    cam.update()
+    return cam.cam_position, rigid_inverse(cam.cam_view_mat)
+
+
+W = H = 40
+
+
+def _compare(ref, mine):
+    """(fraction of pixels with a channel outside 1e-3 relative / 1e-4 absolute over colour, emission and albedo;
+    median relative difference of the colour channels above 1e-3; fraction of those beyond 1e-5 relative)."""
+    bad = np.zeros((H, W), bool)
+    for a, b in zip(ref, mine):
+        a, b = a[..., :3].astype(np.float64), b[..., :3]
+        bad |= np.any(np.abs(a - b) > np.maximum(1e-4, 1e-3 * np.abs(a)), -1)
+    a, b = ref[0][..., :3].astype(np.float64), mine[0][..., :3]
+    m = np.abs(a) > 1e-3
+    rel = np.abs(a - b)[m] / np.abs(a[m])
+    return float(bad.mean()), float(np.median(rel)), float(np.mean(rel > 1e-5))
+
+
+@pytest.fixture(scope="module")
+def oracle_frames(zoo):
+    eye, rot = _camera(W, H)
+    osc = O.OracleScene(zoo)
+    return [osc.path_trace(W, H, fc, eye, rot) for fc in (0, 7)]
+
+
+@pytest.mark.parametrize("k,fc", [(0, 0), (1, 7)])
+def test_path_tracer_matches_independent_restatement(zoo, oracle_frames, k, fc):
+    """The oracle's frame (fp32, shared built-ins) against the float64 restatement: the same image up to fp32
+    rounding, with branch flips on at most 1 % of the pixels. frameCounter 0 and 7: different Sobol points."""
+    eye, rot = _camera(W, H)
+    mine = Restatement(zoo).frame(W, H, fc, eye, rot)
+    frac, med, loose = _compare(oracle_frames[k], mine)
+    lit = np.mean(oracle_frames[k][0][..., :3] > 0)
+    print(f"frameCounter {fc}: pixels outside 1e-3: {frac:.4f}, colour median relative difference {med:.2e}, "
+          f"beyond 1e-5: {loose:.4f}, lit {lit:.2f}")
+    assert lit > 0.5  # the frame is mostly surface, lit (not a test of an empty image)
+    assert frac <= 0.01, frac       # branch flips (measured 0.4-0.5 %)
+    assert med <= 1e-6, med         # fp32 rounding (measured 1.4e-7)
+    assert loose <= 0.02, loose     # flips and precision-amplified channels (measured 1.1 %)
+
+
+@pytest.mark.parametrize("const,value", [("PI", 3.15), ("PI", 3.1416), ("CLEARCOAT_W", 0.3), ("POINT_PDF", 2.2),
+                                         ("HDR_HALF", 1), ("GGX_CC", 0.3)])
+def test_changed_constant_fails(zoo, oracle_frames, const, value):
+    """The comparison has teeth: one reference constant changed in the restatement (PI = 3.1415926 :52, the clearcoat
+    weight 0.25 :666/:759, the point-light pdf 2 PI / n :890, the HDR pdf's hdrResolution^2 / 2 :829, the clearcoat
+    smithG alpha 0.25 :659) and the frames no longer agree — PI = 3.1416 too, a 3e-6 relative change. The clearcoat
+    constants act on the teapot only (5-6 % of the colour channels move beyond 1e-5, against 1.1 % unmutated)."""
+    eye, rot = _camera(W, H)
+    r = Restatement(zoo)
+    setattr(r, const, value)
+    frac, med, loose = _compare(oracle_frames[0], r.frame(W, H, 0, eye, rot))
+    print(f"{const} = {value}: pixels outside 1e-3: {frac:.4f}, colour median relative difference {med:.2e}, "
+          f"beyond 1e-5: {loose:.4f}")
+    assert med > 1e-6 or loose > 0.04, (const, frac, med, loose)
+
+
+def test_sobol_table_is_joe_kuo():
+    """The Sobol table's provenance, without the shader: dimension 0 is the van der Corput sequence (1 << 31-j) and
+    dimensions 1, 2, 3, 4 and 6 are Joe & Kuo's direction numbers (new-joe-kuo-6.21201: dims 2-5 and 7, polynomial
+    degree s, coefficients a, initial m). Dimensions 5 and 7 match no degree <= 5 primitive-polynomial recurrence from
+    their own initial values: the reference lists other numbers there (used only from bounce 3 on, beyond the default
+    depth 2), which the product keeps as listed."""
+    V = SOBOL_V.reshape(8, 32).tolist()
+    assert V[0] == [1 << (31 - j) for j in range(32)]
+    for dim, (s, a, m) in {1: (1, 0, [1]), 2: (2, 1, [1, 3]), 3: (3, 1, [1, 3, 1]), 4: (3, 2, [1, 1, 1]),
+                           6: (4, 4, [1, 3, 5, 13])}.items():
+        assert V[dim] == _joe_kuo(s, a, m), dim
+    for dim in (5, 7):
+        m = [V[dim][k] >> (31 - k) for k in range(5)]
+        assert not any(V[dim] == _joe_kuo(s, a, m[:s]) for s in range(1, 6) for a in range(1 << (s - 1))), dim

@@ -165,11 +165,28 @@ def test_output_oracle_matches_shader_restatement():
     _close(O.output(c), output_ref(c))
 
 
+def tex_linear(img, u, v):
+    """texture2D(img, (u, v)) under GL_LINEAR + GL_CLAMP_TO_EDGE (getTextureRGB32F, help_func.h:22-32): texel (i, j)
+    centred at ((i + 0.5) / W, (j + 0.5) / H), the two nearest texels per axis blended, indices clamped to the edge;
+    sub-texel weights in 8-bit fixed point, rounded (the texture-unit precision GL leaves to the implementation,
+    SURVEY.md §7 hard part 3). A fetch at a texel centre returns that texel."""
+    H, W = img.shape[:2]
+    qx = np.floor((u * W - 0.5) * 256.0 + 0.5)
+    qy = np.floor((v * H - 0.5) * 256.0 + 0.5)
+    x0, y0 = int(qx // 256), int(qy // 256)
+    ax, ay = (qx - 256.0 * x0) / 256.0, (qy - 256.0 * y0) / 256.0
+    xa, xb = min(max(x0, 0), W - 1), min(max(x0 + 1, 0), W - 1)
+    ya, yb = min(max(y0, 0), H - 1), min(max(y0 + 1, 0), H - 1)
+    top = img[ya, xa] * (1.0 - ax) + img[ya, xb] * ax
+    bot = img[yb, xa] * (1.0 - ax) + img[yb, xb] * ax
+    return top * (1.0 - ay) + bot * ay
+
+
 def reproject_ref(motion, color, albedo, emission, prev_illum, prev_moments, nd, prev_nd, fw, depth_thr=10.0,
                   normal_thr=16.0):
-    """svgf_reproject.frag:26-204 for motions of whole texels, so every tap (uv - motion + 0 / 1 texel, the 3x3
-    fallback) sits on a texel centre and the sampler's filter and wrap modes cannot matter; the history-length tap at
-    uv - motion is kept inside the frame by the inputs."""
+    """svgf_reproject.frag:26-204. Every history fetch (the four taps' previous normal / depth, illumination and
+    moments, the 3x3 fallback, the history length at uv - motion) is a LINEAR texture fetch (tex_linear); the
+    current-frame planes are read at the pixel's own centre (plain texels)."""
     f = lambda a: a.astype(np.float64)  # noqa: E731
     motion, color, albedo, emission, prev_illum, prev_moments, nd, prev_nd, fw = map(
         f, (motion, color, albedo, emission, prev_illum, prev_moments, nd, prev_nd, fw))
@@ -191,31 +208,27 @@ def reproject_ref(motion, color, albedo, emission, prev_illum, prev_moments, nd,
             fwn, fwz = fw[y, x, 0], fw[y, x, 1]
             ncur = nd[y, x, :3]
 
-            def texel(loc):
-                return int(np.floor(loc[1] * H)), int(np.floor(loc[0] * W))
-
             def valid_at(loc):
                 if loc[0] < 0.0 or loc[0] > 1.0 or loc[1] < 0.0 or loc[1] > 1.0:
                     return False
-                ty, tx = texel(loc)
-                pz, pn = prev_nd[ty, tx, 3], prev_nd[ty, tx, :3]
-                if abs(pz - zc) / (fwz + 1e-2) > depth_thr:
+                pnd = tex_linear(prev_nd, *loc)
+                if abs(pnd[3] - zc) / (fwz + 1e-2) > depth_thr:
                     return False
-                return not (np.linalg.norm(ncur - pn) / (fwn + 1e-2) > normal_thr)
+                return not (np.linalg.norm(ncur - pnd[:3]) / (fwn + 1e-2) > normal_thr)
 
             offs = [(0.0, 0.0), (iw, 0.0), (0.0, ih), (iw, ih)]
             v = [valid_at(prev + np.array(o)) for o in offs]
             pi, pm, ok = np.zeros(4), np.zeros(2), any(v)
             if ok:
-                fx = prev[0] - int(prev[0] / iw) * iw
+                fx = prev[0] - int(prev[0] / iw) * iw  # the shader's "bilinear weights" in UV units (:84-91)
                 fy = prev[1] - int(prev[1] / ih) * ih
                 wts = [(1 - fx) * (1 - fy), fx * (1 - fy), (1 - fx) * fy, fx * fy]
                 sw = 0.0
                 for k, o in enumerate(offs):
                     if v[k]:
-                        ty, tx = texel(prev + np.array(o))
-                        pi += wts[k] * prev_illum[ty, tx]
-                        pm += wts[k] * prev_moments[ty, tx, :2]
+                        loc = prev + np.array(o)
+                        pi += wts[k] * tex_linear(prev_illum, *loc)
+                        pm += wts[k] * tex_linear(prev_moments, *loc)[:2]
                         sw += wts[k]
                 ok = sw >= 0.01
                 pi, pm = (pi / sw, pm / sw) if ok else (np.zeros(4), np.zeros(2))
@@ -225,16 +238,14 @@ def reproject_ref(motion, color, albedo, emission, prev_illum, prev_moments, nd,
                     for xx in (-1, 0, 1):
                         loc = prev + np.array([xx * iw, yy * ih])
                         if valid_at(loc):
-                            ty, tx = texel(loc)
-                            pi += prev_illum[ty, tx]
-                            pm += prev_moments[ty, tx, :2]
+                            pi += tex_linear(prev_illum, *loc)
+                            pm += tex_linear(prev_moments, *loc)[:2]
                             n += 1.0
                 if n > 0:
                     ok = True
                     pi, pm = pi / n, pm / n
             if ok:
-                ty, tx = texel(prev)
-                hl = prev_moments[ty, tx, 2]
+                hl = tex_linear(prev_moments, *prev)[2]
             else:
                 pi, pm, hl = np.zeros(4), np.zeros(2), 0.0
             hl = min(32.0, hl + 1.0 if ok else 1.0)
@@ -247,9 +258,17 @@ def reproject_ref(motion, color, albedo, emission, prev_illum, prev_moments, nd,
     return oi, om
 
 
-def test_reproject_oracle_matches_shader_restatement():
+@pytest.mark.parametrize("subtexel", [False, True])
+def test_reproject_oracle_matches_shader_restatement(subtexel):
+    """Whole-texel motions (every tap on a texel centre) and sub-texel motions (the bilinear fetches the camera
+    actually produces, svgf_reproject.frag:63-109 and :146). A sub-texel motion is (k + f) texels with f a multiple
+    of 1/256 other than 1/2: every tap then sits on a step of the sampler's 8-bit sub-texel grid, half a step from
+    where its rounding changes (and never on a texel boundary the shader's int() or the frame test could decide
+    either way), so float64 and fp32 take the same sampler weights and the comparison tests the arithmetic, not a
+    coin flip at a quantisation boundary. Invalid history (flipped normals, depth jumps), a fallback-only corner, a
+    NaN sample."""
     H, W = 20, 24
-    rng = np.random.default_rng(8)
+    rng = np.random.default_rng(8 + int(subtexel))
     p = _planes(9, W, H)
     n = np.zeros((H, W, 3))
     n[..., 2] = 1.0
@@ -267,6 +286,11 @@ def test_reproject_oracle_matches_shader_restatement():
     yy, xx = np.mgrid[0:H, 0:W]
     mx = np.clip(rng.integers(-2, 3, (H, W)), xx - (W - 1), xx)  # uv - motion stays on a texel of the frame
     my = np.clip(rng.integers(-2, 3, (H, W)), yy - (H - 1), yy)
+    if subtexel:
+        fx, fy = rng.integers(1, 256, (H, W)), rng.integers(1, 256, (H, W))
+        fx[fx == 128], fy[fy == 128] = 64, 192
+        mx = mx + fx / 256.0 * rng.choice([-1.0, 1.0], (H, W))
+        my = my + fy / 256.0 * rng.choice([-1.0, 1.0], (H, W))
     motion = np.zeros((H, W, 4))
     motion[..., 0], motion[..., 1] = mx / W, my / H
     color = p["illum"].astype(np.float64) * 2.0
