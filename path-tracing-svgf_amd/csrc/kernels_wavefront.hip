@@ -40,6 +40,14 @@ constexpr int kTB = 128;  // threads per traversal block (LDS stack: kStack*kTB*
 #define PT_TRACE_ATTR
 #endif
 
+// LDS stack entries of the 4-wide lane-refill walks. Unlike the binary walks (sized by the tree's depth: kStack /
+// kStackSmall), a 4-wide walk whose pushes would overflow hands its ray to the cooperative walk (wide_step), so the
+// stack can be smaller than the deepest path: it bounds the resident waves (kTB x entries x 4 B of LDS per block).
+#ifndef PT_WIDE_KS
+#define PT_WIDE_KS 24
+#endif
+constexpr int kWideKS = PT_WIDE_KS;
+
 __device__ __forceinline__ void pix_xy(const PTParams& p, int pid, int* x, int* y) {
   *x = pid % p.W;
   *y = p.y0 + pid / p.W;
@@ -1270,7 +1278,7 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s) {
       int* strag = p.wf.counters + kWfCtr * i + kCtrStragC;
       if constexpr (!DEEP)
         if (wide) {
-          hipLaunchKernelGGL((wf_trace_closest_refill<KS, false, true>), dim3(refill_blocks(nb * N)), dim3(kTB), 0, st,
+          hipLaunchKernelGGL((wf_trace_closest_refill<kWideKS, false, true>), dim3(refill_blocks(nb * N)), dim3(kTB), 0, st,
                              p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQClosest, strag);
         }
       if (!wide)
@@ -1302,7 +1310,7 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s) {
       int* strag = p.wf.counters + kWfCtr * i + kCtrStrag;  // shadow rays handed to the cooperative walk
       if constexpr (!DEEP)
         if (wide) {
-          hipLaunchKernelGGL((wf_trace_shadow_refill<KS, false, true>), dim3(refill_blocks(2 * nb * N)), dim3(kTB), 0,
+          hipLaunchKernelGGL((wf_trace_shadow_refill<kWideKS, false, true>), dim3(refill_blocks(2 * nb * N)), dim3(kTB), 0,
                              s, p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQShadow, strag);
         }
       if (!wide)

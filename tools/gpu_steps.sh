@@ -1,6 +1,7 @@
 #!/bin/bash
 # One parametrised GPU session (replaces round 3's one-off tools/gpu_r03_g*.sh scripts, which are in git history).
-# Usage (on the GPU box, e.g. gpurun -- bash tools/gpu_steps.sh STEP...), each STEP one quoted word list:
+# Usage (on the GPU box, e.g. gpurun -- bash tools/gpu_steps.sh STEP...), each STEP one quoted word list (split like a
+# shell command line, so an argument with spaces is quoted inside it):
 #   "tests [pytest args]"       GPU tests (default: every -m gpu test), log gpurun_out/<tag>_tests.log
 #   "bench TAG [bench args]"    bench.py -> gpurun_out/TAG.json (+ .err)
 #   "profile NAME"              tools/gpu_profile.sh NAME (env FIF, VIEW, PASSES as that script reads them)
@@ -15,7 +16,7 @@ T=${STEP_TIMEOUT:-900}
 n=0
 for step in "$@"; do
   n=$((n + 1))
-  read -r -a a <<< "$step"
+  eval "a=($step)"  # shell word splitting: quote an argument that holds spaces ("tests -k 'a or b'")
   kind=${a[0]}
   args=("${a[@]:1}")
   echo "[$(date +%H:%M:%S)] step $n: $step"
