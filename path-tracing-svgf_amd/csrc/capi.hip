@@ -1245,8 +1245,9 @@ int pt_wf_setup(Pass* p, PTParams& k, SceneGPU* sg, const WFState& st) {
     k.refill_waves = std::max(0, ui(p, "refill_waves", 0));
     const int ntiles = wf_subset_tiles(k.W, std::max(0, k.y1 - k.y0), k.tile_stride, k.tile_offset);  // wf_primary's grid
     TRY(tile_order_begin(p, ntiles, &k.tiles));
-    // primary rays by tile-binned rasterisation of the reference leaves (default; 0 = the per-pixel walk)
-    if (ui(p, "primary_raster", 1) && k.tile_stride == 1 && k.tile_offset == 0) {
+    // primary rays by tile-binned rasterisation of the reference leaves (default; 0 = the per-pixel walk); the leaves
+    // are binned to every tile of the band, a tile subset rasterises its own tiles
+    if (ui(p, "primary_raster", 1)) {
       TRY(bins_for(p->bins, sg->nleaves, k.W, k.y0, k.y1, ui(p, "raster_pair_cap", 0), &k.leaf_bins));
       k.primary_raster = 1;
     }

@@ -212,7 +212,13 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
   bool count_ray = true;
   if (p.pr_fix) {  // after wf_primary_raster: walk only the pixels it flagged, or all of them after an overflow
     if (p.pr_fix[2]) {
-      if (threadIdx.x == 0) p.leaf_bins.tile_count[gt] = 0;  // the skipped scatter did not count them back to zero
+      // the skipped scatter did not count the tiles back to zero: the block of subset slot `tile` clears the tiles of
+      // its stride group (the last slot also the band's tail), so every band tile is cleared once
+      if (threadIdx.x == 0) {
+        const int all = ntx * ((p.y1 - p.y0 + 15) / 16), lo = tile * p.tile_stride;
+        const int hi = tile + 1 == (int)gridDim.x ? all : min(all, lo + p.tile_stride);
+        for (int j = lo; j < hi; ++j) p.leaf_bins.tile_count[j] = 0;
+      }
     } else {
       if (p.closest_tree) return;  // the flagged pixels went to wf_primary_coop
       valid = valid && ldnt(&p.wf.hit[pid]).x == kTieFix;
@@ -352,9 +358,10 @@ __global__ void __launch_bounds__(256) wf_primary_raster(PTParams p) {
   const Bins& bn = p.leaf_bins;
   if (bn.ctr[2]) return;  // overflow: wf_primary walks every pixel
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-  const int tile = blockIdx.x, ntx = (p.W + 15) / 16;
-  const int x = (tile % ntx) * 16 + (wv & 1) * 8 + (ln & 7);
-  const int y = p.y0 + (tile / ntx) * 16 + (wv >> 1) * 8 + (ln >> 3);
+  // subset slot -> band tile (PTParams::tile_stride: a pass may trace every tile_stride-th tile; the bins cover all)
+  const int tile = blockIdx.x, gt = tile * p.tile_stride + p.tile_offset, ntx = (p.W + 15) / 16;
+  const int x = (gt % ntx) * 16 + (wv & 1) * 8 + (ln & 7);
+  const int y = p.y0 + (gt / ntx) * 16 + (wv >> 1) * 8 + (ln >> 3);
   const bool valid = x < p.W && y < p.y1;
   const int pid = (y - p.y0) * p.W + x;
   const v3 S = mk(p.eye[0], p.eye[1], p.eye[2]);
@@ -374,7 +381,7 @@ __global__ void __launch_bounds__(256) wf_primary_raster(PTParams p) {
   int best = -1;
   bool tied = false;
   uint32_t steps = 0;
-  const int off = bn.tile_off[tile], total = bn.tile_off[tile + 1] - off;
+  const int off = bn.tile_off[gt], total = bn.tile_off[gt + 1] - off;
   for (int base = 0; base < total; base += kPChunk) {
     __syncthreads();
     const int j = base + (int)threadIdx.x;
@@ -1243,7 +1250,7 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s) {
   if (ntiles <= 0) return 0;
   for (int b = 0; b < nb; ++b) {
     const PTParams& f = ps[b];
-    if (f.primary_raster) {  // every tile of the band (the host enables it only without tile subsets)
+    if (f.primary_raster) {  // leaves binned to every tile of the band; the subset's tiles rasterised
       if (f.scene.nleaves > 0) hipLaunchKernelGGL(pr_setup, dim3((f.scene.nleaves + 255) / 256), dim3(256), 0, s, f);
       const int rc = launch_bins(f.leaf_bins, s);
       if (rc) return rc;

@@ -283,16 +283,20 @@ def test_wavefront_equals_megakernel(gpu, scene_small):
         assert np.array_equal(outs[0][k], outs[1][k]), k
 
 
-@pytest.mark.parametrize("W,H,stride", [(96, 64, 3), (100, 70, 4)])
-def test_tile_subsets_compose_to_full_frame(gpu, scene_small, W, H, stride):
+@pytest.mark.parametrize("W,H,stride,cap", [(96, 64, 3, 0), (100, 70, 4, 0), (96, 64, 3, 16)])
+def test_tile_subsets_compose_to_full_frame(gpu, scene_small, W, H, stride, cap):
     """tile_stride / tile_offset: each subset writes exactly its 16x16 tiles (others keep their contents) and
-    the subsets of one frame together give the full-frame bits (ragged edge tiles included)."""
+    the subsets of one frame together give the full-frame bits (ragged edge tiles included). The primaries of a subset
+    are rasterised by tile-binned leaves like a whole band's (the bins cover every tile, the subset's tiles run);
+    cap = 16: a leaf-pair list too small for the frame, so every subset overflows, walks its pixels and must clear
+    the tile counts of the whole band (not only its own tiles) for the next subset's binning."""
     gl = gpu
     a = _renderer(scene_small, W, H, mode="fast", run_taa=False, run_output=False)
     a.frame()
     want = {k: gl.readback(a.planes()[k]) for k in ("color", "emission", "albedo")}
     b = _renderer(scene_small, W, H, mode="fast", run_taa=False, run_output=False)
     pt = b.pass_path_tracing
+    pt.set_uniform_int("raster_pair_cap", cap)
     pt.set_uniform_int("tile_stride", stride)
     pt.set_uniform_int("tile_offset", 0)
     b.frame()

@@ -37,7 +37,7 @@ def main(src: str, dst: str, pixels: int, view: str = "default") -> None:
         shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
     acc = defaultdict(lambda: defaultdict(list))
     replay = defaultdict(list)  # counter -> a-trous tile kernel values in dispatch order (every instantiation)
-    for sub in ("fetch", "write", "sq", "l2", "sq2"):
+    for sub in ("fetch", "write", "sq", "l2", "sq2", "ta"):
         path = os.path.join(src, sub, "run_counter_collection.csv")
         if not os.path.exists(path):
             continue
