@@ -104,13 +104,16 @@ def parse():
                     help="multi-GPU: skip the untimed bitwise check of the gathered bands against a one-GPU frame")
     ap.add_argument("--equal-bands", action="store_true",
                     help="multi-GPU: equal band heights (no balancing of the measured band work)")
-    ap.add_argument("--shard", default="frames", choices=("frames", "bands"),
+    ap.add_argument("--shard", default="frames", choices=("frames", "tiles", "bands"),
                     help="multi-GPU: 'frames' = rank f %% N traces frame f whole and scatters its rows to the band owners, "
-                         "the SVGF chain banded (dist.FrameShardRenderer); 'bands' = every pass banded (dist.BandRenderer)")
+                         "the SVGF chain banded (dist.FrameShardRenderer); 'tiles' = every rank traces the 16x16 tiles "
+                         "k*N + rank of every frame, one all-to-all per frame to the band owners, the SVGF chain banded "
+                         "(dist.TileShardRenderer); 'bands' = every pass banded (dist.BandRenderer)")
     ap.add_argument("--ship-gbuffer", type=int, default=0, choices=(0, 1),
                     help="--shard frames: the tracing rank also sends the bands their G-buffer rows (they draw none)")
     ap.add_argument("--own-slots", type=int, default=4,
-                    help="--shard frames: whole frames a rank traces at once (its path tracer's frames in flight)")
+                    help="--shard frames / tiles: whole frames / tile subsets a rank traces at once (its path tracer's "
+                         "frames in flight)")
     ap.add_argument("--breakdown", action="store_true", help="print per-pass ms to stderr")
     ap.add_argument("--pt-kernel", type=int, default=0, help="0 wavefront (production), 1 megakernel (A/B)")
     ap.add_argument("--trace-batch", type=int, default=None,
@@ -322,6 +325,9 @@ def main():
             # has arrived (simulated, tools/frame_shard_sim.py: N = 2 K = 10 / 16 / 24: 294 / 333 / 321 fps; N = 8
             # K = 34 / 50 within noise)
             args.frames_in_flight = k1080 = max(16, 4 * world + 2)
+        if world > 1 and args.shard == "tiles":
+            # band slots cover back_lag (2) + the subsets' frames in flight
+            args.frames_in_flight = k1080 = 8
     if args.trace_batch is None:
         args.trace_batch = 1
     # every frame slot must have run once before the timed region (a slot's first frame allocates its
@@ -372,6 +378,10 @@ def main():
             r = make_frame_shard_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,
                                           own_slots=args.own_slots, frames_in_flight=K,
                                           ship_gbuffer=bool(args.ship_gbuffer))
+        elif world > 1 and args.shard == "tiles":
+            from ptsvgf.dist import TileShardRenderer, make_frame_shard_renderer
+            r = make_frame_shard_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,
+                                          cls=TileShardRenderer, own_slots=args.own_slots, frames_in_flight=K)
         elif world > 1:
             from ptsvgf.dist import make_band_renderer
             r = make_band_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,
@@ -427,6 +437,21 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         out = {"dt": dt, "rows": r.rows_rendered() if hasattr(r, "rows_rendered") else H}
+        rr = getattr(r, "r", r)
+        if K > 1 and probes:
+            # camera-to-modulate latency (untimed frames): from a frame's camera reaching the GPU to the end of its
+            # SVGF chain, HIP events; in frames of the timed rate
+            rr.latency_events = []
+            for _ in range(3 * K):
+                step()
+            lat = rr.latency_ms()
+            rr.latency_events = None
+            if dist:
+                t = torch.tensor([lat], dtype=torch.float64, device="cuda")
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                lat = float(t.item())
+            out["latency"] = {"camera_to_modulate_ms": round(lat, 3),
+                              "frames": round(lat / (dt / args.steps * 1e3), 2), "back_lag": rr.lag}
         if world > 1:  # the band plan the calibration chose: (slowest band ms, bounds) per measured plan
             ex = r.exchange_ms()
             r.time_exchanges(False)
@@ -440,7 +465,7 @@ def main():
                                                       if k in ex or v > 0},
                             "exchange_ms_rank0": ex,
                             "calibration": [[round(m, 3), list(b)] for m, b in getattr(r, "calibration", [])]}
-            if getattr(r, "scatter_log", None):  # --shard frames: bytes a rank sends per frame it traces
+            if getattr(r, "scatter_log", None):  # --shard frames: bytes a rank sends per frame it traces (tiles: per frame)
                 out["bands"]["scatter_mb_per_traced_frame"] = round(sum(r.scatter_log) / len(r.scatter_log) / 1e6, 3)
         log(f"  {args.steps} frames in {dt:.3f} s = {args.steps / dt:.2f} frames/s")
         if probes:
@@ -614,14 +639,17 @@ def main():
                                        + (f" {args.view} view" if args.view != "default" else ""),
                            "resolution": [W, H], "spp": 1, "max_tracing_depth": cfg.max_tracing_depth,
                            "atrous_iterations": cfg.num_atrous_iterations, "triangles": scene.ntris,
-                           "parallelism": (f"frames{world}+svgf_bands{world}" if world > 1 and args.shard == "frames"
-                                           else f"bands{world}"), "frames_in_flight": K,
+                           "parallelism": (f"{args.shard}{world}+svgf_bands{world}"
+                                           if world > 1 and args.shard in ("frames", "tiles") else f"bands{world}"),
+                           "frames_in_flight": K,
                            "trace_batch": min(args.trace_batch, K)},
                 "roofline": atrous_roofline(res, W, res["rows"], args.view), "cpu_baseline": cpu,
                 "path_tracer": pt_rates(res, fps), **extra,
                 "passes_ms": {k: round(v, 4) for k, v in res["per_pass"].items()}}
         if "max_history_rows" in res:
             line["max_history_rows"] = res["max_history_rows"]
+        if "latency" in res:
+            line["latency"] = res["latency"]
         if "bands" in res:
             line["bands"] = res["bands"]
         if res.get("band_parity") is not None:

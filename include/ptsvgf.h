@@ -143,6 +143,19 @@ int pt_raster_pass_share(uint32_t pass, uint32_t src_pass);
  * derive what a draw makes beside its planes (the a-trous's compact depth-fwidth plane and per-tile surface flags,
  * "atrous_rows_begin" / "_end" as for a draw) on the current stream. No reference counterpart. */
 int pt_raster_pass_adopt(uint32_t pass, int y_begin, int y_end);
+/* Tile shard (multi-GPU, no GL counterpart): a path-tracing pass with "tile_stride" = S and "tile_offset" = o draws the
+ * 16 x 16 tiles t = k * S + o of its rows, numbered row-major from its first row (tile_y0) with frame_w / 16 tiles per
+ * row. pt_tiles_copy moves the pixels of such subsets between textures (RGBA32F, the same width, a multiple of 16) and
+ * packed device buffers, one segment per (rows, subset, buffer): unpack = 0 writes the segment's packed block from the
+ * textures, 1 writes the textures from it. A block holds, for each texture in order, each row of [y_begin, y_end) in
+ * order, each row's subset tiles in x order: pt_tiles_count(...) pixels per texture (16 B each). Asynchronous on the
+ * library stream; segment rows must lie in every texture's stored rows. */
+typedef struct {
+  int y_begin, y_end, offset;
+  void* packed;
+} PtTileSeg;
+int pt_tiles_count(int frame_w, int tile_y0, int stride, int offset, int y_begin, int y_end, int64_t* out_pixels);
+int pt_tiles_copy(const uint32_t* tex, int ntex, int tile_y0, int stride, const PtTileSeg* segs, int nseg, int unpack);
 int pt_pass_reset_texture_slot(uint32_t pass);
 int pt_pass_set_texture(uint32_t pass, uint32_t target, uint32_t tex, const char* name);
 int pt_pass_set_uniform_mat4(uint32_t pass, const char* name, const float* m16);

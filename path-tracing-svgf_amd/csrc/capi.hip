@@ -2118,6 +2118,58 @@ int pt_raster_pass_adopt(uint32_t pass, int y_begin, int y_end) {
   return PT_OK;
 }
 
+int pt_tiles_count(int frame_w, int tile_y0, int stride, int offset, int y_begin, int y_end, int64_t* out_pixels) {
+  if (!out_pixels || frame_w <= 0 || frame_w % 16 || stride < 1 || offset < 0 || offset >= stride || y_begin > y_end ||
+      y_begin < tile_y0)
+    return err(PT_ERR_ARG, "pt_tiles_count: width a multiple of 16, 0 <= offset < stride, tile_y0 <= y_begin <= y_end");
+  *out_pixels = ptk::shard_pixels(frame_w, tile_y0, stride, offset, y_begin, y_end);
+  return PT_OK;
+}
+
+int pt_tiles_copy(const uint32_t* tex, int ntex, int tile_y0, int stride, const PtTileSeg* segs, int nseg, int unpack) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  if (!tex || ntex < 1 || ntex > 4 || (nseg > 0 && !segs) || nseg < 0 || stride < 1)
+    return err(PT_ERR_ARG, "pt_tiles_copy: 1..4 textures, segments, stride >= 1");
+  ptk::ShardCopy c;
+  memset(&c, 0, sizeof(c));
+  c.tile_y0 = tile_y0;
+  c.stride = stride;
+  c.nplanes = ntex;
+  c.unpack = unpack ? 1 : 0;
+  Texture* ts[4] = {nullptr, nullptr, nullptr, nullptr};
+  for (int j = 0; j < ntex; ++j) {
+    Texture* t = tex_of(tex[j]);
+    if (!t || t->target != PT_TEXTURE_2D || !t->dev) return err(PT_ERR_INVALID_HANDLE, "pt_tiles_copy: invalid texture");
+    if (j > 0 && t->W != ts[0]->W) return err(PT_ERR_ARG, "pt_tiles_copy: textures of different widths");
+    if (t->W % 16) return err(PT_ERR_ARG, "pt_tiles_copy: the frame width must be a multiple of 16");
+    ts[j] = t;
+    c.plane[j] = (float4*)t->dev;
+    c.row0[j] = t->row0;
+  }
+  c.W = ts[0]->W;
+  for (int s = 0; s < nseg; ++s) {
+    const PtTileSeg& q = segs[s];
+    if (q.offset < 0 || q.offset >= stride || q.y_begin < tile_y0 || q.y_begin > q.y_end || (!q.packed && q.y_end > q.y_begin))
+      return err(PT_ERR_ARG, "pt_tiles_copy: bad segment");
+    for (int j = 0; j < ntex; ++j)
+      if (q.y_end > q.y_begin && (q.y_begin < ts[j]->row0 || q.y_end > ts[j]->row0 + ts[j]->rows))
+        return err(PT_ERR_ARG, "pt_tiles_copy: segment rows outside a texture's stored rows");
+  }
+  for (int s0 = 0; s0 < nseg; s0 += ptk::kShardSegs) {  // one launch per kShardSegs segments
+    c.nseg = std::min(ptk::kShardSegs, nseg - s0);
+    for (int s = 0; s < c.nseg; ++s) {
+      const PtTileSeg& q = segs[s0 + s];
+      c.seg[s] = ptk::ShardSeg{q.y_begin, q.y_end, q.offset, (float4*)q.packed};
+    }
+    const int rc = ptk::launch_shard_copy(c, g.stream);
+    if (rc) return hip_err((hipError_t)rc, "pt_tiles_copy");
+  }
+  if (unpack)
+    for (int j = 0; j < ntex; ++j) ts[j]->version++;  // new texels, as after a draw
+  return PT_OK;
+}
+
 int pt_pass_reset_texture_slot(uint32_t pass) {
   Pass* p = pass_of(pass);
   if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");

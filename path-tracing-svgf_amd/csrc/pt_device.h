@@ -304,11 +304,28 @@ struct TAAParams {
   uint32_t frameCounter;
 };
 
+// Tile-shard transfer (kernels_shard.hip): the pixels of the 16 x 16 tile subset (t = k * stride + seg.offset, tiles
+// numbered row-major from row tile_y0, W / 16 per row) in rows [seg.y0, seg.y1) of each plane, to (unpack = 0) or from
+// (1) the segment's packed block: plane-major, rows in order, each row's subset tiles in x order.
+constexpr int kShardSegs = 16;
+struct ShardSeg {
+  int y0, y1, offset;
+  float4* packed;
+};
+struct ShardCopy {
+  int W, tile_y0, stride, nseg, nplanes, unpack;
+  float4* plane[4];
+  int row0[4];
+  ShardSeg seg[kShardSegs];
+};
+
 }  // namespace ptk
 
 #if defined(__HIPCC__)
 namespace ptk {
 // Launchers (kernels_*.hip). Return hipError_t as int.
+int launch_shard_copy(const ShardCopy& c, hipStream_t s);
+long long shard_pixels(int W, int tile_y0, int stride, int offset, int y0, int y1);  // per plane
 int launch_pathtrace(const PTParams& p, hipStream_t s);
 int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s);
 int wf_list_capacity(int W, int rows);  // per-segment capacity of the compacted ray lists (8 segments)

@@ -925,6 +925,206 @@ class FrameShardRenderer(BandRenderer):
         self._recv_stream = None
 
 
+def exchange_tiles(send, sends, recv, recvs, dist, group=None) -> int:
+    """One tile-shard frame's all-to-all: sends = [(peer, first, end)] element ranges of the flat device buffer `send`
+    (this rank's tiles of peer's band rows, every plane), recvs = [(source, first, end)] of `recv` (the source's tiles
+    of this band's rows). One symmetric batch (every rank pairs its sends with its peers' receives), every link at
+    once. RCCL: the current stream waits for the batch; gloo (tests): blocking, staged through host memory. Returns the
+    bytes sent."""
+    gloo = dist.get_backend(group) == "gloo"
+    ops, staged, nbytes = [], [], 0
+    hsend = send.cpu() if gloo and send.is_cuda else send
+    for k, a, b in sends:
+        ops.append(dist.P2POp(dist.isend, hsend[a:b], k, group))
+        nbytes += (b - a) * send.element_size()
+    for s, a, b in recvs:
+        buf = recv[a:b]
+        if gloo and recv.is_cuda:
+            h = buf.cpu()
+            staged.append((buf, h))
+            buf = h
+        ops.append(dist.P2POp(dist.irecv, buf, s, group))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    for t, h in staged:
+        t.copy_(h)
+    return nbytes
+
+
+class TileShardRenderer(BandRenderer):
+    """Screen tiles across ranks for the path tracer, bands for the SVGF chain (north_star: "frames shard by
+    screen-tile across the 8 GPUs").
+
+    Every frame, rank r traces the 16 x 16 tiles t = k * N + r of the WHOLE frame (the path tracer's tile_stride /
+    tile_offset subset; RNG seeds use global pixel coordinates, path_tracing.frag:433-436, so the N subsets compose to
+    the one-GPU frame bit for bit): every rank holds an even share of the expensive tiles, and each traversal launch
+    carries an N-th of the frame's rays. The SVGF chain is sequential through its history, so it stays banded exactly
+    as in FrameShardRenderer (ghost zone, BandRenderer ghost_zone): every rank draws its band's G-buffer and runs
+    reproject / variance / a-trous with the modulate fused, and only the histories cross ranks.
+
+    Between the two, one all-to-all per frame (exchange_tiles, on a communicator of its own, scatter_group): each rank
+    packs its tiles of every other band's zone rows (plan.zone: the band widened by the reprojection's margin) into
+    one contiguous message per peer (pt_tiles_copy, one launch for all peers and planes), the messages travel over
+    every xGMI link at once, and the band unpacks the N subsets of its zone into its colour / emission / albedo planes
+    (one launch). The back end of frame f waits for that frame's exchange only, so it runs back_lag frames behind its
+    front end (default 2: the host's motion-bound wait finds a G-buffer issued two frames earlier), not N as in the
+    frame shard. own_slots = subsets this rank traces at once (the path tracer's frames in flight)."""
+
+    PT_PLANES = 3  # colour, emission, albedo (the path tracer's outputs the SVGF chain reads)
+
+    def __init__(self, scene, W, H, cfg, rank, world, dist, own_slots: int = 2, **kw):
+        import torch
+
+        from . import gl
+        from .renderer import Renderer, acquire_stream
+
+        if W % 16:
+            raise ValueError(f"the tile shard needs a frame width that is a multiple of 16 (the path tracer's tiles), got {W}")
+        K = kw.get("frames_in_flight", 1)
+        kw.setdefault("back_lag", min(2, max(0, K - 1)))
+        if K < 2:
+            raise ValueError("TileShardRenderer needs frames_in_flight >= 2")
+        self._full_tensors = {}
+        dev = torch.device("cuda", torch.cuda.current_device())
+
+        def full_factory(w, h):
+            t = torch.zeros((h, w, 4), dtype=torch.float32, device=dev)
+            handle = gl.wrap_device_texture(t.data_ptr(), w, h)
+            self._full_tensors[handle] = t
+            return handle
+
+        gl.set_band(W, H, 0, H, 0, H)  # process-global band state: the subset's planes are whole frames
+        self.full = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, tex_factory=full_factory,
+                             run_taa=False, run_output=False, frames_in_flight=max(2, int(own_slots)))
+        for p, _ in self.full.pt_slots:
+            p.set_rows(0, H)
+            p.set_uniform_int("tile_stride", world)
+            p.set_uniform_int("tile_offset", rank)
+        self.own_slots = self.full.K
+        self._own_free = [None] * self.own_slots  # event: the pack that read the slot's last subset is done
+        kw.setdefault("front_streams", 1)
+        kw["ghost_zone"] = True
+        super().__init__(scene, W, H, cfg, rank, world, dist, pt_source=self._pt_source, **kw)
+        self.full.camera = self.r.camera
+        self.pass_path_tracing = self.full.pass_path_tracing
+        if self.r.K > 1:  # the subset's launches carry an N-th of the rays: the band's traversal settings (BandRenderer)
+            self.pass_path_tracing.set_uniform_int("shadow_budget", BAND_VISIT_BUDGET)
+            self.pass_path_tracing.set_uniform_int("closest_budget", BAND_VISIT_BUDGET)
+            self.pass_path_tracing.set_uniform_int("refill_waves", BAND_REFILL_WAVES)
+        self._sgroup = scatter_group(dist) if world > 1 else None
+        self._recv_stream = acquire_stream()
+        # message layout, fixed per plan: my tiles of band k's zone (k != me), then the N subsets of my zone
+        p, n3 = self.plan, self.PT_PLANES * 4
+        self._send_segs, self._sends, off = [], [], 0
+        for k in range(world):
+            if k == rank:
+                continue
+            z0, z1 = p.zone(k)
+            n = gl.tiles_count(W, world, rank, z0, z1)
+            self._send_segs.append((z0, z1, rank, off))
+            self._sends.append((k, off * n3, (off + n) * n3))
+            off += n
+        self._send = torch.empty(max(1, off) * n3, dtype=torch.float32, device=dev)
+        z0, z1 = p.zone(rank)
+        self._recv_segs, self._recvs, off = [], [], 0
+        for s in range(world):
+            n = gl.tiles_count(W, world, s, z0, z1)
+            self._recv_segs.append((z0, z1, s, off))
+            if s != rank:
+                self._recvs.append((s, off * n3, (off + n) * n3))
+            off += n
+        self._recv = torch.empty(max(1, off) * n3, dtype=torch.float32, device=dev)
+        self.scatter_log = []  # bytes sent per frame
+
+    def _segs(self, segs, buf):
+        base = buf.data_ptr()
+        return [(a, b, o, base + off * self.PT_PLANES * 16) for a, b, o, off in segs]
+
+    def _pt_source(self, f: int, slot: int, stream):
+        """Renderer pt_source: trace this rank's tiles of frame f (own slot f % own_slots), exchange every band's
+        rows of the frame, unpack this band's zone. Returns the holder whose "ev" the back end of f waits for."""
+        import torch
+
+        from . import gl
+
+        r, p, fr = self.r, self.plan, self.full
+        o = f % self.own_slots
+        st = fr._streams[o]
+        if self._own_free[o] is not None:
+            st.wait_event(self._own_free[o])
+        fr._use_slot(o)
+        fr._stream_to(st)
+        fr.frame_index = f
+        fr._path_trace(None)  # the subset's primaries come from its own tile-binned raster (no G-buffer hint)
+        done = torch.cuda.Event()
+        done.record(st)
+        rs = self._recv_stream
+        rs.wait_event(done)
+        free = r._slot_free[f % r.K]  # the band slot's planes: read by the SVGF chain of frame f - K
+        if free is not None:
+            rs.wait_event(free)
+        r._stream_to(rs)
+        full = list(fr.pt_slots[o][1])
+        band = list(r.pt_slots[slot][1])
+        # my tiles: every other band's zone into the send buffer, my own band's zone straight into my slot of the recv
+        gl.tiles_copy(full, p.world, self._segs(self._send_segs, self._send)
+                      + [s for s in self._segs(self._recv_segs, self._recv) if s[2] == p.rank], unpack=False)
+        packed = torch.cuda.Event()
+        packed.record(rs)
+        self._own_free[o] = packed
+        with torch.cuda.stream(rs):
+            nbytes = exchange_tiles(self._send, self._sends, self._recv, self._recvs, self.dist,
+                                    self._sgroup) if p.world > 1 else 0
+        r._stream_to(rs)
+        gl.tiles_copy(band, p.world, self._segs(self._recv_segs, self._recv), unpack=True)
+        ev = torch.cuda.Event()
+        ev.record(rs)
+        r._stream_to(stream)
+        self.scatter_log.append(nbytes)
+        return {"ev": ev}
+
+    def trace_stats(self) -> dict:
+        """Traversal counters of one frame: each rank counts its tiles (bench sums over ranks)."""
+        import torch
+
+        buf = torch.zeros(len(self.r.STAT_KEYS), dtype=torch.int64, device="cuda")
+        self.r.flush()
+        torch.cuda.synchronize()
+        for q, _ in self.full.pt_slots:
+            q.set_trace_stats(buf.data_ptr())
+        try:
+            self.r.frame()
+            self.r.flush()
+            torch.cuda.synchronize()
+        finally:
+            for q, _ in self.full.pt_slots:
+                q.set_trace_stats(0)
+        return dict(zip(self.r.STAT_KEYS, (int(v) for v in buf.cpu().tolist())))
+
+    def profile(self, on: bool) -> None:
+        self.r.profile(on)
+        self.full.profile(on)
+
+    band_ms = FrameShardRenderer.band_ms
+
+    def pass_times(self) -> dict:
+        out = self.r.pass_times()
+        for k, v in self.full.pass_times().items():
+            if k == "pathtrace":
+                out["tiles_" + k] = v
+        return out
+
+    def close(self) -> None:
+        from .renderer import release_stream
+
+        super().close()
+        self.full.close()
+        self._full_tensors.clear()
+        release_stream(self._recv_stream)
+        self._recv_stream = None
+
+
 def gather_bands(owned: dict, plan: BandPlan, dist, dst: int = 0) -> dict | None:
     """Assemble full frames on rank `dst` from every rank's owned rows: owned maps plane names to (y1 - y0, W, C)
     float32 numpy arrays; returns {name: (H, W, C)} on dst, None elsewhere. Point-to-point sends of device tensors
@@ -994,16 +1194,19 @@ def fit_row_cost(visits, rows, ms):
     return 0.0, float(t.sum() / max(A[:, 1].sum(), 1.0))
 
 
-def make_frame_shard_renderer(scene, W, H, cfg, rank, world, dist, balance: bool = True, rounds: int = 2, **kw):
+def make_frame_shard_renderer(scene, W, H, cfg, rank, world, dist, balance: bool = True, rounds: int = 2, cls=None,
+                              **kw):
     """FrameShardRenderer whose bands equalise the band work (G-buffer + SVGF chain: the plant's rows cost several
     times a sky row; every rank's whole-frame path tracer is the same). Each round measures every rank's band work
     (band_ms), spreads it evenly over the band's rows and cuts new bands at equal quantiles of the mean of the rounds'
     per-row estimates; the measured plan with the smallest slowest band wins and the renderer is rebuilt on it
-    (calibration frames are discarded). Every rank derives the same bounds from all-reduced times."""
+    (calibration frames are discarded). Every rank derives the same bounds from all-reduced times. cls: the renderer
+    (FrameShardRenderer, or TileShardRenderer, whose path tracer is the same share of every frame on every rank)."""
     import numpy as np
     import torch
 
-    r = FrameShardRenderer(scene, W, H, cfg, rank, world, dist, **kw)
+    cls = cls or FrameShardRenderer
+    r = cls(scene, W, H, cfg, rank, world, dist, **kw)
     if not balance or world == 1:
         return r
     est, tried = [], []
@@ -1022,10 +1225,10 @@ def make_frame_shard_renderer(scene, W, H, cfg, rank, world, dist, balance: bool
         est.append(cost)
         bounds = balanced_bounds(np.mean(est, axis=0), world)
         r.close()
-        r = FrameShardRenderer(scene, W, H, cfg, rank, world, dist, bounds=bounds, **kw)
+        r = cls(scene, W, H, cfg, rank, world, dist, bounds=bounds, **kw)
     best = min(tried, key=lambda x: x[0])[1]
     r.close()
-    r = FrameShardRenderer(scene, W, H, cfg, rank, world, dist, bounds=best, **kw)
+    r = cls(scene, W, H, cfg, rank, world, dist, bounds=best, **kw)
     r.calibration = tried  # (slowest band's work ms per frame, bounds) per measured plan
     return r
 

@@ -107,6 +107,24 @@ def bvh_build(tri_in: int, tri_out: int, node_out: int, leaf_n: int = 8, ploc_ra
     return n.value, ms.value
 
 
+class PtTileSeg(C.Structure):
+    _fields_ = [("y_begin", C.c_int), ("y_end", C.c_int), ("offset", C.c_int), ("packed", C.c_void_p)]
+
+
+def tiles_count(frame_w: int, stride: int, offset: int, y0: int, y1: int, tile_y0: int = 0) -> int:
+    """Pixels per texture of the tile subset k * stride + offset in rows [y0, y1) (pt_tiles_count)."""
+    n = C.c_int64()
+    check(pt().pt_tiles_count(frame_w, tile_y0, stride, offset, y0, y1, C.byref(n)))
+    return n.value
+
+
+def tiles_copy(textures, stride: int, segs, unpack: bool, tile_y0: int = 0) -> None:
+    """pt_tiles_copy: segs = [(y0, y1, offset, packed device pointer)]; one launch on the library stream."""
+    tex = (C.c_uint32 * len(textures))(*textures)
+    arr = (PtTileSeg * max(1, len(segs)))(*[PtTileSeg(a, b, o, C.c_void_p(p)) for a, b, o, p in segs])
+    check(pt().pt_tiles_copy(tex, len(textures), tile_y0, stride, C.cast(arr, C.c_void_p), len(segs), int(bool(unpack))))
+
+
 def texture_array(layers: np.ndarray) -> int:
     """main.cpp:184-205: glTexStorage3D(GL_TEXTURE_2D_ARRAY, 1, GL_RGBA8, w, h, n) + one glTexSubImage3D per layer
     (help_func.h:4-20). `layers` is (n, h, w, 3|4) uint8, rows already in GL order (stbi flipped on load)."""

@@ -258,6 +258,9 @@ class Renderer:
         self._profile = False
         self._times: dict = {}
         self.back_events = None  # [start, end] HIP events per back end when set to a list (frames in flight only)
+        # (camera, modulate done) HIP events per frame when set to a list (frames in flight only): latency_ms()
+        self.latency_events = None
+        self._clock = None  # the stream camera-time events are recorded on (idle)
 
     # ------------------------------------------------------------ passes ---
     def _svgf_pass(self, frag: str, atts) -> RenderPass:
@@ -537,6 +540,16 @@ class Renderer:
         s = f % len(self.pt_slots)
         self._use_slot(s)
         done = None
+        t_cam = None
+        if self.latency_events is not None and self.K > 1:
+            # camera time: an event on a stream nothing else uses completes as soon as it is issued, so its timestamp is
+            # the moment this frame's camera went to the GPU (a busy front-end stream would record it later)
+            import torch
+
+            if self._clock is None:
+                self._clock = acquire_stream()
+            t_cam = torch.cuda.Event(enable_timing=True)
+            t_cam.record(self._clock)
         if self.K > 1:                                         # front end on stream s, after SVGF(f - K)
             import torch
 
@@ -559,7 +572,7 @@ class Renderer:
                     self._issue_batch()
         else:
             self._gbuffer_and_pt(f % ng)
-        return dict(f=f, slot=s, done=done, ready=self._ready, frame_counter=self.camera.frameCounter)
+        return dict(f=f, slot=s, done=done, ready=self._ready, frame_counter=self.camera.frameCounter, t_cam=t_cam)
 
     def _back_fast(self, ctx: dict):
         """The SVGF chain of the frame whose front end made ctx (back-end stream, sequential over frames)."""
@@ -736,6 +749,16 @@ class Renderer:
                 p.set_trace_stats(0)
         return dict(zip(self.STAT_KEYS, (int(v) for v in buf.cpu().tolist())))
 
+    def latency_ms(self) -> float | None:
+        """Mean camera-to-modulate latency (ms) of the frames recorded since latency_events was set to a list: from
+        the moment a frame's camera went to the GPU to the end of its SVGF chain (flushes and synchronises)."""
+        import torch
+
+        self.flush()
+        torch.cuda.synchronize()
+        ev = self.latency_events or []
+        return sum(a.elapsed_time(b) for a, b in ev) / len(ev) if ev else None
+
     def _stream_to(self, stream) -> None:
         """Issue the following draws on this torch stream."""
         _set_stream(stream)
@@ -828,6 +851,10 @@ class Renderer:
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record(self._back)
                 self.back_events[-1][1] = e1
+            if self.latency_events is not None and ctx is not None and ctx.get("t_cam") is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record(self._back)
+                self.latency_events.append((ctx["t_cam"], e1))
             self._slot_free[f % self.K] = ev
 
     # --------------------------------------------------------- accessors ---
@@ -868,10 +895,11 @@ class Renderer:
             import torch
 
             torch.cuda.synchronize()  # frames may still be in flight on the renderer's streams
-            for st in self._streams + [self._back]:
+            for st in self._streams + [self._back] + ([self._clock] if self._clock is not None else []):
                 release_stream(st)
             self._streams = []
             self._back = None
+            self._clock = None
         for v in list(vars(self).values()):
             if isinstance(v, PassGroup):
                 continue  # its passes are the pt_slots' (destroyed below)

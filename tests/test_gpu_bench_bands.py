@@ -27,11 +27,15 @@ def _port():
 
 @pytest.mark.parametrize("world,moving,balance,shard", [(2, True, True, "bands"), (4, False, False, "bands"),
                                                         (2, True, False, "frames"), (3, True, True, "frames"),
-                                                        (4, True, False, "frames"), (3, True, False, "frames+gbuffer")])
+                                                        (4, True, False, "frames"), (3, True, False, "frames+gbuffer"),
+                                                        (2, True, False, "tiles"), (3, True, True, "tiles"),
+                                                        (4, False, False, "tiles")])
 def test_bench_band_parity_gloo(world, moving, balance, shard):
     """shard = "bands": every rank traces its band; "frames": rank f % N traces frame f whole and scatters the
     path tracer's rows to the band owners (dist.FrameShardRenderer); "frames+gbuffer": and its G-buffer rows, which
-    the bands adopt instead of drawing (ship_gbuffer, an option)."""
+    the bands adopt instead of drawing (ship_gbuffer, an option); "tiles": every rank traces the 16x16 tiles
+    k * N + rank of every frame and one all-to-all per frame carries them to the band owners (dist.TileShardRenderer;
+    320 / 16 = 20 tiles per row, so at N = 3 the subsets are not column stripes)."""
     ship = shard == "frames+gbuffer"
     shard = "frames" if ship else shard
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
@@ -50,8 +54,9 @@ def test_bench_band_parity_gloo(world, moving, balance, shard):
     assert bp["backend"] == "gloo" and bp["frames"] >= 4
     assert bp["bit_exact"], bp
     assert line["bands"]["shard"] == shard and line["bands"].get("ship_gbuffer", False) == ship
-    if shard == "frames":
+    if shard in ("frames", "tiles"):
         assert line["bands"]["scatter_mb_per_traced_frame"] > 0
+    assert line["latency"]["camera_to_modulate_ms"] > 0 and line["latency"]["back_lag"] == line["bands"]["back_lag"]
     ex = line["bands"]["exchange_ms_per_frame"]
     if shard == "bands":
         assert {"reproject", "variance", "atrous0", "atrous4"} <= set(ex)

@@ -10,7 +10,11 @@ modelled RCCL time (20 us + bytes / 50 GB/s by default, XLAT_US / XGBS to change
 The arrival of another rank's frame is not delayed by that rank's path tracer: the run measures a rank's throughput
 (frames in flight cover the latency), not the latency itself. Prints each simulated rank's ms per frame; the
 predicted N-GPU frame is the slowest rank.
-usage: python tools/frame_shard_sim.py [N] [W] [H]   (RANKS=0,3 to simulate a subset; FRAMES, OWN, K)"""
+SHARD=tiles simulates dist.TileShardRenderer instead: every rank traces the tiles k * N + rank of every frame, and one
+all-to-all per frame (exchange_tiles: latency + the largest per-peer message / bandwidth, on the receive stream) carries
+them to the band owners. Both modes report the camera-to-modulate latency (HIP events, Renderer.latency_ms) in ms and
+in frames of the rank's rate.
+usage: python tools/frame_shard_sim.py [N] [W] [H]   (RANKS=0,3 to simulate a subset; FRAMES, OWN, K, SHARD)"""
 import os
 import sys
 import time
@@ -32,6 +36,7 @@ XLAT_US = float(os.environ.get("XLAT_US", "20"))
 XGBS = float(os.environ.get("XGBS", "50"))
 _CYC_PER_US = None
 LOG = {"halo": 0, "send": 0, "recv": 0}
+SHARD = os.environ.get("SHARD", "frames")
 
 
 class FakeDist:
@@ -131,8 +136,24 @@ def fake_window(window, plan, dist, group=None, rows=None):
     return sent
 
 
+def fake_tiles(send, sends, recv, recvs, dist, group=None):
+    """exchange_tiles stand-in: every peer's message over its own link at once: latency + the largest one."""
+    per_peer = {}
+    for k, a, b in sends:
+        per_peer[("s", k)] = (b - a) * 4
+    for k, a, b in recvs:
+        per_peer[("r", k)] = (b - a) * 4
+        LOG["recv"] += (b - a) * 4
+    sent = sum(v for (d, _), v in per_peer.items() if d == "s")
+    LOG["send"] += sent
+    if per_peer:
+        _spin(_xfer_us(max(per_peer.values())))
+    return sent
+
+
 D.halo_exchange = fake_exchange
 D.exchange_window = fake_window
+D.exchange_tiles = fake_tiles
 D.scatter_group = lambda dist: None
 torch.cuda.set_device(0)
 gl.init(0)
@@ -143,12 +164,15 @@ scene = build_scene("table_clock_plant")
 cfg = parameter_config()
 FRAMES = int(os.environ.get("FRAMES", str(max(96, 24 * N))))
 OWN = int(os.environ.get("OWN", "4"))
-K = int(os.environ.get("K", str(max(16, 4 * N + 2))))  # bench.py's defaults
+K = int(os.environ.get("K", str(max(16, 4 * N + 2) if SHARD == "frames" else 8)))  # bench.py's defaults
 
 
 def sim_rank(rk, bounds=None):
-    r = D.FrameShardRenderer(scene, W, H, cfg, rk, N, FakeDist(), own_slots=OWN, frames_in_flight=K, bounds=bounds,
-                             ship_gbuffer=os.environ.get("SHIP", "0") == "1")
+    if SHARD == "tiles":
+        r = D.TileShardRenderer(scene, W, H, cfg, rk, N, FakeDist(), own_slots=OWN, frames_in_flight=K, bounds=bounds)
+    else:
+        r = D.FrameShardRenderer(scene, W, H, cfg, rk, N, FakeDist(), own_slots=OWN, frames_in_flight=K,
+                                 bounds=bounds, ship_gbuffer=os.environ.get("SHIP", "0") == "1")
     r.camera.frameCounter += int(os.environ.get("FC_OFFSET", "0"))  # experiment: which frames a rank traces
     for kv in filter(None, os.environ.get("PT_UNIFORMS", "").split(",")):  # name=value,... on the path tracer
         name, val = kv.split("=")
@@ -160,6 +184,7 @@ def sim_rank(rk, bounds=None):
     for k in LOG:
         LOG[k] = 0
     r.r.back_events = []
+    r.r.latency_events = []
     waits = []  # host time blocked on the G-buffer motion bound (BandRenderer._motion): the GPU being full
     orig_motion = D.BandRenderer._motion
 
@@ -183,6 +208,8 @@ def sim_rank(rk, bounds=None):
     ev = [(a, b) for a, b in r.r.back_events if b is not None]
     r.r.back_events = None
     busy = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
+    lat = r.r.latency_ms()
+    r.r.latency_events = None
     r.profile(True)  # the band's passes alone (a draw at a time, synchronised): the floor of its SVGF stream
     for _ in range(N):
         r.frame()
@@ -191,7 +218,7 @@ def sim_rank(rk, bounds=None):
     pp = r.pass_times()
     r.profile(False)
     out = dict(rows=(r.plan.y0, r.plan.y1), wall=wall * 1e3, issue=issue * 1e3, cpu=cpu * 1e3, back=busy,
-               wait=sum(waits) / FRAMES * 1e3, pp={k: v / N for k, v in pp.items()},
+               wait=sum(waits) / FRAMES * 1e3, pp={k: v / N for k, v in pp.items()}, latency=lat,
                halo_mb=LOG["halo"] / FRAMES / 1e6, send_mb=LOG["send"] / FRAMES / 1e6,
                recv_mb=LOG["recv"] / FRAMES / 1e6)
     r.close()
@@ -199,7 +226,7 @@ def sim_rank(rk, bounds=None):
 
 
 def report(tag, ranks, bounds):
-    print(f"--- frame shard ({tag}): N={N} {W}x{H} K={K} own slots {OWN}, {FRAMES} frames per rank, "
+    print(f"--- {SHARD} shard ({tag}): N={N} {W}x{H} K={K} own slots {OWN}, {FRAMES} frames per rank, "
           f"links {XLAT_US:g} us + bytes / {XGBS:g} GB/s", flush=True)
     res = []
     for rk in ranks:
@@ -207,11 +234,14 @@ def report(tag, ranks, bounds):
         res.append(s)
         print(f"rank {rk}: rows {s['rows'][0]}..{s['rows'][1]} wall {s['wall']:.3f} ms/frame ({1e3 / s['wall']:.1f} fps) "
               f"issue {s['issue']:.3f} (host cpu {s['cpu']:.3f}, motion wait {s['wait']:.3f})  SVGF stream busy {s['back']:.3f} ms/frame  per frame: "
-              f"halo {s['halo_mb']:.2f} MB, sent {s['send_mb']:.1f} MB, received {s['recv_mb']:.1f} MB", flush=True)
+              f"halo {s['halo_mb']:.2f} MB, sent {s['send_mb']:.1f} MB, received {s['recv_mb']:.1f} MB; camera-to-modulate "
+              f"{s['latency']:.2f} ms = {s['latency'] / s['wall']:.1f} frames", flush=True)
         print("   passes alone, ms per frame: " + " ".join(f"{k} {v:.3f}" for k, v in sorted(s["pp"].items())),
               flush=True)
     mx = max(s["wall"] for s in res)
-    print(f"predicted frame (slowest simulated rank): {mx:.3f} ms = {1e3 / mx:.1f} fps", flush=True)
+    lat = max(s["latency"] for s in res)
+    print(f"predicted frame (slowest simulated rank): {mx:.3f} ms = {1e3 / mx:.1f} fps; latency (largest) {lat:.2f} ms "
+          f"= {lat / mx:.1f} frames", flush=True)
     return res
 
 
