@@ -109,6 +109,9 @@ def parse():
                          "the SVGF chain banded (dist.FrameShardRenderer); 'tiles' = every rank traces the 16x16 tiles "
                          "k*N + rank of every frame, one all-to-all per frame to the band owners, the SVGF chain banded "
                          "(dist.TileShardRenderer); 'bands' = every pass banded (dist.BandRenderer)")
+    ap.add_argument("--window", type=int, default=None,
+                    help="--shard frames: frames whose rows travel in one exchange (default N: one all-to-all per N "
+                         "frames, back_lag N; 1: one-to-all per frame, back_lag 1)")
     ap.add_argument("--ship-gbuffer", type=int, default=0, choices=(0, 1),
                     help="--shard frames: the tracing rank also sends the bands their G-buffer rows (they draw none)")
     ap.add_argument("--own-slots", type=int, default=4,
@@ -377,7 +380,7 @@ def main():
             from ptsvgf.dist import make_frame_shard_renderer
             r = make_frame_shard_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,
                                           own_slots=args.own_slots, frames_in_flight=K,
-                                          ship_gbuffer=bool(args.ship_gbuffer))
+                                          ship_gbuffer=bool(args.ship_gbuffer), window=args.window)
         elif world > 1 and args.shard == "tiles":
             from ptsvgf.dist import TileShardRenderer, make_frame_shard_renderer
             r = make_frame_shard_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,
@@ -459,6 +462,7 @@ def main():
             mx = torch.tensor([ex.get(k, 0.0) for k in EXCHANGE_STAGES], dtype=torch.float64, device="cuda")
             dist.all_reduce(mx, op=dist.ReduceOp.MAX)
             out["bands"] = {"shard": args.shard, "ship_gbuffer": bool(getattr(r, "ship_gbuffer", False)),
+                            "window": getattr(r, "window", None),
                             "bounds": list(r.plan.bounds), "back_lag": r.r.lag,
                             "frames_in_flight": r.r.K,
                             "exchange_ms_per_frame": {k: round(v, 4) for k, v in zip(EXCHANGE_STAGES, mx.tolist())

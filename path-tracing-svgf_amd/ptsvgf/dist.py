@@ -669,8 +669,14 @@ class FrameShardRenderer(BandRenderer):
     GBUF_PLANES = (1, 2, 3)  # G-buffer attachments the SVGF chain reads: normal/depth, motion, depth-fwidth
 
     def __init__(self, scene, W, H, cfg, rank, world, dist, own_slots: int = 2, ship_gbuffer: bool | None = None,
-                 **kw):
-        """ship_gbuffer (default off): the frame's tracing rank also sends each band the rows of its G-buffer
+                 window: int | None = None, **kw):
+        """window (default N): frames whose rows travel in one exchange. N: one all-to-all per N frames (every rank
+        sends its traced frame and receives the N - 1 others, all links at once), and a frame's back end waits for its
+        window: back_lag = N. 1: frame f's rows go out from rank f % N alone as soon as they are traced (one-to-all per
+        frame), back_lag = 1, so fewer band slots (frames_in_flight) cover the same path-tracer latency and the
+        camera-to-modulate latency falls with them.
+
+        ship_gbuffer (default off): the frame's tracing rank also sends each band the rows of its G-buffer
         (normal/depth, motion, depth-fwidth on the band's G-buffer rows), which the band adopts (pt_raster_pass_adopt)
         instead of drawing its own. A band's G-buffer draw costs 0.06-0.25 ms per frame (the plant's rows dominate)
         against 0.01 for the adoption, for twice the window's bytes (≈ 150 MB per window and link at 8 ranks); the
@@ -682,7 +688,10 @@ class FrameShardRenderer(BandRenderer):
         from .renderer import Renderer, acquire_stream
 
         K = kw.get("frames_in_flight", 1)
-        kw.setdefault("back_lag", world)  # a frame's back end is issued after its window's exchange
+        self.window = int(window) if window else world
+        if not 1 <= self.window <= world:
+            raise ValueError(f"window must be in [1, {world}], got {window}")
+        kw.setdefault("back_lag", self.window)  # a frame's back end is issued after its window's exchange
         if K <= kw["back_lag"]:
             raise ValueError(f"FrameShardRenderer needs frames_in_flight > back_lag = {kw['back_lag']}, got {K}")
         self._full_tensors = {}
@@ -740,7 +749,7 @@ class FrameShardRenderer(BandRenderer):
         import torch
 
         r, p = self.r, self.plan
-        if len(self._win) == p.world:
+        if len(self._win) == self.window:
             self._exchange()
         holder = {}
         gset = f % len(r.gbuf)

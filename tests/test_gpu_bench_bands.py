@@ -29,21 +29,23 @@ def _port():
                                                         (2, True, False, "frames"), (3, True, True, "frames"),
                                                         (4, True, False, "frames"), (3, True, False, "frames+gbuffer"),
                                                         (2, True, False, "tiles"), (3, True, True, "tiles"),
-                                                        (4, False, False, "tiles")])
+                                                        (4, False, False, "tiles"), (3, True, False, "frames+w1")])
 def test_bench_band_parity_gloo(world, moving, balance, shard):
     """shard = "bands": every rank traces its band; "frames": rank f % N traces frame f whole and scatters the
     path tracer's rows to the band owners (dist.FrameShardRenderer); "frames+gbuffer": and its G-buffer rows, which
-    the bands adopt instead of drawing (ship_gbuffer, an option); "tiles": every rank traces the 16x16 tiles
+    the bands adopt instead of drawing (ship_gbuffer, an option); "frames+w1": each frame's rows sent alone as soon as traced (window 1); "tiles": every rank traces the 16x16 tiles
     k * N + rank of every frame and one all-to-all per frame carries them to the band owners (dist.TileShardRenderer;
     320 / 16 = 20 tiles per row, so at N = 3 the subsets are not column stripes)."""
     ship = shard == "frames+gbuffer"
-    shard = "frames" if ship else shard
+    w1 = shard == "frames+w1"  # per-frame exchanges (window 1, back_lag 1)
+    shard = "frames" if ship or w1 else shard
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "bench.py"),
            "--gpus", str(world), "--backend", "gloo", "--width", "320", "--height", "256", "--steps", "4",
            "--warmup", "2", "--no-extras", "--no-1080p", "--no-cpu-baseline", "--shard", shard,
            "--ship-gbuffer", "1" if ship else "0"]
     cmd += ["--moving"] if moving else []
+    cmd += ["--window", "1", "--frames-in-flight", "6"] if w1 else []
     cmd += [] if balance else ["--equal-bands"]
     p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-4000:]
@@ -54,6 +56,8 @@ def test_bench_band_parity_gloo(world, moving, balance, shard):
     assert bp["backend"] == "gloo" and bp["frames"] >= 4
     assert bp["bit_exact"], bp
     assert line["bands"]["shard"] == shard and line["bands"].get("ship_gbuffer", False) == ship
+    if w1:
+        assert line["bands"]["window"] == 1 and line["bands"]["back_lag"] == 1
     if shard in ("frames", "tiles"):
         assert line["bands"]["scatter_mb_per_traced_frame"] > 0
     assert line["latency"]["camera_to_modulate_ms"] > 0 and line["latency"]["back_lag"] == line["bands"]["back_lag"]
