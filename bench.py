@@ -110,8 +110,10 @@ def parse():
                          "k*N + rank of every frame, one all-to-all per frame to the band owners, the SVGF chain banded "
                          "(dist.TileShardRenderer); 'bands' = every pass banded (dist.BandRenderer)")
     ap.add_argument("--window", type=int, default=None,
-                    help="--shard frames: frames whose rows travel in one exchange (default N: one all-to-all per N "
-                         "frames, back_lag N; 1: one-to-all per frame, back_lag 1)")
+                    help="--shard frames: frames whose rows travel in one exchange, = back_lag (default min(N, 4); N: one "
+                         "all-to-all per N frames; 1: one-to-all per frame)")
+    ap.add_argument("--burst", type=int, default=1,
+                    help="--shard frames: consecutive frames one rank traces (frame f on rank (f // burst) %% N)")
     ap.add_argument("--ship-gbuffer", type=int, default=0, choices=(0, 1),
                     help="--shard frames: the tracing rank also sends the bands their G-buffer rows (they draw none)")
     ap.add_argument("--own-slots", type=int, default=4,
@@ -324,15 +326,19 @@ def main():
         args.frames_in_flight = 4 if world <= 4 else 8
         k1080 = 6 if world == 1 else 8
         if world > 1 and args.shard == "frames":
-            # band slots cover another rank's whole-frame path tracer: a band's SVGF of frame f starts when f's window
-            # has arrived (simulated, tools/frame_shard_sim.py: N = 2 K = 10 / 16 / 24: 294 / 333 / 321 fps; N = 8
-            # K = 34 / 50 within noise)
-            args.frames_in_flight = k1080 = max(16, 4 * world + 2)
+            # band slots cover another rank's whole-frame path tracer (a band's SVGF of frame f starts when f's window
+            # has arrived), and the host runs as far ahead as they allow, so they also set the camera-to-modulate
+            # latency. Simulated at 4K (tools/frame_shard_sim.py, profiles/r04/shard/, DESIGN.md "Which partition"),
+            # window 4: N = 8 K = 12 912 fps at 15.2 ms (window 8 K = 34, round 3's default: 909 fps at 39 ms); N = 4
+            # K = 12 / 18: 611 / 623 fps at 23.6 / 30.6 ms; N = 2 (window 2) K = 12 / 16: 351 / 348 fps at 35 / 45 ms
+            args.frames_in_flight = k1080 = 12
         if world > 1 and args.shard == "tiles":
             # band slots cover back_lag (2) + the subsets' frames in flight
             args.frames_in_flight = k1080 = 8
     if args.trace_batch is None:
         args.trace_batch = 1
+    if args.window is None and world > 1 and args.shard == "frames":
+        args.window = min(world, 4)  # a back end waits for 4 frames' rows, not N (DESIGN.md "Which partition")
     # every frame slot must have run once before the timed region (a slot's first frame allocates its
     # wavefront state, and hipMalloc stalls the queues): at least K + 1 untimed frames
     args.warmup = max(args.warmup, args.frames_in_flight + 1)
@@ -380,7 +386,8 @@ def main():
             from ptsvgf.dist import make_frame_shard_renderer
             r = make_frame_shard_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,
                                           own_slots=args.own_slots, frames_in_flight=K,
-                                          ship_gbuffer=bool(args.ship_gbuffer), window=args.window)
+                                          ship_gbuffer=bool(args.ship_gbuffer), window=args.window,
+                                          burst=args.burst)
         elif world > 1 and args.shard == "tiles":
             from ptsvgf.dist import TileShardRenderer, make_frame_shard_renderer
             r = make_frame_shard_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,
@@ -462,7 +469,7 @@ def main():
             mx = torch.tensor([ex.get(k, 0.0) for k in EXCHANGE_STAGES], dtype=torch.float64, device="cuda")
             dist.all_reduce(mx, op=dist.ReduceOp.MAX)
             out["bands"] = {"shard": args.shard, "ship_gbuffer": bool(getattr(r, "ship_gbuffer", False)),
-                            "window": getattr(r, "window", None),
+                            "window": getattr(r, "window", None), "burst": getattr(r, "burst", None),
                             "bounds": list(r.plan.bounds), "back_lag": r.r.lag,
                             "frames_in_flight": r.r.K,
                             "exchange_ms_per_frame": {k: round(v, 4) for k, v in zip(EXCHANGE_STAGES, mx.tolist())

@@ -27,12 +27,15 @@ namespace ptk {
 #define PT_WIDE_SHADOW_SORT 0  // shadow rays' 4-wide walk: 1 = nearest child first, 0 = slot order
 #endif
 constexpr int kTB = 128;  // threads per traversal block (LDS stack: kStack*kTB*4 = 16 KiB)
-// Resident waves per SIMD the traversal kernels are compiled for. Left to itself the compiler gives the lane-refill
-// kernels 98 VGPRs (4 waves/SIMD: 104-register allocation); asking for 5 fits them in 96 without spills: 4K 179.8 ->
-// 185.8 fps, surface view 59.9 -> 62.0 (same box, tools/env_ab_views.sh, profiles/r03/occupancy_ab.log); 6 spills
-// (36 / 98 VGPRs of the refill kernels to scratch) and measured 181 / 60.4.
+// Resident waves per SIMD the traversal kernels are compiled for. Round 3 (SLP vectorizer on): 98 VGPRs left alone,
+// 96 at 5 waves (4K 179.8 -> 185.8 fps, profiles/r03/occupancy_ab.log). With SLP off the 4-wide refill walks need
+// 63-67 VGPRs; 8 waves fits them in 64 without spills, which pays once the LDS stack allows 8 waves (PT_WIDE_KS 16:
+// 8 KiB per 2-wave block). Round 4, same box, two alternating repetitions (profiles/r04/occupancy_ab.log): default
+// 24 entries / 5 waves 210.8 / 210.5 fps at 4K, 68.5 / 68.6 surface view; 16 / 5 waves 212.2 / 211.7, 68.9 / 68.6;
+// 16 / 8 waves 214.7 / 212.3, 69.4 / 69.0; 12 / 8 waves 199.9 / 198.3, 59.9 / 59.2 (more rays overflow to the
+// cooperative walk).
 #ifndef PT_TRACE_WAVES_PER_EU
-#define PT_TRACE_WAVES_PER_EU 5
+#define PT_TRACE_WAVES_PER_EU 8
 #endif
 #if PT_TRACE_WAVES_PER_EU > 0
 #define PT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(PT_TRACE_WAVES_PER_EU)))
@@ -44,7 +47,7 @@ constexpr int kTB = 128;  // threads per traversal block (LDS stack: kStack*kTB*
 // kStackSmall), a 4-wide walk whose pushes would overflow hands its ray to the cooperative walk (wide_step), so the
 // stack can be smaller than the deepest path: it bounds the resident waves (kTB x entries x 4 B of LDS per block).
 #ifndef PT_WIDE_KS
-#define PT_WIDE_KS 24
+#define PT_WIDE_KS 16
 #endif
 constexpr int kWideKS = PT_WIDE_KS;
 

@@ -669,8 +669,12 @@ class FrameShardRenderer(BandRenderer):
     GBUF_PLANES = (1, 2, 3)  # G-buffer attachments the SVGF chain reads: normal/depth, motion, depth-fwidth
 
     def __init__(self, scene, W, H, cfg, rank, world, dist, own_slots: int = 2, ship_gbuffer: bool | None = None,
-                 window: int | None = None, **kw):
-        """window (default N): frames whose rows travel in one exchange. N: one all-to-all per N frames (every rank
+                 window: int | None = None, burst: int = 1, **kw):
+        """burst (default 1): consecutive frames one rank traces, frame f on rank (f // burst) % N. With 2 a rank's
+        two path tracers are issued one frame apart and overlap (their launch tails fill each other's idle CUs, as frames
+        in flight do on one GPU) instead of starting N frames apart.
+
+        window (default N): frames whose rows travel in one exchange. N: one all-to-all per N frames (every rank
         sends its traced frame and receives the N - 1 others, all links at once), and a frame's back end waits for its
         window: back_lag = N. 1: frame f's rows go out from rank f % N alone as soon as they are traced (one-to-all per
         frame), back_lag = 1, so fewer band slots (frames_in_flight) cover the same path-tracer latency and the
@@ -689,6 +693,9 @@ class FrameShardRenderer(BandRenderer):
 
         K = kw.get("frames_in_flight", 1)
         self.window = int(window) if window else world
+        self.burst = int(burst)
+        if self.burst < 1:
+            raise ValueError(f"burst must be >= 1, got {burst}")
         if not 1 <= self.window <= world:
             raise ValueError(f"window must be in [1, {world}], got {window}")
         kw.setdefault("back_lag", self.window)  # a frame's back end is issued after its window's exchange
@@ -737,6 +744,14 @@ class FrameShardRenderer(BandRenderer):
         self._recv_stream = acquire_stream()
         self.scatter_log = []  # per exchange that carried a frame of this rank: bytes sent
 
+    def source(self, f: int) -> int:
+        """The rank that traces frame f."""
+        return (f // self.burst) % self.plan.world
+
+    def own_index(self, f: int) -> int:
+        """Ordinal of frame f among the frames its rank traces."""
+        return (f // (self.burst * self.plan.world)) * self.burst + f % self.burst
+
     def _band_rows(self, handle):
         p = self.plan
         a, b = p.zone(p.rank)
@@ -754,7 +769,7 @@ class FrameShardRenderer(BandRenderer):
         holder = {}
         gset = f % len(r.gbuf)
         self._set_frame[gset] = f
-        item = dict(src=f % p.world, outs=[self._band_rows(h) for h in r.pt_slots[slot][1]],
+        item = dict(src=self.source(f), outs=[self._band_rows(h) for h in r.pt_slots[slot][1]],
                     free=r._slot_free[f % r.K], holder=holder, gset=gset)
         if self.ship_gbuffer:
             g0, g1 = p.gbuffer_rows()
@@ -807,7 +822,7 @@ class FrameShardRenderer(BandRenderer):
 
         f = self._set_frame[self.r.back_set if b is None else b]
         m = 0.0
-        if f % self.plan.world == self.plan.rank:
+        if self.source(f) == self.plan.rank:
             o = self._own_mb.pop(f)
             self._fmb_event[o].synchronize()
             m = float(self._fmb_host[o:o + 1].numpy().view(np.float32)[0])
@@ -853,7 +868,7 @@ class FrameShardRenderer(BandRenderer):
         import torch
 
         fr, p = self.full, self.plan
-        o = (f // p.world) % self.own_slots
+        o = self.own_index(f) % self.own_slots
         st = fr._streams[o]
         if self._own_free[o] is not None:
             st.wait_event(self._own_free[o])

@@ -29,16 +29,19 @@ def _port():
                                                         (2, True, False, "frames"), (3, True, True, "frames"),
                                                         (4, True, False, "frames"), (3, True, False, "frames+gbuffer"),
                                                         (2, True, False, "tiles"), (3, True, True, "tiles"),
-                                                        (4, False, False, "tiles"), (3, True, False, "frames+w1")])
+                                                        (4, False, False, "tiles"), (3, True, False, "frames+w1"),
+                                                        (3, True, False, "frames+b2")])
 def test_bench_band_parity_gloo(world, moving, balance, shard):
     """shard = "bands": every rank traces its band; "frames": rank f % N traces frame f whole and scatters the
     path tracer's rows to the band owners (dist.FrameShardRenderer); "frames+gbuffer": and its G-buffer rows, which
-    the bands adopt instead of drawing (ship_gbuffer, an option); "frames+w1": each frame's rows sent alone as soon as traced (window 1); "tiles": every rank traces the 16x16 tiles
+    the bands adopt instead of drawing (ship_gbuffer, an option); "frames+w1": each frame's rows sent alone as soon as traced (window 1); "frames+b2": each
+    rank traces two consecutive frames (burst 2); "tiles": every rank traces the 16x16 tiles
     k * N + rank of every frame and one all-to-all per frame carries them to the band owners (dist.TileShardRenderer;
     320 / 16 = 20 tiles per row, so at N = 3 the subsets are not column stripes)."""
     ship = shard == "frames+gbuffer"
     w1 = shard == "frames+w1"  # per-frame exchanges (window 1, back_lag 1)
-    shard = "frames" if ship or w1 else shard
+    b2 = shard == "frames+b2"  # two consecutive frames per rank (burst 2): a window holds two frames of one source
+    shard = "frames" if ship or w1 or b2 else shard
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "bench.py"),
            "--gpus", str(world), "--backend", "gloo", "--width", "320", "--height", "256", "--steps", "4",
@@ -46,6 +49,7 @@ def test_bench_band_parity_gloo(world, moving, balance, shard):
            "--ship-gbuffer", "1" if ship else "0"]
     cmd += ["--moving"] if moving else []
     cmd += ["--window", "1", "--frames-in-flight", "6"] if w1 else []
+    cmd += ["--burst", "2"] if b2 else []
     cmd += [] if balance else ["--equal-bands"]
     p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-4000:]
@@ -58,6 +62,8 @@ def test_bench_band_parity_gloo(world, moving, balance, shard):
     assert line["bands"]["shard"] == shard and line["bands"].get("ship_gbuffer", False) == ship
     if w1:
         assert line["bands"]["window"] == 1 and line["bands"]["back_lag"] == 1
+    if b2:
+        assert line["bands"]["burst"] == 2
     if shard in ("frames", "tiles"):
         assert line["bands"]["scatter_mb_per_traced_frame"] > 0
     assert line["latency"]["camera_to_modulate_ms"] > 0 and line["latency"]["back_lag"] == line["bands"]["back_lag"]
@@ -72,8 +78,8 @@ def test_bench_band_parity_gloo(world, moving, balance, shard):
 def test_bench_frame_shard_8_ranks_1080p_gloo():
     """the default multi-GPU mode (--shard frames: rank f % 8 traces frame f whole, the SVGF chain
     banded with the ghost zone and the early history exchange) at a BASELINE size and rank count — 8 ranks, 1920 x
-    1080 (configs[1]), a moving camera, frames_in_flight at its 8-rank default (34 band slots, back_lag 8) — rehearsed
-    with gloo on the one GPU. 16 timed frames = 2 full windows of 8 after the warm-up's windows; the gathered bands must
+    1080 (configs[1]), a moving camera, frames_in_flight and the exchange window at their 8-rank defaults (12 band slots, window = back_lag 4) — rehearsed
+    with gloo on the one GPU. 16 timed frames = 4 full windows of 4 after the warm-up's windows; the gathered bands must
     equal a one-GPU render of the same camera path bit for bit (reference: main.cpp:436-535 per frame,
     svgf_Atrous.frag:92-97 and svgf_reproject.frag:45-156 for what crosses bands). Equal bands: the calibration only
     moves the bounds, which the 3-rank balanced case above covers."""
@@ -90,7 +96,7 @@ def test_bench_frame_shard_8_ranks_1080p_gloo():
     print(json.dumps(bp), json.dumps(bands["exchange_ms_per_frame"]), bands["frames_in_flight"], bands["back_lag"],
           line.get("max_history_rows"))
     assert line["n_gpus"] == world and bands["shard"] == "frames"
-    assert bands["back_lag"] == world and bands["frames_in_flight"] == 4 * world + 2
-    assert bp["backend"] == "gloo" and bp["frames"] >= 2 * world + 16  # warm-up windows + 2 timed windows + probes
+    assert bands["back_lag"] == bands["window"] == 4 and bands["frames_in_flight"] == 12  # bench.py's 8-rank defaults
+    assert bp["backend"] == "gloo" and bp["frames"] >= 2 * world + 16  # warm-up windows + 4 timed windows + probes
     assert bp["bit_exact"], bp
     assert line.get("max_history_rows", 0) > 3  # the orbit moved the history (reprojection reach beyond the taps)

@@ -14,7 +14,7 @@ SHARD=tiles simulates dist.TileShardRenderer instead: every rank traces the tile
 all-to-all per frame (exchange_tiles: latency + the largest per-peer message / bandwidth, on the receive stream) carries
 them to the band owners. Both modes report the camera-to-modulate latency (HIP events, Renderer.latency_ms) in ms and
 in frames of the rank's rate.
-usage: python tools/frame_shard_sim.py [N] [W] [H]   (RANKS=0,3 to simulate a subset; FRAMES, OWN, K, SHARD, WINDOW)"""
+usage: python tools/frame_shard_sim.py [N] [W] [H]   (RANKS=0,3 to simulate a subset; FRAMES, OWN, K, SHARD, WINDOW, BURST)"""
 import os
 import sys
 import time
@@ -173,7 +173,8 @@ def sim_rank(rk, bounds=None):
     else:
         r = D.FrameShardRenderer(scene, W, H, cfg, rk, N, FakeDist(), own_slots=OWN, frames_in_flight=K,
                                  bounds=bounds, ship_gbuffer=os.environ.get("SHIP", "0") == "1",
-                                 window=int(os.environ.get("WINDOW", "0")) or None)
+                                 window=int(os.environ.get("WINDOW", "0")) or None,
+                                 burst=int(os.environ.get("BURST", "1")))
     r.camera.frameCounter += int(os.environ.get("FC_OFFSET", "0"))  # experiment: which frames a rank traces
     for kv in filter(None, os.environ.get("PT_UNIFORMS", "").split(",")):  # name=value,... on the path tracer
         name, val = kv.split("=")
@@ -227,7 +228,8 @@ def sim_rank(rk, bounds=None):
 
 
 def report(tag, ranks, bounds):
-    print(f"--- {SHARD} shard ({tag}): N={N} {W}x{H} K={K} own slots {OWN} window {os.environ.get('WINDOW') or N}, "
+    print(f"--- {SHARD} shard ({tag}): N={N} {W}x{H} K={K} own slots {OWN} window {os.environ.get('WINDOW') or N} "
+          f"burst {os.environ.get('BURST', '1')}, "
           f"{FRAMES} frames per rank, "
           f"links {XLAT_US:g} us + bytes / {XGBS:g} GB/s", flush=True)
     res = []
