@@ -195,7 +195,8 @@ int pt_pass_draw(uint32_t pass);
  * once (no GL counterpart: the reference draws one frame at a time). Results are
  * those of drawing each pass alone. passes[0] owns the shared wavefront state,
  * sized for max(count, its "trace_batch" uniform) frames; the batch is timed as
- * its draw. Accumulation (lastFrame) and tile subsets are refused. */
+ * its draw. Accumulation (lastFrame) is refused; tile subsets are batched when every pass traces the same one
+ * ("tile_stride" / "tile_offset"). */
 int pt_pass_draw_batch(const uint32_t* passes, int count);
 /* Time the last draw of this pass (ms, HIP events on the library stream; syncs). */
 int pt_pass_last_ms(uint32_t pass, float* ms);

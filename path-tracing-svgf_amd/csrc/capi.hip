@@ -609,7 +609,7 @@ static int ref_count_of(int ref) { return (-(ref + 1)) & 15; }
 // replace it (a union, or the widened fine boxes below a reference leaf, which only cull): a ray passing a kept box
 // passed the skipped one too (slab rounding is monotone under containment), so the candidate triangles, and with
 // them every closest t and any-hit verdict, are the binary tree's. Exact ties are re-walked on the reference tree.
-// Layout (7 x float4 = 112 B): lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] refs[4]; refs >= 0 node index,
+// Layout (kWideStride x float4: 7 used = 112 B, padded to 128 B at 8): lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] refs[4]; refs >= 0 node index,
 // < 0 leaf, kNoneRef an empty slot. *need: the most stack entries a walk can hold (sum over a path of the
 // children pushed beside the one taken); the kernels check pushes against their stack anyway.
 static int pack_wide(const std::vector<SahNode>& nodes, const std::function<int(int, int)>& leaf_ref,
@@ -639,18 +639,18 @@ static int pack_wide(const std::vector<SahNode>& nodes, const std::function<int(
       ch[best + 1] = nodes[b].right;
       ++nc;
     }
-    const int k = (int)(out.size() / 7);
-    out.resize(out.size() + 7, float4{0, 0, 0, 0});
+    const int k = (int)(out.size() / ptk::kWideStride);
+    out.resize(out.size() + ptk::kWideStride, float4{0, 0, 0, 0});
     const int here = acc + nc - 1;
     *need = std::max(*need, here + 1);
     int refs[4] = {kNoneRef, kNoneRef, kNoneRef, kNoneRef};
     for (int c = 0; c < nc; ++c) {
       const SahNode& n = nodes[ch[c]];
-      float* q = (float*)&out[7 * (size_t)k];
+      float* q = (float*)&out[ptk::kWideStride * (size_t)k];
       for (int a = 0; a < 3; ++a) { q[8 * a + c] = n.lo[a]; q[8 * a + 4 + c] = n.hi[a]; }
       refs[c] = n.n > 0 ? ref_of(n) : build(ch[c], here);  // may reallocate `out`
     }
-    memcpy(&out[7 * (size_t)k + 6], refs, 16);
+    memcpy(&out[ptk::kWideStride * (size_t)k + 6], refs, 16);
     return k;
   };
   build(0, 0);
@@ -1296,8 +1296,11 @@ int draw_pathtrace_batch(Pass** ps, int n) {
     if (sb != sg || k[b].W != k[0].W || k[b].y0 != k[0].y0 || k[b].y1 != k[0].y1 || k[b].max_depth != k[0].max_depth ||
         k[b].scene.bvh_any != k[0].scene.bvh_any || !agree)
       return err(PT_ERR_ARG, "a path-tracing batch needs one scene, size, band, depth and traversal settings");
-    if (ui(ps[b], "pt_kernel", 0) != 0 || k[b].tile_stride != 1 || k[b].accumulate)
-      return err(PT_ERR_ARG, "a path-tracing batch needs the wavefront path tracer on whole frames, no accumulation");
+    // a tile subset (tile_stride / tile_offset) is batched as a whole frame is, provided every frame traces the same
+    // subset: the per-frame launches (primaries, bounce-0 shade, finalize) are sized by that subset's tile count
+    if (ui(ps[b], "pt_kernel", 0) != 0 || k[b].accumulate || k[b].tile_stride != k[0].tile_stride ||
+        k[b].tile_offset != k[0].tile_offset)
+      return err(PT_ERR_ARG, "a path-tracing batch needs the wavefront path tracer, one tile subset, no accumulation");
   }
   const int cap = std::max(n, std::min(kMaxBatch, ui(h, "trace_batch", n)));
   TRY(wf_alloc(h->wf, k[0].W, std::max(0, k[0].y1 - k[0].y0), cap));

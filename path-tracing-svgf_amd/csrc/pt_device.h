@@ -37,6 +37,13 @@ namespace ptk {
 #ifndef PT_KSTACK
 #define PT_KSTACK 32
 #endif
+// float4s per node of the 4-wide tree (pack_wide): 7 hold the four child boxes and refs. PT_WIDE_STRIDE = 8 pads a
+// node to one 128-B cache line (at 7, 112-B nodes straddle two lines for most indices): measured SLOWER, 211.5 ->
+// 202.6 fps at 4K and 69.2 -> 62.9 on the surface view (three alternating repetitions, profiles/r04/wide_stride_ab.log).
+#ifndef PT_WIDE_STRIDE
+#define PT_WIDE_STRIDE 7
+#endif
+constexpr int kWideStride = PT_WIDE_STRIDE;
 constexpr int kStack = PT_KSTACK;  // traversal stack depth (host checks BVH depth < kStack)
 // Traversal counters: a node visit counts PT_NODE_VISIT (1; a diagnostic build with 0 counts triangle tests only)
 #ifndef PT_NODE_VISIT

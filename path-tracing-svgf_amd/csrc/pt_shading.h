@@ -546,7 +546,7 @@ __device__ int closest_coop_walk(const SceneDev& sc, int* __restrict__ st, int c
 template <int KS, bool SORT, class Stk>
 __device__ __forceinline__ bool wide_step(const float4* __restrict__ tree, int& node, Stk& st, int& sp, v3 S, v3 inv,
                                           float lim) {
-  const float4* q = tree + 7 * node;
+  const float4* q = tree + kWideStride * node;
   const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5], rf = q[6];
   const float alx[4] = {lx.x, lx.y, lx.z, lx.w}, ahx[4] = {hx.x, hx.y, hx.z, hx.w};
   const float aly[4] = {ly.x, ly.y, ly.z, ly.w}, ahy[4] = {hy.x, hy.y, hy.z, hy.w};
@@ -618,7 +618,7 @@ __device__ int anyhit4(const SceneDev& sc, int* __restrict__ stk, v3 S, v3 d, bo
   while (node != kNone || leaf != kNone) {
     while (node >= 0) {
       nvis += PT_NODE_VISIT;
-      const float4* q = sc.bvh4 + 7 * node;
+      const float4* q = sc.bvh4 + kWideStride * node;
       const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5], rf = q[6];
       const float alx[4] = {lx.x, lx.y, lx.z, lx.w}, ahx[4] = {hx.x, hx.y, hx.z, hx.w};
       const float aly[4] = {ly.x, ly.y, ly.z, ly.w}, ahy[4] = {hy.x, hy.y, hy.z, hy.w};

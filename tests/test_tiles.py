@@ -148,3 +148,45 @@ def test_tile_subsets_exchanged_compose_to_frame(gpu, scene_small):
         for t in tex:
             gl.destroy_texture(t)
     a.close()
+
+
+@pytest.mark.gpu
+def test_batched_tile_subsets_equal_single_draws(gpu, scene_small):
+    """pt_pass_draw_batch of several frames' draws of ONE tile subset (a tile-shard rank batching its frames, so each
+    traversal launch carries several subsets' rays) writes what each frame's own subset draw writes, bit for bit; a
+    batch mixing subsets is refused."""
+    import torch
+
+    from ptsvgf.camera import parameter_config
+    from ptsvgf.renderer import Renderer
+    from ptsvgf._lib import check, pt
+
+    gl = gpu
+    W, H, N, B = 160, 96, 3, 3
+    check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
+    outs = []
+    for batch in (1, B):
+        r = Renderer(scene_small, W, H, parameter_config(), mode="fast", run_taa=False, run_output=False,
+                     frames_in_flight=B, trace_batch=batch)
+        r._stream_to(torch.cuda.current_stream())
+        r.pass_path_tracing.set_uniform_int("tile_stride", N)
+        r.pass_path_tracing.set_uniform_int("tile_offset", 1)
+        r.pass_path_tracing.set_uniform_int("trace_refill", 90)
+        passes = []
+        for s in range(B):
+            r._use_slot(s)
+            r._path_trace()
+            passes.append(r.pt_pass)
+            r.camera.frameCounter += 1
+        if batch > 1:
+            gl.draw_batch(passes)
+            with pytest.raises(Exception):  # one subset per batch
+                passes[1].set_uniform_int("tile_offset", 2)
+                gl.draw_batch(passes)
+        torch.cuda.synchronize()
+        outs.append([[gl.readback(t) for t in r.pt_slots[s][1]] for s in range(B)])
+        r.close()
+    for s in range(B):
+        for j in range(3):
+            assert np.array_equal(outs[0][s][j], outs[1][s][j]), (s, j)
+    assert np.any(outs[0][1][0])  # the subset drew something

@@ -1,7 +1,9 @@
 """Kernel-level cost of a tile-subset path tracer (the tile shard's per-rank draw): FRAMES draws of the subset
 k * STRIDE + OFFSET of the 4K bench frame, one at a time (K = 1), wall-clock per draw; run it under
-rocprofv3 --kernel-trace --stats to see which launches the subset pays for whole-frame sizes.
-usage: STRIDE=8 OFFSET=0 FRAMES=20 python tools/pt_subset_prof.py [W] [H]"""
+rocprofv3 --kernel-trace --stats to see which launches the subset pays for at whole-frame size. BATCH = B > 1: the
+subsets of B consecutive frames drawn as one batch (pt_pass_draw_batch), as a tile-shard rank batching its frames
+would; the time is reported per batch and per frame.
+usage: STRIDE=8 OFFSET=0 FRAMES=20 BATCH=1 python tools/pt_subset_prof.py [W] [H]"""
 import os
 import sys
 import time
@@ -20,6 +22,7 @@ H = int(sys.argv[2]) if len(sys.argv) > 2 else 2160
 STRIDE = int(os.environ.get("STRIDE", "8"))
 OFFSET = int(os.environ.get("OFFSET", "0"))
 FRAMES = int(os.environ.get("FRAMES", "20"))
+B = int(os.environ.get("BATCH", "1"))
 
 torch.cuda.set_device(0)
 gl.init(0)
@@ -27,21 +30,36 @@ from ptsvgf._lib import check, pt  # noqa: E402
 
 check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
 r = Renderer(build_scene("table_clock_plant"), W, H, parameter_config(), mode="fast", aspect_corrected=True,
-             run_taa=False, run_output=False)
-for stride, off in ((STRIDE, OFFSET),):
-    r.pass_path_tracing.set_uniform_int("tile_stride", stride)
-    r.pass_path_tracing.set_uniform_int("tile_offset", off)
-    for uv in filter(None, os.environ.get("PT_UNIFORMS", "").split(",")):
-        k, v = uv.split("=")
-        r.pass_path_tracing.set_uniform_int(k, int(v))
-    for _ in range(3):
-        r._path_trace()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(FRAMES):
-        r._path_trace()
+             run_taa=False, run_output=False, frames_in_flight=max(2, B), trace_batch=B)
+r._stream_to(torch.cuda.current_stream())  # every draw on one stream: batches one after another
+r.pass_path_tracing.set_uniform_int("tile_stride", STRIDE)
+r.pass_path_tracing.set_uniform_int("tile_offset", OFFSET)
+r.pass_path_tracing.set_uniform_int("trace_refill", 90)  # the lane-refill walks, as with frames in flight
+for uv in filter(None, os.environ.get("PT_UNIFORMS", "").split(",")):
+    k, v = uv.split("=")
+    r.pass_path_tracing.set_uniform_int(k, int(v))
+
+
+def batch():
+    passes = []
+    for s in range(B):
+        r._use_slot(s)
+        r._path_trace()  # uniforms (with trace_batch > 1 it returns before drawing)
+        passes.append(r.pt_pass)
         r.camera.frameCounter += 1
-    torch.cuda.synchronize()
-    print(f"stride {stride} offset {off}: {(time.perf_counter() - t0) * 1e3 / FRAMES:.3f} ms per draw", flush=True)
+    if B > 1:
+        gl.draw_batch(passes)
+
+
+for _ in range(3):
+    batch()
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+n = max(1, FRAMES // B)
+for _ in range(n):
+    batch()
+torch.cuda.synchronize()
+ms = (time.perf_counter() - t0) * 1e3 / n
+print(f"stride {STRIDE} offset {OFFSET} batch {B}: {ms:.3f} ms per draw, {ms / B:.3f} ms per frame", flush=True)
 r.close()
 gl.shutdown()
