@@ -112,6 +112,9 @@ def parse():
     ap.add_argument("--window", type=int, default=None,
                     help="--shard frames: frames whose rows travel in one exchange, = back_lag (default min(N, 4); N: one "
                          "all-to-all per N frames; 1: one-to-all per frame)")
+    ap.add_argument("--tile-batch", type=int, default=1,
+                    help="--shard tiles: the subsets of this many consecutive frames traced as one batched draw and "
+                         "exchanged together (back_lag max(2, B))")
     ap.add_argument("--burst", type=int, default=1,
                     help="--shard frames: consecutive frames one rank traces (frame f on rank (f // burst) %% N)")
     ap.add_argument("--ship-gbuffer", type=int, default=0, choices=(0, 1),
@@ -391,7 +394,8 @@ def main():
         elif world > 1 and args.shard == "tiles":
             from ptsvgf.dist import TileShardRenderer, make_frame_shard_renderer
             r = make_frame_shard_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,
-                                          cls=TileShardRenderer, own_slots=args.own_slots, frames_in_flight=K)
+                                          cls=TileShardRenderer, own_slots=args.own_slots, frames_in_flight=K,
+                                          batch=args.tile_batch)
         elif world > 1:
             from ptsvgf.dist import make_band_renderer
             r = make_band_renderer(scene, W, H, cfg, rank, world, dist, balance=not args.equal_bands,
@@ -470,6 +474,7 @@ def main():
             dist.all_reduce(mx, op=dist.ReduceOp.MAX)
             out["bands"] = {"shard": args.shard, "ship_gbuffer": bool(getattr(r, "ship_gbuffer", False)),
                             "window": getattr(r, "window", None), "burst": getattr(r, "burst", None),
+                            "tile_batch": getattr(r, "batch", None),
                             "bounds": list(r.plan.bounds), "back_lag": r.r.lag,
                             "frames_in_flight": r.r.K,
                             "exchange_ms_per_frame": {k: round(v, 4) for k, v in zip(EXCHANGE_STAGES, mx.tolist())

@@ -987,17 +987,22 @@ class TileShardRenderer(BandRenderer):
     as in FrameShardRenderer (ghost zone, BandRenderer ghost_zone): every rank draws its band's G-buffer and runs
     reproject / variance / a-trous with the modulate fused, and only the histories cross ranks.
 
-    Between the two, one all-to-all per frame (exchange_tiles, on a communicator of its own, scatter_group): each rank
-    packs its tiles of every other band's zone rows (plan.zone: the band widened by the reprojection's margin) into
-    one contiguous message per peer (pt_tiles_copy, one launch for all peers and planes), the messages travel over
-    every xGMI link at once, and the band unpacks the N subsets of its zone into its colour / emission / albedo planes
-    (one launch). The back end of frame f waits for that frame's exchange only, so it runs back_lag frames behind its
-    front end (default 2: the host's motion-bound wait finds a G-buffer issued two frames earlier), not N as in the
-    frame shard. own_slots = subsets this rank traces at once (the path tracer's frames in flight)."""
+    Between the two, one all-to-all per batch of frames (exchange_tiles, on a communicator of its own, scatter_group):
+    each rank packs its tiles of every other band's zone rows (plan.zone: the band widened by the reprojection's margin)
+    into one contiguous message per peer (pt_tiles_copy, one launch per frame for all peers and planes), the messages
+    travel over every xGMI link at once, and the band unpacks the N subsets of its zone into its colour / emission /
+    albedo planes (one launch per frame).
+
+    batch = B (default 1): the subsets of B consecutive frames are traced as one batched draw (pt_pass_draw_batch: each
+    traversal launch carries B subsets' rays, so it fills the chip B times better — a lone subset's launches end on the
+    frame's longest walks like a whole frame's) and exchanged as one message per peer. A frame's back end waits for its
+    batch, so it runs back_lag = max(2, B) frames behind its front end (2: the host's motion-bound wait finds a G-buffer
+    issued two frames earlier). own_slots = subsets this rank holds at once (at least 2B: one batch in flight while the
+    next registers)."""
 
     PT_PLANES = 3  # colour, emission, albedo (the path tracer's outputs the SVGF chain reads)
 
-    def __init__(self, scene, W, H, cfg, rank, world, dist, own_slots: int = 2, **kw):
+    def __init__(self, scene, W, H, cfg, rank, world, dist, own_slots: int = 2, batch: int = 1, **kw):
         import torch
 
         from . import gl
@@ -1005,10 +1010,14 @@ class TileShardRenderer(BandRenderer):
 
         if W % 16:
             raise ValueError(f"the tile shard needs a frame width that is a multiple of 16 (the path tracer's tiles), got {W}")
+        self.batch = int(batch)
+        if not 1 <= self.batch <= 8:
+            raise ValueError(f"batch must be in [1, 8] (pt_pass_draw_batch), got {batch}")
         K = kw.get("frames_in_flight", 1)
-        kw.setdefault("back_lag", min(2, max(0, K - 1)))
-        if K < 2:
-            raise ValueError("TileShardRenderer needs frames_in_flight >= 2")
+        kw.setdefault("back_lag", min(max(2, self.batch), max(0, K - 1)))
+        if K < 2 or kw["back_lag"] < self.batch - 1:
+            raise ValueError(f"TileShardRenderer needs frames_in_flight >= 2 and back_lag >= batch - 1, got K = {K}, "
+                             f"back_lag = {kw['back_lag']}")
         self._full_tensors = {}
         dev = torch.device("cuda", torch.cuda.current_device())
 
@@ -1019,94 +1028,131 @@ class TileShardRenderer(BandRenderer):
             return handle
 
         gl.set_band(W, H, 0, H, 0, H)  # process-global band state: the subset's planes are whole frames
+        slots = max(2, int(own_slots), 2 * self.batch if self.batch > 1 else 1)
         self.full = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, tex_factory=full_factory,
-                             run_taa=False, run_output=False, frames_in_flight=max(2, int(own_slots)))
+                             run_taa=False, run_output=False, frames_in_flight=slots, trace_batch=self.batch)
         for p, _ in self.full.pt_slots:
             p.set_rows(0, H)
             p.set_uniform_int("tile_stride", world)
             p.set_uniform_int("tile_offset", rank)
         self.own_slots = self.full.K
         self._own_free = [None] * self.own_slots  # event: the pack that read the slot's last subset is done
+        self._open = []  # frames of the batch being registered: (f, own slot, band slot, holder)
         kw.setdefault("front_streams", 1)
         kw["ghost_zone"] = True
-        super().__init__(scene, W, H, cfg, rank, world, dist, pt_source=self._pt_source, **kw)
+        super().__init__(scene, W, H, cfg, rank, world, dist, pt_source=self._pt_source, pt_flush=self._flush_batch,
+                         **kw)
         self.full.camera = self.r.camera
         self.pass_path_tracing = self.full.pass_path_tracing
-        if self.r.K > 1:  # the subset's launches carry an N-th of the rays: the band's traversal settings (BandRenderer)
+        if self.r.K > 1 and self.batch == 1:
+            # a lone subset's launches carry an N-th of the rays: the band's traversal settings (BandRenderer)
             self.pass_path_tracing.set_uniform_int("shadow_budget", BAND_VISIT_BUDGET)
             self.pass_path_tracing.set_uniform_int("closest_budget", BAND_VISIT_BUDGET)
             self.pass_path_tracing.set_uniform_int("refill_waves", BAND_REFILL_WAVES)
         self._sgroup = scatter_group(dist) if world > 1 else None
         self._recv_stream = acquire_stream()
-        # message layout, fixed per plan: my tiles of band k's zone (k != me), then the N subsets of my zone
-        p, n3 = self.plan, self.PT_PLANES * 4
-        self._send_segs, self._sends, off = [], [], 0
+        # message layout, fixed per plan (pixels; 3 planes x 16 B each): send [peer k][frame b] blocks of my tiles of
+        # band k's zone, n_k pixels per frame; recv [source s][frame b] blocks of s's tiles of my zone (my own slot
+        # included: the pack writes it, the unpack reads it with the others)
+        p, B = self.plan, self.batch
+        self._n_send, self._send_base, off = {}, {}, 0
         for k in range(world):
-            if k == rank:
-                continue
-            z0, z1 = p.zone(k)
-            n = gl.tiles_count(W, world, rank, z0, z1)
-            self._send_segs.append((z0, z1, rank, off))
-            self._sends.append((k, off * n3, (off + n) * n3))
-            off += n
-        self._send = torch.empty(max(1, off) * n3, dtype=torch.float32, device=dev)
+            if k != rank:
+                z0, z1 = p.zone(k)
+                self._n_send[k] = gl.tiles_count(W, world, rank, z0, z1)
+                self._send_base[k] = off
+                off += B * self._n_send[k]
+        self._send = torch.empty(max(1, off) * self.PT_PLANES * 4, dtype=torch.float32, device=dev)
         z0, z1 = p.zone(rank)
-        self._recv_segs, self._recvs, off = [], [], 0
-        for s in range(world):
-            n = gl.tiles_count(W, world, s, z0, z1)
-            self._recv_segs.append((z0, z1, s, off))
-            if s != rank:
-                self._recvs.append((s, off * n3, (off + n) * n3))
-            off += n
-        self._recv = torch.empty(max(1, off) * n3, dtype=torch.float32, device=dev)
+        self._n_recv, self._recv_base, off = {}, {}, 0
+        for s_ in range(world):
+            self._n_recv[s_] = gl.tiles_count(W, world, s_, z0, z1)
+            self._recv_base[s_] = off
+            off += B * self._n_recv[s_]
+        self._recv = torch.empty(max(1, off) * self.PT_PLANES * 4, dtype=torch.float32, device=dev)
         self.scatter_log = []  # bytes sent per frame
 
-    def _segs(self, segs, buf):
-        base = buf.data_ptr()
-        return [(a, b, o, base + off * self.PT_PLANES * 16) for a, b, o, off in segs]
+    def _ptr(self, buf, pixels: int) -> int:
+        return buf.data_ptr() + pixels * self.PT_PLANES * 16
 
     def _pt_source(self, f: int, slot: int, stream):
-        """Renderer pt_source: trace this rank's tiles of frame f (own slot f % own_slots), exchange every band's
-        rows of the frame, unpack this band's zone. Returns the holder whose "ev" the back end of f waits for."""
+        """Renderer pt_source: register frame f in the open batch (its subset's uniforms on own slot f % own_slots) and,
+        when the batch is full, trace, exchange and unpack it. Returns the holder whose "ev" the back end of f waits
+        for (set when f's batch is flushed)."""
+        fr = self.full
+        o = f % self.own_slots
+        fr._use_slot(o)
+        fr.frame_index = f
+        holder = {}
+        self._open.append((f, o, slot, holder))
+        if self.batch == 1:  # a lone subset: drawn now, on its own stream
+            st = fr._streams[o]
+            if self._own_free[o] is not None:
+                st.wait_event(self._own_free[o])
+            fr._stream_to(st)
+            fr._path_trace(None)  # the subset's primaries come from its own tile-binned raster (no G-buffer hint)
+            self._flush_batch(drawn=st)
+        else:
+            fr._path_trace(None)  # uniforms only (trace_batch > 1): drawn with its batch
+            if len(self._open) == self.batch:
+                self._flush_batch()
+        self.r._stream_to(stream)
+        return holder
+
+    def _flush_batch(self, drawn=None) -> None:
+        """Trace the open batch (one pt_pass_draw_batch on the stream of its last own slot, unless `drawn` holds the
+        lone subset's stream), pack every frame's tiles per peer, exchange them in one batch, unpack this band's zone.
+        Every rank registers the same frames, so every rank flushes at the same point (batch full, or flush())."""
         import torch
 
         from . import gl
 
+        items, self._open = self._open, []
+        if not items:
+            return
         r, p, fr = self.r, self.plan, self.full
-        o = f % self.own_slots
-        st = fr._streams[o]
-        if self._own_free[o] is not None:
-            st.wait_event(self._own_free[o])
-        fr._use_slot(o)
-        fr._stream_to(st)
-        fr.frame_index = f
-        fr._path_trace(None)  # the subset's primaries come from its own tile-binned raster (no G-buffer hint)
+        st = drawn
+        if st is None:
+            st = fr._streams[items[-1][1]]
+            for _, o, _, _ in items:
+                if self._own_free[o] is not None:
+                    st.wait_event(self._own_free[o])
+            fr._stream_to(st)
+            gl.draw_batch([fr.pt_slots[o][0] for _, o, _, _ in items])
         done = torch.cuda.Event()
         done.record(st)
         rs = self._recv_stream
         rs.wait_event(done)
-        free = r._slot_free[f % r.K]  # the band slot's planes: read by the SVGF chain of frame f - K
-        if free is not None:
-            rs.wait_event(free)
+        for f, _, _, _ in items:
+            free = r._slot_free[f % r.K]  # the band slot's planes: read by the SVGF chain of frame f - K
+            if free is not None:
+                rs.wait_event(free)
         r._stream_to(rs)
-        full = list(fr.pt_slots[o][1])
-        band = list(r.pt_slots[slot][1])
-        # my tiles: every other band's zone into the send buffer, my own band's zone straight into my slot of the recv
-        gl.tiles_copy(full, p.world, self._segs(self._send_segs, self._send)
-                      + [s for s in self._segs(self._recv_segs, self._recv) if s[2] == p.rank], unpack=False)
+        me, c = p.rank, len(items)
+        for b, (_, o, _, _) in enumerate(items):
+            # my tiles: every other band's zone into the send buffer, my own band's zone straight into my recv slot
+            segs = [(*p.zone(k), me, self._ptr(self._send, self._send_base[k] + b * n)) for k, n in self._n_send.items()]
+            segs.append((*p.zone(me), me, self._ptr(self._recv, self._recv_base[me] + b * self._n_recv[me])))
+            gl.tiles_copy(list(fr.pt_slots[o][1]), p.world, segs, unpack=False)
         packed = torch.cuda.Event()
         packed.record(rs)
-        self._own_free[o] = packed
+        for _, o, _, _ in items:
+            self._own_free[o] = packed
+        e = self.PT_PLANES * 4  # floats per pixel of a message
+        sends = [(k, self._send_base[k] * e, (self._send_base[k] + c * n) * e) for k, n in self._n_send.items()]
+        recvs = [(s_, self._recv_base[s_] * e, (self._recv_base[s_] + c * n) * e) for s_, n in self._n_recv.items()
+                 if s_ != me]
         with torch.cuda.stream(rs):
-            nbytes = exchange_tiles(self._send, self._sends, self._recv, self._recvs, self.dist,
-                                    self._sgroup) if p.world > 1 else 0
+            nbytes = exchange_tiles(self._send, sends, self._recv, recvs, self.dist, self._sgroup) if p.world > 1 else 0
         r._stream_to(rs)
-        gl.tiles_copy(band, p.world, self._segs(self._recv_segs, self._recv), unpack=True)
+        for b, (_, _, slot, _) in enumerate(items):
+            segs = [(*p.zone(me), s_, self._ptr(self._recv, self._recv_base[s_] + b * n)) for s_, n in self._n_recv.items()]
+            gl.tiles_copy(list(r.pt_slots[slot][1]), p.world, segs, unpack=True)
         ev = torch.cuda.Event()
         ev.record(rs)
-        r._stream_to(stream)
-        self.scatter_log.append(nbytes)
-        return {"ev": ev}
+        for _, _, _, holder in items:
+            holder["ev"] = ev
+        self.scatter_log += [nbytes / c] * c
 
     def trace_stats(self) -> dict:
         """Traversal counters of one frame: each rank counts its tiles (bench sums over ranks)."""

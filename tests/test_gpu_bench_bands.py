@@ -30,7 +30,7 @@ def _port():
                                                         (4, True, False, "frames"), (3, True, False, "frames+gbuffer"),
                                                         (2, True, False, "tiles"), (3, True, True, "tiles"),
                                                         (4, False, False, "tiles"), (3, True, False, "frames+w1"),
-                                                        (3, True, False, "frames+b2")])
+                                                        (3, True, False, "frames+b2"), (3, True, False, "tiles+b3")])
 def test_bench_band_parity_gloo(world, moving, balance, shard):
     """shard = "bands": every rank traces its band; "frames": rank f % N traces frame f whole and scatters the
     path tracer's rows to the band owners (dist.FrameShardRenderer); "frames+gbuffer": and its G-buffer rows, which
@@ -41,7 +41,8 @@ def test_bench_band_parity_gloo(world, moving, balance, shard):
     ship = shard == "frames+gbuffer"
     w1 = shard == "frames+w1"  # per-frame exchanges (window 1, back_lag 1)
     b2 = shard == "frames+b2"  # two consecutive frames per rank (burst 2): a window holds two frames of one source
-    shard = "frames" if ship or w1 or b2 else shard
+    tb3 = shard == "tiles+b3"  # tile subsets of 3 consecutive frames in one batched draw and one exchange
+    shard = "frames" if ship or w1 or b2 else "tiles" if tb3 else shard
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "bench.py"),
            "--gpus", str(world), "--backend", "gloo", "--width", "320", "--height", "256", "--steps", "4",
@@ -50,6 +51,7 @@ def test_bench_band_parity_gloo(world, moving, balance, shard):
     cmd += ["--moving"] if moving else []
     cmd += ["--window", "1", "--frames-in-flight", "6"] if w1 else []
     cmd += ["--burst", "2"] if b2 else []
+    cmd += ["--tile-batch", "3"] if tb3 else []
     cmd += [] if balance else ["--equal-bands"]
     p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-4000:]
@@ -64,6 +66,8 @@ def test_bench_band_parity_gloo(world, moving, balance, shard):
         assert line["bands"]["window"] == 1 and line["bands"]["back_lag"] == 1
     if b2:
         assert line["bands"]["burst"] == 2
+    if tb3:
+        assert line["bands"]["tile_batch"] == 3 and line["bands"]["back_lag"] == 3
     if shard in ("frames", "tiles"):
         assert line["bands"]["scatter_mb_per_traced_frame"] > 0
     assert line["latency"]["camera_to_modulate_ms"] > 0 and line["latency"]["back_lag"] == line["bands"]["back_lag"]

@@ -14,7 +14,7 @@ SHARD=tiles simulates dist.TileShardRenderer instead: every rank traces the tile
 all-to-all per frame (exchange_tiles: latency + the largest per-peer message / bandwidth, on the receive stream) carries
 them to the band owners. Both modes report the camera-to-modulate latency (HIP events, Renderer.latency_ms) in ms and
 in frames of the rank's rate.
-usage: python tools/frame_shard_sim.py [N] [W] [H]   (RANKS=0,3 to simulate a subset; FRAMES, OWN, K, SHARD, WINDOW, BURST)"""
+usage: python tools/frame_shard_sim.py [N] [W] [H]   (RANKS=0,3 to simulate a subset; FRAMES, OWN, K, SHARD, WINDOW, BURST, TBATCH)"""
 import os
 import sys
 import time
@@ -169,7 +169,8 @@ K = int(os.environ.get("K", str(max(16, 4 * N + 2) if SHARD == "frames" else 8))
 
 def sim_rank(rk, bounds=None):
     if SHARD == "tiles":
-        r = D.TileShardRenderer(scene, W, H, cfg, rk, N, FakeDist(), own_slots=OWN, frames_in_flight=K, bounds=bounds)
+        r = D.TileShardRenderer(scene, W, H, cfg, rk, N, FakeDist(), own_slots=OWN, frames_in_flight=K, bounds=bounds,
+                                batch=int(os.environ.get("TBATCH", "1")))
     else:
         r = D.FrameShardRenderer(scene, W, H, cfg, rk, N, FakeDist(), own_slots=OWN, frames_in_flight=K,
                                  bounds=bounds, ship_gbuffer=os.environ.get("SHIP", "0") == "1",
@@ -229,7 +230,7 @@ def sim_rank(rk, bounds=None):
 
 def report(tag, ranks, bounds):
     print(f"--- {SHARD} shard ({tag}): N={N} {W}x{H} K={K} own slots {OWN} window {os.environ.get('WINDOW') or N} "
-          f"burst {os.environ.get('BURST', '1')}, "
+          f"burst {os.environ.get('BURST', '1')} tile batch {os.environ.get('TBATCH', '1')}, "
           f"{FRAMES} frames per rank, "
           f"links {XLAT_US:g} us + bytes / {XGBS:g} GB/s", flush=True)
     res = []
