@@ -34,8 +34,8 @@ def _port():
 def test_bench_band_parity_gloo(world, moving, balance, shard):
     """shard = "bands": every rank traces its band; "frames": rank f % N traces frame f whole and scatters the
     path tracer's rows to the band owners (dist.FrameShardRenderer); "frames+gbuffer": and its G-buffer rows, which
-    the bands adopt instead of drawing (ship_gbuffer, an option); "frames+w1": each frame's rows sent alone as soon as traced (window 1); "frames+b2": each
-    rank traces two consecutive frames (burst 2); "tiles": every rank traces the 16x16 tiles
+    the bands adopt instead of drawing (ship_gbuffer, an option); "frames+w1": each frame's rows sent alone as soon
+    as traced (window 1); "frames+b2": each rank traces two consecutive frames (burst 2); "tiles": every rank traces the 16x16 tiles
     k * N + rank of every frame and one all-to-all per frame carries them to the band owners (dist.TileShardRenderer;
     320 / 16 = 20 tiles per row, so at N = 3 the subsets are not column stripes)."""
     ship = shard == "frames+gbuffer"
@@ -79,18 +79,19 @@ def test_bench_band_parity_gloo(world, moving, balance, shard):
 
 
 @pytest.mark.timeout(900)
-def test_bench_frame_shard_8_ranks_1080p_gloo():
+@pytest.mark.parametrize("W,H", [(1920, 1080), (3840, 2160)])
+def test_bench_frame_shard_8_ranks_gloo(W, H):
     """the default multi-GPU mode (--shard frames: rank f % 8 traces frame f whole, the SVGF chain
-    banded with the ghost zone and the early history exchange) at a BASELINE size and rank count — 8 ranks, 1920 x
-    1080 (configs[1]), a moving camera, frames_in_flight and the exchange window at their 8-rank defaults (12 band slots, window = back_lag 4) — rehearsed
-    with gloo on the one GPU. 16 timed frames = 4 full windows of 4 after the warm-up's windows; the gathered bands must
+    banded with the ghost zone and the early history exchange) at the BASELINE sizes and rank count — 8 ranks, 1920 x
+    1080 (configs[1]) and 3840 x 2160 (configs[3] / [4]), a moving camera, frames_in_flight and the exchange window at
+    their 8-rank defaults (12 band slots, window = back_lag 4) — rehearsed with gloo on the one GPU (4K: ≈ 30 s). 16 timed frames = 4 full windows of 4 after the warm-up's windows; the gathered bands must
     equal a one-GPU render of the same camera path bit for bit (reference: main.cpp:436-535 per frame,
     svgf_Atrous.frag:92-97 and svgf_reproject.frag:45-156 for what crosses bands). Equal bands: the calibration only
     moves the bounds, which the 3-rank balanced case above covers."""
     world = 8
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "bench.py"),
-           "--gpus", str(world), "--backend", "gloo", "--width", "1920", "--height", "1080", "--steps", "16",
+           "--gpus", str(world), "--backend", "gloo", "--width", str(W), "--height", str(H), "--steps", "16",
            "--warmup", "2", "--no-extras", "--no-1080p", "--no-cpu-baseline", "--shard", "frames", "--moving",
            "--equal-bands"]
     p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=850)
