@@ -949,12 +949,45 @@ class FrameShardRenderer(BandRenderer):
         self._recv_stream = None
 
 
+def tile_layout(plan: BandPlan, W: int, batch: int, count):
+    """The tile shard's message layout (pixels, every plane of a pixel together), fixed per plan: send [peer k][frame b]
+    blocks of this rank's tiles of band k's zone (n_send[k] pixels per frame), recv [source s][frame b] blocks of s's
+    tiles of this band's zone (n_recv[s] per frame; this rank's own block included: the pack writes it, the unpack reads
+    it with the others). count(offset, y0, y1): pixels of the subset `offset` in rows [y0, y1) (pt_tiles_count).
+    Returns (n_send, send_base, n_recv, recv_base, send pixels, recv pixels)."""
+    me = plan.rank
+    n_send, send_base, off = {}, {}, 0
+    for k in range(plan.world):
+        if k != me:
+            n_send[k] = count(me, *plan.zone(k))
+            send_base[k] = off
+            off += batch * n_send[k]
+    n_recv, recv_base, off2 = {}, {}, 0
+    for s in range(plan.world):
+        n_recv[s] = count(s, *plan.zone(me))
+        recv_base[s] = off2
+        off2 += batch * n_recv[s]
+    return n_send, send_base, n_recv, recv_base, off, off2
+
+
+def tile_messages(layout, me: int, frames: int, elems: int):
+    """(peer, first, end) element ranges of one batch of `frames` frames (elems elements per pixel): one message per
+    peer each way, its frames contiguous. Both ends derive a pair's sizes from the same counts (my tiles of k's zone ==
+    k's count of source me in its zone), so the batch pairs up."""
+    n_send, send_base, n_recv, recv_base = layout[:4]
+    sends = [(k, send_base[k] * elems, (send_base[k] + frames * n) * elems) for k, n in n_send.items()]
+    recvs = [(s, recv_base[s] * elems, (recv_base[s] + frames * n) * elems) for s, n in n_recv.items() if s != me]
+    return sends, recvs
+
+
 def exchange_tiles(send, sends, recv, recvs, dist, group=None) -> int:
     """One tile-shard frame's all-to-all: sends = [(peer, first, end)] element ranges of the flat device buffer `send`
     (this rank's tiles of peer's band rows, every plane), recvs = [(source, first, end)] of `recv` (the source's tiles
     of this band's rows). One symmetric batch (every rank pairs its sends with its peers' receives), every link at
     once. RCCL: the current stream waits for the batch; gloo (tests): blocking, staged through host memory. Returns the
     bytes sent."""
+    import torch
+
     gloo = dist.get_backend(group) == "gloo"
     ops, staged, nbytes = [], [], 0
     hsend = send.cpu() if gloo and send.is_cuda else send
@@ -964,7 +997,7 @@ def exchange_tiles(send, sends, recv, recvs, dist, group=None) -> int:
     for s, a, b in recvs:
         buf = recv[a:b]
         if gloo and recv.is_cuda:
-            h = buf.cpu()
+            h = torch.empty(buf.shape, dtype=buf.dtype)
             staged.append((buf, h))
             buf = h
         ops.append(dist.P2POp(dist.irecv, buf, s, group))
@@ -1051,25 +1084,10 @@ class TileShardRenderer(BandRenderer):
             self.pass_path_tracing.set_uniform_int("refill_waves", BAND_REFILL_WAVES)
         self._sgroup = scatter_group(dist) if world > 1 else None
         self._recv_stream = acquire_stream()
-        # message layout, fixed per plan (pixels; 3 planes x 16 B each): send [peer k][frame b] blocks of my tiles of
-        # band k's zone, n_k pixels per frame; recv [source s][frame b] blocks of s's tiles of my zone (my own slot
-        # included: the pack writes it, the unpack reads it with the others)
-        p, B = self.plan, self.batch
-        self._n_send, self._send_base, off = {}, {}, 0
-        for k in range(world):
-            if k != rank:
-                z0, z1 = p.zone(k)
-                self._n_send[k] = gl.tiles_count(W, world, rank, z0, z1)
-                self._send_base[k] = off
-                off += B * self._n_send[k]
-        self._send = torch.empty(max(1, off) * self.PT_PLANES * 4, dtype=torch.float32, device=dev)
-        z0, z1 = p.zone(rank)
-        self._n_recv, self._recv_base, off = {}, {}, 0
-        for s_ in range(world):
-            self._n_recv[s_] = gl.tiles_count(W, world, s_, z0, z1)
-            self._recv_base[s_] = off
-            off += B * self._n_recv[s_]
-        self._recv = torch.empty(max(1, off) * self.PT_PLANES * 4, dtype=torch.float32, device=dev)
+        lay = tile_layout(self.plan, W, self.batch, lambda o, a, b: gl.tiles_count(W, world, o, a, b))
+        self._n_send, self._send_base, self._n_recv, self._recv_base, ns, nr = lay
+        self._send = torch.empty(max(1, ns) * self.PT_PLANES * 4, dtype=torch.float32, device=dev)
+        self._recv = torch.empty(max(1, nr) * self.PT_PLANES * 4, dtype=torch.float32, device=dev)
         self.scatter_log = []  # bytes sent per frame
 
     def _ptr(self, buf, pixels: int) -> int:
@@ -1138,10 +1156,8 @@ class TileShardRenderer(BandRenderer):
         packed.record(rs)
         for _, o, _, _ in items:
             self._own_free[o] = packed
-        e = self.PT_PLANES * 4  # floats per pixel of a message
-        sends = [(k, self._send_base[k] * e, (self._send_base[k] + c * n) * e) for k, n in self._n_send.items()]
-        recvs = [(s_, self._recv_base[s_] * e, (self._recv_base[s_] + c * n) * e) for s_, n in self._n_recv.items()
-                 if s_ != me]
+        sends, recvs = tile_messages((self._n_send, self._send_base, self._n_recv, self._recv_base), me, c,
+                                     self.PT_PLANES * 4)
         with torch.cuda.stream(rs):
             nbytes = exchange_tiles(self._send, sends, self._recv, recvs, self.dist, self._sgroup) if p.world > 1 else 0
         r._stream_to(rs)

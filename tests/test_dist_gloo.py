@@ -339,3 +339,72 @@ def _gather_worker(rank, world, port, W, H, bounds):
 def test_gather_bands_assembles_full_frame(world, bounds):
     """bench.py's band_parity gathers every rank's owned rows on rank 0 (ptsvgf.dist.gather_bands)."""
     mp.spawn(_gather_worker, args=(world, _free_port(), 6, 40, bounds), nprocs=world, join=True)
+
+
+def _tile_worker(rank, world, port, W, H, bounds, batches):
+    """TileShardRenderer's data path on the CPU: each rank packs its tile subset of every peer band's zone per the
+    shared layout (dist.tile_layout / tile_messages; pixel order restated in numpy as test_tiles.subset_index, which is
+    pinned there against pt_tiles_copy), the ranks exchange one batch with dist.exchange_tiles over gloo, and each rank
+    unpacks every source's block into its zone: the zone rows must equal the frame's, for full batches and a batch cut
+    short."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "path-tracing-svgf_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from test_tiles import subset_index
+
+        from ptsvgf import gl
+        from ptsvgf.dist import BandPlan, exchange_tiles, svgf_margins, tile_layout, tile_messages
+
+        plan = BandPlan(W, H, rank, world, ghost=8, bounds=bounds, iterations=1, margins=svgf_margins(1, False))
+        B = max(batches)
+        lay = tile_layout(plan, W, B, lambda o, a, b: gl.tiles_count(W, world, o, a, b))
+        n_send, send_base, n_recv, recv_base, ns, nr = lay
+
+        def frame(f):  # the frame's three planes (every rank knows them; each packs only its subset)
+            return np.stack([np.arange(H * W * 4, dtype=np.float32).reshape(H, W, 4) * (f + 1) + 1000 * c
+                             for c in range(3)])
+
+        def block(planes, s, y0, y1):  # one packed block: plane by plane, the subset's pixels in layout order
+            ys, xs = subset_index(W, world, s, y0, y1)
+            return np.concatenate([planes[j][ys, xs].reshape(-1) for j in range(3)])
+
+        f0 = 0
+        z0, z1 = plan.zone(rank)
+        for c in batches:
+            send = torch.full((max(1, ns) * 12,), float("nan"))
+            recv = torch.full((max(1, nr) * 12,), float("nan"))
+            for b in range(c):
+                pl = frame(f0 + b)
+                for k, n in n_send.items():
+                    o = (send_base[k] + b * n) * 12
+                    send[o:o + n * 12] = torch.from_numpy(block(pl, rank, *plan.zone(k)))
+                o = (recv_base[rank] + b * n_recv[rank]) * 12
+                recv[o:o + n_recv[rank] * 12] = torch.from_numpy(block(pl, rank, z0, z1))
+            sends, recvs = tile_messages(lay, rank, c, 12)
+            sent = exchange_tiles(send, sends, recv, recvs, dist)
+            assert sent == sum(c * n * 48 for n in n_send.values())
+            for b in range(c):
+                got = np.full((3, H, W, 4), np.nan, np.float32)
+                for s, m in n_recv.items():
+                    ys, xs = subset_index(W, world, s, z0, z1)
+                    o = (recv_base[s] + b * m) * 12
+                    blk = recv[o:o + m * 12].numpy().reshape(3, m, 4)
+                    for j in range(3):
+                        got[j][ys, xs] = blk[j]
+                assert np.array_equal(got[:, z0:z1], frame(f0 + b)[:, z0:z1]), (rank, f0 + b)
+            f0 += c
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,W,bounds,batches", [(2, 80, None, [1, 1]), (3, 80, (0, 20, 36, 64), [3, 2]),
+                                                    (4, 48, (0, 8, 30, 40, 64), [2, 2, 1])])
+def test_tile_exchange_gloo(world, W, bounds, batches):
+    """The tile shard's all-to-all (dist.exchange_tiles with the tile_layout / tile_messages layout): every rank's zone
+    (its band widened by the ghost zone's reprojection margin) is assembled from the N subsets bit for bit; 80 / 16 = 5
+    tiles per row, so the subsets are not column stripes; batches of 1-3 frames, one cut short as flush() cuts it."""
+    mp.spawn(_tile_worker, args=(world, _free_port(), W, 64, bounds, batches), nprocs=world, join=True)
