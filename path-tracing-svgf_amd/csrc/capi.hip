@@ -900,6 +900,12 @@ int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU*
       sg.has4 = true;
       sg.root4 = root4;
       sg.need4 = need4;
+      if (getenv("PTSVGF_SCENE_INFO"))  // diagnostics: the walks' working set (DESIGN.md "The traversal in round 4")
+        fprintf(stderr, "ptsvgf scene: %zu triangles (geometry %zu B, shading %zu B), reference tree %zu B, any-hit "
+                        "tree %zu B, 4-wide tree %zu nodes = %zu B, stack need %d / %d / %d\n",
+                (size_t)ntris, (size_t)ntris * 64, (size_t)ntris * 144, bvh.size() * sizeof(float4),
+                any.size() * sizeof(float4), bvh4.size() / ptk::kWideStride, bvh4.size() * sizeof(float4),
+                sg.stack_need, sg.need_any, need4);
     } else {
       for (float4** b : {&sg.bvh_any, &sg.bvh4})
         if (*b) { (void)hipFree(*b); *b = nullptr; }
