@@ -639,6 +639,15 @@ static int pack_wide(const std::vector<SahNode>& nodes, const std::function<int(
       ch[best + 1] = nodes[b].right;
       ++nc;
     }
+#if PT_WIDE_ORDER
+    // slot order = build order: the first interior child is stored right after this node (depth first), so the
+    // second cache line of this node's fetch holds most of it. Put the child a ray most likely enters there (largest
+    // surface area). Slots only order ties between equally near children; the candidates, hence every result, are
+    // the same.
+    std::stable_sort(ch, ch + nc, [&](int x, int y) {
+      return sah_area(nodes[x].lo, nodes[x].hi) > sah_area(nodes[y].lo, nodes[y].hi);
+    });
+#endif
     const int k = (int)(out.size() / ptk::kWideStride);
     out.resize(out.size() + ptk::kWideStride, float4{0, 0, 0, 0});
     const int here = acc + nc - 1;

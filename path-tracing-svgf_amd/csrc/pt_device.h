@@ -44,6 +44,13 @@ namespace ptk {
 #define PT_WIDE_STRIDE 7
 #endif
 constexpr int kWideStride = PT_WIDE_STRIDE;
+// PT_WIDE_ORDER = 1 (default): pack_wide stores a node's largest child first, i.e. right after the node, where the
+// node's own fetch already brings most of it into L1 (capi.hip). Same box, three alternating repetitions
+// (profiles/r04/wide_order_ab.log): 4K 210.6 / 212.2 / 210.4 -> 213.0 / 214.2 / 213.0 fps, surface view
+// 68.6 / 68.9 / 68.5 -> 69.7 / 69.7 / 69.7.
+#ifndef PT_WIDE_ORDER
+#define PT_WIDE_ORDER 1
+#endif
 constexpr int kStack = PT_KSTACK;  // traversal stack depth (host checks BVH depth < kStack)
 // Traversal counters: a node visit counts PT_NODE_VISIT (1; a diagnostic build with 0 counts triangle tests only)
 #ifndef PT_NODE_VISIT
