@@ -233,6 +233,16 @@ struct SceneGPU {
   uint64_t tri_ver = 0, node_ver = 0;
 };
 
+// The environment map with its importance cache's pdf channel beside it (PTParams::hdr_pdf): built on the device
+// when a path-tracing draw binds an hdrMap and an hdrCache of one size, rebuilt when either changes (versions), freed
+// with either texture.
+struct HdrMerged {
+  float4* buf = nullptr;
+  const void *hdr_dev = nullptr, *cache_dev = nullptr;
+  uint64_t vh = 0, vc = 0;
+  int W = 0, H = 0;
+};
+
 struct Lib {
   bool init = false;
   int device = 0;
@@ -242,6 +252,7 @@ struct Lib {
   std::map<uint32_t, std::unique_ptr<Texture>> textures;
   std::map<uint32_t, std::unique_ptr<Pass>> passes;
   std::map<std::pair<uint32_t, uint32_t>, SceneGPU> scenes;
+  std::map<std::pair<uint32_t, uint32_t>, HdrMerged> hdr_merged;  // keyed by (hdrMap, hdrCache) handles
   uint32_t unit0 = 0;  // GL texture unit 0 binding (global)
   int band_w = 0, band_h = 0, band_y0 = 0, band_y1 = 0, band_row0 = 0, band_rows = 0;
   bool profiling = false;
@@ -1199,11 +1210,34 @@ int pt_params(Pass* p, PTParams& k, SceneGPU*& sg) {
     k.scene.tex_layers = ma->layers;
   }
   k.scene.use_normal_map = ui(p, "use_normal_map", 0);
-  Texture* hm = sampler(p, "hdrMap");
-  Texture* hc = sampler(p, "hdrCache");
+  uint32_t hmh = 0, hch = 0;
+  Texture* hm = sampler(p, "hdrMap", &hmh);
+  Texture* hc = sampler(p, "hdrCache", &hch);
   if (!hm || !hc || !hm->dev || !hc->dev) return err(PT_ERR_MISSING_TEXTURE, "path_tracing needs hdrMap and hdrCache");
   k.hdr = Tex{(const float4*)hm->dev, hm->W, hm->H};
   k.cache = Tex{(const float4*)hc->dev, hc->W, hc->H};
+  k.hdr_pdf = Tex{nullptr, 0, 0};
+  // A/B switch hdr_merge (default 1): the NEE's radiance and pdf fetches at one direction from one merged texture
+  if (ui(p, "hdr_merge", 1) && hm != hc && hm->W == hc->W && hm->H == hc->H && hm->target == PT_TEXTURE_2D &&
+      hc->target == PT_TEXTURE_2D && hm->rows == hm->H && hc->rows == hc->H) {
+    HdrMerged& m = g.hdr_merged[{hmh, hch}];
+    if (!m.buf || m.W != hm->W || m.H != hm->H) {
+      if (m.buf) (void)hipFree(m.buf);
+      m = HdrMerged{};
+      HIPCHK(hipMalloc((void**)&m.buf, (size_t)hm->W * hm->H * sizeof(float4)));
+      m.W = hm->W;
+      m.H = hm->H;
+    }
+    if (m.hdr_dev != hm->dev || m.cache_dev != hc->dev || m.vh != hm->version || m.vc != hc->version) {
+      const int rc = ptk::launch_hdr_merge((const float4*)hm->dev, (const float4*)hc->dev, m.buf, m.W * m.H, g.stream);
+      if (rc) return hip_err((hipError_t)rc, "hdr merge");
+      m.hdr_dev = hm->dev;
+      m.cache_dev = hc->dev;
+      m.vh = hm->version;
+      m.vc = hc->version;
+    }
+    k.hdr_pdf = Tex{m.buf, m.W, m.H};
+  }
   k.hdrResolution = ui(p, "hdrResolution", hm->W);
   k.pointLightSize = ui(p, "pointLightSize", 0);
   k.frameCounter = uu(p, "frameCounter", 0);
@@ -1629,6 +1663,9 @@ int pt_shutdown(void) {
     if (p->ev1) (void)hipEventDestroy(p->ev1);
   }
   for (auto& kv : g.scenes) free_scene(kv.second);
+  for (auto& kv : g.hdr_merged)
+    if (kv.second.buf) (void)hipFree(kv.second.buf);
+  g.hdr_merged.clear();
   if (g_lbvh.base) (void)hipFree(g_lbvh.base);
   g_lbvh = ptk::LbvhWork{};
   if (g.own) (void)hipStreamDestroy(g.own);
@@ -1924,6 +1961,14 @@ int pt_texture_destroy(uint32_t tex) {
   if (it->second->aux) (void)hipFree(it->second->aux);
   if (it->second->tflags) (void)hipFree(it->second->tflags);
   g.textures.erase(it);
+  for (auto hm = g.hdr_merged.begin(); hm != g.hdr_merged.end();) {  // merged environments built from it
+    if (hm->first.first == tex || hm->first.second == tex) {
+      if (hm->second.buf) (void)hipFree(hm->second.buf);
+      hm = g.hdr_merged.erase(hm);
+    } else {
+      ++hm;
+    }
+  }
   // the device scenes decoded from this buffer (keyed by (triangles, nodes) handles) go with it
   for (auto sc = g.scenes.begin(); sc != g.scenes.end();) {
     if (sc->first.first == tex || sc->first.second == tex) {

@@ -566,6 +566,20 @@ int launch_gbuffer_raster(const GBufParams& p, hipStream_t s) {
   return launch_gbuffer(p, s);
 }
 
+// The merged environment texture (PTParams::hdr_pdf): per texel hdrMap's radiance and hdrCache's pdf channel.
+__global__ void __launch_bounds__(256) hdr_merge_kernel(const float4* __restrict__ hdr, const float4* __restrict__ cache,
+                                                        float4* __restrict__ out, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float4 h = hdr[i];
+  out[i] = make_float4(h.x, h.y, h.z, cache[i].z);
+}
+int launch_hdr_merge(const float4* hdr, const float4* cache, float4* out, int n, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(hdr_merge_kernel, dim3((n + 255) / 256), dim3(256), 0, s, hdr, cache, out, n);
+  return (int)hipGetLastError();
+}
+
 int launch_pathtrace(const PTParams& p, hipStream_t s) {
   if (p.y1 <= p.y0) return 0;
   dim3 grid((p.W + 15) / 16, (p.y1 - p.y0 + 15) / 16);

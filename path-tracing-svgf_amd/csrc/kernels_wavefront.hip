@@ -1126,9 +1126,9 @@ __global__ void __launch_bounds__(256) PT_SHADE_ATTR wf_shade(PTParams p, int bo
         float r1 = u32_to_unit(wang_hash(&seed));
         float r2 = u32_to_unit(wang_hash(&seed));
         v3 hd = sample_hdr(p, r1, r2);
-        v3 hv = hdr_color(p, hd);
+        float hpdf;
+        v3 hv = hdr_color_pdf(p, hd, &hpdf);
         v3 hb = brdf_eval(V, h.normal, hd, h.m);
-        float hpdf = hdr_pdf(p, hd);
         v3 hcalc = divs(mul(muls(hb, f_abs(dot(hd, h.normal))), hv), hpdf);
         // calculatePointLight, as if unoccluded (:884-919)
         v3 pcalc = splat(0.0f);

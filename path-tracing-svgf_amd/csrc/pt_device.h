@@ -192,6 +192,9 @@ struct PTParams {
   Plane color, emission, albedo, last;  // outputs (+ lastFrame input)
   SceneDev scene;
   Tex hdr, cache;
+  // hdrMap's radiance (.xyz) and hdrCache's pdf (.z) of each texel in one float4 (capi.hip hdr_merged), when both
+  // textures have one size: the NEE's hdr_color + hdr_pdf at one direction then read one texture (null: two)
+  Tex hdr_pdf;
   int hdrResolution;
   int pointLightSize;
   uint32_t frameCounter;
@@ -362,6 +365,7 @@ int launch_modulate_after(const AtrousParams& p, hipStream_t s);
 int launch_output(const OutputParams& p, hipStream_t s);
 int launch_taa(const TAAParams& p, hipStream_t s);
 int launch_tile_sort(uint32_t* cost, int* perm, int ntiles, hipStream_t s);  // cost -> perm, clears cost
+int launch_hdr_merge(const float4* hdr, const float4* cache, float4* out, int n, hipStream_t s);  // (hdr.xyz, cache.z)
 }  // namespace ptk
 
 namespace ptk {

@@ -894,6 +894,26 @@ __device__ __forceinline__ float hdr_pdf(const PTParams& p, v3 L) {  // :821-832
   float conv = (float)(p.hdrResolution * p.hdrResolution / 2) / (((2.0f * PT_PI) * PT_PI) * st);
   return pdf * conv;
 }
+// hdr_color(p, L) and hdr_pdf(p, L) of one direction: with the merged texture (PTParams::hdr_pdf) one bilinear fetch
+// serves both — the same texels, weights and mixes as tex_lin on each texture, so the same bits.
+__device__ __forceinline__ v3 hdr_color_pdf(const PTParams& p, v3 L, float* pdf) {
+  if (!p.hdr_pdf.p) {
+    *pdf = hdr_pdf(p, L);
+    return hdr_color(p, L);
+  }
+  float u, v;
+  to_sph(normalize(L), &u, &v);
+  const Tex& T = p.hdr_pdf;
+  Bilin b = bilin_setup(u, v, T.W, T.H);
+  float4 c00 = T.p[(size_t)b.y0 * T.W + b.x0], c10 = T.p[(size_t)b.y0 * T.W + b.x1];
+  float4 c01 = T.p[(size_t)b.y1 * T.W + b.x0], c11 = T.p[(size_t)b.y1 * T.W + b.x1];
+  const float theta = PT_PI * (0.5f - v);
+  const float st = f_max(g_sin(theta), 1e-10f);
+  const float conv = (float)(p.hdrResolution * p.hdrResolution / 2) / (((2.0f * PT_PI) * PT_PI) * st);
+  *pdf = bilin_mix(b, c00.w, c10.w, c01.w, c11.w) * conv;
+  return mk(bilin_mix(b, c00.x, c10.x, c01.x, c11.x), bilin_mix(b, c00.y, c10.y, c01.y, c11.y),
+            bilin_mix(b, c00.z, c10.z, c01.z, c11.z));
+}
 __device__ __forceinline__ v3 sample_hdr(const PTParams& p, float xi1, float xi2) {  // :787-799
   float4 c = tex_lin(p.cache, xi1, xi2);
   float yy = 1.0f - c.y;

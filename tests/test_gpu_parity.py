@@ -320,6 +320,26 @@ def test_tile_subsets_compose_to_full_frame(gpu, scene_small, W, H, stride, cap)
     b.close()
 
 
+def test_merged_environment_equals_two_fetches(gpu, scene_small):
+    """hdr_merge (default 1): the NEE's radiance and pdf at one direction (path_tracing.frag:813-832) fetched from one
+    merged texture (hdrMap's .xyz beside hdrCache's .z) give the bits of the two separate fetches; a new environment
+    upload rebuilds the merged copy."""
+    gl = gpu
+    W, H = 64, 48
+    outs = []
+    for merge in (0, 1):
+        r = _renderer(scene_small, W, H, mode="fast", run_taa=False, run_output=False)
+        r.pass_path_tracing.set_uniform_int("hdr_merge", merge)
+        r.frame()
+        first = gl.readback(r.planes()["color"])
+        gl.upload_rgb32f(r.hdrMap, scene_small.hdr[::-1].copy())  # a different environment: the merged copy follows
+        r.frame()
+        outs.append((first, gl.readback(r.planes()["color"])))
+        r.close()
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    assert not np.array_equal(outs[1][0], outs[1][1])
+
+
 def test_fast_driver_equals_reference_driver(gpu, scene_small):
     """Pointer-swapped fast driver == main.cpp call sequence with copies, bit for bit."""
     gl = gpu
