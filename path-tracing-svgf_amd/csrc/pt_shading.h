@@ -883,7 +883,8 @@ __device__ __forceinline__ void to_sph(v3 v, float* u, float* w) {  // :804-810
 __device__ __forceinline__ v3 hdr_color(const PTParams& p, v3 L) {  // :813-817
   float u, v;
   to_sph(normalize(L), &u, &v);
-  return xyz(tex_lin(p.hdr, u, v));
+  // the merged texture holds hdrMap's texels in .xyz: the same bits, and the environment is read from one array
+  return xyz(tex_lin(p.hdr_pdf.p ? p.hdr_pdf : p.hdr, u, v));
 }
 __device__ __forceinline__ float hdr_pdf(const PTParams& p, v3 L) {  // :821-832
   float u, v;
