@@ -253,6 +253,7 @@ struct Lib {
   std::map<uint32_t, std::unique_ptr<Pass>> passes;
   std::map<std::pair<uint32_t, uint32_t>, SceneGPU> scenes;
   std::map<std::pair<uint32_t, uint32_t>, HdrMerged> hdr_merged;  // keyed by (hdrMap, hdrCache) handles
+  std::map<hipStream_t, ptk::WfFork> forks;  // per draw stream: the path tracer's side stream (uniform trace_fork)
   uint32_t unit0 = 0;  // GL texture unit 0 binding (global)
   int band_w = 0, band_h = 0, band_y0 = 0, band_y1 = 0, band_row0 = 0, band_rows = 0;
   bool profiling = false;
@@ -1303,6 +1304,26 @@ int pt_wf_setup(Pass* p, PTParams& k, SceneGPU* sg, const WFState& st) {
     return PT_OK;
 }
 
+// The side stream and events of path-tracing draws issued on `s` (uniform trace_fork = 1), created on first use: one
+// per draw stream, so frames in flight on different streams do not queue behind each other's shadow walks.
+const ptk::WfFork* wf_fork(Pass* p, hipStream_t s, int* rc) {
+  *rc = PT_OK;
+  if (!ui(p, "trace_fork", 0)) return nullptr;
+  auto it = g.forks.find(s);
+  if (it != g.forks.end()) return &it->second;
+  ptk::WfFork f{};
+  hipError_t e = hipStreamCreateWithFlags(&f.side, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&f.fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&f.join, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    if (f.side) (void)hipStreamDestroy(f.side);
+    if (f.fork) (void)hipEventDestroy(f.fork);
+    *rc = hip_err(e, "trace_fork side stream");
+    return nullptr;
+  }
+  return &(g.forks[s] = f);
+}
+
 int draw_pathtrace(Pass* p) {
   PTParams k;
   SceneGPU* sg = nullptr;
@@ -1318,7 +1339,9 @@ int draw_pathtrace(Pass* p) {
     TRY(wf_alloc(p->wf, k.W, std::max(0, k.y1 - k.y0)));
     if (wf_spill(p->wf, k.stack_need) != PT_OK) return err(PT_ERR_HIP, "spill stack allocation failed");
     TRY(pt_wf_setup(p, k, sg, p->wf.st));
-    rc = launch_pathtrace_wavefront(k, g.stream);
+    const ptk::WfFork* fk = wf_fork(p, g.stream, &rc);
+    if (rc) return rc;
+    rc = launch_pathtrace_wavefront(k, g.stream, fk);
     if (!rc && k.tiles.cost) p->order.ordered = true;
   }
   return rc ? hip_err((hipError_t)rc, "pathtrace launch") : PT_OK;
@@ -1339,7 +1362,7 @@ int draw_pathtrace_batch(Pass** ps, int n) {
     // compared at its effective value (the default pt_params / pt_wf_setup apply when a pass never set it)
     struct Same { const char* name; int dflt; };
     const Same same[] = {{"trace_refill", 0}, {"shadow_budget", 0}, {"closest_budget", 0}, {"wide_bvh", 1},
-                         {"refill_waves", 0}};
+                         {"refill_waves", 0}, {"trace_fork", 0}};
     bool agree = true;
     for (const Same& u : same) agree = agree && ui(ps[b], u.name, u.dflt) == ui(ps[0], u.name, u.dflt);
     if (sb != sg || k[b].W != k[0].W || k[b].y0 != k[0].y0 || k[b].y1 != k[0].y1 || k[b].max_depth != k[0].max_depth ||
@@ -1355,7 +1378,10 @@ int draw_pathtrace_batch(Pass** ps, int n) {
   TRY(wf_alloc(h->wf, k[0].W, std::max(0, k[0].y1 - k[0].y0), cap));
   if (wf_spill(h->wf, k[0].stack_need) != PT_OK) return err(PT_ERR_HIP, "spill stack allocation failed");
   for (int b = 0; b < n; ++b) TRY(pt_wf_setup(ps[b], k[b], sg, h->wf.stb[b]));
-  const int rc = launch_pathtrace_wavefront_batch(k, n, g.stream);
+  int rc;
+  const ptk::WfFork* fk = wf_fork(h, g.stream, &rc);
+  if (rc) return rc;
+  rc = launch_pathtrace_wavefront_batch(k, n, g.stream, fk);
   for (int b = 0; b < n && !rc; ++b)
     if (k[b].tiles.cost) ps[b]->order.ordered = true;
   return rc ? hip_err((hipError_t)rc, "pathtrace batch launch") : PT_OK;
@@ -1666,6 +1692,12 @@ int pt_shutdown(void) {
   for (auto& kv : g.hdr_merged)
     if (kv.second.buf) (void)hipFree(kv.second.buf);
   g.hdr_merged.clear();
+  for (auto& kv : g.forks) {
+    (void)hipEventDestroy(kv.second.fork);
+    (void)hipEventDestroy(kv.second.join);
+    (void)hipStreamDestroy(kv.second.side);
+  }
+  g.forks.clear();
   if (g_lbvh.base) (void)hipFree(g_lbvh.base);
   g_lbvh = ptk::LbvhWork{};
   if (g.own) (void)hipStreamDestroy(g.own);

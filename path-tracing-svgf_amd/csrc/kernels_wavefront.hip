@@ -282,7 +282,6 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
 // triangles share (the reference keeps the one its depth-first order meets first) or that finds nothing below the
 // G-buffer bound is flagged and walked by wf_primary, as is every pixel if a list overflows. Same bits as wf_primary.
 constexpr int kPChunk = 256;  // leaves staged in LDS per round
-
 // per reference leaf: the pixel box of the primary rays that can pass its box — each face clipped to the widened
 // frustum and projected; a box holding the eye covers the band — and the nearest t they can meet it at (t along
 // the normalised ray is at least the camera-space depth w of the point)
@@ -1232,16 +1231,16 @@ int wf_subset_tiles(int W, int rows, int stride, int offset) {
   return offset < n ? (n - offset + stride - 1) / stride : 0;
 }
 
-// Launch order of one frame. With an auxiliary stream the closest-hit trace of bounce i+1 (it needs only the
-// rays and live list shade(i) wrote) runs concurrently with the shadow trace and finish of bounce i; the join
-// comes before shade(i+1), which needs both. Two traversal launches then end together, so the frame's
-// dependency chain carries one tail fewer per bounce. Without `aux` the launches are serial.
+// Launch order of one frame. With a WfFork (uniform trace_fork) the closest-hit trace of bounce 1 (it needs only the
+// rays and live list the bounce-0 shade wrote) runs beside the bounce-0 shadow trace and finish on the side stream;
+// the join comes before the bounce-1 shade, which reuses the shadow list and reads the finished throughput. The two
+// traversal launches then fill each other's tails. Without `fk` the launches are serial.
 // nb > 1: a batch of frames (pt_pass_draw_batch) — per-frame launches for the primaries, shades and finishes, ONE
 // launch per bounce for the list-driven traversals of every frame's rays (lane-refill kernels; the one-ray-per-lane
 // kernels run per frame). Frame b's wavefront state lies at pid offset b * N of ps[0]'s, its counters at
 // ps[0].wf.counters + b * kWfCounters; the batched launches use frame 0's work-queue heads and straggler lists.
 template <int KS, bool DEEP>
-int launch_wavefront(const PTParams* ps, int nb, hipStream_t s) {
+int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, const WfFork* fk) {
   const PTParams& p = ps[0];
   const int rows = p.y1 - p.y0;
   if (rows <= 0) return 0;
@@ -1302,14 +1301,27 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s) {
                            (const int*)(ps[b].wf.counters + kWfCtr * (i - 1)), cap);
     }
   };
+  // deep trees keep one stream: both walks would use the pixel's spill columns
+  const bool split = fk && !DEEP && p.max_depth > 1;
   for (int i = 0; i < p.max_depth; ++i) {
     if (i > 0) closest(i);
+    if (i == 1 && split) {
+      const hipError_t e = hipStreamWaitEvent(s, fk->join, 0);
+      if (e != hipSuccess) return (int)e;
+    }
     for (int b = 0; b < nb; ++b) {
       const PTParams& f = ps[b];
       const int* live_in = f.wf.counters + kWfCtr * (i > 0 ? i - 1 : 0);
       hipLaunchKernelGGL(wf_shade, dim3(i == 0 ? gS0 : gN), dim3(256), 0, s, f, i, (const int*)lst(f, i + 1), live_in,
                          lst(f, i), f.wf.counters + kWfCtr * i, f.wf.shadow_list, f.wf.counters + kWfCtr * i + kCtrHdr,
                          cap);
+    }
+    hipStream_t ss = s;  // the shadow walk's and finish's stream
+    if (i == 0 && split) {
+      hipError_t e = hipEventRecord(fk->fork, s);
+      if (e == hipSuccess) e = hipStreamWaitEvent(fk->side, fk->fork, 0);
+      if (e != hipSuccess) return (int)e;
+      ss = fk->side;
     }
     if (p.refill) {
       ListBatch lb{nb, N, {}, {}};
@@ -1321,48 +1333,52 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s) {
       if constexpr (!DEEP)
         if (wide) {
           hipLaunchKernelGGL((wf_trace_shadow_refill<kWideKS, false, true>), dim3(refill_blocks(2 * nb * N)), dim3(kTB), 0,
-                             s, p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQShadow, strag);
+                             ss, p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQShadow, strag);
         }
       if (!wide)
-        hipLaunchKernelGGL((wf_trace_shadow_refill<KS, DEEP, false>), dim3(refill_blocks(2 * nb * N)), dim3(kTB), 0, s,
+        hipLaunchKernelGGL((wf_trace_shadow_refill<KS, DEEP, false>), dim3(refill_blocks(2 * nb * N)), dim3(kTB), 0, ss,
                            p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQShadow, strag);
       if (p.wf.shadow_budget || wide)
-        hipLaunchKernelGGL(wf_shadow_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, s, p, (const int*)strag);
+        hipLaunchKernelGGL(wf_shadow_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, ss, p, (const int*)strag);
     } else {
       for (int b = 0; b < nb; ++b) {
         const PTParams& f = ps[b];
         const int* shadow = f.wf.counters + kWfCtr * i + kCtrHdr;
         int* strag = f.wf.counters + kWfCtr * i + kCtrStrag;
         if (f.scene.bvh4)
-          hipLaunchKernelGGL((wf_trace_shadow<KS, true, DEEP>), dim3(gT2), dim3(kTB), 0, s, f,
+          hipLaunchKernelGGL((wf_trace_shadow<KS, true, DEEP>), dim3(gT2), dim3(kTB), 0, ss, f,
                              (const int*)f.wf.shadow_list, shadow, cap, strag);
         else
-          hipLaunchKernelGGL((wf_trace_shadow<KS, false, DEEP>), dim3(gT2), dim3(kTB), 0, s, f,
+          hipLaunchKernelGGL((wf_trace_shadow<KS, false, DEEP>), dim3(gT2), dim3(kTB), 0, ss, f,
                              (const int*)f.wf.shadow_list, shadow, cap, strag);
         if (f.wf.shadow_budget)
-          hipLaunchKernelGGL(wf_shadow_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, s, f, (const int*)strag);
+          hipLaunchKernelGGL(wf_shadow_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, ss, f, (const int*)strag);
       }
     }
     for (int b = 0; b < nb; ++b)
-      hipLaunchKernelGGL(wf_finish, dim3(gN), dim3(256), 0, s, ps[b], (const int*)lst(ps[b], i),
+      hipLaunchKernelGGL(wf_finish, dim3(gN), dim3(256), 0, ss, ps[b], (const int*)lst(ps[b], i),
                          (const int*)(ps[b].wf.counters + kWfCtr * i), cap);
+    if (i == 0 && split) {
+      const hipError_t e = hipEventRecord(fk->join, ss);
+      if (e != hipSuccess) return (int)e;
+    }
   }
   for (int b = 0; b < nb; ++b) hipLaunchKernelGGL(wf_finalize, dim3(gN), dim3(256), 0, s, ps[b]);
   return (int)hipGetLastError();
 }
 
-int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s) {
+int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s, const WfFork* fk) {
   // the LDS stack bounds resident waves: a tree that fits the small stack gets more of them
-  if (p.wf.spill) return launch_wavefront<kSpillKS, true>(&p, 1, s);  // deep tree
-  return p.stack_need <= kStackSmall ? launch_wavefront<kStackSmall, false>(&p, 1, s)
-                                     : launch_wavefront<kStack, false>(&p, 1, s);
+  if (p.wf.spill) return launch_wavefront<kSpillKS, true>(&p, 1, s, fk);  // deep tree
+  return p.stack_need <= kStackSmall ? launch_wavefront<kStackSmall, false>(&p, 1, s, fk)
+                                     : launch_wavefront<kStack, false>(&p, 1, s, fk);
 }
 
-int launch_pathtrace_wavefront_batch(const PTParams* ps, int nb, hipStream_t s) {
+int launch_pathtrace_wavefront_batch(const PTParams* ps, int nb, hipStream_t s, const WfFork* fk) {
   if (nb < 1 || nb > kMaxBatch) return (int)hipErrorInvalidValue;
-  if (ps[0].wf.spill) return launch_wavefront<kSpillKS, true>(ps, nb, s);
-  return ps[0].stack_need <= kStackSmall ? launch_wavefront<kStackSmall, false>(ps, nb, s)
-                                         : launch_wavefront<kStack, false>(ps, nb, s);
+  if (ps[0].wf.spill) return launch_wavefront<kSpillKS, true>(ps, nb, s, fk);
+  return ps[0].stack_need <= kStackSmall ? launch_wavefront<kStackSmall, false>(ps, nb, s, fk)
+                                         : launch_wavefront<kStack, false>(ps, nb, s, fk);
 }
 
 }  // namespace ptk

@@ -344,7 +344,14 @@ namespace ptk {
 int launch_shard_copy(const ShardCopy& c, hipStream_t s);
 long long shard_pixels(int W, int tile_y0, int stride, int offset, int y0, int y1);  // per plane
 int launch_pathtrace(const PTParams& p, hipStream_t s);
-int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s);
+// A side stream for the wavefront's bounce-0 shadow rays: they and the bounce-1 closest-hit rays both come from the
+// bounce-0 shade and touch disjoint buffers, so the two walks run at once and fill each other's launch tails.
+// `fork` is recorded on the draw's stream after that shade, `join` on the side stream after the bounce-0 finish.
+struct WfFork {
+  hipStream_t side;
+  hipEvent_t fork, join;
+};
+int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s, const WfFork* fk = nullptr);
 int wf_list_capacity(int W, int rows);  // per-segment capacity of the compacted ray lists (8 segments)
 int wf_subset_tiles(int W, int rows, int stride, int offset);  // tiles of a PTParams tile subset (< 0: invalid)
 int launch_gbuffer(const GBufParams& p, hipStream_t s);
@@ -352,7 +359,7 @@ int launch_gbuffer_raster(const GBufParams& p, hipStream_t s);
 int launch_gbuffer_adopt(const GBufParams& p, hipStream_t s);  // side data of G-buffer planes written elsewhere  // bins, resolves, and the ray cast on overflow
 int launch_bins(const Bins& b, hipStream_t s);  // after the item setup kernel: large items, scan, scatter
 // nb frames' path tracing with batched traversal launches (ps[b]: frame b, its wavefront state at pid offset b * n)
-int launch_pathtrace_wavefront_batch(const PTParams* ps, int nb, hipStream_t s);
+int launch_pathtrace_wavefront_batch(const PTParams* ps, int nb, hipStream_t s, const WfFork* fk = nullptr);
 int launch_reproject(const ReprojParams& p, hipStream_t s);
 int launch_variance(const VarianceParams& p, hipStream_t s);
 int launch_atrous_exact(const AtrousParams& p, hipStream_t s);

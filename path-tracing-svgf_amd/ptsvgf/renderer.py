@@ -346,6 +346,10 @@ class Renderer:
             # chunk rounds per wave 75 / 85 / 90 / 95 % measured 183.1 / 184.3 / 183.7 / 183.9 fps at 4K and 57.2 / 58.7 /
             # 59.5 / 60.6 fps on the surface view, 1080p and 8 bands within noise (tools/refill_pct_sweep.sh)
             p.set_uniform_int("trace_refill", 90 if self.K > 1 else 0)
+            # one frame at a time: the bounce-0 shadow walk on a side stream beside the bounce-1 closest-hit walk
+            # (their launch tails overlap): 4K serial 131.3 -> 145.4 fps, surface view 48.3 -> 49.3; with frames in
+            # flight the other frames already fill those tails (215.7 / 215.6 fps at K = 4, profiles/r04/fork/)
+            p.set_uniform_int("trace_fork", 1 if self.K == 1 else 0)
             p.set_uniform_int("trace_batch", self.B)
             self.pt_slots.append((p, outs))
         self.pass_path_tracing = PassGroup([p for p, _ in self.pt_slots])  # settings apply to every slot

@@ -268,6 +268,32 @@ def test_cooperative_closest_walk_is_result_preserving(gpu, scene_name, request)
             assert np.array_equal(outs[0][k].view(np.uint32), o[k].view(np.uint32)), k
 
 
+@pytest.mark.parametrize("refill,K,B", [(0, 1, 1), (75, 1, 1), (90, 3, 1), (90, 4, 2)])
+def test_trace_fork_is_result_preserving(gpu, scene_small, refill, K, B):
+    """trace_fork = 1 (kernels_wavefront.hip launch_wavefront: the bounce-0 shadow walk and finish on a side stream
+    beside the bounce-1 closest-hit walk) gives the serial launch order's bits: one-ray-per-lane and lane-refill
+    kernels, frames in flight on several streams (each with its own side stream) and batched draws, moving camera."""
+    gl = gpu
+    W, H = 96, 64
+    outs = []
+    for fork in (0, 1):
+        r = _renderer(scene_small, W, H, mode="fast", run_taa=False, run_output=False, frames_in_flight=K,
+                      trace_batch=B)
+        r.pass_path_tracing.set_uniform_int("trace_refill", refill)
+        r.pass_path_tracing.set_uniform_int("trace_fork", fork)
+        got = []
+        for f in range(K + 3):
+            r.camera.orbit(1.0, 0.0)
+            r.frame()
+            if f % 2:
+                got.append({k: gl.readback(r.planes()[k]) for k in ("color", "emission", "albedo")})
+        outs.append(got)
+        r.close()
+    for a, b in zip(*outs):
+        for k in a:
+            assert np.array_equal(a[k].view(np.uint32), b[k].view(np.uint32)), k
+
+
 def test_wavefront_equals_megakernel(gpu, scene_small):
     """The staged (wavefront) path tracer and the single-kernel form give identical bits."""
     gl = gpu
