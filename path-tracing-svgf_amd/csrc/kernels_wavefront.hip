@@ -383,19 +383,45 @@ __global__ void __launch_bounds__(256) wf_primary_raster(PTParams p) {
   int best = -1;
   bool tied = false;
   uint32_t steps = 0;
+  // The tile's loosest pruning bound: a pixel's bound (tbest) only falls, so a leaf entered beyond the largest bound of
+  // the tile's pixels, with a wider margin than the walk's (below), is skipped by every pixel — it is left out of the
+  // staged chunk. Surface tiles drop the leaves hidden behind their surfaces; a tile with a background pixel keeps all.
+  __shared__ float wmax[4];
+  __shared__ int wcount[4];
+  float tb = valid ? bound : 0.0f;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) tb = fmaxf(tb, __shfl_xor(tb, o));
+  if (ln == 0) wmax[wv] = tb;
+  __syncthreads();
+  const float tile_lim = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])) * 1.0004f + 4.0e-4f;
   const int off = bn.tile_off[gt], total = bn.tile_off[gt + 1] - off;
   for (int base = 0; base < total; base += kPChunk) {
     __syncthreads();
     const int j = base + (int)threadIdx.x;
+    int leaf = 0;
+    float tm = 0.0f;
     if (j < total) {
-      const int leaf = bn.pairs[off + j];
-      slo[threadIdx.x] = p.scene.leaves[2 * leaf];
-      shi[threadIdx.x] = p.scene.leaves[2 * leaf + 1];
-      sbox[threadIdx.x] = bn.box[leaf];
-      stmin[threadIdx.x] = bn.tmin[leaf];
+      leaf = bn.pairs[off + j];
+      tm = bn.tmin[leaf];
+    }
+    const bool keep = j < total && !(tm > tile_lim);
+    const unsigned long long km = __ballot(keep);
+    if (ln == 0) wcount[wv] = __popcll(km);
+    __syncthreads();
+    int n = 0, slot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      slot += w < wv ? wcount[w] : 0;
+      n += wcount[w];
+    }
+    if (keep) {  // compacted in thread order
+      slot += __popcll(km & ((1ull << ln) - 1ull));
+      slo[slot] = p.scene.leaves[2 * leaf];
+      shi[slot] = p.scene.leaves[2 * leaf + 1];
+      sbox[slot] = bn.box[leaf];
+      stmin[slot] = tm;
     }
     __syncthreads();
-    const int n = min(kPChunk, total - base);
     if (!valid) continue;
     for (int k = 0; k < n; ++k) {
       const int4 b = sbox[k];
