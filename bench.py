@@ -332,9 +332,10 @@ def main():
             # band slots cover another rank's whole-frame path tracer (a band's SVGF of frame f starts when f's window
             # has arrived), and the host runs as far ahead as they allow, so they also set the camera-to-modulate
             # latency. Simulated at 4K (tools/frame_shard_sim.py, profiles/r04/shard/, DESIGN.md "Which partition"),
-            # window 4: N = 8 K = 12 912 fps at 15.2 ms (window 8 K = 34, round 3's default: 909 fps at 39 ms); N = 4
-            # K = 12 / 18: 611 / 623 fps at 23.6 / 30.6 ms; N = 2 (window 2) K = 12 / 16: 351 / 348 fps at 35 / 45 ms
-            args.frames_in_flight = k1080 = 12
+            # window 4, N = 8, one box: K = 12 / 16 / 24 925 / 1014 / 1030 fps at 15.0 / 16.6 / 22.3 ms (window 8
+            # K = 34, round 3's default: 909 fps at 39 ms); N = 4 K = 12 / 18: 611 / 623 fps at 23.6 / 30.6 ms; N = 2
+            # (window 2) K = 12 / 16: 351 / 348 fps at 35 / 45 ms
+            args.frames_in_flight = k1080 = 16 if world > 4 else 12
         if world > 1 and args.shard == "tiles":
             # band slots cover back_lag (2) + the subsets' frames in flight
             args.frames_in_flight = k1080 = 8

@@ -556,6 +556,7 @@ class BandRenderer:
         p, H = self.plan, self.r.H
         dev = torch.device("cuda", torch.cuda.current_device())
         counts = torch.zeros(p.y1 - p.y0, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()  # zeroed before the path tracer adds to it on the renderer's front-end stream
         self.exchange = False
         try:
             self.pass_path_tracing.set_row_cost(counts.data_ptr())
@@ -572,13 +573,14 @@ class BandRenderer:
             frame_ms = (time.perf_counter() - t0) * 1e3 / frames
         finally:
             self.exchange = True
-        visits = torch.zeros(H, dtype=torch.float64, device=dev)
-        visits[p.y0:p.y1] = counts.to(torch.float64)
-        per_rank = torch.zeros(p.world, dtype=torch.float64, device=dev)
+        # host tensors over the host group (gloo): every rank must read the same sums, since they cut the next bands
+        visits = torch.zeros(H, dtype=torch.float64)
+        visits[p.y0:p.y1] = counts.cpu().to(torch.float64)
+        per_rank = torch.zeros(p.world, dtype=torch.float64)
         per_rank[p.rank] = frame_ms
-        self.dist.all_reduce(visits)
-        self.dist.all_reduce(per_rank)
-        self.last_band_ms = per_rank.cpu().numpy()  # every rank's band time alone (ms per frame)
+        self.dist.all_reduce(visits, group=self._group)
+        self.dist.all_reduce(per_rank, group=self._group)
+        self.last_band_ms = per_rank.numpy()  # every rank's band time alone (ms per frame)
         return band_row_cost(visits.cpu().numpy(), p.bounds, self.last_band_ms)
 
 
@@ -1280,6 +1282,18 @@ def fit_row_cost(visits, rows, ms):
     return 0.0, float(t.sum() / max(A[:, 1].sum(), 1.0))
 
 
+def agree_bounds(bounds, dist, group=None) -> tuple:
+    """Rank 0's band bounds on every rank. A calibration must end in ONE plan: ranks that cut their bands differently
+    each still trace their own rows right, but exchange halo rows for bands their peers do not hold, so the SVGF
+    chain silently leaves the one-GPU frame (seen once with the every-pass bands, whose calibration all-reduced
+    device tensors over gloo). Collective over `group` (the host group: a CPU tensor)."""
+    import torch
+
+    t = torch.tensor([int(b) for b in bounds], dtype=torch.int64)
+    dist.broadcast(t, src=0, group=group)
+    return tuple(int(v) for v in t.tolist())
+
+
 def make_frame_shard_renderer(scene, W, H, cfg, rank, world, dist, balance: bool = True, rounds: int = 2, cls=None,
                               **kw):
     """FrameShardRenderer whose bands equalise the band work (G-buffer + SVGF chain: the plant's rows cost several
@@ -1309,10 +1323,10 @@ def make_frame_shard_renderer(scene, W, H, cfg, rank, world, dist, balance: bool
         for k in range(world):
             cost[b[k]:b[k + 1]] = times[k] / (b[k + 1] - b[k])
         est.append(cost)
-        bounds = balanced_bounds(np.mean(est, axis=0), world)
+        bounds = agree_bounds(balanced_bounds(np.mean(est, axis=0), world), dist, r._group)
         r.close()
         r = cls(scene, W, H, cfg, rank, world, dist, bounds=bounds, **kw)
-    best = min(tried, key=lambda x: x[0])[1]
+    best = agree_bounds(min(tried, key=lambda x: x[0])[1], dist, r._group)
     r.close()
     r = cls(scene, W, H, cfg, rank, world, dist, bounds=best, **kw)
     r.calibration = tried  # (slowest band's work ms per frame, bounds) per measured plan
@@ -1340,10 +1354,10 @@ def make_band_renderer(scene, W, H, cfg, rank, world, dist, balance: bool = True
         if i == max(rounds, 1):
             break
         est.append(cost)
-        bounds = balanced_bounds(np.mean(est, axis=0), world)
+        bounds = agree_bounds(balanced_bounds(np.mean(est, axis=0), world), dist, r._group)
         r.close()
         r = BandRenderer(scene, W, H, cfg, rank, world, dist, bounds=bounds, **kw)
-    best = min(tried, key=lambda x: x[0])[1]
+    best = agree_bounds(min(tried, key=lambda x: x[0])[1], dist, r._group)
     r.close()  # calibration frames are discarded: the renderer starts fresh (frame 0, empty history)
     r = BandRenderer(scene, W, H, cfg, rank, world, dist, bounds=best, **kw)
     r.calibration = tried  # (slowest band ms, bounds) per measured plan

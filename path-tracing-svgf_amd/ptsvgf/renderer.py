@@ -261,6 +261,14 @@ class Renderer:
         # (camera, modulate done) HIP events per frame when set to a list (frames in flight only): latency_ms()
         self.latency_events = None
         self._clock = None  # the stream camera-time events are recorded on (idle)
+        if self.K > 1:
+            # the planes were zero-filled on the stream current at their creation (the library's memset, a tex_factory's
+            # torch.zeros) and frames draw on the renderer's own streams, which do not wait for that one: a first frame
+            # could read (or be overwritten by) a late fill. Memory a closed renderer freed still holds its old values,
+            # so this showed as a history differing from the one-GPU frame after band calibration.
+            import torch
+
+            torch.cuda.synchronize()
 
     # ------------------------------------------------------------ passes ---
     def _svgf_pass(self, frag: str, atts) -> RenderPass:

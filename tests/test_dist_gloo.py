@@ -408,3 +408,24 @@ def test_tile_exchange_gloo(world, W, bounds, batches):
     (its band widened by the ghost zone's reprojection margin) is assembled from the N subsets bit for bit; 80 / 16 = 5
     tiles per row, so the subsets are not column stripes; batches of 1-3 frames, one cut short as flush() cuts it."""
     mp.spawn(_tile_worker, args=(world, _free_port(), W, 64, bounds, batches), nprocs=world, join=True)
+
+
+def _agree_worker(rank, world, port):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "path-tracing-svgf_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ptsvgf.dist import agree_bounds
+
+        mine = (0, 100 + 8 * rank, 180 + rank, 256)  # each rank's own (diverging) calibration choice
+        got = agree_bounds(tuple(np.int64(v) for v in mine), dist)
+        assert got == (0, 100, 180, 256) and all(type(v) is int for v in got), (rank, got)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_agree_bounds_gloo():
+    """A band calibration ends in rank 0's plan on every rank (dist.agree_bounds): ranks whose own choices differ
+    (their timings raced) would otherwise cut different bands and exchange halo rows their peers do not hold."""
+    mp.spawn(_agree_worker, args=(3, _free_port()), nprocs=3, join=True)

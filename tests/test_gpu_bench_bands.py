@@ -84,7 +84,7 @@ def test_bench_frame_shard_8_ranks_gloo(W, H):
     """the default multi-GPU mode (--shard frames: rank f % 8 traces frame f whole, the SVGF chain
     banded with the ghost zone and the early history exchange) at the BASELINE sizes and rank count — 8 ranks, 1920 x
     1080 (configs[1]) and 3840 x 2160 (configs[3] / [4]), a moving camera, frames_in_flight and the exchange window at
-    their 8-rank defaults (12 band slots, window = back_lag 4) — rehearsed with gloo on the one GPU (4K: ≈ 30 s). 16 timed frames = 4 full windows of 4 after the warm-up's windows; the gathered bands must
+    their 8-rank defaults (16 band slots, window = back_lag 4) — rehearsed with gloo on the one GPU (4K: ≈ 30 s). 16 timed frames = 4 full windows of 4 after the warm-up's windows; the gathered bands must
     equal a one-GPU render of the same camera path bit for bit (reference: main.cpp:436-535 per frame,
     svgf_Atrous.frag:92-97 and svgf_reproject.frag:45-156 for what crosses bands). Equal bands: the calibration only
     moves the bounds, which the 3-rank balanced case above covers."""
@@ -101,7 +101,7 @@ def test_bench_frame_shard_8_ranks_gloo(W, H):
     print(json.dumps(bp), json.dumps(bands["exchange_ms_per_frame"]), bands["frames_in_flight"], bands["back_lag"],
           line.get("max_history_rows"))
     assert line["n_gpus"] == world and bands["shard"] == "frames"
-    assert bands["back_lag"] == bands["window"] == 4 and bands["frames_in_flight"] == 12  # bench.py's 8-rank defaults
+    assert bands["back_lag"] == bands["window"] == 4 and bands["frames_in_flight"] == 16  # bench.py's 8-rank defaults
     assert bp["backend"] == "gloo" and bp["frames"] >= 2 * world + 16  # warm-up windows + 4 timed windows + probes
     assert bp["bit_exact"], bp
     assert line.get("max_history_rows", 0) > 3  # the orbit moved the history (reprojection reach beyond the taps)
