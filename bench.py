@@ -122,6 +122,9 @@ def parse():
     ap.add_argument("--own-slots", type=int, default=4,
                     help="--shard frames / tiles: whole frames / tile subsets a rank traces at once (its path tracer's "
                          "frames in flight)")
+    ap.add_argument("--host-pace", type=int, default=1, choices=(0, 1),
+                    help="one GPU: the host waits for frame f - K's SVGF before issuing frame f (Renderer host_pace): "
+                         "camera-to-modulate 36 -> 18 ms at 4K, same frame rate (profiles/r04/pace/)")
     ap.add_argument("--breakdown", action="store_true", help="print per-pass ms to stderr")
     ap.add_argument("--pt-kernel", type=int, default=0, help="0 wavefront (production), 1 megakernel (A/B)")
     ap.add_argument("--trace-batch", type=int, default=None,
@@ -404,7 +407,7 @@ def main():
         else:
             from ptsvgf.renderer import Renderer
             r = Renderer(scene, W, H, cfg, mode="fast", aspect_corrected=True, run_taa=False, run_output=False,
-                         frames_in_flight=K, trace_batch=min(args.trace_batch, K))
+                         frames_in_flight=K, trace_batch=min(args.trace_batch, K), host_pace=bool(args.host_pace))
         r.pass_path_tracing.set_uniform_int("pt_kernel", args.pt_kernel)
         for kv in args.pt_uniform:
             name, val = kv.split("=")

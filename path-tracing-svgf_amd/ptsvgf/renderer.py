@@ -84,7 +84,8 @@ class Renderer:
                  atrous_exact: bool = False, run_taa: bool = True, run_output: bool = True, tex_factory=None,
                  halo=None, gbuffer_rows=None, frames_in_flight: int = 1, after_gbuffer=None, back_lag: int = 0,
                  trace_batch: int = 1, front_streams: int | None = None, pt_source=None, pt_flush=None,
-                 stage_rows=None, early_history=None, draw_gbuffer: bool = True, fuse_modulate: bool = True):
+                 stage_rows=None, early_history=None, draw_gbuffer: bool = True, fuse_modulate: bool = True,
+                 host_pace: bool = False):
         """band = (y0, y1, row0, rows) for screen-band sharding; tex_factory(w, h) -> handle allocates the
         frame-sized planes (ptsvgf.dist wraps torch tensors); halo(stage, {plane name: handle}) is called before
         the SVGF passes that read rows beyond the band (dist.HALO_SCHEDULE names the planes); after_gbuffer(set,
@@ -116,7 +117,12 @@ class Renderer:
         (dist.FrameShardRenderer: some rank traced the whole frame) once the slot is free; it is called right after the
         G-buffer of f is issued on `stream` and returns a holder dict whose "ev" (a torch event, set by the time the
         back end of f is issued) the back end waits for; pt_flush() is called by flush() before the pending back
-        ends are issued."""
+        ends are issued.
+
+        host_pace (frames in flight only): before issuing frame f's front end the host waits for the back end of
+        frame f - K, which that front end waits for on the GPU anyway. Without it the host queues frames as fast as it
+        can issue them and each frame's camera reaches the GPU long before its G-buffer runs (camera-to-modulate ≈ 8
+        frames at K = 4); with it at most K frames are queued."""
         if mode not in ("fast", "reference"):
             raise ValueError(mode)
         self.mode = mode
@@ -171,6 +177,7 @@ class Renderer:
         if not 1 <= self.B <= min(self.K, 8) or (self.B > 1 and mode != "fast"):
             raise ValueError(f"trace_batch must be in [1, min(frames_in_flight, 8)] (fast driver), got {trace_batch}")
         self.lag = max(int(back_lag), self.B - 1)
+        self.host_pace = bool(host_pace) and self.K > 1
         if not 0 <= self.lag < self.K:
             raise ValueError(f"back_lag must be in [0, frames_in_flight) = [0, {self.K}), got {back_lag}")
         self._nfs = self.K if front_streams is None else int(front_streams)
@@ -820,6 +827,8 @@ class Renderer:
     def frame(self) -> None:
         """One iteration of main.cpp's while-loop body (436-602), headless (with back_lag D: this frame's front
         end and frame f - D's back end)."""
+        if self.host_pace and self._slot_free[self.frame_index % self.K] is not None:
+            self._slot_free[self.frame_index % self.K].synchronize()  # before the camera is read (host_pace)
         self.camera.update()
         if self._serial_stream is not None:
             self._stream_to(self._serial_stream)

@@ -464,6 +464,25 @@ def test_frames_in_flight_equal_serial(gpu, scene_small, K, lag, B):
     b.close()
 
 
+def test_host_pace_equals_serial(gpu, scene_small):
+    """host_pace (the host waits for frame f - K's SVGF before issuing frame f) changes only when the host issues:
+    the frames are the serial driver's bits, moving camera, no readback in between."""
+    gl = gpu
+    W, H = 96, 64
+    kw = dict(mode="fast", run_taa=False, run_output=False)
+    a = _renderer(scene_small, W, H, **kw)
+    b = _renderer(scene_small, W, H, frames_in_flight=3, host_pace=True, **kw)
+    for _ in range(8):
+        for r in (a, b):
+            r.camera.orbit(1.0, 0.0)
+            r.frame()
+    pa, pb = _readback(gl, a), _readback(gl, b)
+    for key in ("color", "modulate", "atrous"):
+        assert np.array_equal(pa[key].view(np.uint32), pb[key].view(np.uint32)), key
+    a.close()
+    b.close()
+
+
 def test_fast_atrous_within_tolerance(gpu, scene_small):
     """Production a-trous (hardware exp2/log2) vs the exact oracle on real frame data."""
     gl = gpu
