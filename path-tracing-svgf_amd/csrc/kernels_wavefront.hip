@@ -631,8 +631,11 @@ constexpr int kRefillRounds = PT_REFILL_ROUNDS, kRefillMin = PT_REFILL_MIN;
 // 367 -> 312 fps with R = 4 everywhere; with R from the length 380 fps at 1080p, 156.6 at 4K). kResidentWaves: 256 CUs
 // x 20 waves (86 VGPRs: 5 waves per SIMD). Estimates of 16 / 12 / 8 waves per CU (more rounds per wave) measured
 // 182.8 / 181.2 / 177.5 fps against 183.7 at 4K, the surface view unchanged (end of round 2).
+// Round 4: the refill kernels now run 8 waves per SIMD (32 per CU); re-measured with that occupancy, 26 per CU gave
+// 221.4 / 221.1 fps at 4K against 219.1 / 218.7 for 20 and 220.7 / 220.4 for 32, the surface view within noise
+// (profiles/r04/refill_waves_ab.log).
 #ifndef PT_RESIDENT_WAVES
-#define PT_RESIDENT_WAVES (256 * 20)
+#define PT_RESIDENT_WAVES (256 * 26)
 #endif
 constexpr int kResidentWaves = PT_RESIDENT_WAVES;
 #ifndef PT_REFILL_DIV
