@@ -360,7 +360,9 @@ class Renderer:
             # share of each bounce / shadow list traced by lane-refill waves (frames in flight only); with up to 12
             # chunk rounds per wave 75 / 85 / 90 / 95 % measured 183.1 / 184.3 / 183.7 / 183.9 fps at 4K and 57.2 / 58.7 /
             # 59.5 / 60.6 fps on the surface view, 1080p and 8 bands within noise (tools/refill_pct_sweep.sh)
-            p.set_uniform_int("trace_refill", 90 if self.K > 1 else 0)
+            # (round 4, 8 waves per SIMD, 26 resident waves per CU: 100 % gave 4K 220.9 / 221.2 against 221.4 / 220.3 for
+            # 90 and the surface view 74.4 / 74.2 against 71.3 / 72.1, profiles/r04/refill_pct_ab.log)
+            p.set_uniform_int("trace_refill", 100 if self.K > 1 else 0)
             # one frame at a time: the bounce-0 shadow walk on a side stream beside the bounce-1 closest-hit walk
             # (their launch tails overlap): 4K serial 131.3 -> 145.4 fps, surface view 48.3 -> 49.3; with frames in
             # flight the other frames already fill those tails (215.7 / 215.6 fps at K = 4, profiles/r04/fork/)
