@@ -23,8 +23,11 @@ every rank owns one horizontal band of the frame for the SVGF chain and exchange
 its halo rows with the other bands over RCCL (ptsvgf.dist); the G-buffer + path
 tracer of frame f run over the whole frame on rank f % N, which sends each band's
 rows of colour / emission / albedo to its owner (--shard frames, the default), or
-every rank traces its own band of every frame (--shard bands). Strong scaling:
-the frame sequence is fixed, N ranks render it together.
+every rank traces its own band of every frame (--shard bands), or the 16x16 tiles
+k*N + rank of every frame (--shard tiles). The frame sequence is fixed and N ranks
+render it together; "scaling" is "throughput" for --shard frames (frames/s scale,
+a frame's camera-to-modulate latency does not: see "latency") and "strong" for
+tiles / bands (every frame is split).
 """
 from __future__ import annotations
 
@@ -652,7 +655,10 @@ def main():
     if rank == 0:
         line = {"metric": METRIC, "value": round(fps, 3),
                 "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+                "ms_per_step": round(ms, 3), "higher_is_better": True, "vs_baseline": None,
+                # --shard frames: every rank traces whole frames, so frames/s scales but a frame's latency does not
+                # (the line's "latency"); tiles / bands split every frame (strong scaling)
+                "scaling": "throughput" if world > 1 and args.shard == "frames" else "strong",
                 "dtype": "f32", "data": "synthetic",
                 "config": {"workload": f"{args.scene} {W}x{H} 1spp depth2 + 5-iter SVGF"
                                        + (" moving camera" if args.moving else "")

@@ -148,14 +148,22 @@ class BandPlan:
 
     def set_motion(self, m: float) -> int:
         """This frame's all-reduced largest |motion.y| (UV) -> rows the history exchanges carry."""
-        n = motion_rows(m, self.H)
+        return self.set_rows(motion_rows(m, self.H))
+
+    def set_rows(self, n: int) -> int:
+        """Rows the history exchanges carry this frame (n = motion_rows of a bound on the frame's motion)."""
         # ghost zone: the reprojection's margin rows read the previous G-buffer's normal/depth n rows further out
         reach = n + (self.margins["reproject"] if self.margins is not None else 0)
         if reach > self.ghost:
             raise RuntimeError(f"the camera moved {n - REPROJ_REACH} rows in one frame; a band holds {self.ghost} "
                                f"ghost rows (history reach {reach}): build the band renderer with a larger ghost")
-        self.motion = n
-        return n
+        self.motion = int(n)
+        return self.motion
+
+    def capacity(self) -> int:
+        """The most history rows a frame can exchange: every ghost row the reprojection's taps may reach (a camera
+        moving capacity() - REPROJ_REACH rows or fewer per frame fits)."""
+        return self.ghost - (self.margins["reproject"] if self.margins is not None else 0)
 
     def stage_rows(self, stage: str) -> tuple:
         """Ghost zone: the rows the SVGF pass `stage` draws (the band widened by its margin, clipped to the frame)."""
@@ -307,12 +315,116 @@ def host_group(dist):
 
 
 def allreduce_motion(m: float, dist, group=None) -> float:
-    """MAX over ranks of the per-rank largest |motion.y| (host float)."""
+    """MAX over ranks of the per-rank largest |motion.y| (host float). (The CPU oracle tests size their halos with
+    it; the GPU band renderers use a bound the host already holds, MotionCheck, and no per-frame collective.)"""
     import torch
 
     t = torch.tensor([m], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
+
+
+def camera_moved(cam, pre_viewproj) -> bool:
+    """True unless this frame's projection * view equals the previous frame's pre_viewproj bit for bit. The G-buffer
+    kernel forms both clip positions of a surface point with the same float arithmetic from those two matrices
+    (kernels_pt.hip: motion = now - prev, capi.hip builds projection * view as camera.mat_mul does), so a camera that
+    did not move gives motion exactly 0 at every pixel."""
+    import numpy as np
+
+    from .camera import mat_mul
+
+    cur = mat_mul(cam.cam_proj_mat, cam.cam_view_mat)
+    return not np.array_equal(cur.view(np.uint32), np.asarray(pre_viewproj, np.float32).reshape(16).view(np.uint32))
+
+
+class MotionCheck:
+    """The history rows of each frame from a bound the host holds when it issues the frame's back end — no wait for
+    the G-buffer and no per-frame collective (round 4 synchronised on the G-buffer's motion bound and all-reduced it
+    over gloo on every frame, a host round trip on every rank's critical path):
+      * a camera that did not move (camera_moved False): motion is 0 at every pixel, the taps reach REPROJ_REACH rows;
+      * a moved camera: the plan's capacity() — every ghost row the taps can reach (a camera moving further than that
+        in one frame was already an error).
+    Every rank derives the same count from the same camera path, so the exchanges pair up without communicating. The
+    device bound the G-buffer kernel reduces (pt_pass_set_motion_bound) is still copied to pinned host memory behind
+    each G-buffer and checked later, once its copy has landed (poll; never waited for unless a ring slot comes round
+    again), against the rows the frame used: a frame whose motion exceeded them raises (verify) — the bound is
+    verified, not trusted."""
+
+    RING = 64
+
+    def __init__(self, plan: BandPlan):
+        import torch
+
+        self.plan = plan
+        self.host = torch.zeros(self.RING, dtype=torch.int32).pin_memory()
+        self.ev = [None] * self.RING
+        self.slot_frame = [None] * self.RING
+        self.pending = []   # ring slots with a copy in flight, capture order
+        self.moved = {}     # frame -> camera moved (host)
+        self.used = {}      # frame -> history rows its exchange carried
+        self.log = []       # (frame, rows the measured motion needs, rows used)
+
+    def note_camera(self, f: int, moved: bool) -> None:
+        self.moved[f] = bool(moved)
+
+    def capture(self, f: int, dev_word, stream) -> None:
+        """Copy frame f's device motion bound (its G-buffer wrote it on `stream`) to the host ring."""
+        import torch
+
+        j = f % self.RING
+        if self.slot_frame[j] is not None:
+            self._check(j, block=True)
+        with torch.cuda.stream(stream):
+            self.host[j:j + 1].copy_(dev_word, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        self.ev[j], self.slot_frame[j] = ev, f
+        self.pending.append(j)
+
+    def rows(self, f: int) -> int:
+        """History rows for frame f (host bound; plan.set_rows checks the ghost)."""
+        moved = self.moved.pop(f, True)
+        n = self.plan.capacity() if moved else REPROJ_REACH
+        self.used[f] = n
+        if len(self.used) > 2 * self.RING:  # frames whose bound another rank captures (shipped G-buffer)
+            for old in sorted(self.used)[:len(self.used) - self.RING]:
+                del self.used[old]
+        self.poll()
+        return n
+
+    def poll(self, block: bool = False) -> None:
+        """Check every captured bound whose copy has landed (block: wait for all of them)."""
+        keep = []
+        for j in self.pending:
+            f = self.slot_frame[j]
+            if f in self.used and (block or self.ev[j].query()):
+                self._check(j, block=block)
+            else:
+                keep.append(j)
+        self.pending = keep
+
+    def _check(self, j: int, block: bool) -> None:
+        import numpy as np
+
+        f, ev = self.slot_frame[j], self.ev[j]
+        if block:
+            ev.synchronize()
+        self.slot_frame[j] = self.ev[j] = None
+        if j in self.pending:
+            self.pending.remove(j)
+        n = self.used.pop(f, None)
+        if n is None:  # the frame's back end never exchanged a history (calibration frames, a renderer closed early)
+            return
+        m = float(self.host[j:j + 1].numpy().view(np.float32)[0])
+        need = motion_rows(m, self.plan.H)
+        self.log.append((f, need, n))
+        if need > n:
+            raise RuntimeError(f"frame {f}: the G-buffer's motion needs {need} history rows but {n} were exchanged "
+                               f"(camera moved without the host seeing it: pre_viewproj and projection * view disagree)")
+
+    def verify(self) -> None:
+        """Wait for every captured bound and check it (flush / close: the frames drawn so far)."""
+        self.poll(block=True)
 
 
 class _StageFilter:
@@ -366,6 +478,11 @@ class BandRenderer:
 
         kw.setdefault("run_taa", False)
         kw.setdefault("run_output", False)
+        # frames in flight: the host issues frame f once frame f - K's SVGF is done (Renderer host_pace), which frame
+        # f's front end waits for on the GPU anyway. The host no longer blocks on anything per frame otherwise
+        # (MotionCheck), so unpaced it would queue frames without bound and each camera would reach the GPU long
+        # before its frame's result
+        kw.setdefault("host_pace", True)
         # frames in flight: issue the back end one frame behind the front end, so the host's wait for the motion
         # bound (before the reprojection exchange) finds a G-buffer issued a frame earlier (Renderer back_lag)
         if kw.get("frames_in_flight", 1) > 1:
@@ -388,14 +505,13 @@ class BandRenderer:
             for p in self.r.init_pass:
                 p.set_uniform_int("atrous_rows_begin", a0)
                 p.set_uniform_int("atrous_rows_end", a1)
-        # per G-buffer set: the device motion bound the G-buffer kernel writes, its pinned host copy, an event
+        # per G-buffer set: the device motion bound the G-buffer kernel writes (checked later, MotionCheck)
         ng = len(self.r.gbuf)
         self._mb_dev = torch.zeros(ng, dtype=torch.int32, device=dev)
-        self._mb_host = torch.zeros(ng, dtype=torch.int32).pin_memory()
-        self._mb_event = [torch.cuda.Event() for _ in range(ng)]
         for b, p in enumerate(self.r.init_pass):
             p.set_motion_bound(self._mb_dev[b:b + 1].data_ptr())
-        self.motion_log = []  # per frame: (all-reduced |motion.y| in rows, history rows exchanged)
+        self.mcheck = MotionCheck(self.plan)
+        self._set_frame = {}  # G-buffer set -> the frame whose front end last used it
         self.camera = self.r.camera
         self.pass_path_tracing = self.r.pass_path_tracing
         if self.r.K > 1:
@@ -409,26 +525,31 @@ class BandRenderer:
             # (8 simulated bands, same box: slowest non-edge band 1.35 -> 1.27 ms, profiles/r03/band_sim_r03.log)
             self.pass_path_tracing.set_uniform_int("refill_waves", BAND_REFILL_WAVES)
 
-    def _after_gbuffer(self, b: int, stream) -> None:
-        """The G-buffer of set b was issued on `stream`: fetch its motion bound behind it (no wait here)."""
-        import torch
+    @property
+    def motion_log(self) -> list:
+        """Per checked frame: (history rows its measured motion needs, rows exchanged)."""
+        return [(need, n) for _, need, n in self.mcheck.log]
 
-        with torch.cuda.stream(stream):
-            self._mb_host[b:b + 1].copy_(self._mb_dev[b:b + 1], non_blocking=True)
-            self._mb_event[b].record(stream)
+    def _note_frame(self, b: int) -> None:
+        """Frame r.frame_index's front end uses G-buffer set b: remember whether its camera moved (host)."""
+        f = self.r.frame_index
+        self._set_frame[b] = f
+        self.mcheck.note_camera(f, camera_moved(self.r.camera, self.r.pre_viewproj))
+
+    def _after_gbuffer(self, b: int, stream) -> None:
+        """The G-buffer of set b was issued on `stream`: copy its motion bound to the host behind it (checked later)."""
+        self._note_frame(b)
+        self.mcheck.capture(self.r.frame_index, self._mb_dev[b:b + 1], stream)
 
     def _motion(self, b: int | None = None) -> int:
-        """History reach of the frame whose back end is being issued (or of G-buffer set b): wait for its G-buffer's
-        bound (issued with its front end, back_lag frames earlier), MAX over ranks on the host."""
-        import numpy as np
-
+        """History reach of the frame whose back end is being issued (or of G-buffer set b), from the bound the host
+        holds (MotionCheck: no wait, no collective)."""
         b = self.r.back_set if b is None else b
-        self._mb_event[b].synchronize()
-        m = float(self._mb_host[b:b + 1].numpy().view(np.float32)[0])
-        m = allreduce_motion(m, self.dist, self._group)
-        n = self.plan.set_motion(m)
-        self.motion_log.append((m * self.plan.H, n))
-        return n
+        return self.plan.set_rows(self.mcheck.rows(self._set_frame[b]))
+
+    def verify_motion(self) -> None:
+        """Check every frame's device motion bound against the history rows it exchanged (waits for the frames)."""
+        self.mcheck.verify()
 
     def _early_history(self, handles: dict, next_set) -> None:
         """Ghost zone, Renderer early_history: the a-trous iteration that writes the next frame's history has been
@@ -534,9 +655,12 @@ class BandRenderer:
         return self.plan.y1 - self.plan.y0
 
     def planes(self) -> dict:
-        return self.r.planes()
+        pl = self.r.planes()
+        self.verify_motion()
+        return pl
 
     def close(self) -> None:
+        self.verify_motion()  # the frames whose back end was issued
         self.r.close()
         self._tensors.clear()
 
@@ -608,8 +732,9 @@ def scatter_group(dist):
 
 
 def exchange_window(window, plan: BandPlan, dist, group=None, rows=None) -> int:
-    """The point-to-point transfers of one frame-shard window: consecutive frames, at most one per source rank (frame
-    f is traced by rank f % N). window = [(src, planes)]: for a frame this rank traced, planes are its whole-frame
+    """The point-to-point transfers of one frame-shard window: consecutive frames (frame f is traced by rank
+    (f // burst) % N, so a source holds up to min(burst, window) of them, each in its own slot). window = [(src,
+    planes)] in frame order: for a frame this rank traced, planes are its whole-frame
     (H, W, C) tensors and every other band's rows (plan.zone: the band, widened by the ghost zone's reprojection
     margin) go to that band's owner; for a frame rank src traced, planes are this band's zone rows, received from src. Every rank builds the same window, so the batch is symmetric: an
     all-to-all over the window's sources, every link busy at once, one communicator. rows[j](k) (default plan.zone):
@@ -671,7 +796,7 @@ class FrameShardRenderer(BandRenderer):
     GBUF_PLANES = (1, 2, 3)  # G-buffer attachments the SVGF chain reads: normal/depth, motion, depth-fwidth
 
     def __init__(self, scene, W, H, cfg, rank, world, dist, own_slots: int = 2, ship_gbuffer: bool | None = None,
-                 window: int | None = None, burst: int = 1, **kw):
+                 window: int | None = None, burst: int = 1, own_budget: int = 0, own_refill_waves: int = 0, **kw):
         """burst (default 1): consecutive frames one rank traces, frame f on rank (f // burst) % N. With 2 a rank's
         two path tracers are issued one frame apart and overlap (their launch tails fill each other's idle CUs, as frames
         in flight do on one GPU) instead of starting N frames apart.
@@ -687,7 +812,12 @@ class FrameShardRenderer(BandRenderer):
         instead of drawing its own. A band's G-buffer draw costs 0.06-0.25 ms per frame (the plant's rows dominate)
         against 0.01 for the adoption, for twice the window's bytes (≈ 150 MB per window and link at 8 ranks); the
         8-rank simulation measured it within noise (0.93-1.11 vs 0.90-0.99 ms per frame,
-        profiles/r03/frame_shard/fs_ship*.log), so it stays an option."""
+        profiles/r03/frame_shard/fs_ship*.log), so it stays an option.
+
+        own_budget / own_refill_waves (0: the one-GPU settings): the whole-frame path tracer's cooperative-walk visit
+        budget (shadow_budget / closest_budget) and the resident waves its lane-refill launches are sized for
+        (refill_waves) — the tail tools the band and tile renderers use; a rank's own frames are N frames apart, so
+        its path tracer runs nearly alone, as one frame at a time does on one GPU."""
         import torch
 
         from . import gl
@@ -700,6 +830,11 @@ class FrameShardRenderer(BandRenderer):
             raise ValueError(f"burst must be >= 1, got {burst}")
         if not 1 <= self.window <= world:
             raise ValueError(f"window must be in [1, {world}], got {window}")
+        # a window may hold min(burst, window) frames this rank traces; each needs its own slot until the window's
+        # exchange has sent it (_render_own waits only for the exchange that sent a slot's previous frame)
+        if max(2, int(own_slots)) < min(self.burst, self.window):
+            raise ValueError(f"own_slots = {own_slots} < min(burst, window) = {min(self.burst, self.window)}: a window "
+                             f"would reuse a slot whose frame it has not sent yet")
         kw.setdefault("back_lag", self.window)  # a frame's back end is issued after its window's exchange
         if K <= kw["back_lag"]:
             raise ValueError(f"FrameShardRenderer needs frames_in_flight > back_lag = {kw['back_lag']}, got {K}")
@@ -729,19 +864,21 @@ class FrameShardRenderer(BandRenderer):
             raise ValueError("ship_gbuffer needs the ghost zone")
         if self.ship_gbuffer:
             kw["draw_gbuffer"] = False
-            # the tracing rank's whole-frame G-buffer reduces the frame's motion bound (the bands draw none)
+            # the tracing rank's whole-frame G-buffer reduces the frame's motion bound (the bands draw none); that rank
+            # checks it against the rows every band exchanged (MotionCheck)
             nb = len(self.full.init_pass)
             self._fmb_dev = torch.zeros(nb, dtype=torch.int32, device=dev)
-            self._fmb_host = torch.zeros(nb, dtype=torch.int32).pin_memory()
-            self._fmb_event = [torch.cuda.Event() for _ in range(nb)]
             for b, p in enumerate(self.full.init_pass):
                 p.set_motion_bound(self._fmb_dev[b:b + 1].data_ptr())
-        self._set_frame = {}  # band G-buffer set -> the frame that last used it
-        self._own_mb = {}     # own frame -> its full G-buffer set (motion bound)
         super().__init__(scene, W, H, cfg, rank, world, dist, pt_source=self._pt_source, pt_flush=self._exchange,
                          **kw)
         self.full.camera = self.r.camera  # one camera: the full front end draws the band renderer's frame
         self.pass_path_tracing = self.full.pass_path_tracing
+        if own_budget > 0:
+            self.pass_path_tracing.set_uniform_int("shadow_budget", int(own_budget))
+            self.pass_path_tracing.set_uniform_int("closest_budget", int(own_budget))
+        if own_refill_waves > 0:
+            self.pass_path_tracing.set_uniform_int("refill_waves", int(own_refill_waves))
         self._sgroup = scatter_group(dist) if world > 1 else None
         self._recv_stream = acquire_stream()
         self.scatter_log = []  # per exchange that carried a frame of this rank: bytes sent
@@ -770,7 +907,8 @@ class FrameShardRenderer(BandRenderer):
             self._exchange()
         holder = {}
         gset = f % len(r.gbuf)
-        self._set_frame[gset] = f
+        if self.ship_gbuffer:  # (drawn G-buffers note their frame in _after_gbuffer)
+            self._note_frame(gset)
         item = dict(src=self.source(f), outs=[self._band_rows(h) for h in r.pt_slots[slot][1]],
                     free=r._slot_free[f % r.K], holder=holder, gset=gset)
         if self.ship_gbuffer:
@@ -814,24 +952,6 @@ class FrameShardRenderer(BandRenderer):
         r = self.r
         r._stream_to(stream)
         r.init_pass[gset].adopt(*self.plan.gbuffer_rows())
-
-    def _motion(self, b: int | None = None) -> int:
-        """Shipped G-buffer: the frame's motion bound comes from its tracing rank's whole-frame G-buffer (the bands
-        draw none): MAX over ranks of (that rank's bound, 0 elsewhere)."""
-        if not self.ship_gbuffer:
-            return super()._motion(b)
-        import numpy as np
-
-        f = self._set_frame[self.r.back_set if b is None else b]
-        m = 0.0
-        if self.source(f) == self.plan.rank:
-            o = self._own_mb.pop(f)
-            self._fmb_event[o].synchronize()
-            m = float(self._fmb_host[o:o + 1].numpy().view(np.float32)[0])
-        m = allreduce_motion(m, self.dist, self._group)
-        n = self.plan.set_motion(m)
-        self.motion_log.append((m * self.plan.H, n))
-        return n
 
     def _exchange(self) -> None:
         """Send / receive the rows of the registered window (every rank registers the same frames, so every rank
@@ -879,11 +999,8 @@ class FrameShardRenderer(BandRenderer):
         fr.pre_viewproj = self.r.pre_viewproj
         fr.frame_index = f
         fr._gbuffer(o)
-        if self.ship_gbuffer:  # the frame's motion bound, read by every rank's _motion through the all-reduce
-            with torch.cuda.stream(st):
-                self._fmb_host[o:o + 1].copy_(self._fmb_dev[o:o + 1], non_blocking=True)
-                self._fmb_event[o].record(st)
-            self._own_mb[f] = o
+        if self.ship_gbuffer:  # the whole frame's motion bound, checked here for every band (MotionCheck)
+            self.mcheck.capture(f, self._fmb_dev[o:o + 1], st)
         fr._path_trace(fr.gbuf[o])
         done = torch.cuda.Event()
         done.record(st)

@@ -17,6 +17,7 @@ TAA and the output tonemap run in both modes (main.cpp:537-590).
 from __future__ import annotations
 
 import os
+import time
 
 import numpy as np
 
@@ -178,6 +179,7 @@ class Renderer:
             raise ValueError(f"trace_batch must be in [1, min(frames_in_flight, 8)] (fast driver), got {trace_batch}")
         self.lag = max(int(back_lag), self.B - 1)
         self.host_pace = bool(host_pace) and self.K > 1
+        self.pace_wait_s = 0.0  # host time spent in host_pace's waits (diagnostics)
         if not 0 <= self.lag < self.K:
             raise ValueError(f"back_lag must be in [0, frames_in_flight) = [0, {self.K}), got {back_lag}")
         self._nfs = self.K if front_streams is None else int(front_streams)
@@ -830,7 +832,9 @@ class Renderer:
         """One iteration of main.cpp's while-loop body (436-602), headless (with back_lag D: this frame's front
         end and frame f - D's back end)."""
         if self.host_pace and self._slot_free[self.frame_index % self.K] is not None:
+            t0 = time.perf_counter()
             self._slot_free[self.frame_index % self.K].synchronize()  # before the camera is read (host_pace)
+            self.pace_wait_s += time.perf_counter() - t0
         self.camera.update()
         if self._serial_stream is not None:
             self._stream_to(self._serial_stream)

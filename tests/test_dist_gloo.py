@@ -236,6 +236,47 @@ def test_band_motion_beyond_ghost_raises():
     assert BandPlan(64, 600, 0, 2, ghost=128, iterations=6).nd_rows == 64
 
 
+def test_host_motion_bound_rows():
+    """MotionCheck's host bound: a static camera reaches REPROJ_REACH rows, a moved one the plan's capacity (every ghost
+    row the taps can reach); camera_moved compares the matrices bit for bit, as the G-buffer kernel's arithmetic does."""
+    import numpy as np
+
+    from ptsvgf.camera import Camera, mat_mul
+    from ptsvgf.dist import GHOST_ZONE_GHOST, REPROJ_REACH, BandPlan, camera_moved, svgf_margins
+    p = BandPlan(64, 400, 0, 2, ghost=40)
+    assert p.capacity() == 40 and p.set_rows(p.capacity()) == 40
+    gz = BandPlan(3840, 2160, 3, 8, ghost=GHOST_ZONE_GHOST, margins=svgf_margins(5, False))
+    assert gz.capacity() == GHOST_ZONE_GHOST - gz.margins["reproject"] == 63
+    assert gz.set_rows(gz.capacity()) == 63
+    with pytest.raises(RuntimeError):
+        gz.set_rows(64)
+    assert gz.set_rows(REPROJ_REACH) == REPROJ_REACH
+    cam = Camera(64, 48)
+    cam.update()
+    pre = mat_mul(cam.cam_proj_mat, cam.cam_view_mat)
+    assert not camera_moved(cam, pre)
+    cam.update()  # recomputing the same camera gives the same bits
+    assert not camera_moved(cam, pre)
+    cam.orbit(0.01, 0.0)
+    cam.update()
+    assert camera_moved(cam, pre)
+    pre2 = pre.copy()
+    pre2[5] = np.nextafter(pre2[5], np.float32(2))  # one ulp of one entry is a move
+    cam2 = Camera(64, 48)
+    cam2.update()
+    assert camera_moved(cam2, pre2)
+
+
+def test_frame_shard_burst_needs_own_slots():
+    """ADVICE r04: a window holding more of one rank's frames than it has own slots would overwrite an unsent frame;
+    the constructor refuses before touching the GPU."""
+    from ptsvgf.camera import parameter_config
+    from ptsvgf.dist import FrameShardRenderer
+    with pytest.raises(ValueError, match="own_slots"):
+        FrameShardRenderer(None, 64, 64, parameter_config(), 0, 4, None, own_slots=2, window=4, burst=3,
+                           frames_in_flight=8)
+
+
 def test_halo_intervals_cover_exactly_what_is_read():
     """need()/owned() bookkeeping: for every rank pair the rows sent equal the rows received, and the union of what
     a rank receives is exactly its n-row halo (minus frame edges)."""

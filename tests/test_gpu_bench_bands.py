@@ -79,21 +79,22 @@ def test_bench_band_parity_gloo(world, moving, balance, shard):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("W,H", [(1920, 1080), (3840, 2160)])
-def test_bench_frame_shard_8_ranks_gloo(W, H):
+@pytest.mark.parametrize("W,H,balance", [(1920, 1080, False), (3840, 2160, False), (1920, 1080, True)])
+def test_bench_frame_shard_8_ranks_gloo(W, H, balance):
     """the default multi-GPU mode (--shard frames: rank f % 8 traces frame f whole, the SVGF chain
     banded with the ghost zone and the early history exchange) at the BASELINE sizes and rank count — 8 ranks, 1920 x
     1080 (configs[1]) and 3840 x 2160 (configs[3] / [4]), a moving camera, frames_in_flight and the exchange window at
     their 8-rank defaults (16 band slots, window = back_lag 4) — rehearsed with gloo on the one GPU (4K: ≈ 30 s). 16 timed frames = 4 full windows of 4 after the warm-up's windows; the gathered bands must
     equal a one-GPU render of the same camera path bit for bit (reference: main.cpp:436-535 per frame,
-    svgf_Atrous.frag:92-97 and svgf_reproject.frag:45-156 for what crosses bands). Equal bands: the calibration only
-    moves the bounds, which the 3-rank balanced case above covers."""
+    svgf_Atrous.frag:92-97 and svgf_reproject.frag:45-156 for what crosses bands). balance: the bench's exact 8-rank
+    default, balanced bands calibrated by make_frame_shard_renderer (round 4's rank-disagreement bug
+    lived in that calibration path, dist.agree_bounds)."""
     world = 8
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "bench.py"),
            "--gpus", str(world), "--backend", "gloo", "--width", str(W), "--height", str(H), "--steps", "16",
-           "--warmup", "2", "--no-extras", "--no-1080p", "--no-cpu-baseline", "--shard", "frames", "--moving",
-           "--equal-bands"]
+           "--warmup", "2", "--no-extras", "--no-1080p", "--no-cpu-baseline", "--shard", "frames", "--moving"]
+    cmd += [] if balance else ["--equal-bands"]
     p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=850)
     assert p.returncode == 0, p.stderr[-4000:]
     line = json.loads(p.stdout.strip().splitlines()[-1])
@@ -105,3 +106,11 @@ def test_bench_frame_shard_8_ranks_gloo(W, H):
     assert bp["backend"] == "gloo" and bp["frames"] >= 2 * world + 16  # warm-up windows + 4 timed windows + probes
     assert bp["bit_exact"], bp
     assert line.get("max_history_rows", 0) > 3  # the orbit moved the history (reprojection reach beyond the taps)
+    assert line["scaling"] == "throughput"  # whole frames per rank: frames/s scale, a frame's latency does not
+    equal = [(H * k) // world for k in range(world + 1)]
+    if balance:
+        # make_frame_shard_renderer measured its rounds (equal bands first) and every rank holds rank 0's choice
+        assert len(bands["calibration"]) == 3 and bands["calibration"][0][1] == equal, bands
+        assert bands["bounds"] in [b for _, b in bands["calibration"]], bands
+    else:
+        assert bands["bounds"] == equal

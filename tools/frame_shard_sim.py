@@ -40,7 +40,8 @@ SHARD = os.environ.get("SHARD", "frames")
 
 
 class FakeDist:
-    """Stands in for torch.distributed: this rank's own motion bound is the all-reduced one."""
+    """Stands in for torch.distributed (the frame loop itself makes no host collective since round 5: the history rows
+    come from the host's own bound, dist.MotionCheck; calibration all-reduces are no-ops here)."""
     class ReduceOp:
         MAX = "max"
 
@@ -188,7 +189,10 @@ def sim_rank(rk, bounds=None):
         LOG[k] = 0
     r.r.back_events = []
     r.r.latency_events = []
-    waits = []  # host time blocked on the G-buffer motion bound (BandRenderer._motion): the GPU being full
+    # host time in BandRenderer._motion (round 4: a wait for the G-buffer's bound + the per-frame all-reduce; round 5:
+    # the host's own bound, MotionCheck) and in the host pacing (Renderer host_pace: frame f waits for SVGF(f - K))
+    waits = []
+    pace0 = r.r.pace_wait_s
     orig_motion = D.BandRenderer._motion
 
     def timed_motion(self, *a):
@@ -205,6 +209,7 @@ def sim_rank(rk, bounds=None):
     cpu = (time.process_time() - c0) / FRAMES
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / FRAMES
+    pace = (r.r.pace_wait_s - pace0) / FRAMES
     D.BandRenderer._motion = orig_motion
     r.r.flush()
     torch.cuda.synchronize()
@@ -221,7 +226,7 @@ def sim_rank(rk, bounds=None):
     pp = r.pass_times()
     r.profile(False)
     out = dict(rows=(r.plan.y0, r.plan.y1), wall=wall * 1e3, issue=issue * 1e3, cpu=cpu * 1e3, back=busy,
-               wait=sum(waits) / FRAMES * 1e3, pp={k: v / N for k, v in pp.items()}, latency=lat,
+               wait=sum(waits) / FRAMES * 1e3, pace=pace * 1e3, pp={k: v / N for k, v in pp.items()}, latency=lat,
                halo_mb=LOG["halo"] / FRAMES / 1e6, send_mb=LOG["send"] / FRAMES / 1e6,
                recv_mb=LOG["recv"] / FRAMES / 1e6)
     r.close()
@@ -238,7 +243,7 @@ def report(tag, ranks, bounds):
         s = sim_rank(rk, bounds)
         res.append(s)
         print(f"rank {rk}: rows {s['rows'][0]}..{s['rows'][1]} wall {s['wall']:.3f} ms/frame ({1e3 / s['wall']:.1f} fps) "
-              f"issue {s['issue']:.3f} (host cpu {s['cpu']:.3f}, motion wait {s['wait']:.3f})  SVGF stream busy {s['back']:.3f} ms/frame  per frame: "
+              f"issue {s['issue']:.3f} (host cpu {s['cpu']:.3f}, motion {s['wait']:.3f}, pace wait {s['pace']:.3f})  SVGF stream busy {s['back']:.3f} ms/frame  per frame: "
               f"halo {s['halo_mb']:.2f} MB, sent {s['send_mb']:.1f} MB, received {s['recv_mb']:.1f} MB; camera-to-modulate "
               f"{s['latency']:.2f} ms = {s['latency'] / s['wall']:.1f} frames", flush=True)
         print("   passes alone, ms per frame: " + " ".join(f"{k} {v:.3f}" for k, v in sorted(s["pp"].items())),

@@ -6,7 +6,8 @@
 #   "bench TAG [bench args]"    bench.py -> gpurun_out/TAG.json (+ .err)
 #   "profile NAME"              tools/gpu_profile.sh NAME (env FIF, VIEW, PASSES as that script reads them)
 #   "ab UNIFORM V0 V1 [...]"    tools/uniform_ab_views.sh (same-box A/B of a path-tracer uniform, both views)
-#   "py SCRIPT [args]"          any python tool under tools/ (e.g. frame_shard_sim.py)
+#   "py [K=V ...] SCRIPT [args]" any python tool under tools/ (e.g. frame_shard_sim.py); leading K=V words are exported
+#                               for that step only
 # Every step runs under its own time limit (STEP_TIMEOUT, default 900 s) and the session stops at the first failure
 # (no GPU step after a fault, abort, time limit or hang: the script exits with that step's status).
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -35,7 +36,9 @@ for step in "$@"; do
     ab)
       timeout -k 10 "$T" bash tools/uniform_ab_views.sh "${args[@]}"; rc=$? ;;
     py)
-      timeout -k 10 "$T" python -u "tools/${args[0]}" "${args[@]:1}" > "gpurun_out/${TAG}_py$n.log" 2>&1
+      envs=()
+      while [[ ${#args[@]} -gt 0 && "${args[0]}" == *=* ]]; do envs+=("${args[0]}"); args=("${args[@]:1}"); done
+      timeout -k 10 "$T" env "${envs[@]}" python -u "tools/${args[0]}" "${args[@]:1}" > "gpurun_out/${TAG}_py$n.log" 2>&1
       rc=$?; tail -20 "gpurun_out/${TAG}_py$n.log" ;;
     *) echo "unknown step kind '$kind'"; exit 2 ;;
   esac
