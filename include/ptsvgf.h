@@ -101,7 +101,9 @@ int pt_program_create(const char* frag_path, const char* vert_path, uint32_t* ou
 int pt_texture2d_create(int width, int height, uint32_t* out_tex);                 /* RGBA32F, zeroed */
 int pt_texture2d_upload(uint32_t tex, int width, int height, uint32_t fmt,         /* PT_RGB32F | PT_RGBA32F */
                         const float* host_data);
-int pt_texture2d_wrap(void* device_ptr, int width, int height, uint32_t* out_tex); /* RGBA32F, not owned */
+int pt_texture2d_wrap(void* device_ptr, int width, int height, uint32_t* out_tex); /* RGBA32F, not owned;
+    the library does not see writes to wrapped memory: a wrapped hdrMap / hdrCache whose contents change must be
+    wrapped again (a new handle) for the path tracer's merged environment to be rebuilt */
 int pt_texbuffer_create(const void* host_data, size_t bytes, uint32_t fmt, uint32_t* out_tex); /* RGB32F */
 /* GPU BVH builder for dynamic scenes. The reference builds once on the host
  * (buildBVHwithSAH, Utils/BVH.h:42-173, main.cpp:88-96) and encodes triangles and nodes (main.cpp:101-151);

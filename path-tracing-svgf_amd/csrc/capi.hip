@@ -1221,7 +1221,15 @@ int pt_params(Pass* p, PTParams& k, SceneGPU*& sg) {
   // A/B switch hdr_merge (default 1): the NEE's radiance and pdf fetches at one direction from one merged texture
   if (ui(p, "hdr_merge", 1) && hm != hc && hm->W == hc->W && hm->H == hc->H && hm->target == PT_TEXTURE_2D &&
       hc->target == PT_TEXTURE_2D && hm->rows == hm->H && hc->rows == hc->H) {
+    // Built on the draw's stream, but read by the path tracers of every frame in flight on other streams: a rebuild
+    // (first bind, an uploaded hdrMap / hdrCache, a new size) first waits for the whole device (no draw still reads the
+    // old contents) and then for itself (no draw reads a half-written buffer). Rebuilds are rare: binds, uploads.
+    // Staleness follows Texture::version, which uploads bump; a texture wrapped around external device memory
+    // (pt_texture2d_wrap) is not tracked, so new contents there must be re-bound (a new handle) to be merged.
     HdrMerged& m = g.hdr_merged[{hmh, hch}];
+    const bool stale = !m.buf || m.W != hm->W || m.H != hm->H || m.hdr_dev != hm->dev || m.cache_dev != hc->dev ||
+                       m.vh != hm->version || m.vc != hc->version;
+    if (stale && m.buf) HIPCHK(hipDeviceSynchronize());
     if (!m.buf || m.W != hm->W || m.H != hm->H) {
       if (m.buf) (void)hipFree(m.buf);
       m = HdrMerged{};
@@ -1229,9 +1237,10 @@ int pt_params(Pass* p, PTParams& k, SceneGPU*& sg) {
       m.W = hm->W;
       m.H = hm->H;
     }
-    if (m.hdr_dev != hm->dev || m.cache_dev != hc->dev || m.vh != hm->version || m.vc != hc->version) {
+    if (stale) {
       const int rc = ptk::launch_hdr_merge((const float4*)hm->dev, (const float4*)hc->dev, m.buf, m.W * m.H, g.stream);
       if (rc) return hip_err((hipError_t)rc, "hdr merge");
+      HIPCHK(hipStreamSynchronize(g.stream));
       m.hdr_dev = hm->dev;
       m.cache_dev = hc->dev;
       m.vh = hm->version;
@@ -1305,7 +1314,11 @@ int pt_wf_setup(Pass* p, PTParams& k, SceneGPU* sg, const WFState& st) {
 }
 
 // The side stream and events of path-tracing draws issued on `s` (uniform trace_fork = 1), created on first use: one
-// per draw stream, so frames in flight on different streams do not queue behind each other's shadow walks.
+// per draw stream, so frames in flight on different streams do not queue behind each other's shadow walks. Entries
+// live until pt_shutdown: the map holds one entry per stream that ever drew with trace_fork, which the host's stream
+// pool bounds (ptsvgf.renderer.acquire_stream recycles streams; torch never destroys them). A handle reused by a new
+// stream after its old stream was destroyed finds the old entry, which stays correct: the side stream is the library's
+// own, and both events are re-recorded on every draw before they are waited on.
 const ptk::WfFork* wf_fork(Pass* p, hipStream_t s, int* rc) {
   *rc = PT_OK;
   if (!ui(p, "trace_fork", 0)) return nullptr;

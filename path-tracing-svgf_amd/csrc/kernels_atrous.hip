@@ -103,10 +103,38 @@ __global__ void __launch_bounds__(256) atrous_fast_kernel(AtrousParams p) {
 // exponent. Border blocks run the checked path with the same arithmetic.
 typedef float f2v __attribute__((ext_vector_type(2)));
 
+// Luminance (svgf_Atrous.frag:57-59) of a tap's illumination, and the tap's luminance term |lp - lc| * kL: the
+// tiled kernels of steps 1-4 (tile_stage_lum) stage lp per texel in LDS, so a tap's term is ONE FMA,
+// |fma(lp, kL, -(lc * kL))|, instead of deriving it in each of up to 24 taps; the other steps keep the prescaled form
+// |fma(z, wLb, fma(y, wLg, fma(x, wLr, -(lc * kL))))| (3 FMAs, no staged plane). The step kernel uses each step's form,
+// so the tiled kernels stay bit-identical to it.
+__device__ __forceinline__ float tap_luminance(float4 ip) {
+  return __builtin_fmaf(0.0721f, ip.z, __builtin_fmaf(0.7154f, ip.y, 0.2125f * ip.x));
+}
+template <int S> constexpr bool tile_stage_lum() { return S <= 4; }
+
+struct LumTerm {
+  float lc, kL, cL, wLr, wLg, wLb;
+  __device__ __forceinline__ void init(float4 ic, float kL_) {
+    lc = tap_luminance(ic);
+    kL = kL_;
+    cL = -(lc * kL);
+    wLr = 0.2125f * kL;
+    wLg = 0.7154f * kL;
+    wLb = 0.0721f * kL;
+  }
+  // lp - lc scaled by kL (its absolute value is the tap's term); LUM: lp given
+  template <bool LUM>
+  __device__ __forceinline__ float scaled(float4 ip, float lp) const {
+    if (LUM) return __builtin_fmaf(lp, kL, cL);
+    return __builtin_fmaf(ip.z, wLb, __builtin_fmaf(ip.y, wLg, __builtin_fmaf(ip.x, wLr, cL)));
+  }
+};
+
 struct AtrousCentre {
   float4 ic, nd;
-  float wLr, wLg, wLb, cL;      // kL * luminance weights, -(lc * kL)
-  float lc, kD1, kD2, kD4, kD5, kD8, phiN;
+  LumTerm lum;
+  float kD1, kD2, kD4, kD5, kD8, phiN;
 };
 
 // The 24 taps of one pixel. FLAT: phiIllumination == 0 (variance <= -1e-10 or NaN),
@@ -138,13 +166,13 @@ __device__ __forceinline__ void atrous_taps(const AtrousParams& p, const AtrousC
       const float4 q = Nr[px];
       const float dn = fminf(fmaxf(__builtin_fmaf(c.nd.z, q.z, __builtin_fmaf(c.nd.y, q.y, c.nd.x * q.x)), 0.0f),
                              1.0f);
+      constexpr bool LUM = tile_stage_lum<S>();
       float a;
       if (FLAT) {
-        const float lp = (0.2125f * ip.x + 0.7154f * ip.y) + 0.0721f * ip.z;
-        a = lp == c.lc ? fabsf(c.nd.w - q.w) * kDl : __builtin_inff();
+        a = tap_luminance(ip) == c.lum.lc ? fabsf(c.nd.w - q.w) * kDl : __builtin_inff();
       } else {
-        const float tl = __builtin_fmaf(ip.z, c.wLb, __builtin_fmaf(ip.y, c.wLg, __builtin_fmaf(ip.x, c.wLr, c.cL)));
-        a = __builtin_fmaf(fabsf(c.nd.w - q.w), kDl, fabsf(tl));
+        const float lp = LUM ? tap_luminance(ip) : 0.0f;
+        a = __builtin_fmaf(fabsf(c.nd.w - q.w), kDl, fabsf(c.lum.scaled<LUM>(ip, lp)));
       }
       const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(c.phiN, __builtin_amdgcn_logf(dn), -a)) * kern;
       sumW += w;
@@ -167,15 +195,9 @@ __device__ __forceinline__ void atrous_pixel(const AtrousParams& p, int x, int y
     return;
   }
   const float LOG2E = 1.4426950408889634f;
-  c.lc = (0.2125f * c.ic.x + 0.7154f * c.ic.y) + 0.0721f * c.ic.z;
   const float phiL = p.phi_color * __builtin_sqrtf(fmaxf(0.0f, 1e-10f + c.ic.w));
   const float fwz = p.fwidth.aux ? fabsf(p.fwidth.aux[(size_t)ly * W + x]) : p.fwidth.p[(size_t)ly * W + x].y;
-  const float kL = LOG2E / phiL;
-  // |lc - lp| * kL = |lp*kL - lc*kL|: luminance weights pre-scaled, centre folded into the first FMA
-  c.wLr = 0.2125f * kL;
-  c.wLg = 0.7154f * kL;
-  c.wLb = 0.0721f * kL;
-  c.cL = -(c.lc * kL);
+  c.lum.init(c.ic, LOG2E / phiL);  // |lc - lp| * kL = |lp * kL - lc * kL|
   const float kD = LOG2E / (fmaxf(fwz, 1e-8f) * (float)S);
   // kD / |offset| for |offset|^2 = 1, 2, 4, 5, 8
   c.kD1 = kD;
@@ -238,6 +260,10 @@ __global__ void __launch_bounds__(256) atrous_step_kernel(AtrousParams p) {
 // 100 -> 91.5 us on the 4K bench inputs, tools/exp_atrous_real.hip), the other steps are fastest with NX = 1.
 template <int S> constexpr int tile_nx() { return atrous_tile_nx(S); }
 template <int S> constexpr int tile_tj() { return atrous_tile_tj(S); }  // tile rows = waves per 64-column strip
+// tile_stage_lum: stage every texel's luminance beside it (4 B more LDS per staged texel and 3 VALU per staged texel,
+// against 2 VALU per tap: each staged texel serves up to 24 taps). Steps 8 and 16 keep the prescaled per-tap form:
+// their tiles are the widest (C = 64 NX + 4S columns), and the extra plane would cost them a resident block per CU
+// (S = 8: 36.9 -> 41.5 KB, 4 -> 3 blocks; S = 16: 73.8 -> 83 KB, 2 -> 1).
 
 __device__ __forceinline__ bool aux_flag(float a) { return (__float_as_uint(a) >> 31) != 0; }
 
@@ -245,33 +271,29 @@ __device__ __forceinline__ bool aux_flag(float a) { return (__float_as_uint(a) >
 // order, so every tiled form is bit-identical to the step kernel). FLAT: phiIllumination == 0 (see atrous_taps).
 struct TapPixel {
   float4 nd;
-  float lc, wLr, wLg, wLb, cL, sumW;
+  LumTerm lum;
+  float sumW;
   float kDr[5];
   f2v s01, s23;
   bool flat;
   __device__ __forceinline__ void init(float4 ic, float4 nd_, float fwz, float phi_color, int S) {
     const float LOG2E = 1.4426950408889634f;
     nd = nd_;
-    lc = (0.2125f * ic.x + 0.7154f * ic.y) + 0.0721f * ic.z;
     const float phiL = phi_color * __builtin_sqrtf(fmaxf(0.0f, 1e-10f + ic.w));
     flat = !(phiL > 0.0f);
-    const float kL = LOG2E / phiL;
+    lum.init(ic, LOG2E / phiL);
     const float kD = LOG2E / (fmaxf(fwz, 1e-8f) * (float)S);
     kDr[0] = kD;
     kDr[1] = kD * 0.70710678f;
     kDr[2] = kD * 0.5f;
     kDr[3] = kD * 0.44721360f;
     kDr[4] = kD * 0.35355339f;
-    wLr = 0.2125f * kL;
-    wLg = 0.7154f * kL;
-    wLb = 0.0721f * kL;
-    cL = -(lc * kL);
     sumW = 1.0f;
     s01 = f2v{ic.x, ic.y};
     s23 = f2v{ic.z, ic.w};
   }
-  template <bool FLAT>
-  __device__ __forceinline__ void tap(float4 ip, float4 q, int xx, int yy, float phi_normal) {
+  template <bool FLAT, bool LUM>
+  __device__ __forceinline__ void tap(float4 ip, float4 q, float lp, int xx, int yy, float phi_normal) {
     const int r2 = xx * xx + yy * yy;
     const float kDl = r2 == 1 ? kDr[0] : r2 == 2 ? kDr[1] : r2 == 4 ? kDr[2] : r2 == 5 ? kDr[3] : kDr[4];
     const int ax = xx < 0 ? -xx : xx, ay = yy < 0 ? -yy : yy;
@@ -280,11 +302,9 @@ struct TapPixel {
     const float dn = fminf(fmaxf(__builtin_fmaf(nd.z, q.z, __builtin_fmaf(nd.y, q.y, nd.x * q.x)), 0.0f), 1.0f);
     float a;
     if (FLAT) {
-      const float lp = (0.2125f * ip.x + 0.7154f * ip.y) + 0.0721f * ip.z;
-      a = lp == lc ? fabsf(nd.w - q.w) * kDl : __builtin_inff();
+      a = (LUM ? lp : tap_luminance(ip)) == lum.lc ? fabsf(nd.w - q.w) * kDl : __builtin_inff();
     } else {
-      const float tl = __builtin_fmaf(ip.z, wLb, __builtin_fmaf(ip.y, wLg, __builtin_fmaf(ip.x, wLr, cL)));
-      a = __builtin_fmaf(fabsf(nd.w - q.w), kDl, fabsf(tl));
+      a = __builtin_fmaf(fabsf(nd.w - q.w), kDl, fabsf(lum.scaled<LUM>(ip, lp)));
     }
     const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(phi_normal, __builtin_amdgcn_logf(dn), -a)) * kern;
     sumW += w;
@@ -292,10 +312,10 @@ struct TapPixel {
     s23 = __builtin_elementwise_fma(f2v{w, w * w}, f2v{ip.z, ip.w}, s23);
   }
   // the 24 taps of a window whose top-left texel is Li / Ln (row stride C, column step S); EDGE: skip taps outside
-  // the frame for the pixel at (x, y)
-  template <bool FLAT, bool EDGE, int S, int C>
-  __device__ __forceinline__ void window(const float4* Li, const float4* Ln, int x, int y, int W, int H,
-                                         float phi_normal) {
+  // the frame for the pixel at (x, y). Ll: the staged luminance of the texels (null: derived per tap)
+  template <bool FLAT, bool EDGE, int S, int C, bool LUM>
+  __device__ __forceinline__ void window(const float4* Li, const float4* Ln, const float* Ll, int x, int y, int W,
+                                         int H, float phi_normal) {
 #pragma unroll
     for (int yy = -2; yy <= 2; ++yy) {
       if (EDGE && (y + yy * S < 0 || y + yy * S >= H)) continue;
@@ -304,7 +324,7 @@ struct TapPixel {
         if (xx == 0 && yy == 0) continue;
         if (EDGE && (x + xx * S < 0 || x + xx * S >= W)) continue;
         const int o = (yy + 2) * C + (xx + 2) * S;
-        tap<FLAT>(Li[o], Ln[o], xx, yy, phi_normal);
+        tap<FLAT, LUM>(Li[o], Ln[o], LUM ? Ll[o] : 0.0f, xx, yy, phi_normal);
       }
     }
   }
@@ -338,8 +358,10 @@ template <int S, bool AUX>
 __global__ void __launch_bounds__(64 * tile_tj<S>() * tile_nx<S>()) atrous_tile_kernel(AtrousParams p) {
   constexpr int NX = tile_nx<S>();
   constexpr int TJ = tile_tj<S>(), NW = TJ * NX, R = TJ + 4, C = 64 * NX + 4 * S, NT = 64 * NW;
+  constexpr bool LUM = tile_stage_lum<S>();
   __shared__ float4 LI[R * C];
   __shared__ float4 LN[R * C];
+  __shared__ float LL[LUM ? R * C : 1];
   const int W = p.illum.W, row0 = p.illum.row0;
   const float4* __restrict__ I = p.illum.p;
   const float4* __restrict__ ND = p.nd.p;
@@ -396,13 +418,16 @@ __global__ void __launch_bounds__(64 * tile_tj<S>() * tile_nx<S>()) atrous_tile_
     gy = gy < lo ? lo : (gy > hi ? hi : gy);
     gx = gx < 0 ? 0 : (gx >= p.W ? p.W - 1 : gx);
     const size_t gi = (size_t)(gy - row0) * W + gx;
-    LI[e] = I[gi];
+    const float4 v = I[gi];
+    LI[e] = v;
     LN[e] = ND[gi];
+    if (LUM) LL[e] = tap_luminance(v);
   }
   __syncthreads();
   if (!own) return;
   const float4* Li = LI + j * C + xl;  // top-left tap of this pixel's window
   const float4* Ln = LN + j * C + xl;
+  const float* Ll = LL + (LUM ? j * C + xl : 0);
   const float4 ic = Li[2 * C + 2 * S];
   float4* out = p.out.p + ci;
   if (bg) {
@@ -418,10 +443,10 @@ __global__ void __launch_bounds__(64 * tile_tj<S>() * tile_nx<S>()) atrous_tile_
   // compiler schedules freely (LDS reads of later taps issued ahead of earlier taps' arithmetic). A per-tap `edge`
   // test in that path compiles to an exec-masked branch per tap, each behind its own LDS wait (the r02 kernel).
   if (__builtin_expect(!px.flat, 1)) {
-    if (__builtin_expect(!edge, 1)) px.window<false, false, S, C>(Li, Ln, x, y, p.W, p.H, p.phi_normal);
-    else px.window<false, true, S, C>(Li, Ln, x, y, p.W, p.H, p.phi_normal);
+    if (__builtin_expect(!edge, 1)) px.window<false, false, S, C, LUM>(Li, Ln, Ll, x, y, p.W, p.H, p.phi_normal);
+    else px.window<false, true, S, C, LUM>(Li, Ln, Ll, x, y, p.W, p.H, p.phi_normal);
   } else {
-    px.window<true, true, S, C>(Li, Ln, x, y, p.W, p.H, p.phi_normal);  // FLAT: rare
+    px.window<true, true, S, C, LUM>(Li, Ln, Ll, x, y, p.W, p.H, p.phi_normal);  // FLAT: rare
   }
   const float4 r = px.result();
   *out = r;
