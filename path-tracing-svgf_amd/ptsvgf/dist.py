@@ -51,7 +51,8 @@ TAA_NEIGHBOURS = 2  # rows of the TAA 3x3 neighbourhood: +-1 texel, plus the LIN
 GHOST = 96        # default stored rows either side of a band (storage only); motion up to GHOST - 3 rows per frame
 GHOST_ZONE_GHOST = 128  # ghost zone: storage for 65 margin rows + up to 63 rows of history reach per frame
 MIN_BAND_ROWS = 16
-BAND_VISIT_BUDGET = 256  # shadow / closest-hit visits before a band's ray goes to the cooperative walk
+BAND_VISIT_BUDGET = 256  # shadow / closest-hit visits before a band's ray goes to the cooperative walk (the renderer's
+                         # default since round 5, renderer.VISIT_BUDGET)
 BAND_REFILL_WAVES = 1280  # resident waves a band's lane-refill launch is sized for (the chip: 5120)
 
 # stage -> ((plane, rows), ...) exchanged before that stage; rows: int, or "reproj" / "reproj_nd" (set from this
@@ -814,10 +815,12 @@ class FrameShardRenderer(BandRenderer):
         8-rank simulation measured it within noise (0.93-1.11 vs 0.90-0.99 ms per frame,
         profiles/r03/frame_shard/fs_ship*.log), so it stays an option.
 
-        own_budget / own_refill_waves (0: the one-GPU settings): the whole-frame path tracer's cooperative-walk visit
-        budget (shadow_budget / closest_budget) and the resident waves its lane-refill launches are sized for
-        (refill_waves) — the tail tools the band and tile renderers use; a rank's own frames are N frames apart, so
-        its path tracer runs nearly alone, as one frame at a time does on one GPU."""
+        own_budget / own_refill_waves (0: the one-GPU settings, renderer.VISIT_BUDGET and the whole chip): the
+        whole-frame path tracer's cooperative-walk visit budget (shadow_budget / closest_budget) and the resident waves
+        its lane-refill launches are sized for (refill_waves) — the tail tools; a rank's own frames are N frames apart,
+        so its path tracer runs nearly alone, as one frame at a time does on one GPU (8-rank simulation, window 4, K 16:
+        0.962 ms equal bands without budgets, 0.913 balanced with them; K 24 balanced 0.890 / 0.887 without / with,
+        profiles/r05/shard/)."""
         import torch
 
         from . import gl

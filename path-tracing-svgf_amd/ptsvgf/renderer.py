@@ -27,6 +27,7 @@ from .gl import GL_TEXTURE_2D, GL_TEXTURE_2D_ARRAY, GL_TEXTURE_BUFFER, RenderPas
 from .scene import Scene
 
 SHADERS = "./shaders/"
+VISIT_BUDGET = 256  # node + triangle visits before a ray goes to the wave-cooperative walk (_ensure_slots)
 
 
 def _prog(frag: str, vert: str = "vert.vert") -> int:
@@ -364,11 +365,18 @@ class Renderer:
             # 59.5 / 60.6 fps on the surface view, 1080p and 8 bands within noise (tools/refill_pct_sweep.sh)
             # (round 4, 8 waves per SIMD, 26 resident waves per CU: 100 % gave 4K 220.9 / 221.2 against 221.4 / 220.3 for
             # 90 and the surface view 74.4 / 74.2 against 71.3 / 72.1, profiles/r04/refill_pct_ab.log)
-            p.set_uniform_int("trace_refill", 100 if self.K > 1 else 0)
+            # (round 5: also one frame at a time, now that the visit budgets below cut the refill waves' tails)
+            p.set_uniform_int("trace_refill", 100)
             # one frame at a time: the bounce-0 shadow walk on a side stream beside the bounce-1 closest-hit walk
             # (their launch tails overlap): 4K serial 131.3 -> 145.4 fps, surface view 48.3 -> 49.3; with frames in
             # flight the other frames already fill those tails (215.7 / 215.6 fps at K = 4, profiles/r04/fork/)
             p.set_uniform_int("trace_fork", 1 if self.K == 1 else 0)
+            # a ray still walking past VISIT_BUDGET node + triangle visits is finished by the wave-cooperative walk
+            # (same bits): the launches no longer end on a few long walks. Round 5, same box (profiles/r05/serial/):
+            # one frame at a time with lane refill 145.2 -> 160.8 fps at 4K (budgets 128 / 512: 151.3 / 151.8; refill
+            # without budgets 146.6; without the fork 133.6); K = 4 219.8 / 220.7 -> 223.9 (512 / 1024: 222.1 / 220.0)
+            p.set_uniform_int("shadow_budget", VISIT_BUDGET)
+            p.set_uniform_int("closest_budget", VISIT_BUDGET)
             p.set_uniform_int("trace_batch", self.B)
             self.pt_slots.append((p, outs))
         self.pass_path_tracing = PassGroup([p for p, _ in self.pt_slots])  # settings apply to every slot
