@@ -223,6 +223,7 @@ struct SceneGPU {
   int nleaves = 0;
   int root_any = 0, need_any = 0;
   bool has4 = false;  // bvh4: the 4-wide form of bvh_any (pack_wide)
+  bool nan4 = false;  // a child box of bvh4 has a NaN coordinate (PT_WIDE_SIGNED walks need lo <= hi: not walked)
   int root4 = 0, need4 = 0;
   // refine_leaves' fine boxes are padded for rays whose origin lies within kFineEyeReach x the scene's largest vertex
   // coordinate; an eye further out (pt_params) walks the reference tree instead
@@ -920,6 +921,14 @@ int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU*
       if ((rc = upload_vec(bvh4, &sg.bvh4)) != PT_OK) return rc;
       sg.has4 = true;
       sg.root4 = root4;
+      sg.nan4 = false;
+      for (size_t k = 0; k + ptk::kWideStride <= bvh4.size(); k += ptk::kWideStride) {
+        const float* q = (const float*)&bvh4[k];
+        int refs[4];
+        memcpy(refs, q + 24, 16);
+        for (int c = 0; c < 4; ++c)
+          for (int i = 0; i < 6; ++i) sg.nan4 = sg.nan4 || (refs[c] != kNoneRef && std::isnan(q[4 * i + c]));
+      }
       sg.need4 = need4;
       if (getenv("PTSVGF_SCENE_INFO"))  // diagnostics: the walks' working set (DESIGN.md "The traversal in round 4")
         fprintf(stderr, "ptsvgf scene: %zu triangles (geometry %zu B, shading %zu B), reference tree %zu B, any-hit "
@@ -1193,7 +1202,8 @@ int pt_params(Pass* p, PTParams& k, SceneGPU*& sg) {
   // wide_bvh = 1 (default): the traversal kernels walk the 4-wide form of the any-hit tree: 28 % fewer node + triangle
   // visits, same bits. With the library built without the SLP vectorizer: 4K 197.7 / 198.9 -> 203.9 / 203.3 fps,
   // surface view 65.4 / 65.2 -> 67.3 / 67.1 (profiles/r03/wide_ab.log; with SLP it measured no faster)
-  k.scene.bvh4 = (k.scene.bvh_any && sg->has4 && ui(p, "wide_bvh", 1)) ? sg->bvh4 : nullptr;
+  k.scene.bvh4 = (k.scene.bvh_any && sg->has4 && !(PT_WIDE_SIGNED && sg->nan4) && ui(p, "wide_bvh", 1)) ? sg->bvh4
+                                                                                                     : nullptr;
   k.scene.root4 = sg->root4;
   k.scene.ntris = sg->ntris;
   k.scene.leaves = sg->leaves;

@@ -33,9 +33,11 @@ constexpr int kTB = 128;  // threads per traversal block (LDS stack: kStack*kTB*
 // 8 KiB per 2-wave block). Round 4, same box, two alternating repetitions (profiles/r04/occupancy_ab.log): default
 // 24 entries / 5 waves 210.8 / 210.5 fps at 4K, 68.5 / 68.6 surface view; 16 / 5 waves 212.2 / 211.7, 68.9 / 68.6;
 // 16 / 8 waves 214.7 / 212.3, 69.4 / 69.0; 12 / 8 waves 199.9 / 198.3, 59.9 / 59.2 (more rays overflow to the
-// cooperative walk).
+// cooperative walk). Round 5: the sign-selected planes of the 4-wide step (PT_WIDE_SIGNED) need a few more VGPRs; at
+// 8 waves they spill 40-44 B per lane, at 7 (72 VGPRs) 8-12 B outside the walk loop: 7 kept (pt_device.h PT_WIDE_SIGNED,
+// profiles/r05/wide_signed/).
 #ifndef PT_TRACE_WAVES_PER_EU
-#define PT_TRACE_WAVES_PER_EU 8
+#define PT_TRACE_WAVES_PER_EU 7
 #endif
 #if PT_TRACE_WAVES_PER_EU > 0
 #define PT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(PT_TRACE_WAVES_PER_EU)))
@@ -727,8 +729,9 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
         sp = 0;
         node = WIDE ? p.scene.root4 : sc.root_ref;
         leaf = kNone;
-        ovf = false;
+        ovf = WIDE && PT_WIDE_SIGNED && !finite3(inv);  // axis-parallel (wide_step's signed planes): the coop walk
         if (node < 0) { leaf = node; node = kNone; }
+        if (ovf) node = leaf = kNone;
         if constexpr (DEEP) st = ray_stack<kTB, KS, DEEP>(stk + threadIdx.x, p, pid);
         have = true;
         ++nray;
@@ -867,13 +870,14 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTP
         tree = p.scene.bvh_any;
         node = WIDE ? p.scene.root4 : p.scene.root_any;
         rewalk = false;
-        ovf = false;
+        ovf = WIDE && PT_WIDE_SIGNED && !finite3(inv);  // axis-parallel (wide_step's signed planes): the coop walk
         tbest = PT_INF;
         best = -1;
         tied = false;
         sp = 0;
         leaf = kNone;
         if (node < 0) { leaf = node; node = kNone; }
+        if (ovf) node = leaf = kNone;
         if constexpr (DEEP) st = ray_stack<kTB, KS, DEEP>(stk + threadIdx.x, p, pid);
         have = true;
         rvis = 0;

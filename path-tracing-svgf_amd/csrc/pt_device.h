@@ -51,6 +51,15 @@ constexpr int kWideStride = PT_WIDE_STRIDE;
 #ifndef PT_WIDE_ORDER
 #define PT_WIDE_ORDER 1
 #endif
+// PT_WIDE_SIGNED = 1 (default since round 5): the 4-wide walks pick each child's near / far planes by the ray's
+// direction signs (which float4 is loaded) instead of slab's 6 min / max per child (pt_shading.h wide_step): 99 -> 92
+// VALU per shadow node step in the ISA. Same bits. With the traversal kernels at 7 waves per SIMD (kernels_wavefront.hip
+// PT_TRACE_WAVES_PER_EU), same box, two alternating repetitions (profiles/r05/wide_signed/): 4K 222.5 / 222.4 ->
+// 225.3 / 225.2 fps, surface view 73.9 / 74.0 -> 78.1 / 78.0 (at 8 waves it spills 40-44 B per lane: 223.0, 77.1;
+// at 6: 223.0, 76.6)
+#ifndef PT_WIDE_SIGNED
+#define PT_WIDE_SIGNED 1
+#endif
 constexpr int kStack = PT_KSTACK;  // traversal stack depth (host checks BVH depth < kStack)
 // Traversal counters: a node visit counts PT_NODE_VISIT (1; a diagnostic build with 0 counts triangle tests only)
 #ifndef PT_NODE_VISIT

@@ -543,26 +543,62 @@ __device__ int closest_coop_walk(const SceneDev& sc, int* __restrict__ st, int c
 // no hit child it pops.
 // Returns false, leaving the stack as it was, when the pushes would overflow the KS-entry stack: the caller hands the
 // ray to the cooperative walk.
+__device__ __forceinline__ bool finite3(v3 a) {
+  return __builtin_isfinite(a.x) && __builtin_isfinite(a.y) && __builtin_isfinite(a.z);
+}
+
 template <int KS, bool SORT, class Stk>
 __device__ __forceinline__ bool wide_step(const float4* __restrict__ tree, int& node, Stk& st, int& sp, v3 S, v3 inv,
                                           float lim) {
   const float4* q = tree + kWideStride * node;
-  const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5], rf = q[6];
-  const float alx[4] = {lx.x, lx.y, lx.z, lx.w}, ahx[4] = {hx.x, hx.y, hx.z, hx.w};
-  const float aly[4] = {ly.x, ly.y, ly.z, ly.w}, ahy[4] = {hy.x, hy.y, hy.z, hy.w};
-  const float alz[4] = {lz.x, lz.y, lz.z, lz.w}, ahz[4] = {hz.x, hz.y, hz.z, hz.w};
-  int ref[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
-  float key[4];  // hitAABB's distance of a hit child, +inf otherwise
+  int ref[4];
+  float key[4];  // hitAABB's distance of a hit child (PT_WIDE_SIGNED: its entry t0), +inf otherwise
   int nh = 0;
+#if PT_WIDE_SIGNED
+  // For a ray whose inv components are all finite (the kernels hand the others to the cooperative walk) and a box
+  // with lo <= hi (a tree with a NaN coordinate in a child box is not walked 4-wide: capi.hip), the near plane of an
+  // axis is the lo plane when inv >= 0 (+0 included) and the hi plane otherwise: (b - o) * inv rounds monotonically
+  // in b, so slab's min(fx, nx) IS that plane's value and its max(fx, nx) the other's — the same floats, picked by
+  // which float4 is loaded instead of by 6 min / max per child. hitAABB's d > 0 is t1 >= t0 && t1 > 0 (d is t0 when
+  // t0 > 0, then t1 >= t0 > 0; else d is t1). Sort key: the entry t0 (the order only decides which hit child is
+  // walked first: the candidate triangles, hence the closest t, a unique closest triangle, an exact tie met and every
+  // any-hit verdict do not depend on it).
+  {
+    const int sx = inv.x < 0.0f, sy = inv.y < 0.0f, sz = inv.z < 0.0f;
+    const float4 nx4 = q[sx], fx4 = q[1 - sx], ny4 = q[2 + sy], fy4 = q[3 - sy], nz4 = q[4 + sz], fz4 = q[5 - sz];
+    const float4 rf = q[6];
+    const float anx[4] = {nx4.x, nx4.y, nx4.z, nx4.w}, afx[4] = {fx4.x, fx4.y, fx4.z, fx4.w};
+    const float any_[4] = {ny4.x, ny4.y, ny4.z, ny4.w}, afy[4] = {fy4.x, fy4.y, fy4.z, fy4.w};
+    const float anz[4] = {nz4.x, nz4.y, nz4.z, nz4.w}, afz[4] = {fz4.x, fz4.y, fz4.z, fz4.w};
+    const int rr[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    float t0;
-    const float dist = slab(S, inv, alx[c], aly[c], alz[c], ahx[c], ahy[c], ahz[c], &t0);
-    const bool hit = ref[c] != kNone && dist > 0.0f && !(t0 > lim);
-    key[c] = hit ? dist : __builtin_inff();
-    ref[c] = hit ? ref[c] : kNone;
-    nh += hit ? 1 : 0;
+    for (int c = 0; c < 4; ++c) {
+      const float t1 = fminf((afx[c] - S.x) * inv.x, fminf((afy[c] - S.y) * inv.y, (afz[c] - S.z) * inv.z));
+      const float t0 = fmaxf((anx[c] - S.x) * inv.x, fmaxf((any_[c] - S.y) * inv.y, (anz[c] - S.z) * inv.z));
+      const bool hit = rr[c] != kNone && t1 >= t0 && t1 > 0.0f && !(t0 > lim);
+      key[c] = hit ? t0 : __builtin_inff();
+      ref[c] = hit ? rr[c] : kNone;
+      nh += hit ? 1 : 0;
+    }
   }
+#else
+  {
+    const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5], rf = q[6];
+    const float alx[4] = {lx.x, lx.y, lx.z, lx.w}, ahx[4] = {hx.x, hx.y, hx.z, hx.w};
+    const float aly[4] = {ly.x, ly.y, ly.z, ly.w}, ahy[4] = {hy.x, hy.y, hy.z, hy.w};
+    const float alz[4] = {lz.x, lz.y, lz.z, lz.w}, ahz[4] = {hz.x, hz.y, hz.z, hz.w};
+    const int rr[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float t0;
+      const float dist = slab(S, inv, alx[c], aly[c], alz[c], ahx[c], ahy[c], ahz[c], &t0);
+      const bool hit = rr[c] != kNone && dist > 0.0f && !(t0 > lim);
+      key[c] = hit ? dist : __builtin_inff();
+      ref[c] = hit ? rr[c] : kNone;
+      nh += hit ? 1 : 0;
+    }
+  }
+#endif
   if (nh == 0) {
     node = sp > 0 ? st.get(--sp) : kNone;
     return true;
