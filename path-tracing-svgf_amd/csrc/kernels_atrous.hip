@@ -359,9 +359,10 @@ __global__ void __launch_bounds__(64 * tile_tj<S>() * tile_nx<S>()) atrous_tile_
   constexpr int NX = tile_nx<S>();
   constexpr int TJ = tile_tj<S>(), NW = TJ * NX, R = TJ + 4, C = 64 * NX + 4 * S, NT = 64 * NW;
   constexpr bool LUM = tile_stage_lum<S>();
-  __shared__ float4 LI[R * C];
-  __shared__ float4 LN[R * C];
-  __shared__ float LL[LUM ? R * C : 1];
+  constexpr int PAD = (R * C) % NT ? 16 : 0;  // dummy slots of the staging's last trip (16: S = 2 keeps 5 blocks/CU)
+  __shared__ float4 LI[R * C + PAD];
+  __shared__ float4 LN[R * C + PAD];
+  __shared__ float LL[LUM ? R * C + PAD : 1];
   const int W = p.illum.W, row0 = p.illum.row0;
   const float4* __restrict__ I = p.illum.p;
   const float4* __restrict__ ND = p.nd.p;
@@ -380,7 +381,7 @@ __global__ void __launch_bounds__(64 * tile_tj<S>() * tile_nx<S>()) atrous_tile_
   const bool pre = AUX && p.tile_any != nullptr;
   bool tile_any = true;
   if (pre) tile_any = p.tile_any[(g * S + b) * gridDim.x + bx] != 0;
-  if (own && tile_any) {
+  if (!pre && own) {  // (with the flags the pixel's own flag is read beside the staging loads, below)
     if (AUX) {
       const float a = p.fwidth.aux[ci];
       bg = aux_flag(a);
@@ -411,17 +412,38 @@ __global__ void __launch_bounds__(64 * tile_tj<S>() * tile_nx<S>()) atrous_tile_
   }
   // stage: tile row r <-> frame row ybase + S*(r-2), column c <-> x0 - 2S + c; rows outside the frame and
   // columns outside [0, W) are clamped (their taps are skipped below), rows outside the stored band clamp too.
+  // All of a thread's staging loads are issued before its first LDS write (NIT = 2 or 3 texels per thread), so a
+  // tile waits for one memory latency, not one per loop trip; a thread past the tile's end loads the last texel again
+  // (an address inside the planes) into a dummy slot.
   const int lo = max(0, row0), hi = min(p.H, row0 + p.illum.rows) - 1;
-  for (int e = tid; e < R * C; e += NT) {
+  // the pixel's flag and depth fwidth (a pixel outside the frame or band reads its clamped neighbour's, unused)
+  float own_aux = 0.0f;
+  if (pre) own_aux = p.fwidth.aux[(size_t)(min(y, p.y1 - 1) - row0) * W + min(x, p.W - 1)];
+  constexpr int NIT = (R * C + NT - 1) / NT;
+  float4 sv[NIT], sn[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int e = min(tid + k * NT, R * C - 1);
     const int r = e / C, c = e - r * C;
     int gy = ybase + S * (r - 2), gx = x0 - 2 * S + c;
     gy = gy < lo ? lo : (gy > hi ? hi : gy);
     gx = gx < 0 ? 0 : (gx >= p.W ? p.W - 1 : gx);
     const size_t gi = (size_t)(gy - row0) * W + gx;
-    const float4 v = I[gi];
-    LI[e] = v;
-    LN[e] = ND[gi];
-    if (LUM) LL[e] = tap_luminance(v);
+    sv[k] = I[gi];
+    sn[k] = ND[gi];
+  }
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    // every trip stores (past the tile's end into one of PAD dummy slots): a conditional store would let the compiler
+    // sink its loads into the branch, one memory latency per trip again
+    const int e = tid + k * NT < R * C ? tid + k * NT : R * C + (lane & (PAD - 1));
+    LI[e] = sv[k];
+    LN[e] = sn[k];
+    if (LUM) LL[e] = tap_luminance(sv[k]);
+  }
+  if (pre && own) {
+    bg = aux_flag(own_aux);
+    fwz = fabsf(own_aux);
   }
   __syncthreads();
   if (!own) return;
