@@ -663,6 +663,14 @@ static int pack_wide(const std::vector<SahNode>& nodes, const std::function<int(
 #endif
     const int k = (int)(out.size() / ptk::kWideStride);
     out.resize(out.size() + ptk::kWideStride, float4{0, 0, 0, 0});
+    {  // empty slots: lo = +inf, hi = -inf, a box no ray enters (wide_step's signed test needs no slot check)
+      float* q = (float*)&out[ptk::kWideStride * (size_t)k];
+      for (int a = 0; a < 3; ++a)
+        for (int c = nc; c < 4; ++c) {
+          q[8 * a + c] = INFINITY;
+          q[8 * a + 4 + c] = -INFINITY;
+        }
+    }
     const int here = acc + nc - 1;
     *need = std::max(*need, here + 1);
     int refs[4] = {kNoneRef, kNoneRef, kNoneRef, kNoneRef};

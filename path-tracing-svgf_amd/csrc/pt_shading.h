@@ -566,17 +566,35 @@ __device__ __forceinline__ bool wide_step(const float4* __restrict__ tree, int& 
   {
     const int sx = inv.x < 0.0f, sy = inv.y < 0.0f, sz = inv.z < 0.0f;
     const float4 nx4 = q[sx], fx4 = q[1 - sx], ny4 = q[2 + sy], fy4 = q[3 - sy], nz4 = q[4 + sz], fz4 = q[5 - sz];
-    const float4 rf = q[6];
+    float4 rf = q[6];
     const float anx[4] = {nx4.x, nx4.y, nx4.z, nx4.w}, afx[4] = {fx4.x, fx4.y, fx4.z, fx4.w};
     const float any_[4] = {ny4.x, ny4.y, ny4.z, ny4.w}, afy[4] = {fy4.x, fy4.y, fy4.z, fy4.w};
     const float anz[4] = {nz4.x, nz4.y, nz4.z, nz4.w}, afz[4] = {fz4.x, fz4.y, fz4.z, fz4.w};
-    const int rr[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
+    // t1 >= t0 && t1 > 0 && !(t0 > lim) as ONE compare: t1 > 0 is t1 >= the least subnormal (f32 subnormals are kept),
+    // and lim > 0 (a shadow ray's maxd scaled + 2e-4, a bounce ray's best t scaled + 2e-4, or +inf), so with
+    // t0c = max(t0, least subnormal) it is t0c <= min(t1, lim) (no NaN: finite planes and inv, or the +-inf planes of
+    // an empty slot). An empty slot (pack_wide: lo = +inf, hi = -inf) has t0 = +inf, t1 = -inf: never hit, so the
+    // slot's ref is not tested. The sort key is t0c (order among children entered at t0 <= 0 is free, see above).
+    const float tiny = __builtin_bit_cast(float, 1u);
+    float t0c[4], t1l[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const float t1 = fminf((afx[c] - S.x) * inv.x, fminf((afy[c] - S.y) * inv.y, (afz[c] - S.z) * inv.z));
       const float t0 = fmaxf((anx[c] - S.x) * inv.x, fmaxf((any_[c] - S.y) * inv.y, (anz[c] - S.z) * inv.z));
-      const bool hit = rr[c] != kNone && t1 >= t0 && t1 > 0.0f && !(t0 > lim);
-      key[c] = hit ? t0 : __builtin_inff();
+      t0c[c] = fmaxf(t0, tiny);
+      t1l[c] = fminf(t1, lim);
+    }
+    // the refs are needed only once a child is hit; without this use (after the box arithmetic, so the box loads'
+    // arithmetic still overlaps the refs' arrival) the compiler loads them after the hit test: a second dependent
+    // fetch per node step instead of one fetch of the node's seven float4
+    asm volatile("" : "+v"(rf.x), "+v"(rf.y), "+v"(rf.z), "+v"(rf.w)
+                 : "v"(t0c[0]), "v"(t0c[1]), "v"(t0c[2]), "v"(t0c[3]), "v"(t1l[0]), "v"(t1l[1]), "v"(t1l[2]),
+                   "v"(t1l[3]));
+    const int rr[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const bool hit = t0c[c] <= t1l[c];
+      key[c] = hit ? t0c[c] : __builtin_inff();
       ref[c] = hit ? rr[c] : kNone;
       nh += hit ? 1 : 0;
     }
