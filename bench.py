@@ -585,8 +585,7 @@ def main():
                 "background_fraction": round(bgf, 4)}
 
     def shadow_split(st):
-        return {"point_rays": int(st.get("shadow_point_rays", 0)), "occluded": int(st.get("shadow_occluded", 0)),
-                "decided_by_occluder_cache": int(st.get("shadow_probed", 0))}
+        return {"point_rays": int(st.get("shadow_point_rays", 0)), "occluded": int(st.get("shadow_occluded", 0))}
 
     def pt_rates(res, fps):
         """Rays and BVH node + triangle visits per frame (traversal counters), as rates at the measured frame rate
@@ -603,7 +602,7 @@ def main():
                 # share of SIMD lanes doing traversal work: a wave runs as long as its longest ray
                 "lane_efficiency": {k: round(st[f"{k}_visits"] / st[f"{k}_slots"], 3) if st.get(f"{k}_slots") else None
                                     for k in ("primary", "bounce", "shadow")},
-                # shadow rays (lane-refill walks): toward point lights, occluded, decided by the occluder cache
+                # shadow rays (lane-refill walks): toward point lights, occluded
                 "shadow_split": shadow_split(st),
                 "rays_per_s": round(rays * fps, 0), "visits_per_s": round(visits * fps, 0),
                 "pt_ms_profiled": round(pt_ms, 4) if pt_ms else None,

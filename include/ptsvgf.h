@@ -182,14 +182,14 @@ int pt_pass_set_row_cost(uint32_t pass, void* device_counts);
  * No reference counterpart (the single-GPU reference reads the whole frame). */
 int pt_pass_set_motion_bound(uint32_t pass, void* device_u32);
 /* Traversal counters (path-tracing pass, wavefront kernel): while set, every
- * draw ADDS to device_u64[0..14] (caller zeroes): primary rays, primary node +
+ * draw ADDS to device_u64[0..13] (caller zeroes): primary rays, primary node +
  * triangle visits, bounce rays, bounce visits, shadow rays, shadow visits,
  * exact-tie re-walks on the reference tree, primary rays retried unbounded after
  * the G-buffer bound, rays whose stack spilled past the LDS stack (reference
  * trees deeper than 32 levels), the lane slots of primary / bounce / shadow
  * waves (64 x the wave's largest visit count), and of the shadow rays of the
- * lane-refill walks: point-light rays, occluded rays, and rays the occluder
- * cache's probe decided. device_u64 holds 15 counters.
+ * lane-refill walks: point-light rays and occluded rays. device_u64 holds 14
+ * counters.
  * Wave-aggregated atomics; NULL disables (the default). */
 int pt_pass_set_trace_stats(uint32_t pass, void* device_u64);
 int pt_pass_draw(uint32_t pass);

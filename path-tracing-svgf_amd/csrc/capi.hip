@@ -99,30 +99,7 @@ struct WFBuffers {
   int* spill = nullptr;  // deep reference trees: stack entries past the LDS stack (WFState::spill)
   int spill_levels = 0;
   size_t spill_cols = 0;
-  int2* occ_cache = nullptr;  // WFState::occ_cache: kOccCacheBounces x 2 kinds x the batch's pixels
-  size_t occ_cols = 0;
 };
-
-// The shadow occluder cache of a pass's wavefront state (uniform "shadow_cache": bit b = bounce b, 0 = off), allocated
-// on first use and filled with (-1, -1) (no entry); kept while the pass's size holds. Entries only ever name a triangle
-// to test first (the verdict stays exact whatever they hold), so frames, cameras and scenes may share it.
-int wf_occ_cache(WFBuffers& b, int mask) {
-  const size_t m = b.n * (size_t)b.nb;
-  if (mask && (!b.occ_cache || b.occ_cols != m)) {
-    if (b.occ_cache) (void)hipFree(b.occ_cache);
-    b.occ_cache = nullptr;
-    const size_t bytes = (size_t)ptk::kOccCacheBounces * 2 * m * sizeof(int2);
-    if (hipMalloc((void**)&b.occ_cache, bytes) != hipSuccess) { b.occ_cache = nullptr; return PT_ERR_HIP; }
-    if (hipMemset(b.occ_cache, 0xff, bytes) != hipSuccess) return PT_ERR_HIP;  // once per allocation
-    b.occ_cols = m;
-  }
-  for (int f = 0; f < b.nb; ++f) {
-    b.stb[f].occ_cache = mask ? b.occ_cache : nullptr;  // indexed by the batch's global pid
-    b.stb[f].occ_cache_mask = mask;
-  }
-  b.st = b.stb[0];
-  return PT_OK;
-}
 
 // Spill columns for a tree needing `need` stack entries (> the LDS stack): (need - kSpillKS + 1) entries per
 // pixel of the band, allocated on first use and kept while the depth fits.
@@ -244,7 +221,6 @@ struct SceneGPU {
   float4* bvh_any = nullptr;  // any-hit tree over the reference leaves (build_anyhit_tree)
   float4* leaves = nullptr;   // the reference leaves: (box lo, leaf ref bits), (box hi, 0) (wf_primary_raster)
   int nleaves = 0;
-  int* tri_leaf = nullptr;    // per triangle its leaf's index in `leaves`, -1 none (the shadow occluder cache)
   int root_any = 0, need_any = 0;
   bool has4 = false;  // bvh4: the 4-wide form of bvh_any (pack_wide)
   bool nan4 = false;  // a child box of bvh4 has a NaN coordinate (PT_WIDE_SIGNED walks need lo <= hi: not walked)
@@ -847,8 +823,6 @@ void free_scene(SceneGPU& sg) {
     if (*b) (void)hipFree(*b);
     *b = nullptr;
   }
-  if (sg.tri_leaf) (void)hipFree(sg.tri_leaf);
-  sg.tri_leaf = nullptr;
 }
 
 template <class T>
@@ -860,12 +834,10 @@ int upload_vec(const std::vector<T>& v, T** dst) {
   return PT_OK;
 }
 
-// The reference tree's leaves with their own boxes (the primary-ray tile rasteriser's items) and, per triangle, the
-// index of the leaf holding it (the shadow occluder cache tests a cached triangle on that leaf's box). The caller has
-// checked the leaf ranges (pack_bvh).
-static int upload_leaves(const float* ne, size_t nnodes, size_t ntris, SceneGPU& sg) {
+// The reference tree's leaves with their own boxes (the primary-ray tile rasteriser's items). The caller has checked
+// the leaf ranges (pack_bvh).
+static int upload_leaves(const float* ne, size_t nnodes, SceneGPU& sg) {
   std::vector<float4> lv;
-  std::vector<int> tl(ntris, -1);
   for (size_t i = 1; i < nnodes; ++i) {
     const float* f = ne + i * 12;
     const int n = (int)f[3], first = (int)f[4];
@@ -873,15 +845,11 @@ static int upload_leaves(const float* ne, size_t nnodes, size_t ntris, SceneGPU&
     const int ref = -(first * 16 + n) - 1;
     float rf;
     memcpy(&rf, &ref, 4);
-    for (int t = first; t < first + n; ++t)
-      if (t >= 0 && (size_t)t < ntris) tl[t] = (int)(lv.size() / 2);
     lv.push_back(float4{f[6], f[7], f[8], rf});
     lv.push_back(float4{f[9], f[10], f[11], 0.0f});
   }
   sg.nleaves = (int)(lv.size() / 2);
-  int rc = upload_vec(lv, &sg.leaves);
-  if (rc == PT_OK) rc = upload_vec(tl, &sg.tri_leaf);
-  return rc;
+  return upload_vec(lv, &sg.leaves);
 }
 
 // A scene pt_bvh_build wrote (dynamic scenes): its triangles are decoded on the device (decode_tris: the host
@@ -895,7 +863,7 @@ int get_scene_lbvh(Texture* tris, Texture* nodes, SceneGPU& sg, SceneGPU** out) 
   int root = 0;
   int rc = pack_bvh((const float*)nodes->host.data(), (int)nnodes, bvh, &root, (int)ntris, &sg.stack_need);
   if (rc != PT_OK) return rc;
-  if ((rc = upload_leaves((const float*)nodes->host.data(), nnodes, ntris, sg)) != PT_OK) return rc;
+  if ((rc = upload_leaves((const float*)nodes->host.data(), nnodes, sg)) != PT_OK) return rc;
   if (bvh.empty()) bvh.push_back(float4{0, 0, 0, 0});
   if ((rc = upload_vec(bvh, &sg.bvh)) != PT_OK) return rc;
   float4** opt[2] = {&sg.bvh4, &sg.bvh_any};
@@ -987,7 +955,7 @@ int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU*
       sg.need_any = sg.root_any = sg.need4 = sg.root4 = 0;
     }
   }
-  if ((rc = upload_leaves((const float*)nodes->host.data(), nnodes, ntris, sg)) != PT_OK) return rc;
+  if ((rc = upload_leaves((const float*)nodes->host.data(), nnodes, sg)) != PT_OK) return rc;
   if ((rc = upload_vec(geom, &sg.geom)) != PT_OK) return rc;
   if ((rc = upload_vec(shade, &sg.shade)) != PT_OK) return rc;
   if (bvh.empty()) bvh.push_back(float4{0, 0, 0, 0});
@@ -1238,7 +1206,6 @@ int pt_params(Pass* p, PTParams& k, SceneGPU*& sg) {
   k.scene.ntris = sg->ntris;
   k.scene.leaves = sg->leaves;
   k.scene.nleaves = sg->nleaves;
-  k.scene.tri_leaf = sg->tri_leaf;
   if (lt && lt->target == PT_TEXTURE_BUFFER) {
     k.scene.lights = (const float*)lt->dev;
     k.scene.nlights_buf = (int)(lt->bytes / (6 * sizeof(float)));
@@ -1378,10 +1345,6 @@ const ptk::WfFork* wf_fork(Pass* p, hipStream_t s, int* rc) {
   return &(g.forks[s] = f);
 }
 
-// uniform "shadow_cache": the bounces whose shadow rays use the occluder cache (bit b = bounce b; 0 = off)
-constexpr int kOccCacheDefault = 3;
-static int occ_cache_mask(Pass* p) { return ui(p, "shadow_cache", kOccCacheDefault) & ((1 << ptk::kOccCacheBounces) - 1); }
-
 int draw_pathtrace(Pass* p) {
   PTParams k;
   SceneGPU* sg = nullptr;
@@ -1396,7 +1359,6 @@ int draw_pathtrace(Pass* p) {
   } else {                            // 0: wavefront (kernels_wavefront.hip), production
     TRY(wf_alloc(p->wf, k.W, std::max(0, k.y1 - k.y0)));
     if (wf_spill(p->wf, k.stack_need) != PT_OK) return err(PT_ERR_HIP, "spill stack allocation failed");
-    if (wf_occ_cache(p->wf, occ_cache_mask(p)) != PT_OK) return err(PT_ERR_HIP, "occluder cache allocation failed");
     TRY(pt_wf_setup(p, k, sg, p->wf.st));
     const ptk::WfFork* fk = wf_fork(p, g.stream, &rc);
     if (rc) return rc;
@@ -1421,7 +1383,7 @@ int draw_pathtrace_batch(Pass** ps, int n) {
     // compared at its effective value (the default pt_params / pt_wf_setup apply when a pass never set it)
     struct Same { const char* name; int dflt; };
     const Same same[] = {{"trace_refill", 0}, {"shadow_budget", 0}, {"closest_budget", 0}, {"wide_bvh", 1},
-                         {"refill_waves", 0}, {"trace_fork", 0}, {"shadow_cache", kOccCacheDefault}};
+                         {"refill_waves", 0}, {"trace_fork", 0}};
     bool agree = true;
     for (const Same& u : same) agree = agree && ui(ps[b], u.name, u.dflt) == ui(ps[0], u.name, u.dflt);
     if (sb != sg || k[b].W != k[0].W || k[b].y0 != k[0].y0 || k[b].y1 != k[0].y1 || k[b].max_depth != k[0].max_depth ||
@@ -1436,7 +1398,6 @@ int draw_pathtrace_batch(Pass** ps, int n) {
   const int cap = std::max(n, std::min(kMaxBatch, ui(h, "trace_batch", n)));
   TRY(wf_alloc(h->wf, k[0].W, std::max(0, k[0].y1 - k[0].y0), cap));
   if (wf_spill(h->wf, k[0].stack_need) != PT_OK) return err(PT_ERR_HIP, "spill stack allocation failed");
-  if (wf_occ_cache(h->wf, occ_cache_mask(h)) != PT_OK) return err(PT_ERR_HIP, "occluder cache allocation failed");
   for (int b = 0; b < n; ++b) TRY(pt_wf_setup(ps[b], k[b], sg, h->wf.stb[b]));
   int rc;
   const ptk::WfFork* fk = wf_fork(h, g.stream, &rc);
@@ -1743,7 +1704,6 @@ int pt_shutdown(void) {
     if (p->bins.base) (void)hipFree(p->bins.base);
     if (p->wf.base) (void)hipFree(p->wf.base);
     if (p->wf.spill) (void)hipFree(p->wf.spill);
-    if (p->wf.occ_cache) (void)hipFree(p->wf.occ_cache);
     if (p->order.cost) (void)hipFree(p->order.cost);
     if (p->order.perm) (void)hipFree(p->order.perm);
     if (p->ev0) (void)hipEventDestroy(p->ev0);
@@ -2498,7 +2458,6 @@ int pt_pass_destroy(uint32_t pass) {
   if (p->bins.base) (void)hipFree(p->bins.base);
   if (p->wf.base) (void)hipFree(p->wf.base);
   if (p->wf.spill) (void)hipFree(p->wf.spill);
-  if (p->wf.occ_cache) (void)hipFree(p->wf.occ_cache);
   if (p->order.cost) (void)hipFree(p->order.cost);
   if (p->order.perm) (void)hipFree(p->order.perm);
   if (p->ev0) (void)hipEventDestroy(p->ev0);

@@ -674,58 +674,6 @@ __host__ __device__ constexpr int refill_blocks(int items_max) {
                          : (items_max + kTB - 1) / kTB;  // enough 64-item waves for every item (spare waves exit)
 }
 
-// Shadow occluder probe (before the lane-refill shadow walk of a bounce; cache = this bounce's region of
-// WFState::occ_cache, cm = the batch's pixels, base = frame b's first global pid): each shadow ray of frame b first
-// tests the triangle that occluded its pixel's last ray of the same kind and bounce, on that triangle's reference leaf
-// box. A ray that passes the leaf box (hitAABB, with the walk's pruning bound) and hits the triangle (hitTriangle's
-// acceptance; :905-909 for point lights) is occluded in the reference too: the leaf box passing means every box above
-// it in the reference tree passes (a parent's box encloses its children's and, for a finite inv, slab rounding is
-// monotone), so the reference walk reaches that leaf unless it stops at another hit first — either way the verdict is
-// "occluded". Any cached triangle therefore gives the exact verdict; the probe writes it (1), and the walk skips the
-// ray. An entry whose probe fails is cleared; the walk stores the occluder it finds.
-__global__ void __launch_bounds__(256) wf_shadow_probe(PTParams p, const int* __restrict__ list,
-                                                       const int* __restrict__ counts, int cap,
-                                                       int2* __restrict__ cache, int cm, int base) {
-  const int nh = seg_total(counts);
-  int tot = nh;
-#pragma unroll
-  for (int c = 0; c < kPointBins; ++c) tot += seg_total(counts + (1 + c) * kSeg);
-  const SceneDev& sc = p.scene;
-  uint32_t nray = 0;
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < tot; k += gridDim.x * blockDim.x) {
-    int pid;
-    bool point;
-    if (!shadow_item(list, counts, cap, nh, k, &pid, &point)) continue;
-    const int slot = (point ? cm : 0) + base + pid;
-    const int2 ce = cache[slot];
-    if (ce.x < 0) continue;
-    bool occ = false;
-    if (ce.x < sc.ntris && ce.y >= 0 && ce.y < sc.nleaves) {
-      const float4 o = ldnt(&p.wf.ray_o[pid]);
-      const float4 dir = point ? ldnt(&p.wf.sh_p[pid]) : ldnt(&p.wf.sh_h[pid]);
-      const v3 S = xyz(o), d = xyz(dir);
-      const v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-      const float maxd = dir.w, lim = point ? maxd * 1.0002f + 2.0e-4f : __builtin_inff();
-      if (finite3(inv)) {
-        const float4 blo = sc.leaves[2 * ce.y], bhi = sc.leaves[2 * ce.y + 1];
-        float t0, t;
-        const float dist = slab(S, inv, blo.x, blo.y, blo.z, bhi.x, bhi.y, bhi.z, &t0);
-        occ = dist > 0.0f && !(t0 > lim) && tri_hit(sc.tri_geom, ce.x, S, d, &t) && t < PT_INF &&
-              (!point || length(sub(add(S, muls(d, t)), S)) < maxd);
-      }
-    }
-    if (occ) {
-      (point ? p.wf.occ_p : p.wf.occ_h)[pid] = 1;
-      ++nray;
-    } else {
-      cache[slot] = make_int2(-1, -1);
-    }
-  }
-  // (the walk counts these rays, as decided with no visits of its own)
-  stat_add(p, kStatShadowVisits, 2 * nray);  // a leaf box and a triangle each
-  stat_add(p, kStatShadowProbed, nray);
-}
-
 // Traversal counters only (PTParams::wf.stats set): of one frame's shadow rays of a bounce, those toward point lights
 // and those found occluded (by the walks or the occluder probe), from the verdicts.
 __global__ void __launch_bounds__(256) wf_shadow_stats(PTParams p, const int* __restrict__ list,
@@ -756,14 +704,10 @@ __global__ void __launch_bounds__(256) wf_shadow_stats(PTParams p, const int* __
 // walk (wf_shadow_coop) and its lane takes the next item, as in wf_trace_shadow.
 // WIDE: the walk runs on the 4-wide form of the any-hit tree (pack_wide: the same candidate triangles); a ray whose
 // pushes would overflow the LDS stack goes to the cooperative walk like a ray past the visit budget.
-// Occluder cache (cache non-null: this bounce's region of WFState::occ_cache, cm = the batch's pixels): a ray
-// wf_shadow_probe decided (its verdict already 1) is taken and finished at once, without a walk; a ray the walk finds
-// occluded stores its occluder.
 template <int KS, bool DEEP, bool WIDE>
 __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTParams p, ListBatch lb, int cap,
                                                                              int* __restrict__ heads,
-                                                                             int* __restrict__ strag_count,
-                                                                             int2* __restrict__ cache, int cm) {
+                                                                             int* __restrict__ strag_count) {
   __shared__ int stk[KS * kTB];
   const int lane = threadIdx.x & 63;
   int nh[kMaxBatch], tot[kMaxBatch];
@@ -786,8 +730,6 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
   float lim = 0.0f, maxd = 0.0f;
   uint32_t nvis = 0, nray = 0, rvis = 0;
   const uint32_t budget = p.wf.shadow_budget;
-  int hit_tri = -1;      // the occluder the walk found (occluder cache)
-  bool pre_hit = false;  // this lane's new ray was found occluded by wf_shadow_probe
   while (true) {
     const unsigned long long idle = __ballot(!have);
     if (__popcll(idle) >= (__ballot(have) ? kRefillMin : 1) && (q.next < q.end || q.grab())) {
@@ -797,8 +739,6 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
       if (!have && fb >= 0 && shadow_item(lb.list[fb], lb.counts[fb], cap, nh[fb], k, &pid, &point)) {
         pid += fb * lb.n;
         rvis = 0;
-        // a ray wf_shadow_probe found occluded by its pixel's cached occluder is decided (its verdict written)
-        const bool probed = cache && (point ? p.wf.occ_p : p.wf.occ_h)[pid] != 0;
         const float4 o = ldnt(&p.wf.ray_o[pid]);
         const float4 dir = point ? ldnt(&p.wf.sh_p[pid]) : ldnt(&p.wf.sh_h[pid]);  // point: (direction, distance)
         S = xyz(o);
@@ -811,13 +751,10 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
         leaf = kNone;
         ovf = WIDE && PT_WIDE_SIGNED && !finite3(inv);  // axis-parallel (wide_step's signed planes): the coop walk
         if (node < 0) { leaf = node; node = kNone; }
-        if (ovf || probed) node = leaf = kNone;  // (probed: decided below without a walk)
-        pre_hit = probed;
-        ovf = ovf && !probed;
+        if (ovf) node = leaf = kNone;
         if constexpr (DEEP) st = ray_stack<kTB, KS, DEEP>(stk + threadIdx.x, p, pid);
         have = true;
         ++nray;
-        hit_tri = -1;
       }
       q.next = min(q.next + __popcll(idle), q.end);
     }
@@ -861,16 +798,13 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
       }
       if (!__any(leaf == kNone)) break;
     }
-    bool hit = pre_hit;
-    pre_hit = false;
+    bool hit = false;
     while (leaf != kNone) {  // anyhit2's leaf phase
       const int first = ref_leaf_first(leaf), cnt = ref_leaf_count(leaf);
       nvis += (uint32_t)cnt;
       rvis += (uint32_t)cnt;
-      if (leaf_scan(sc.tri_geom, first, cnt, S, d, [&](int i, float t) {
-            const bool occ = t < PT_INF && (!point || length(sub(add(S, muls(d, t)), S)) < maxd);
-            if (occ) hit_tri = i;
-            return occ;
+      if (leaf_scan(sc.tri_geom, first, cnt, S, d, [&](int, float t) {
+            return t < PT_INF && (!point || length(sub(add(S, muls(d, t)), S)) < maxd);
           })) {
         hit = true;
         break;
@@ -883,7 +817,6 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_shadow_refill(PTPa
     }
     if (have && !ovf && (hit || (node == kNone && leaf == kNone))) {  // this lane's ray is decided
       (point ? p.wf.occ_p : p.wf.occ_h)[pid] = hit;
-      if (cache && hit_tri >= 0) cache[(point ? cm : 0) + pid] = make_int2(hit_tri, sc.tri_leaf[hit_tri]);
       have = false;
       node = leaf = kNone;
       spill = spill || st.spilled;
@@ -1450,23 +1383,14 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, const WfFork* fk
         lb.counts[b] = ps[b].wf.counters + kWfCtr * i + kCtrHdr;
       }
       int* strag = p.wf.counters + kWfCtr * i + kCtrStrag;  // shadow rays handed to the cooperative walk
-      // this bounce's occluder cache (both ray kinds of every frame of the batch), when on for it
-      int2* cache = p.wf.occ_cache && i < kOccCacheBounces && ((p.wf.occ_cache_mask >> i) & 1) && p.scene.tri_leaf &&
-                            p.scene.leaves
-                        ? p.wf.occ_cache + (size_t)i * 2 * nb * N
-                        : nullptr;
-      if (cache)
-        for (int b = 0; b < nb; ++b)
-          hipLaunchKernelGGL(wf_shadow_probe, dim3(gN), dim3(256), 0, ss, ps[b], (const int*)ps[b].wf.shadow_list,
-                             (const int*)(ps[b].wf.counters + kWfCtr * i + kCtrHdr), cap, cache, nb * N, b * N);
       if constexpr (!DEEP)
         if (wide) {
           hipLaunchKernelGGL((wf_trace_shadow_refill<kWideKS, false, true>), dim3(refill_blocks(2 * nb * N)), dim3(kTB), 0,
-                             ss, p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQShadow, strag, cache, nb * N);
+                             ss, p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQShadow, strag);
         }
       if (!wide)
         hipLaunchKernelGGL((wf_trace_shadow_refill<KS, DEEP, false>), dim3(refill_blocks(2 * nb * N)), dim3(kTB), 0, ss,
-                           p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQShadow, strag, cache, nb * N);
+                           p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQShadow, strag);
       if (p.wf.shadow_budget || wide)
         hipLaunchKernelGGL(wf_shadow_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, ss, p, (const int*)strag);
     } else {

@@ -130,7 +130,6 @@ struct SceneDev {
   // rasteriser's items (wf_primary_raster)
   const float4* leaves;
   int nleaves;
-  const int* tri_leaf;  // per triangle: the index in `leaves` of the reference leaf holding it, -1 none (occluder cache)
 };
 
 // Wavefront path-tracer state (kernels_wavefront.hip): SoA per band pixel.
@@ -156,22 +155,16 @@ struct WFState {
   unsigned long long* stats;    // optional traversal counters (kStat*), wave-aggregated atomics; may be null
   int* spill;                   // deep trees only: stack entries past the LDS stack, entry kStack + j of pixel pid at
   size_t spill_stride;          // spill[j * spill_stride + pid] (spill_stride = band pixels); null otherwise
-  // shadow occluder cache (lane-refill shadow walk): per bounce b < kOccCacheBounces (bit b of occ_cache_mask), HDR
-  // then point-light rays, per global pid: (triangle, its reference leaf) that occluded the pixel's last such ray, or
-  // (-1, -1); null when off
-  int2* occ_cache;
-  int occ_cache_mask;
 };
-constexpr int kOccCacheBounces = 2;
 // Traversal counters of one path-tracing draw (pt_pass_set_trace_stats): rays traced and node + triangle visits
 // per traversal kind, tie re-walks on the reference tree, primary rays retried unbounded after the G-buffer bound, rays
 // whose stack went past the LDS stack into the spill columns (deep reference trees), and per traversal kind the lane
 // slots its waves occupied (64 x the wave's largest visit count, summed over waves): visits / slots is the share of
 // SIMD lanes doing useful traversal work (divergence: a wave runs as long as its longest ray); of the shadow rays
-// (lane-refill walks), those toward point lights, those found occluded, and those the occluder probe decided.
+// (lane-refill walks), those toward point lights and those found occluded.
 enum { kStatPrimRays, kStatPrimVisits, kStatBounceRays, kStatBounceVisits, kStatShadowRays, kStatShadowVisits,
        kStatTieRewalks, kStatPrimRetries, kStatSpills, kStatPrimSlots, kStatBounceSlots, kStatShadowSlots,
-       kStatShadowPoint, kStatShadowOccluded, kStatShadowProbed, kStatCount };
+       kStatShadowPoint, kStatShadowOccluded, kStatCount };
 
 // A path-tracing draw over several frames' pixels (pt_pass_draw_batch): frame b's pixels are the pids
 // [b * n, (b + 1) * n) of one shared per-pixel wavefront state; its lists hold frame-local pids. The list-driven

@@ -759,8 +759,7 @@ class Renderer:
 
     STAT_KEYS = ("primary_rays", "primary_visits", "bounce_rays", "bounce_visits", "shadow_rays", "shadow_visits",
                  "tie_rewalks", "primary_retries", "spills", "primary_slots", "bounce_slots",
-                 "shadow_slots", "shadow_point_rays", "shadow_occluded",
-                 "shadow_probed")  # pt_pass_set_trace_stats order (pt_device.h kStat*)
+                 "shadow_slots", "shadow_point_rays", "shadow_occluded")  # pt_pass_set_trace_stats order (pt_device.h kStat*)
 
     def trace_stats(self) -> dict:
         """Render one frame with the path tracer's traversal counters on (pt_pass_set_trace_stats): rays traced and

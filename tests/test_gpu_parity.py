@@ -597,7 +597,6 @@ def test_lane_refill_is_result_preserving(gpu, scene_name, request):
         r = _renderer(scene, W, H, mode="fast", run_taa=False, run_output=False)
         r.pass_path_tracing.set_uniform_int("trace_refill", refill)
         r.pass_path_tracing.set_uniform_int("wide_bvh", 0)  # visit counts compare on one tree shape
-        r.pass_path_tracing.set_uniform_int("shadow_cache", 0)  # (the one-ray-per-lane walk has no occluder cache)
         r.frame()
         stats.append(r.trace_stats())
         outs.append({k: gl.readback(r.planes()[k]) for k in ("color", "emission", "albedo")})
@@ -609,38 +608,6 @@ def test_lane_refill_is_result_preserving(gpu, scene_name, request):
             assert st[k] == stats[2][k], (k, stats)
         for k in ("shadow_visits", "bounce_visits"):
             assert abs(st[k] - stats[2][k]) <= 0.01 * stats[2][k], (k, stats)
-
-
-@pytest.mark.parametrize("scene_name,K,B", [("scene_small", 4, 1), ("scene_cornell", 4, 2), ("scene_nan", 1, 1),
-                                             ("scene_cornell", 1, 1)])
-def test_shadow_occluder_cache_is_result_preserving(gpu, scene_name, K, B, request):
-    """The shadow occluder cache (uniform shadow_cache, default 3: bounces 0 and 1; kernels_wavefront.hip
-    wf_shadow_probe) decides a shadow ray as occluded only when its pixel's cached triangle hits it inside that
-    triangle's reference leaf box, which the reference walk would reach: the same bits as without it, over frames in
-    flight, batched draws and a moving camera (cached entries then name triangles that no longer occlude), with the
-    same ray counts; a static camera reuses the entries (fewer shadow visits)."""
-    gl = gpu
-    scene = request.getfixturevalue(scene_name)
-    W, H = 96, 64
-    outs, stats = [], []
-    for cache in (3, 0):
-        r = _renderer(scene, W, H, mode="fast", run_taa=False, run_output=False, frames_in_flight=K, trace_batch=B)
-        r.pass_path_tracing.set_uniform_int("shadow_cache", cache)
-        frames = []
-        for f in range(K + 5):
-            if f in (3, 4):
-                r.camera.orbit(3.0, 1.0)
-            r.frame()
-            frames.append({k: gl.readback(r.planes()[k]) for k in ("color", "emission", "albedo", "modulate")})
-        stats.append(r.trace_stats())
-        outs.append(frames)
-        r.close()
-    for fc, fn in zip(*outs):
-        for k in fc:
-            assert np.array_equal(fc[k].view(np.uint32), fn[k].view(np.uint32)), k
-    for k in ("primary_rays", "bounce_rays", "shadow_rays"):
-        assert stats[0][k] == stats[1][k], (k, stats)
-    print("shadow visits with / without the cache:", stats[0]["shadow_visits"], stats[1]["shadow_visits"])
 
 
 @pytest.mark.parametrize("scene_name", ["scene_small", "scene_cornell", "scene_nan"])
