@@ -675,7 +675,7 @@ __host__ __device__ constexpr int refill_blocks(int items_max) {
 }
 
 // Traversal counters only (PTParams::wf.stats set): of one frame's shadow rays of a bounce, those toward point lights
-// and those found occluded (by the walks or the occluder probe), from the verdicts.
+// and those found occluded, from the verdicts.
 __global__ void __launch_bounds__(256) wf_shadow_stats(PTParams p, const int* __restrict__ list,
                                                        const int* __restrict__ counts, int cap) {
   const int nh = seg_total(counts);
