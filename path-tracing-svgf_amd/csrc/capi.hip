@@ -1549,7 +1549,6 @@ int draw_svgf(Pass* p, int kind) {
     k.step = ui(p, "gStepSize", 1);
     k.phi_color = uf(p, "gPhiColor", 0.0f);
     k.phi_normal = uf(p, "gPhiNormal", 0.0f);
-    k.rows2 = ui(p, "atrous_rows", 2) == 2;  // tiled kernel: pixels per lane down the tile (2: atrous_tile2_kernel)
     // production tiled kernel: per-tile surface flags, derived once per G-buffer from its depth-fwidth plane
     const int si = k.step == 1 ? 0 : k.step == 2 ? 1 : k.step == 4 ? 2 : k.step == 8 ? 3 : k.step == 16 ? 4 : -1;
     const int av = ui(p, "atrous_variant", 0);

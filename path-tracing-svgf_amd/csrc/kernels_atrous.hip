@@ -475,186 +475,6 @@ __global__ void __launch_bounds__(64 * tile_tj<S>() * tile_nx<S>()) atrous_tile_
   if (p.mod.p) modulate_store(p, x, y, r, false);
 }
 
-// Two tile rows per lane (atrous_tile2_kernel, uniform "atrous_rows" = 2): the windows of tile rows j and j + 1 share
-// 4 of their 5 texel rows, so a lane computing both reads the 6 x 5 union once — 30 staged texels for two pixels
-// instead of 48 — and feeds each texel to both pixels' taps. Each pixel still takes its taps in atrous_taps' order
-// (texel rows ascending, columns ascending), so the results are the step kernel's bits.
-template <int S, int C, bool LUM>
-__device__ __forceinline__ void window_pair(TapPixel& a, TapPixel& b, const float4* Li, const float4* Ln,
-                                            const float* Ll, float phi_normal) {
-#pragma unroll
-  for (int r = 0; r < 6; ++r) {
-#pragma unroll
-    for (int xx = -2; xx <= 2; ++xx) {
-      const int o = r * C + (xx + 2) * S;
-      const float4 ip = Li[o], q = Ln[o];
-      const float lp = LUM ? Ll[o] : 0.0f;
-      const int ya = r - 2, yb = r - 3;  // the texel's row offset from pixel a's and pixel b's centre
-      if (r <= 4 && !(xx == 0 && ya == 0)) a.tap<false, LUM>(ip, q, lp, xx, ya, phi_normal);
-      if (r >= 1 && !(xx == 0 && yb == 0)) b.tap<false, LUM>(ip, q, lp, xx, yb, phi_normal);
-    }
-  }
-}
-
-// atrous_tile_kernel's tiles, staging and flags, with a wave per pair of tile rows (TJ / 2 x NX waves a block): an
-// interior pair whose surface pixels are not FLAT goes through window_pair (a background pixel of the pair is computed
-// and discarded, its centre copied); a border tile or a FLAT surface pixel takes the one-pixel windows.
-template <int S, bool AUX>
-__global__ void __launch_bounds__(32 * tile_tj<S>() * tile_nx<S>()) atrous_tile2_kernel(AtrousParams p) {
-  constexpr int NX = tile_nx<S>();
-  constexpr int TJ = tile_tj<S>(), NW = TJ / 2 * NX, R = TJ + 4, C = 64 * NX + 4 * S, NT = 64 * NW;
-  static_assert(TJ % 2 == 0, "two tile rows per wave");
-  constexpr bool LUM = tile_stage_lum<S>();
-  constexpr int PAD = (R * C) % NT ? 16 : 0;
-  __shared__ float4 LI[R * C + PAD];
-  __shared__ float4 LN[R * C + PAD];
-  __shared__ float LL[LUM ? R * C + PAD : 1];
-  const int W = p.illum.W, row0 = p.illum.row0;
-  const float4* __restrict__ I = p.illum.p;
-  const float4* __restrict__ ND = p.nd.p;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int bx = blockIdx.x, g = blockIdx.y / S, b = blockIdx.y - g * S;
-  const int ybase = p.y0 + g * S * TJ + b;
-  const int jp = wv / NX, xl = (wv - jp * NX) * 64 + lane;
-  const int j = 2 * jp;  // tile rows j (pixel a) and j + 1 (pixel b)
-  const int x0 = bx * 64 * NX, x = x0 + xl, ya = ybase + S * j, yb = ya + S;
-  const bool own_a = x < p.W && ya < p.y1, own_b = x < p.W && yb < p.y1;
-  const size_t ca = (size_t)(ya - row0) * W + x, cb = ca + (size_t)S * W;
-  bool bg_a = true, bg_b = true;
-  float fwz_a = 0.0f, fwz_b = 0.0f;
-  const bool pre = AUX && p.tile_any != nullptr;
-  bool tile_any = true;
-  if (pre) tile_any = p.tile_any[(g * S + b) * gridDim.x + bx] != 0;
-  if (!pre) {
-    if (own_a) {
-      if (AUX) {
-        const float v = p.fwidth.aux[ca];
-        bg_a = aux_flag(v);
-        fwz_a = fabsf(v);
-      } else {
-        bg_a = ND[ca].w == 1.0f;
-        fwz_a = p.fwidth.p[ca].y;
-      }
-    }
-    if (own_b) {
-      if (AUX) {
-        const float v = p.fwidth.aux[cb];
-        bg_b = aux_flag(v);
-        fwz_b = fabsf(v);
-      } else {
-        bg_b = ND[cb].w == 1.0f;
-        fwz_b = p.fwidth.p[cb].y;
-      }
-    }
-    __shared__ int any_surface[NW];
-    const bool wave_any = __ballot(!bg_a || !bg_b) != 0ull;
-    if (lane == 0) any_surface[wv] = wave_any;
-    __syncthreads();
-    tile_any = false;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) tile_any |= any_surface[w] != 0;
-  }
-  if (!tile_any) {
-    if (own_a) {
-      const float4 v = I[ca];
-      p.out.p[ca] = v;
-      if (p.mod.p) modulate_store(p, x, ya, v, true);
-    }
-    if (own_b) {
-      const float4 v = I[cb];
-      p.out.p[cb] = v;
-      if (p.mod.p) modulate_store(p, x, yb, v, true);
-    }
-    return;
-  }
-  const int lo = max(0, row0), hi = min(p.H, row0 + p.illum.rows) - 1;
-  float aux_a = 0.0f, aux_b = 0.0f;
-  if (pre) {
-    const int cx = min(x, p.W - 1);
-    aux_a = p.fwidth.aux[(size_t)(min(ya, p.y1 - 1) - row0) * W + cx];
-    aux_b = p.fwidth.aux[(size_t)(min(yb, p.y1 - 1) - row0) * W + cx];
-  }
-  constexpr int NIT = (R * C + NT - 1) / NT;
-  float4 sv[NIT], sn[NIT];
-#pragma unroll
-  for (int k = 0; k < NIT; ++k) {
-    const int e = min(tid + k * NT, R * C - 1);
-    const int r = e / C, c = e - r * C;
-    int gy = ybase + S * (r - 2), gx = x0 - 2 * S + c;
-    gy = gy < lo ? lo : (gy > hi ? hi : gy);
-    gx = gx < 0 ? 0 : (gx >= p.W ? p.W - 1 : gx);
-    const size_t gi = (size_t)(gy - row0) * W + gx;
-    sv[k] = I[gi];
-    sn[k] = ND[gi];
-  }
-#pragma unroll
-  for (int k = 0; k < NIT; ++k) {
-    const int e = tid + k * NT < R * C ? tid + k * NT : R * C + (lane & (PAD - 1));
-    LI[e] = sv[k];
-    LN[e] = sn[k];
-    if (LUM) LL[e] = tap_luminance(sv[k]);
-  }
-  if (pre) {
-    if (own_a) {
-      bg_a = aux_flag(aux_a);
-      fwz_a = fabsf(aux_a);
-    }
-    if (own_b) {
-      bg_b = aux_flag(aux_b);
-      fwz_b = fabsf(aux_b);
-    }
-  }
-  __syncthreads();
-  if (!own_a) return;  // (own_b implies own_a)
-  const float4* Li = LI + j * C + xl;  // top-left tap of pixel a's window; pixel b's is one tile row below
-  const float4* Ln = LN + j * C + xl;
-  const float* Ll = LL + (LUM ? j * C + xl : 0);
-  const float4 ic_a = Li[2 * C + 2 * S], ic_b = Li[3 * C + 2 * S];
-  const bool edge =
-      x0 - 2 * S < 0 || x0 + 64 * NX - 1 + 2 * S >= p.W || ybase - 2 * S < 0 || ybase + S * (TJ + 1) >= p.H;
-  if (bg_a && (bg_b || !own_b)) {  // nothing to filter in this lane
-    p.out.p[ca] = ic_a;
-    if (p.mod.p) modulate_store(p, x, ya, ic_a, true);
-    if (own_b) {
-      p.out.p[cb] = ic_b;
-      if (p.mod.p) modulate_store(p, x, yb, ic_b, true);
-    }
-    return;
-  }
-  TapPixel pa, pb;
-  pa.init(ic_a, Ln[2 * C + 2 * S], fwz_a, p.phi_color, S);
-  pb.init(ic_b, Ln[3 * C + 2 * S], fwz_b, p.phi_color, S);
-  if (__builtin_expect(!edge && (bg_a || !pa.flat) && (bg_b || !pb.flat), 1)) {
-    window_pair<S, C, LUM>(pa, pb, Li, Ln, Ll, p.phi_normal);
-  } else {
-    if (!bg_a) {
-      if (!pa.flat) {
-        if (!edge) pa.window<false, false, S, C, LUM>(Li, Ln, Ll, x, ya, p.W, p.H, p.phi_normal);
-        else pa.window<false, true, S, C, LUM>(Li, Ln, Ll, x, ya, p.W, p.H, p.phi_normal);
-      } else {
-        pa.window<true, true, S, C, LUM>(Li, Ln, Ll, x, ya, p.W, p.H, p.phi_normal);
-      }
-    }
-    if (!bg_b && own_b) {
-      if (!pb.flat) {
-        if (!edge) pb.window<false, false, S, C, LUM>(Li + C, Ln + C, Ll + (LUM ? C : 0), x, yb, p.W, p.H, p.phi_normal);
-        else pb.window<false, true, S, C, LUM>(Li + C, Ln + C, Ll + (LUM ? C : 0), x, yb, p.W, p.H, p.phi_normal);
-      } else {
-        pb.window<true, true, S, C, LUM>(Li + C, Ln + C, Ll + (LUM ? C : 0), x, yb, p.W, p.H, p.phi_normal);
-      }
-    }
-  }
-  const float4 ra = bg_a ? ic_a : pa.result();
-  p.out.p[ca] = ra;
-  if (p.mod.p) modulate_store(p, x, ya, ra, bg_a);
-  if (own_b) {
-    const float4 rb = bg_b ? ic_b : pb.result();
-    p.out.p[cb] = rb;
-    if (p.mod.p) modulate_store(p, x, yb, rb, bg_b);
-  }
-}
-
 // Tile flags of the five step sizes (atrous_tile_kernel's tiles: S = 1 << si, NX = tile_nx<S>(), TJ = tile_tj<S>() rows of one
 // residue class): byte (g * S + b) * NXT + bx of step si is 1 iff an owned pixel of that tile is a surface pixel
 // (the depth-fwidth plane's sign bit clear). One wave per 64 columns of a row; a ballot, then one byte store per step.
@@ -693,11 +513,6 @@ static void launch_tile_s(const AtrousParams& p, bool aux, hipStream_t s) {
   constexpr int NX = tile_nx<S>(), TJ = tile_tj<S>();
   const int groups = (p.y1 - p.y0 + S * TJ - 1) / (S * TJ);
   dim3 grid((p.W + 64 * NX - 1) / (64 * NX), groups * S);
-  if (p.rows2) {
-    if (aux) hipLaunchKernelGGL((atrous_tile2_kernel<S, true>), grid, dim3(32 * TJ * NX), 0, s, p);
-    else hipLaunchKernelGGL((atrous_tile2_kernel<S, false>), grid, dim3(32 * TJ * NX), 0, s, p);
-    return;
-  }
   if (aux) hipLaunchKernelGGL((atrous_tile_kernel<S, true>), grid, dim3(64 * TJ * NX), 0, s, p);
   else hipLaunchKernelGGL((atrous_tile_kernel<S, false>), grid, dim3(64 * TJ * NX), 0, s, p);
 }

@@ -284,7 +284,6 @@ struct AtrousParams {
   // fused modulate (the last iteration of a frame, fast driver): mod.p != null writes modulate_kernel's output of
   // this draw's rows from `out`'s values, albedo and emission (every plane must store the draw's rows)
   Plane albedo, emission, mod;
-  int rows2;  // tiled kernel: two tile rows per lane (atrous_tile2_kernel), else one
 };
 // Tiles of the tiled a-trous (kernels_atrous.hip): 64 * NX columns x TJ rows of one residue class mod S, one wave
 // per 64-column strip of a tile row (64 * TJ * NX <= 1024 threads); tile (g, b, bx) of step S has byte

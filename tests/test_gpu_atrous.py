@@ -112,13 +112,12 @@ def test_interior_tiles_cover_every_step():
 @pytest.mark.parametrize("size", SIZES)
 @pytest.mark.parametrize("step", [1, 2, 4, 8, 16])
 def test_tile_kernel_equals_step_kernel(gpu, step, size):
-    """The LDS-tiled kernels (variant 0: two tile rows per lane by default, atrous_rows = 1 one; with and without the
-    per-tile surface flags; interior tiles run the taps as straight-line code, border tiles test each tap) perform the
-    step kernel's (variant 2) arithmetic in the same tap order: identical bits, NaNs included."""
+    """The LDS-tiled kernel (variant 0, with and without the per-tile surface flags; its interior tiles run the taps
+    as straight-line code, border tiles test each tap) performs the step kernel's (variant 2) arithmetic in the same
+    tap order: identical bits, NaNs included."""
     illum, nd, fw = _planes(seed=5, W=size[0], H=size[1])
     b = _run(gpu, illum, nd, fw, step, 2)
-    cases = [(0, {}), (0, dict(atrous_tile_flags=0)), (0, dict(atrous_rows=1)),
-             (0, dict(atrous_rows=1, atrous_tile_flags=0))]
+    cases = [(0, {}), (0, dict(atrous_tile_flags=0))]
     for v, kw in cases:
         a = _run(gpu, illum, nd, fw, step, v, **kw)
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (v, kw)
