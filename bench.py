@@ -122,9 +122,10 @@ def parse():
                     help="--shard frames: consecutive frames one rank traces (frame f on rank (f // burst) %% N)")
     ap.add_argument("--ship-gbuffer", type=int, default=0, choices=(0, 1),
                     help="--shard frames: the tracing rank also sends the bands their G-buffer rows (they draw none)")
-    ap.add_argument("--own-slots", type=int, default=4,
+    ap.add_argument("--own-slots", type=int, default=2,
                     help="--shard frames / tiles: whole frames / tile subsets a rank traces at once (its path tracer's "
-                         "frames in flight)")
+                         "frames in flight); 8-rank 4K simulation, K 16: 2 -> 0.856 ms per frame, 4 -> 0.879 "
+                         "(profiles/r05/shard/sim_own2_k16.log, sim_w4_k16_onecmp.log)")
     ap.add_argument("--host-pace", type=int, default=1, choices=(0, 1),
                     help="one GPU: the host waits for frame f - K's SVGF before issuing frame f (Renderer host_pace): "
                          "camera-to-modulate 36 -> 18 ms at 4K, same frame rate (profiles/r04/pace/)")
