@@ -359,6 +359,7 @@ __global__ void __launch_bounds__(256) wf_primary_raster(PTParams p) {
   __shared__ float4 slo[kPChunk], shi[kPChunk];
   __shared__ int4 sbox[kPChunk];
   __shared__ float stmin[kPChunk];
+  __shared__ short wlist[4][kPChunk];  // per wave: the chunk's leaves that can meet its pixels
   const Bins& bn = p.leaf_bins;
   if (bn.ctr[2]) return;  // overflow: wf_primary walks every pixel
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
@@ -424,8 +425,30 @@ __global__ void __launch_bounds__(256) wf_primary_raster(PTParams p) {
       stmin[slot] = tm;
     }
     __syncthreads();
+    // this wave's share of the chunk: the staged leaves whose pixel box meets the wave's 8 x 8 pixels and that are not
+    // entered beyond the loosest of its pixels' pruning bounds, in chunk order (the closest t, a unique closest
+    // triangle and an exact tie met do not depend on the order the candidates are tested in); each lane then steps
+    // through that list instead of the whole chunk
+    float wl = valid ? tbest * 1.0002f + 2.0e-4f : 0.0f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wl = fmaxf(wl, __shfl_xor(wl, o));
+    const int wx0 = x - (ln & 7), wy0 = y - (ln >> 3);
+    int wn = 0;
+    for (int k0 = 0; k0 < n; k0 += 64) {
+      const int k = k0 + ln;
+      bool ov = false;
+      if (k < n) {
+        const int4 b = sbox[k];
+        ov = !(b.z < wx0 || b.x > wx0 + 7 || b.w < wy0 || b.y > wy0 + 7) && !(stmin[k] > wl);
+      }
+      const unsigned long long m = __ballot(ov);
+      if (ov) wlist[wv][wn + __popcll(m & ((1ull << ln) - 1ull))] = (short)k;
+      wn += __popcll(m);
+    }
+    __syncthreads();
     if (!valid) continue;
-    for (int k = 0; k < n; ++k) {
+    for (int i = 0; i < wn; ++i) {
+      const int k = wlist[wv][i];
       const int4 b = sbox[k];
       if (x < b.x || x > b.z || y < b.y || y > b.w) continue;  // no primary ray of this pixel passes the box
       const float lim = tbest * 1.0002f + 2.0e-4f;                // the walk's pruning bound (traverse<0>)
