@@ -1032,7 +1032,12 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTP
 // The shadow rays wf_trace_shadow deferred: one wave per ray walks cooperatively (shadow_coop_walk). A fixed
 // grid strides over the straggler list (its length is known only on the device).
 constexpr int kCoopWaves = 4;          // waves per block
-constexpr int kCoopBlocks = 512;       // 2048 waves in flight
+#ifndef PT_COOP_BLOCKS
+#define PT_COOP_BLOCKS 512
+#endif
+// 2048 waves in flight; 1024 / 2048 blocks measured within noise (profiles/r05/coop_blocks/: 4K 229.1 / 229.6 / 229.5 fps,
+// surface view 78.8 / 78.9 / 79.0, one frame at a time 166.3 / 166.4 / 167.1)
+constexpr int kCoopBlocks = PT_COOP_BLOCKS;
 constexpr int kCoopCap = 1024;         // LDS stack entries per wave
 __global__ void __launch_bounds__(64 * kCoopWaves) wf_shadow_coop(PTParams p, const int* __restrict__ strag_count) {
   __shared__ int st[kCoopWaves][kCoopCap];
