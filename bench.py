@@ -122,10 +122,11 @@ def parse():
                     help="--shard frames: consecutive frames one rank traces (frame f on rank (f // burst) %% N)")
     ap.add_argument("--ship-gbuffer", type=int, default=0, choices=(0, 1),
                     help="--shard frames: the tracing rank also sends the bands their G-buffer rows (they draw none)")
-    ap.add_argument("--own-slots", type=int, default=2,
+    ap.add_argument("--own-slots", type=int, default=None,
                     help="--shard frames / tiles: whole frames / tile subsets a rank traces at once (its path tracer's "
-                         "frames in flight); 8-rank 4K simulation, K 16: 2 -> 0.856 ms per frame, 4 -> 0.879 "
-                         "(profiles/r05/shard/sim_own2_k16.log, sim_w4_k16_onecmp.log)")
+                         "frames in flight); default 2 above 4 ranks, else 4 (4K simulation, profiles/r05/shard/: "
+                         "8 ranks K 16: 2 -> 0.856 ms per frame, 4 -> 0.879; 4 ranks K 12: 1.659 / 1.529; 2 ranks "
+                         "K 12: 3.851 / 2.967)")
     ap.add_argument("--host-pace", type=int, default=1, choices=(0, 1),
                     help="one GPU: the host waits for frame f - K's SVGF before issuing frame f (Renderer host_pace): "
                          "camera-to-modulate 36 -> 18 ms at 4K, same frame rate (profiles/r04/pace/)")
@@ -348,6 +349,10 @@ def main():
             args.frames_in_flight = k1080 = 8
     if args.trace_batch is None:
         args.trace_batch = 1
+    if args.own_slots is None:
+        # a rank's own frames come N frames apart: with few ranks its path tracers overlap only with 4 slots, with 8
+        # the fourth-oldest slot only crowds the band's SVGF chain (simulated, see --own-slots)
+        args.own_slots = 2 if world > 4 else 4
     if args.window is None and world > 1 and args.shard == "frames":
         args.window = min(world, 4)  # a back end waits for 4 frames' rows, not N (DESIGN.md "Which partition")
     # every frame slot must have run once before the timed region (a slot's first frame allocates its
@@ -482,7 +487,7 @@ def main():
             dist.all_reduce(mx, op=dist.ReduceOp.MAX)
             out["bands"] = {"shard": args.shard, "ship_gbuffer": bool(getattr(r, "ship_gbuffer", False)),
                             "window": getattr(r, "window", None), "burst": getattr(r, "burst", None),
-                            "tile_batch": getattr(r, "batch", None),
+                            "tile_batch": getattr(r, "batch", None), "own_slots": getattr(r, "own_slots", None),
                             "bounds": list(r.plan.bounds), "back_lag": r.r.lag,
                             "frames_in_flight": r.r.K,
                             "exchange_ms_per_frame": {k: round(v, 4) for k, v in zip(EXCHANGE_STAGES, mx.tolist())
