@@ -105,8 +105,10 @@ def parse():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for --gpus > 1 (nccl = RCCL)")
     ap.add_argument("--no-band-parity", action="store_true",
                     help="multi-GPU: skip the untimed bitwise check of the gathered bands against a one-GPU frame")
-    ap.add_argument("--equal-bands", action="store_true",
-                    help="multi-GPU: equal band heights (no balancing of the measured band work)")
+    ap.add_argument("--equal-bands", type=int, default=None, choices=(0, 1),
+                    help="multi-GPU: 1 = equal band heights (no balancing of the measured band work); default 1 for "
+                         "the frame shard on 2 ranks (its bytes, not its band work, set the frame: simulated 357 vs "
+                         "337 fps at 4K, profiles/r05/shard/sim_n2_own4_k12.log), else 0")
     ap.add_argument("--shard", default="frames", choices=("frames", "tiles", "bands"),
                     help="multi-GPU: 'frames' = rank f %% N traces frame f whole and scatters its rows to the band owners, "
                          "the SVGF chain banded (dist.FrameShardRenderer); 'tiles' = every rank traces the 16x16 tiles "
@@ -349,6 +351,8 @@ def main():
             args.frames_in_flight = k1080 = 8
     if args.trace_batch is None:
         args.trace_batch = 1
+    if args.equal_bands is None:
+        args.equal_bands = 1 if (world == 2 and args.shard == "frames") else 0
     if args.own_slots is None:
         # a rank's own frames come N frames apart: with few ranks its path tracers overlap only with 4 slots, with 8
         # the fourth-oldest slot only crowds the band's SVGF chain (simulated, see --own-slots)

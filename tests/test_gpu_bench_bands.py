@@ -52,7 +52,7 @@ def test_bench_band_parity_gloo(world, moving, balance, shard):
     cmd += ["--window", "1", "--frames-in-flight", "6"] if w1 else []
     cmd += ["--burst", "2"] if b2 else []
     cmd += ["--tile-batch", "3"] if tb3 else []
-    cmd += [] if balance else ["--equal-bands"]
+    cmd += ["--equal-bands", "0" if balance else "1"]
     p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-4000:]
     line = json.loads(p.stdout.strip().splitlines()[-1])
@@ -94,7 +94,7 @@ def test_bench_frame_shard_8_ranks_gloo(W, H, balance):
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "bench.py"),
            "--gpus", str(world), "--backend", "gloo", "--width", str(W), "--height", str(H), "--steps", "16",
            "--warmup", "2", "--no-extras", "--no-1080p", "--no-cpu-baseline", "--shard", "frames", "--moving"]
-    cmd += [] if balance else ["--equal-bands"]
+    cmd += ["--equal-bands", "0" if balance else "1"]
     p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=850)
     assert p.returncode == 0, p.stderr[-4000:]
     line = json.loads(p.stdout.strip().splitlines()[-1])

@@ -6,7 +6,7 @@ W=${W:-3840}; H=${H:-2160}
 P=$(python3 -c "import socket; s=socket.socket(); s.bind(('127.0.0.1',0)); print(s.getsockname()[1])")
 timeout -k 10 ${T:-900} python3 -m torch.distributed.run --nnodes=1 --nproc-per-node=8 --master-addr 127.0.0.1 \
   --master-port=$P "$R/bench.py" --gpus 8 --backend gloo --width $W --height $H --steps 16 --warmup 2 --no-extras \
-  --no-1080p --no-cpu-baseline --moving --equal-bands > "$R/gpurun_out/rehearse8_${W}x${H}.json" \
+  --no-1080p --no-cpu-baseline --moving --equal-bands 1 > "$R/gpurun_out/rehearse8_${W}x${H}.json" \
   2> "$R/gpurun_out/rehearse8_${W}x${H}.err"
 rc=$?
 python3 -c "
