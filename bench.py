@@ -126,9 +126,9 @@ def parse():
                     help="--shard frames: the tracing rank also sends the bands their G-buffer rows (they draw none)")
     ap.add_argument("--own-slots", type=int, default=None,
                     help="--shard frames / tiles: whole frames / tile subsets a rank traces at once (its path tracer's "
-                         "frames in flight); default 2 above 4 ranks, else 4 (4K simulation, profiles/r05/shard/: "
-                         "8 ranks K 16: 2 -> 0.856 ms per frame, 4 -> 0.879; 4 ranks K 12: 1.659 / 1.529; 2 ranks "
-                         "K 12: 3.851 / 2.967)")
+                         "frames in flight); default 2 above 4 ranks, 3 for 3-4, 4 for 2 (4K simulation, "
+                         "profiles/r05/shard/, ms per frame for 2 / 3 / 4 slots: 8 ranks K 16 0.856-0.863 / 0.948 / "
+                         "0.879; 4 ranks K 12 1.659 / 1.477 / 1.529; 2 ranks K 12 3.851 / - / 2.967)")
     ap.add_argument("--host-pace", type=int, default=1, choices=(0, 1),
                     help="one GPU: the host waits for frame f - K's SVGF before issuing frame f (Renderer host_pace): "
                          "camera-to-modulate 36 -> 18 ms at 4K, same frame rate (profiles/r04/pace/)")
@@ -354,9 +354,9 @@ def main():
     if args.equal_bands is None:
         args.equal_bands = 1 if (world == 2 and args.shard == "frames") else 0
     if args.own_slots is None:
-        # a rank's own frames come N frames apart: with few ranks its path tracers overlap only with 4 slots, with 8
-        # the fourth-oldest slot only crowds the band's SVGF chain (simulated, see --own-slots)
-        args.own_slots = 2 if world > 4 else 4
+        # a rank's own frames come N frames apart: with few ranks its path tracers overlap only with several slots,
+        # with 8 a third or fourth slot only crowds the band's SVGF chain (simulated, see --own-slots)
+        args.own_slots = 2 if world > 4 else 3 if world > 2 else 4
     if args.window is None and world > 1 and args.shard == "frames":
         args.window = min(world, 4)  # a back end waits for 4 frames' rows, not N (DESIGN.md "Which partition")
     # every frame slot must have run once before the timed region (a slot's first frame allocates its
