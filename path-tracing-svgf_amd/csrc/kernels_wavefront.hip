@@ -355,7 +355,18 @@ __global__ void __launch_bounds__(256) pr_setup(PTParams p) {
   bins_count_item(p.leaf_bins, i, box, tmin);
 }
 
-__global__ void __launch_bounds__(256) wf_primary_raster(PTParams p) {
+#ifndef PT_RASTER_WAVES
+// waves/SIMD wf_primary_raster is compiled for (0: the compiler's choice, 67 VGPRs = 7 waves). 8 (64 VGPRs, no spill)
+// measured the same (kernel trace, one frame at a time: 916.6 / 921.3 us, surface view 666.3 / 658.9; with PT_SHADE_WAVES
+// 6 as well the frame rate fell 0.5 %: profiles/r05/occupancy_r8/)
+#define PT_RASTER_WAVES 0
+#endif
+#if PT_RASTER_WAVES > 0
+#define PT_RASTER_ATTR __attribute__((amdgpu_waves_per_eu(PT_RASTER_WAVES)))
+#else
+#define PT_RASTER_ATTR
+#endif
+__global__ void __launch_bounds__(256) PT_RASTER_ATTR wf_primary_raster(PTParams p) {
   __shared__ float4 slo[kPChunk], shi[kPChunk];
   __shared__ int4 sbox[kPChunk];
   __shared__ float stmin[kPChunk];
