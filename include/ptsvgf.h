@@ -158,12 +158,6 @@ typedef struct {
 } PtTileSeg;
 int pt_tiles_count(int frame_w, int tile_y0, int stride, int offset, int y_begin, int y_end, int64_t* out_pixels);
 int pt_tiles_copy(const uint32_t* tex, int ntex, int tile_y0, int stride, const PtTileSeg* segs, int nseg, int unpack);
-/* Frame shard (multi-GPU, no GL counterpart): rows [y_begin, y_end) of 1..4 textures (RGBA32F, one width; the path
- * tracer's colour / emission / albedo, alpha 1.0 in every texel) as their rgb channels, texture after texture, each
- * row after row: (y_end - y_begin) * width * 3 floats per texture. unpack = 0 writes `packed` (16-B aligned) from the
- * textures, 1 writes the textures' rgb from it and their alpha 1.0. Asynchronous on the library stream; the rows must
- * lie in every texture's stored rows. */
-int pt_rows_rgb_copy(const uint32_t* tex, int ntex, int y_begin, int y_end, void* packed, int unpack);
 int pt_pass_reset_texture_slot(uint32_t pass);
 int pt_pass_set_texture(uint32_t pass, uint32_t target, uint32_t tex, const char* name);
 int pt_pass_set_uniform_mat4(uint32_t pass, const char* name, const float* m16);

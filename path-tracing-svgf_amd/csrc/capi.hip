@@ -2286,38 +2286,6 @@ int pt_tiles_copy(const uint32_t* tex, int ntex, int tile_y0, int stride, const 
   return PT_OK;
 }
 
-int pt_rows_rgb_copy(const uint32_t* tex, int ntex, int y_begin, int y_end, void* packed, int unpack) {
-  std::lock_guard<std::recursive_mutex> lk(g_mu);
-  TRY(ensure_init());
-  if (!tex || ntex < 1 || ntex > 4 || y_begin > y_end || (!packed && y_end > y_begin) ||
-      ((uintptr_t)packed & 15u) != 0)
-    return err(PT_ERR_ARG, "pt_rows_rgb_copy: 1..4 textures, y_begin <= y_end, a 16-B aligned buffer");
-  ptk::RgbRows c;
-  memset(&c, 0, sizeof(c));
-  c.y0 = y_begin;
-  c.y1 = y_end;
-  c.nplanes = ntex;
-  c.unpack = unpack ? 1 : 0;
-  c.packed = (float*)packed;
-  Texture* ts[4] = {nullptr, nullptr, nullptr, nullptr};
-  for (int j = 0; j < ntex; ++j) {
-    Texture* t = tex_of(tex[j]);
-    if (!t || t->target != PT_TEXTURE_2D || !t->dev) return err(PT_ERR_INVALID_HANDLE, "pt_rows_rgb_copy: invalid texture");
-    if (j > 0 && t->W != ts[0]->W) return err(PT_ERR_ARG, "pt_rows_rgb_copy: textures of different widths");
-    if (y_end > y_begin && (y_begin < t->row0 || y_end > t->row0 + t->rows))
-      return err(PT_ERR_ARG, "pt_rows_rgb_copy: rows outside a texture's stored rows");
-    ts[j] = t;
-    c.plane[j] = (float4*)t->dev;
-    c.row0[j] = t->row0;
-  }
-  c.W = ts[0]->W;
-  const int rc = ptk::launch_rgb_rows(c, g.stream);
-  if (rc) return hip_err((hipError_t)rc, "pt_rows_rgb_copy");
-  if (unpack)
-    for (int j = 0; j < ntex; ++j) ts[j]->version++;  // new texels, as after a draw
-  return PT_OK;
-}
-
 int pt_pass_reset_texture_slot(uint32_t pass) {
   Pass* p = pass_of(pass);
   if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");

@@ -61,51 +61,6 @@ __global__ void __launch_bounds__(256) shard_copy_kernel(ShardCopy c) {
   }
 }
 
-// Rows of the frame shard's planes as rgb (RgbRows): a thread moves 4 consecutive texels of one plane, 4 float4 on
-// the plane side and 3 float4 (their 12 floats) on the packed side, so both sides move whole 16-B vectors (a texel
-// count that is not a multiple of 4 ends in a scalar tail). Unpacking writes alpha 1.0.
-__global__ void __launch_bounds__(256) rgb_rows_kernel(RgbRows c) {
-  const int j = blockIdx.y;
-  const long long n = (long long)(c.y1 - c.y0) * c.W;  // texels per plane
-  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // group of 4 texels
-  if (4 * q >= n) return;
-  float4* plane = c.plane[j] + (size_t)(c.y0 - c.row0[j]) * c.W;
-  float* packed = c.packed + (size_t)j * n * 3;
-  if (4 * q + 4 <= n && n % 4 == 0) {
-    float4* pk = (float4*)packed + 3 * q;  // 16-B aligned: n a multiple of 4, and the buffer is
-    if (c.unpack) {
-      const float4 a = pk[0], b = pk[1], d = pk[2];
-      plane[4 * q + 0] = make_float4(a.x, a.y, a.z, 1.0f);
-      plane[4 * q + 1] = make_float4(a.w, b.x, b.y, 1.0f);
-      plane[4 * q + 2] = make_float4(b.z, b.w, d.x, 1.0f);
-      plane[4 * q + 3] = make_float4(d.y, d.z, d.w, 1.0f);
-    } else {
-      const float4 t0 = plane[4 * q + 0], t1 = plane[4 * q + 1], t2 = plane[4 * q + 2], t3 = plane[4 * q + 3];
-      pk[0] = make_float4(t0.x, t0.y, t0.z, t1.x);
-      pk[1] = make_float4(t1.y, t1.z, t2.x, t2.y);
-      pk[2] = make_float4(t2.z, t3.x, t3.y, t3.z);
-    }
-    return;
-  }
-  for (long long i = 4 * q; i < n && i < 4 * q + 4; ++i) {
-    if (c.unpack) plane[i] = make_float4(packed[3 * i], packed[3 * i + 1], packed[3 * i + 2], 1.0f);
-    else {
-      const float4 t = plane[i];
-      packed[3 * i] = t.x;
-      packed[3 * i + 1] = t.y;
-      packed[3 * i + 2] = t.z;
-    }
-  }
-}
-
-int launch_rgb_rows(const RgbRows& c, hipStream_t s) {
-  const long long n = (long long)(c.y1 - c.y0) * c.W;
-  if (n <= 0 || c.nplanes <= 0) return 0;
-  const long long groups = (n + 3) / 4;
-  hipLaunchKernelGGL(rgb_rows_kernel, dim3((unsigned)((groups + 255) / 256), c.nplanes), dim3(256), 0, s, c);
-  return (int)hipGetLastError();
-}
-
 long long shard_pixels(int W, int tile_y0, int stride, int offset, int y0, int y1) {
   return shard_row_offset(y0, y1, tile_y0, W / 16, stride, offset);
 }

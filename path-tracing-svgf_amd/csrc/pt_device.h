@@ -345,14 +345,6 @@ struct ShardCopy {
   int row0[4];
   ShardSeg seg[kShardSegs];
 };
-// Frame shard (dist.exchange_window): rows [y0, y1) of up to 4 planes (the path tracer's colour / emission / albedo,
-// whose alpha is 1.0 in every texel) as their rgb channels, packed plane after plane: 12 B a texel on the wire.
-struct RgbRows {
-  int W, y0, y1, nplanes, unpack;
-  float4* plane[4];
-  int row0[4];
-  float* packed;
-};
 
 }  // namespace ptk
 
@@ -360,7 +352,6 @@ struct RgbRows {
 namespace ptk {
 // Launchers (kernels_*.hip). Return hipError_t as int.
 int launch_shard_copy(const ShardCopy& c, hipStream_t s);
-int launch_rgb_rows(const RgbRows& c, hipStream_t s);
 long long shard_pixels(int W, int tile_y0, int stride, int offset, int y0, int y1);  // per plane
 int launch_pathtrace(const PTParams& p, hipStream_t s);
 // A side stream for the wavefront's bounce-0 shadow rays: they and the bounce-1 closest-hit rays both come from the

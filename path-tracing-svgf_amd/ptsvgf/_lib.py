@@ -100,7 +100,6 @@ _PT_SIGS = [
     ("pt_raster_pass_adopt", C.c_int, [_u32, C.c_int, C.c_int]),
     ("pt_tiles_count", C.c_int, [C.c_int] * 6 + [C.POINTER(C.c_int64)]),
     ("pt_tiles_copy", C.c_int, [_u32p, C.c_int, C.c_int, C.c_int, _vp, C.c_int, C.c_int]),
-    ("pt_rows_rgb_copy", C.c_int, [_u32p, C.c_int, C.c_int, C.c_int, _vp, C.c_int]),
     ("pt_pass_reset_texture_slot", C.c_int, [_u32]),
     ("pt_pass_set_texture", C.c_int, [_u32, _u32, _u32, C.c_char_p]),
     ("pt_pass_set_uniform_mat4", C.c_int, [_u32, C.c_char_p, _fp]),

@@ -732,13 +732,7 @@ def scatter_group(dist):
     return hit[1]
 
 
-# The path tracer's planes (colour, emission, albedo) lead a window entry's planes; with `rgb` they cross the links as
-# their rgb channels only (pt_rows_rgb_copy: the path tracer writes alpha 1.0 in every texel, the receiver writes it
-# back), 36 instead of 48 bytes a texel.
-WINDOW_RGB_PLANES = 3
-
-
-def exchange_window(window, plan: BandPlan, dist, group=None, rows=None, rgb=None) -> int:
+def exchange_window(window, plan: BandPlan, dist, group=None, rows=None) -> int:
     """The point-to-point transfers of one frame-shard window: consecutive frames (frame f is traced by rank
     (f // burst) % N, so a source holds up to min(burst, window) of them, each in its own slot). window = [(src,
     planes)] in frame order: for a frame this rank traced, planes are its whole-frame
@@ -746,48 +740,25 @@ def exchange_window(window, plan: BandPlan, dist, group=None, rows=None, rgb=Non
     margin) go to that band's owner; for a frame rank src traced, planes are this band's zone rows, received from src. Every rank builds the same window, so the batch is symmetric: an
     all-to-all over the window's sources, every link busy at once, one communicator. rows[j](k) (default plan.zone):
     the rows of band k plane j carries. RCCL: the current stream waits for the batch; gloo (tests): blocking, device
-    tensors staged through host memory. Returns the bytes sent.
-    rgb (device planes only): per window entry the library texture handles of its first WINDOW_RGB_PLANES planes (the
-    whole-frame planes of this rank's frames, the band's slot textures of the others): those planes travel as rgb
-    in one packed buffer per (frame, peer), packed and unpacked on the library stream, which must be the current one."""
+    tensors staged through host memory. Returns the bytes sent."""
     import torch
 
-    if rgb:
-        from . import gl
     gloo = dist.get_backend(group) == "gloo"
-    ops, staged, unpack, nbytes = [], [], [], 0
-    for e, (src, planes) in enumerate(window):
-        handles = rgb[e] if rgb else None
-        first = WINDOW_RGB_PLANES if handles else 0  # planes of this entry that travel packed
+    ops, staged, nbytes = [], [], 0
+    for src, planes in window:
         if src == plan.rank:
             for k in range(plan.world):
                 if k == plan.rank:
                     continue
-                parts = []
-                if first:
-                    y0, y1 = (rows[0] if rows else plan.zone)(k)
-                    buf = torch.empty((first, y1 - y0, planes[0].shape[1], 3), dtype=torch.float32,
-                                      device=planes[0].device)
-                    gl.rows_rgb_copy(handles, y0, y1, buf.data_ptr(), unpack=False)
-                    parts.append(buf)
-                for j in range(first, len(planes)):
+                for j, t in enumerate(planes):
                     y0, y1 = (rows[j] if rows else plan.zone)(k)
-                    parts.append(planes[j][y0:y1])
-                for part in parts:
+                    part = t[y0:y1]
                     if gloo and part.is_cuda:
                         part = part.cpu()
                     ops.append(dist.P2POp(dist.isend, part, k, group))
                     nbytes += part.numel() * part.element_size()
         else:
-            bufs = []
-            if first:
-                t = planes[0]
-                z0, z1 = plan.zone(plan.rank)
-                packed = torch.empty((first, t.shape[0], t.shape[1], 3), dtype=torch.float32, device=t.device)
-                unpack.append((handles, z0, z1, packed))
-                bufs.append(packed)
-            bufs += list(planes[first:])
-            for t in bufs:
+            for t in planes:
                 buf = t
                 if gloo and t.is_cuda:
                     buf = torch.empty(t.shape, dtype=t.dtype)
@@ -798,8 +769,6 @@ def exchange_window(window, plan: BandPlan, dist, group=None, rows=None, rgb=Non
             w.wait()
     for t, h in staged:
         t.copy_(h)
-    for handles, z0, z1, packed in unpack:  # (RCCL: on the current stream, behind the batch)
-        gl.rows_rgb_copy(handles, z0, z1, packed.data_ptr(), unpack=True)
     return nbytes
 
 
@@ -828,8 +797,7 @@ class FrameShardRenderer(BandRenderer):
     GBUF_PLANES = (1, 2, 3)  # G-buffer attachments the SVGF chain reads: normal/depth, motion, depth-fwidth
 
     def __init__(self, scene, W, H, cfg, rank, world, dist, own_slots: int = 2, ship_gbuffer: bool | None = None,
-                 window: int | None = None, burst: int = 1, own_budget: int = 0, own_refill_waves: int = 0,
-                 pack_rgb: bool | None = None, **kw):
+                 window: int | None = None, burst: int = 1, own_budget: int = 0, own_refill_waves: int = 0, **kw):
         """burst (default 1): consecutive frames one rank traces, frame f on rank (f // burst) % N. With 2 a rank's
         two path tracers are issued one frame apart and overlap (their launch tails fill each other's idle CUs, as frames
         in flight do on one GPU) instead of starting N frames apart.
@@ -846,9 +814,6 @@ class FrameShardRenderer(BandRenderer):
         against 0.01 for the adoption, for twice the window's bytes (≈ 150 MB per window and link at 8 ranks); the
         8-rank simulation measured it within noise (0.93-1.11 vs 0.90-0.99 ms per frame,
         profiles/r03/frame_shard/fs_ship*.log), so it stays an option.
-
-        pack_rgb (default on): the window exchange carries the path tracer's planes as rgb (12 instead of 16 bytes a
-        texel, packed and unpacked by pt_rows_rgb_copy on the receive stream; exchange_window's rgb).
 
         own_budget / own_refill_waves (0: the one-GPU settings, renderer.VISIT_BUDGET and the whole chip): the
         whole-frame path tracer's cooperative-walk visit budget (shadow_budget / closest_budget) and the resident waves
@@ -920,7 +885,6 @@ class FrameShardRenderer(BandRenderer):
         self._sgroup = scatter_group(dist) if world > 1 else None
         self._recv_stream = acquire_stream()
         self.scatter_log = []  # per exchange that carried a frame of this rank: bytes sent
-        self.pack_rgb = True if pack_rgb is None else bool(pack_rgb)
 
     def source(self, f: int) -> int:
         """The rank that traces frame f."""
@@ -949,7 +913,7 @@ class FrameShardRenderer(BandRenderer):
         if self.ship_gbuffer:  # (drawn G-buffers note their frame in _after_gbuffer)
             self._note_frame(gset)
         item = dict(src=self.source(f), outs=[self._band_rows(h) for h in r.pt_slots[slot][1]],
-                    h=list(r.pt_slots[slot][1]), free=r._slot_free[f % r.K], holder=holder, gset=gset)
+                    free=r._slot_free[f % r.K], holder=holder, gset=gset)
         if self.ship_gbuffer:
             g0, g1 = p.gbuffer_rows()
             ip = r.init_pass[gset]
@@ -975,7 +939,7 @@ class FrameShardRenderer(BandRenderer):
             ev = torch.cuda.Event()
             ev.record(rs)
             holder["ev"] = ev
-            item.update(o=o, full=full, fh=list(self.full.pt_slots[o][1]))
+            item.update(o=o, full=full)
         self._win.append(item)
         return holder
 
@@ -1005,20 +969,15 @@ class FrameShardRenderer(BandRenderer):
             if it["src"] != p.rank and it["free"] is not None:
                 rs.wait_event(it["free"])
         window = [(it["src"], it["full"] if it["src"] == p.rank else it["outs"]) for it in win]
-        cur = self.r._lib_stream
-        rgb = None
-        if self.pack_rgb:  # the packing draws run on the receive stream, as the exchange does
-            rgb = [it["fh"] if it["src"] == p.rank else it["h"] for it in win]
-            self.r._stream_to(rs)
         with torch.cuda.stream(rs):
-            nbytes = (exchange_window(window, p, self.dist, self._sgroup, rows=self._plane_rows(), rgb=rgb)
-                      if p.world > 1 else 0)
+            nbytes = exchange_window(window, p, self.dist, self._sgroup, rows=self._plane_rows()) if p.world > 1 else 0
         if self.ship_gbuffer:
+            cur = self.r._lib_stream
             for it in win:
                 if it["src"] != p.rank:
                     self._adopt(it["gset"], rs)
-        if (self.pack_rgb or self.ship_gbuffer) and cur is not None:
-            self.r._stream_to(cur)
+            if cur is not None:
+                self.r._stream_to(cur)
         ev = torch.cuda.Event()
         ev.record(rs)
         for it in win:

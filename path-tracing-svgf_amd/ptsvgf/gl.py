@@ -125,13 +125,6 @@ def tiles_copy(textures, stride: int, segs, unpack: bool, tile_y0: int = 0) -> N
     check(pt().pt_tiles_copy(tex, len(textures), tile_y0, stride, C.cast(arr, C.c_void_p), len(segs), int(bool(unpack))))
 
 
-def rows_rgb_copy(textures, y0: int, y1: int, packed_ptr: int, unpack: bool) -> None:
-    """pt_rows_rgb_copy: rows [y0, y1) of the textures as rgb (3 floats a texel, texture after texture) to / from the
-    16-B aligned device buffer at packed_ptr; one launch on the library stream."""
-    tex = (C.c_uint32 * len(textures))(*textures)
-    check(pt().pt_rows_rgb_copy(tex, len(textures), y0, y1, C.c_void_p(packed_ptr), int(bool(unpack))))
-
-
 def texture_array(layers: np.ndarray) -> int:
     """main.cpp:184-205: glTexStorage3D(GL_TEXTURE_2D_ARRAY, 1, GL_RGBA8, w, h, n) + one glTexSubImage3D per layer
     (help_func.h:4-20). `layers` is (n, h, w, 3|4) uint8, rows already in GL order (stbi flipped on load)."""

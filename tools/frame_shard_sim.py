@@ -14,8 +14,7 @@ SHARD=tiles simulates dist.TileShardRenderer instead: every rank traces the tile
 all-to-all per frame (exchange_tiles: latency + the largest per-peer message / bandwidth, on the receive stream) carries
 them to the band owners. Both modes report the camera-to-modulate latency (HIP events, Renderer.latency_ms) in ms and
 in frames of the rank's rate.
-usage: python tools/frame_shard_sim.py [N] [W] [H]   (RANKS=0,3 to simulate a subset; FRAMES, OWN, K, SHARD, WINDOW, BURST, TBATCH,
-PACK=0 for the unpacked float4 wire format)"""
+usage: python tools/frame_shard_sim.py [N] [W] [H]   (RANKS=0,3 to simulate a subset; FRAMES, OWN, K, SHARD, WINDOW, BURST, TBATCH)"""
 import os
 import sys
 import time
@@ -117,37 +116,19 @@ def fake_exchange(items, plan, dist, group=None, wait=True):
     return [FakeWork(done)]
 
 
-def fake_window(window, plan, dist, group=None, rows=None, rgb=None):
+def fake_window(window, plan, dist, group=None, rows=None):
     """exchange_window stand-in: the window's sends and receives run over all links at once, so the batch lasts
-    latency + the largest per-peer volume (sent to or received from one peer) / link bandwidth. With rgb (packed
-    planes, exchange_window's wire format) the packing draws run for real, and each received frame's packed planes
-    are unpacked from a packing of the band's own rows (the draws' cost, the planes' contents kept)."""
+    latency + the largest per-peer volume (sent to or received from one peer) / link bandwidth."""
     per_peer, sent = {}, 0
-    for e, (src, planes) in enumerate(window):
-        handles = rgb[e] if rgb else None
-        first = D.WINDOW_RGB_PLANES if handles else 0
-
-        def plane_bytes(j, t):
-            return t.numel() * (3 if j < first else 4)
-
+    for src, planes in window:
         if src == plan.rank:
             for k in range(plan.world):
                 if k != plan.rank:
-                    if first:
-                        y0, y1 = (rows[0] if rows else plan.zone)(k)
-                        buf = torch.empty((first, y1 - y0, planes[0].shape[1], 3), dtype=torch.float32, device="cuda")
-                        gl.rows_rgb_copy(handles, y0, y1, buf.data_ptr(), unpack=False)
-                    nb = sum(plane_bytes(j, t[slice(*(rows[j] if rows else plan.zone)(k))])
-                             for j, t in enumerate(planes))
+                    nb = sum(t[slice(*(rows[j] if rows else plan.zone)(k))].numel() * 4 for j, t in enumerate(planes))
                     per_peer[("s", k)] = per_peer.get(("s", k), 0) + nb
                     sent += nb
         else:
-            if first:
-                z0, z1 = plan.zone(plan.rank)
-                buf = torch.empty((first, z1 - z0, planes[0].shape[1], 3), dtype=torch.float32, device="cuda")
-                gl.rows_rgb_copy(handles, z0, z1, buf.data_ptr(), unpack=False)
-                gl.rows_rgb_copy(handles, z0, z1, buf.data_ptr(), unpack=True)
-            nb = sum(plane_bytes(j, t) for j, t in enumerate(planes))
+            nb = sum(t.numel() * 4 for t in planes)
             per_peer[("r", src)] = per_peer.get(("r", src), 0) + nb
             LOG["recv"] += nb
     LOG["send"] += sent
@@ -195,8 +176,7 @@ def sim_rank(rk, bounds=None):
         r = D.FrameShardRenderer(scene, W, H, cfg, rk, N, FakeDist(), own_slots=OWN, frames_in_flight=K,
                                  bounds=bounds, ship_gbuffer=os.environ.get("SHIP", "0") == "1",
                                  window=int(os.environ.get("WINDOW", "0")) or None,
-                                 burst=int(os.environ.get("BURST", "1")),
-                                 pack_rgb=os.environ.get("PACK", "1") == "1")
+                                 burst=int(os.environ.get("BURST", "1")))
     r.camera.frameCounter += int(os.environ.get("FC_OFFSET", "0"))  # experiment: which frames a rank traces
     for kv in filter(None, os.environ.get("PT_UNIFORMS", "").split(",")):  # name=value,... on the path tracer
         name, val = kv.split("=")
