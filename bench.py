@@ -107,8 +107,8 @@ def parse():
                     help="multi-GPU: skip the untimed bitwise check of the gathered bands against a one-GPU frame")
     ap.add_argument("--equal-bands", type=int, default=None, choices=(0, 1),
                     help="multi-GPU: 1 = equal band heights (no balancing of the measured band work); default 1 for "
-                         "the frame shard on 2 ranks (its bytes, not its band work, set the frame: simulated 357 vs "
-                         "337 fps at 4K, profiles/r05/shard/sim_n2_own4_k12.log), else 0")
+                         "the frame shard on 2 ranks (simulated 357 vs 337 fps at 4K, "
+                         "profiles/r05/shard/sim_n2_own4_k12.log), else 0")
     ap.add_argument("--shard", default="frames", choices=("frames", "tiles", "bands"),
                     help="multi-GPU: 'frames' = rank f %% N traces frame f whole and scatters its rows to the band owners, "
                          "the SVGF chain banded (dist.FrameShardRenderer); 'tiles' = every rank traces the 16x16 tiles "
