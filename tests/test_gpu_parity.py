@@ -604,8 +604,10 @@ def test_lane_refill_is_result_preserving(gpu, scene_name, request):
     for o, st in zip(outs[:2], stats[:2]):
         for k in o:
             assert np.array_equal(o[k].view(np.uint32), outs[2][k].view(np.uint32)), k
-        for k in ("primary_rays", "bounce_rays", "shadow_rays"):
+        # the shadow split (wf_shadow_stats) counts verdicts: the same in every form
+        for k in ("primary_rays", "bounce_rays", "shadow_rays", "shadow_point_rays", "shadow_occluded"):
             assert st[k] == stats[2][k], (k, stats)
+        assert st["shadow_occluded"] <= st["shadow_rays"] and st["shadow_point_rays"] <= st["shadow_rays"], st
         for k in ("shadow_visits", "bounce_visits"):
             assert abs(st[k] - stats[2][k]) <= 0.01 * stats[2][k], (k, stats)
 
@@ -634,7 +636,7 @@ def test_wide_tree_is_result_preserving(gpu, scene_name, request):
     for fw, fb in zip(*outs):
         for k in fw:
             assert np.array_equal(fw[k].view(np.uint32), fb[k].view(np.uint32)), k
-    for k in ("primary_rays", "bounce_rays", "shadow_rays"):
+    for k in ("primary_rays", "bounce_rays", "shadow_rays", "shadow_point_rays", "shadow_occluded"):
         assert stats[0][k] == stats[1][k], (k, stats)
     print("visits wide / binary:", {k: (stats[0][k], stats[1][k]) for k in ("bounce_visits", "shadow_visits")})
 
