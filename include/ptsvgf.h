@@ -187,9 +187,9 @@ int pt_pass_set_motion_bound(uint32_t pass, void* device_u32);
  * exact-tie re-walks on the reference tree, primary rays retried unbounded after
  * the G-buffer bound, rays whose stack spilled past the LDS stack (reference
  * trees deeper than 32 levels), the lane slots of primary / bounce / shadow
- * waves (64 x the wave's largest visit count), and of the shadow rays of the
- * lane-refill walks: point-light rays and occluded rays. device_u64 holds 14
- * counters.
+ * waves (64 x the wave's largest visit count), and, counted from the shadow
+ * verdicts, the shadow rays toward point lights and the occluded shadow rays.
+ * device_u64 holds 14 counters.
  * Wave-aggregated atomics; NULL disables (the default). */
 int pt_pass_set_trace_stats(uint32_t pass, void* device_u64);
 int pt_pass_draw(uint32_t pass);
