@@ -48,8 +48,8 @@ constexpr int kTB = 128;  // threads per traversal block (LDS stack: kStack*kTB*
 // LDS stack entries of the 4-wide lane-refill walks. Unlike the binary walks (sized by the tree's depth: kStack /
 // kStackSmall), a 4-wide walk whose pushes would overflow hands its ray to the cooperative walk (wide_step), so the
 // stack can be smaller than the deepest path: it bounds the resident waves (kTB x entries x 4 B of LDS per block).
-// Re-measured at 7 waves per SIMD (round 5, profiles/r05/wide_ks/): 20 entries (still 7 waves) and 22 (6.5) within
-// noise of 16 at 4K and on the surface view.
+// Re-measured at 7 waves per SIMD (round 5, profiles/r05/wide_ks/): 20 and 22 entries (both still 7 waves: 10 / 11 KB
+// per 2-wave block) within noise of 16 at 4K and on the surface view.
 #ifndef PT_WIDE_KS
 #define PT_WIDE_KS 16
 #endif
