@@ -5,7 +5,8 @@
 # serialised per-pass HIP-event timing; 4 = the headline configuration, whose traversal launches are the
 # lane-refill kernels (wf_trace_closest_refill / wf_trace_shadow_refill, renderer.py trace_refill).
 # VIEW (default "default"): bench.py --view. PASSES (default "trace fetch write sq l2 sq2"; also "ta": texture-address
-# unit busy cycles, summed over the 256 TAs): which runs.
+# unit busy cycles, summed over the 256 TAs; "tcp": vector L1 tag accesses, its read requests to L2 and their summed
+# latency): which runs.
 # usage: FIF=4 VIEW=surface bash tools/gpu_profile.sh <tag> [extra bench args]
 set -o pipefail
 TAG=${1:-r03}
@@ -30,6 +31,7 @@ for p in $PASSES; do
     l2) A="--pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE" ;;
     sq2) A="--pmc SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" ;;
     ta) A="--pmc TA_TA_BUSY_sum TA_BUSY_avr GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES" ;;
+    tcp) A="--pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum GRBM_GUI_ACTIVE" ;;
     *) echo "unknown pass $p"; exit 2 ;;
   esac
   echo "pass $p: $(date +%T)"
