@@ -396,10 +396,12 @@ def main():
         dist.all_reduce(t)
         return t.tolist()
 
-    def run(W, H, K, view="default", probes=True, parity=False):
+    def run(W, H, K, view="default", probes=True, parity=False, moving=None):
         """Warm up, time exactly args.steps frames (barrier + sync on both sides, max over ranks); then, untimed:
         one frame with the traversal counters on, one profiled frame (per-pass HIP events), the a-trous launches
-        replayed between HIP events, and the surface fraction of the frame."""
+        replayed between HIP events, and the surface fraction of the frame. moving: orbit the camera 1 deg per
+        frame (configs[4]; default --moving), the profiled frame included."""
+        moving = args.moving if moving is None else moving
         check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))  # a previous renderer's streams are gone
         log(f"run {W}x{H} K={K} view={view}")
         if world > 1 and args.shard == "frames":
@@ -442,9 +444,9 @@ def main():
         moves = []  # per frame the band renderer drew: the orbit applied before it (band_parity replays them)
 
         def step():
-            if args.moving:
+            if moving:
                 r.camera.orbit(1.0, 0.0)
-            moves.append((1.0, 0.0) if args.moving else None)
+            moves.append((1.0, 0.0) if moving else None)
             r.frame()
 
         for _ in range(max(args.warmup, K + 1)):
@@ -525,6 +527,19 @@ def main():
                 nd = nd[p.y0 - p.row0:p.y1 - p.row0]
             bg, px = allsum([float(np.count_nonzero(nd[..., 3] == 1.0)), float(nd.shape[0] * nd.shape[1])])
             out["background_fraction"] = bg / px
+            if moving:
+                # the profiled frame's history lengths (reproject's OutMoments_HistoryLength.z, svgf_reproject.frag:
+                # 189-203): 1 = no valid history (bilinear taps and the 3x3 fallback, :111-141, both failed), < 4 =
+                # young history, which svgf_variance.frag:68-96 filters with its 7x7 kernel
+                hl = gl.readback(r.planes()["reproj_moments"])[..., 2]
+                if world > 1:
+                    hl = hl[p.y0 - p.row0:p.y1 - p.row0]
+                surf = nd[..., 3] != 1.0
+                ns, fresh, young = allsum([float(np.count_nonzero(surf)), float(np.count_nonzero(surf & (hl == 1.0))),
+                                           float(np.count_nonzero(surf & (hl < 4.0)))])
+                out["history"] = {"surface_px": int(ns), "no_history_px": int(fresh), "young_history_px": int(young),
+                                  "no_history_fraction": round(fresh / max(ns, 1.0), 5),
+                                  "young_history_fraction": round(young / max(ns, 1.0), 5)}
             if hasattr(r, "motion_log") and r.motion_log:
                 out["max_history_rows"] = int(max(n for _, n in r.motion_log))
         if world > 1 and parity and probes:
@@ -648,6 +663,23 @@ def main():
                                  "path_tracer": pt_rates(sv, sfps),
                                  "passes_ms": {k: round(v, 4) for k, v in sv["per_pass"].items()}}
 
+    if not args.no_extras and world == 1 and not args.moving:
+        # configs[4]'s temporal stress on one GPU: the camera orbits 1 deg every frame (Utils/camera.h:71 resets
+        # frameCounter on each move), so reprojection sees real motion, disocclusions fall back to the 3x3 search
+        # (svgf_reproject.frag:111-141) and young history takes the 7x7 variance (svgf_variance.frag:68-96)
+        mv = run(W, H, K, args.view, moving=True)
+        mfps = args.steps / mv["dt"]
+        extra["moving"] = {"workload": f"{args.scene} {W}x{H} 1spp depth2 + 5-iter SVGF, orbit 1 deg/frame",
+                           "fps": round(mfps, 3), "ms_per_step": round(mv["dt"] / args.steps * 1e3, 3),
+                           "frames_in_flight": K, "latency": mv.get("latency"), "history": mv.get("history"),
+                           # (the orbit sweeps the view; no PMC profile is matched to it: traffic null)
+                           "roofline": atrous_roofline(mv, W, mv["rows"], "moving"),
+                           "path_tracer": pt_rates(mv, mfps),
+                           "passes_ms": {k: round(v, 4) for k, v in mv["per_pass"].items()}}
+        if not args.no_1080p and (W, H) == (3840, 2160):
+            mv2 = run(1920, 1080, k1080, args.view, probes=False, moving=True)
+            extra["moving"]["fps_1080p"] = round(args.steps / mv2["dt"], 3)
+
     if not args.no_extras and world == 1:
         log("dynamic scenes: GPU LBVH rebuilds")
         extra["dynamic_bvh"] = dynamic_bvh(scene, W, H, K, args.steps, args.warmup,
@@ -691,6 +723,8 @@ def main():
             line["max_history_rows"] = res["max_history_rows"]
         if "latency" in res:
             line["latency"] = res["latency"]
+        if "history" in res:
+            line["history"] = res["history"]
         if "bands" in res:
             line["bands"] = res["bands"]
         if res.get("band_parity") is not None:

@@ -76,6 +76,11 @@ int pt_init(int device);                    /* select HIP device, create stream 
 int pt_shutdown(void);                      /* free every handle and the stream */
 int pt_set_stream(void* hip_stream);        /* run on this stream; NULL = HIP default (null) stream */
 int pt_use_own_stream(void);                /* back to the library's own stream (the pt_init default) */
+/* The caller draws no more on this stream (it may be destroyed, or its handle
+ * reused): the library drops its per-stream state (the trace_fork side stream,
+ * the merged environment's reader event) once that state's work is done, and
+ * falls back to its own stream if this one is current. No GL counterpart. */
+int pt_stream_release(void* hip_stream);
 int pt_sync(void);                          /* wait for all queued draws */
 const char* pt_last_error(void);
 int pt_version(void);
@@ -189,9 +194,17 @@ int pt_pass_set_motion_bound(uint32_t pass, void* device_u32);
  * trees deeper than 32 levels), the lane slots of primary / bounce / shadow
  * waves (64 x the wave's largest visit count), and, counted from the shadow
  * verdicts, the shadow rays toward point lights and the occluded shadow rays.
- * device_u64 holds 14 counters.
+ * device_u64 holds `count` counters: counters past count are not written
+ * (pt_trace_stats_count() = how many this library has; count above it is
+ * capped, count <= 0 with a buffer is PT_ERR_ARG).
  * Wave-aggregated atomics; NULL disables (the default). */
+int pt_pass_set_trace_stats_n(uint32_t pass, void* device_u64, int count);
+/* The first form of the call: a buffer of PT_TRACE_STATS_V1 (12) counters,
+ * the first 12 above; the two shadow-split counters are not written. */
+#define PT_TRACE_STATS_V1 12
 int pt_pass_set_trace_stats(uint32_t pass, void* device_u64);
+/* Number of traversal counters this library writes (14). */
+int pt_trace_stats_count(void);
 int pt_pass_draw(uint32_t pass);
 /* Draw `count` (1..8) path-tracing passes — the frames of a batch, each with its
  * own uniforms, samplers and attachments, one scene, size and band — as one

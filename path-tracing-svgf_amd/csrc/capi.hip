@@ -210,7 +210,9 @@ struct Pass {
   bool timed = false;
   uint32_t* row_cost = nullptr;  // pt_pass_set_row_cost (not owned)
   uint32_t* motion_max = nullptr;  // pt_pass_set_motion_bound (not owned)
+  struct HdrMerged* hdr_reads = nullptr;  // the merged environment the draw being issued reads (pt_params)
   unsigned long long* stats = nullptr;  // pt_pass_set_trace_stats (not owned)
+  int stats_n = 0;                      // counters that buffer holds (pt_pass_set_trace_stats_n)
 };
 
 struct SceneGPU {
@@ -242,7 +244,24 @@ struct HdrMerged {
   const void *hdr_dev = nullptr, *cache_dev = nullptr;
   uint64_t vh = 0, vc = 0;
   int W = 0, H = 0;
+  hipEvent_t built = nullptr;                  // recorded after the merge that wrote buf, on the stream that ran it
+  std::map<hipStream_t, hipEvent_t> uses;      // per draw stream: recorded after its latest draw that read buf
+  // buffers a rebuild retired, each with its readers' events: reused (never freed mid-run, so no call blocks the
+  // device) once every event has completed
+  std::vector<std::pair<float4*, std::vector<hipEvent_t>>> spare;
 };
+
+// drops a merged environment: its buffers (the caller has synchronised the streams that read them) and events
+void free_hdr_merged(HdrMerged& m) {
+  if (m.buf) (void)hipFree(m.buf);
+  for (auto& sp : m.spare) {
+    (void)hipFree(sp.first);
+    for (hipEvent_t e : sp.second) (void)hipEventDestroy(e);
+  }
+  for (auto& u : m.uses) (void)hipEventDestroy(u.second);
+  if (m.built) (void)hipEventDestroy(m.built);
+  m = HdrMerged{};
+}
 
 struct Lib {
   bool init = false;
@@ -1229,31 +1248,50 @@ int pt_params(Pass* p, PTParams& k, SceneGPU*& sg) {
   // A/B switch hdr_merge (default 1): the NEE's radiance and pdf fetches at one direction from one merged texture
   if (ui(p, "hdr_merge", 1) && hm != hc && hm->W == hc->W && hm->H == hc->H && hm->target == PT_TEXTURE_2D &&
       hc->target == PT_TEXTURE_2D && hm->rows == hm->H && hc->rows == hc->H) {
-    // Built on the draw's stream, but read by the path tracers of every frame in flight on other streams: a rebuild
-    // (first bind, an uploaded hdrMap / hdrCache, a new size) first waits for the whole device (no draw still reads the
-    // old contents) and then for itself (no draw reads a half-written buffer). Rebuilds are rare: binds, uploads.
+    // Built on the draw's stream, but read by the path tracers of every frame in flight on other streams. A rebuild
+    // (first bind, an uploaded hdrMap / hdrCache) writes a buffer no draw still reads: the current one is retired with
+    // its readers' events (HdrMerged::uses, recorded after each draw that read it) and a retired buffer whose readers
+    // have all finished is taken, or a new one. Every draw's stream waits for the merge's event before reading. No host
+    // wait, so a rebuild never blocks on the device (e.g. on RCCL receives in flight for peers). Rebuilds are rare.
     // Staleness follows Texture::version, which uploads bump; a texture wrapped around external device memory
     // (pt_texture2d_wrap) is not tracked, so new contents there must be re-bound (a new handle) to be merged.
     HdrMerged& m = g.hdr_merged[{hmh, hch}];
     const bool stale = !m.buf || m.W != hm->W || m.H != hm->H || m.hdr_dev != hm->dev || m.cache_dev != hc->dev ||
                        m.vh != hm->version || m.vc != hc->version;
-    if (stale && m.buf) HIPCHK(hipDeviceSynchronize());
-    if (!m.buf || m.W != hm->W || m.H != hm->H) {
-      if (m.buf) (void)hipFree(m.buf);
-      m = HdrMerged{};
-      HIPCHK(hipMalloc((void**)&m.buf, (size_t)hm->W * hm->H * sizeof(float4)));
+    if (stale) {
+      if (m.buf && (m.W != hm->W || m.H != hm->H)) {  // a new size (rarer still): the old buffers go once idle
+        HIPCHK(hipDeviceSynchronize());
+        free_hdr_merged(m);
+      }
+      if (m.buf) {
+        std::vector<hipEvent_t> readers;
+        for (auto& u : m.uses) readers.push_back(u.second);
+        m.uses.clear();
+        m.spare.emplace_back(m.buf, std::move(readers));
+        m.buf = nullptr;
+      }
+      for (size_t i = 0; i < m.spare.size() && !m.buf; ++i) {
+        bool idle = true;
+        for (hipEvent_t e : m.spare[i].second) idle = idle && hipEventQuery(e) == hipSuccess;
+        if (!idle) continue;
+        m.buf = m.spare[i].first;
+        for (hipEvent_t e : m.spare[i].second) (void)hipEventDestroy(e);
+        m.spare.erase(m.spare.begin() + i);
+      }
+      if (!m.buf) HIPCHK(hipMalloc((void**)&m.buf, (size_t)hm->W * hm->H * sizeof(float4)));
       m.W = hm->W;
       m.H = hm->H;
-    }
-    if (stale) {
+      if (!m.built) HIPCHK(hipEventCreateWithFlags(&m.built, hipEventDisableTiming));
       const int rc = ptk::launch_hdr_merge((const float4*)hm->dev, (const float4*)hc->dev, m.buf, m.W * m.H, g.stream);
       if (rc) return hip_err((hipError_t)rc, "hdr merge");
-      HIPCHK(hipStreamSynchronize(g.stream));
+      HIPCHK(hipEventRecord(m.built, g.stream));
       m.hdr_dev = hm->dev;
       m.cache_dev = hc->dev;
       m.vh = hm->version;
       m.vc = hc->version;
     }
+    HIPCHK(hipStreamWaitEvent(g.stream, m.built, 0));  // (a no-op wait once the merge has run)
+    p->hdr_reads = &m;
     k.hdr_pdf = Tex{m.buf, m.W, m.H};
   }
   k.hdrResolution = ui(p, "hdrResolution", hm->W);
@@ -1301,6 +1339,7 @@ int pt_wf_setup(Pass* p, PTParams& k, SceneGPU* sg, const WFState& st) {
     k.wf = st;
     k.wf.row_cost = p->row_cost;
     k.wf.stats = p->stats;
+    k.wf.stats_n = p->stats_n;
     // > 0: shadow rays past this many visits finish in the wave-cooperative walk (A/B switch; off: with frames
     // in flight it measured slower)
     k.wf.shadow_budget = (uint32_t)ui(p, "shadow_budget", 0);
@@ -1322,11 +1361,9 @@ int pt_wf_setup(Pass* p, PTParams& k, SceneGPU* sg, const WFState& st) {
 }
 
 // The side stream and events of path-tracing draws issued on `s` (uniform trace_fork = 1), created on first use: one
-// per draw stream, so frames in flight on different streams do not queue behind each other's shadow walks. Entries
-// live until pt_shutdown: the map holds one entry per stream that ever drew with trace_fork, which the host's stream
-// pool bounds (ptsvgf.renderer.acquire_stream recycles streams; torch never destroys them). A handle reused by a new
-// stream after its old stream was destroyed finds the old entry, which stays correct: the side stream is the library's
-// own, and both events are re-recorded on every draw before they are waited on.
+// per draw stream, so frames in flight on different streams do not queue behind each other's shadow walks. An entry
+// lives until its stream is released (pt_stream_release, which the host's stream pool calls when a renderer gives a
+// stream back: ptsvgf.renderer.release_stream) or pt_shutdown, so a handle value a new stream reuses starts afresh.
 const ptk::WfFork* wf_fork(Pass* p, hipStream_t s, int* rc) {
   *rc = PT_OK;
   if (!ui(p, "trace_fork", 0)) return nullptr;
@@ -1343,6 +1380,18 @@ const ptk::WfFork* wf_fork(Pass* p, hipStream_t s, int* rc) {
     return nullptr;
   }
   return &(g.forks[s] = f);
+}
+
+// after a path-tracing draw that read a merged environment: its stream's use event, so a later rebuild knows when
+// this draw no longer reads the buffer (HdrMerged::uses)
+int note_hdr_read(Pass* p) {
+  HdrMerged* m = p->hdr_reads;
+  p->hdr_reads = nullptr;
+  if (!m || !m->buf) return PT_OK;
+  hipEvent_t& e = m->uses[g.stream];
+  if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(e, g.stream));
+  return PT_OK;
 }
 
 int draw_pathtrace(Pass* p) {
@@ -1365,7 +1414,8 @@ int draw_pathtrace(Pass* p) {
     rc = launch_pathtrace_wavefront(k, g.stream, fk);
     if (!rc && k.tiles.cost) p->order.ordered = true;
   }
-  return rc ? hip_err((hipError_t)rc, "pathtrace launch") : PT_OK;
+  if (rc) return hip_err((hipError_t)rc, "pathtrace launch");
+  return note_hdr_read(p);
 }
 
 // pt_pass_draw_batch: the frames of several path-tracing passes in one wavefront run whose list-driven traversals
@@ -1405,7 +1455,9 @@ int draw_pathtrace_batch(Pass** ps, int n) {
   rc = launch_pathtrace_wavefront_batch(k, n, g.stream, fk);
   for (int b = 0; b < n && !rc; ++b)
     if (k[b].tiles.cost) ps[b]->order.ordered = true;
-  return rc ? hip_err((hipError_t)rc, "pathtrace batch launch") : PT_OK;
+  if (rc) return hip_err((hipError_t)rc, "pathtrace batch launch");
+  for (int b = 0; b < n; ++b) TRY(note_hdr_read(ps[b]));
+  return PT_OK;
 }
 
 // The tile flags of a draw of p over rows [k.y0, k.y1): the rows the a-trous passes draw ("atrous_rows_begin" /
@@ -1680,6 +1732,15 @@ int pt_init(int device) {
   if (device < 0 || device >= n) return err(PT_ERR_ARG, "device index out of range");
   HIPCHK(hipSetDevice(device));
   HIPCHK(hipStreamCreateWithFlags(&g.own, hipStreamNonBlocking));
+  if (PT_WIDE_SIGNED) {
+    const int sub = ptk::subnormal_probe(g.own);
+    if (sub != 1) {
+      (void)hipStreamDestroy(g.own);
+      g.own = nullptr;
+      return sub == 0 ? err(PT_ERR_STATE, "walk kernels flush f32 subnormals: PT_WIDE_SIGNED needs them kept")
+                      : err(PT_ERR_HIP, "subnormal probe failed");
+    }
+  }
   g.stream = g.own;
   g.device = device;
   g.init = true;
@@ -1710,8 +1771,7 @@ int pt_shutdown(void) {
     if (p->ev1) (void)hipEventDestroy(p->ev1);
   }
   for (auto& kv : g.scenes) free_scene(kv.second);
-  for (auto& kv : g.hdr_merged)
-    if (kv.second.buf) (void)hipFree(kv.second.buf);
+  for (auto& kv : g.hdr_merged) free_hdr_merged(kv.second);
   g.hdr_merged.clear();
   for (auto& kv : g.forks) {
     (void)hipEventDestroy(kv.second.fork);
@@ -1731,6 +1791,30 @@ int pt_set_stream(void* s) {
   TRY(ensure_init());
   // s is used as given: NULL is the HIP default (null) stream, which is torch's default stream.
   g.stream = (hipStream_t)s;
+  return PT_OK;
+}
+
+int pt_stream_release(void* s) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  hipStream_t st = (hipStream_t)s;
+  if (st == g.own) return err(PT_ERR_ARG, "the library's own stream is not released");
+  auto it = g.forks.find(st);
+  if (it != g.forks.end()) {  // its side stream's work was joined into st; wait for that side stream only
+    (void)hipStreamSynchronize(it->second.side);
+    (void)hipEventDestroy(it->second.fork);
+    (void)hipEventDestroy(it->second.join);
+    (void)hipStreamDestroy(it->second.side);
+    g.forks.erase(it);
+  }
+  for (auto& kv : g.hdr_merged) {  // the stream's last read of a merged environment: done before the entry goes
+    auto u = kv.second.uses.find(st);
+    if (u == kv.second.uses.end()) continue;
+    (void)hipEventSynchronize(u->second);
+    (void)hipEventDestroy(u->second);
+    kv.second.uses.erase(u);
+  }
+  if (g.stream == st) g.stream = g.own;
   return PT_OK;
 }
 
@@ -2016,7 +2100,8 @@ int pt_texture_destroy(uint32_t tex) {
   g.textures.erase(it);
   for (auto hm = g.hdr_merged.begin(); hm != g.hdr_merged.end();) {  // merged environments built from it
     if (hm->first.first == tex || hm->first.second == tex) {
-      if (hm->second.buf) (void)hipFree(hm->second.buf);
+      (void)hipDeviceSynchronize();  // its readers may run on any stream
+      free_hdr_merged(hm->second);
       hm = g.hdr_merged.erase(hm);
     } else {
       ++hm;
@@ -2370,14 +2455,23 @@ int pt_pass_set_row_cost(uint32_t pass, void* device_counts) {
   return PT_OK;
 }
 
-int pt_pass_set_trace_stats(uint32_t pass, void* device_u64) {
+int pt_pass_set_trace_stats_n(uint32_t pass, void* device_u64, int count) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   Pass* p = pass_of(pass);
   if (!p) return err(PT_ERR_INVALID_HANDLE, "invalid pass");
   if (device_u64 && g.programs[p->program] != PK_PATHTRACE) return err(PT_ERR_ARG, "trace stats need a path-tracing pass");
+  if (device_u64 && count <= 0) return err(PT_ERR_ARG, "trace stats buffer of no counters");
   p->stats = (unsigned long long*)device_u64;
+  p->stats_n = device_u64 ? std::min(count, (int)kStatCount) : 0;
   return PT_OK;
 }
+
+// the entry point as first published took a buffer of 12 counters: it still writes those 12 only
+int pt_pass_set_trace_stats(uint32_t pass, void* device_u64) {
+  return pt_pass_set_trace_stats_n(pass, device_u64, PT_TRACE_STATS_V1);
+}
+
+int pt_trace_stats_count(void) { return kStatCount; }
 
 int pt_pass_set_motion_bound(uint32_t pass, void* device_u32) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);

@@ -257,7 +257,8 @@ __global__ void __launch_bounds__(256) atrous_step_kernel(AtrousParams p) {
 // background pixels read 4 + 16 B and write 16 B.
 // NX: 64-column strips per tile (waves side by side). The halo costs 4S staged columns per tile, so the widest
 // step stages twice its output with NX = 1; S = 16 uses NX = 2 (128 columns, 1024 threads, 74 KB of LDS: measured
-// 100 -> 91.5 us on the 4K bench inputs, tools/exp_atrous_real.hip), the other steps are fastest with NX = 1.
+// 100 -> 91.5 us on the 4K bench inputs, measured with the harness tools/exp_atrous_real.hip of commit 6ee5990,
+// removed in 53232a8: `git show 6ee5990:tools/exp_atrous_real.hip`), the other steps are fastest with NX = 1.
 template <int S> constexpr int tile_nx() { return atrous_tile_nx(S); }
 template <int S> constexpr int tile_tj() { return atrous_tile_tj(S); }  // tile rows = waves per 64-column strip
 // tile_stage_lum: stage every texel's luminance beside it (4 B more LDS per staged texel and 3 VALU per staged texel,

@@ -155,17 +155,35 @@ __device__ __forceinline__ void block_push_shade(bool p_live, int lbin, bool p_h
   }
 }
 
+// PT_WIDE_SIGNED's child test (wide_step) takes t1 > 0 as t1 >= the least f32 subnormal: compiled with this file's
+// flags, max(x, least subnormal) must stay above 0 for x = 0 (x comes from memory, so nothing folds at compile time)
+__global__ void __launch_bounds__(64) subnormal_probe_kernel(const float* zero, int* out) {
+  if (threadIdx.x == 0) out[0] = fmaxf(zero[0], __builtin_bit_cast(float, 1u)) > 0.0f ? 1 : 0;
+}
+int subnormal_probe(hipStream_t s) {
+  void* buf = nullptr;
+  if (hipMalloc(&buf, 8) != hipSuccess) return -1;
+  int host = -1;
+  bool ok = hipMemsetAsync(buf, 0, 8, s) == hipSuccess;
+  if (ok) hipLaunchKernelGGL(subnormal_probe_kernel, dim3(1), dim3(64), 0, s, (const float*)buf, (int*)buf + 1);
+  ok = ok && hipGetLastError() == hipSuccess &&
+       hipMemcpyAsync(&host, (int*)buf + 1, sizeof(int), hipMemcpyDeviceToHost, s) == hipSuccess &&
+       hipStreamSynchronize(s) == hipSuccess;
+  (void)hipFree(buf);
+  return ok ? host : -1;
+}
+
 // traversal counters (PTParams::wf.stats, pt_pass_set_trace_stats): a wave sum, one 64-bit atomic per wave.
 // Call with every lane of the wave active.
 __device__ __forceinline__ void stat_add(const PTParams& p, int k, uint32_t v) {
-  if (!p.wf.stats) return;
+  if (!p.wf.stats || k >= p.wf.stats_n) return;  // (a buffer of fewer counters: those past its end are skipped)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(p.wf.stats + k, (unsigned long long)v);
 }
 
 __device__ __forceinline__ void stat_slots(const PTParams& p, int k, uint32_t v) {  // 64 x the wave maximum
-  if (!p.wf.stats) return;
+  if (!p.wf.stats || k >= p.wf.stats_n) return;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(p.wf.stats + k, 64ull * v);

@@ -153,6 +153,7 @@ struct WFState {
   int* strag_c;                 // bounce rays past closest_budget (count at kCtrStragC): the cooperative closest walk
   uint32_t closest_budget;      // node + triangle visits before a bounce ray is handed to it (0: never; refill kernel)
   unsigned long long* stats;    // optional traversal counters (kStat*), wave-aggregated atomics; may be null
+  int stats_n;                  // counters the caller's buffer holds: counter k is written only when k < stats_n
   int* spill;                   // deep trees only: stack entries past the LDS stack, entry kStack + j of pixel pid at
   size_t spill_stride;          // spill[j * spill_stride + pid] (spill_stride = band pixels); null otherwise
 };
@@ -362,6 +363,9 @@ struct WfFork {
   hipEvent_t fork, join;
 };
 int launch_pathtrace_wavefront(const PTParams& p, hipStream_t s, const WfFork* fk = nullptr);
+// 1 when the walk kernels' translation unit keeps f32 subnormals (max(0, least subnormal) > 0, evaluated on the device
+// with the walk code's compile flags), as PT_WIDE_SIGNED's one-compare child test needs; 0 if it flushes; < 0 a HIP error
+int subnormal_probe(hipStream_t s);
 int wf_list_capacity(int W, int rows);  // per-segment capacity of the compacted ray lists (8 segments)
 int wf_subset_tiles(int W, int rows, int stride, int offset);  // tiles of a PTParams tile subset (< 0: invalid)
 int launch_gbuffer(const GBufParams& p, hipStream_t s);

@@ -547,6 +547,9 @@ __device__ __forceinline__ bool finite3(v3 a) {
   return __builtin_isfinite(a.x) && __builtin_isfinite(a.y) && __builtin_isfinite(a.z);
 }
 
+#if PT_WIDE_SIGNED && (defined(__FAST_MATH__) || __FINITE_MATH_ONLY__)
+#error "PT_WIDE_SIGNED's one-compare child test needs IEEE f32 (subnormals kept, no finite-math): build without fast-math"
+#endif
 template <int KS, bool SORT, class Stk>
 __device__ __forceinline__ bool wide_step(const float4* __restrict__ tree, int& node, Stk& st, int& sp, v3 S, v3 inv,
                                           float lim) {
@@ -575,6 +578,8 @@ __device__ __forceinline__ bool wide_step(const float4* __restrict__ tree, int& 
     // t0c = max(t0, least subnormal) it is t0c <= min(t1, lim) (no NaN: finite planes and inv, or the +-inf planes of
     // an empty slot). An empty slot (pack_wide: lo = +inf, hi = -inf) has t0 = +inf, t1 = -inf: never hit, so the
     // slot's ref is not tested. The sort key is t0c (order among children entered at t0 <= 0 is free, see above).
+    // (needs f32 subnormals kept: a build that flushes them would make tiny 0 and enter children with t1 == 0;
+    // fast-math builds are refused below, and pt_init refuses a device whose walk code flushes, subnormal_probe)
     const float tiny = __builtin_bit_cast(float, 1u);
     float t0c[4], t1l[4];
 #pragma unroll

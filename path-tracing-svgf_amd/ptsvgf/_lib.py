@@ -73,6 +73,7 @@ _PT_SIGS = [
     ("pt_shutdown", C.c_int, []),
     ("pt_set_stream", C.c_int, [_vp]),
     ("pt_use_own_stream", C.c_int, []),
+    ("pt_stream_release", C.c_int, [_vp]),
     ("pt_sync", C.c_int, []),
     ("pt_last_error", C.c_char_p, []),
     ("pt_version", C.c_int, []),
@@ -112,6 +113,8 @@ _PT_SIGS = [
     ("pt_pass_set_row_cost", C.c_int, [_u32, C.c_void_p]),
     ("pt_pass_set_motion_bound", C.c_int, [_u32, C.c_void_p]),
     ("pt_pass_set_trace_stats", C.c_int, [_u32, C.c_void_p]),
+    ("pt_pass_set_trace_stats_n", C.c_int, [_u32, C.c_void_p, C.c_int]),
+    ("pt_trace_stats_count", C.c_int, []),
     ("pt_pass_draw", C.c_int, [_u32]),
     ("pt_pass_draw_batch", C.c_int, [C.POINTER(_u32), C.c_int]),
     ("pt_pass_last_ms", C.c_int, [_u32, _fp]),

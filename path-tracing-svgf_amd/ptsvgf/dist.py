@@ -1018,7 +1018,7 @@ class FrameShardRenderer(BandRenderer):
         self.r.flush()
         torch.cuda.synchronize()
         for p, _ in self.full.pt_slots:
-            p.set_trace_stats(buf.data_ptr())
+            p.set_trace_stats(buf.data_ptr(), buf.numel())
         try:
             self.r.frame()
             self.r.flush()
@@ -1300,7 +1300,7 @@ class TileShardRenderer(BandRenderer):
         self.r.flush()
         torch.cuda.synchronize()
         for q, _ in self.full.pt_slots:
-            q.set_trace_stats(buf.data_ptr())
+            q.set_trace_stats(buf.data_ptr(), buf.numel())
         try:
             self.r.frame()
             self.r.flush()

@@ -238,9 +238,10 @@ class RenderPass:
         """Accumulate per-row BVH visits into a device uint32 array (path tracer; 0 disables)."""
         check(pt().pt_pass_set_row_cost(self._handle(), C.c_void_p(device_ptr or None)))
 
-    def set_trace_stats(self, device_ptr: int) -> None:
-        """Path-tracing pass: add traversal counters (12 x uint64, pt_pass_set_trace_stats) on every draw (0 disables)."""
-        check(pt().pt_pass_set_trace_stats(self._handle(), C.c_void_p(device_ptr or None)))
+    def set_trace_stats(self, device_ptr: int, count: int = 14) -> None:
+        """Path-tracing pass: add traversal counters (`count` x uint64, pt_pass_set_trace_stats_n; the library writes
+        pt_trace_stats_count() = 14, and none past `count`) on every draw (0 disables)."""
+        check(pt().pt_pass_set_trace_stats_n(self._handle(), C.c_void_p(device_ptr or None), count))
 
     def set_motion_bound(self, device_ptr: int) -> None:
         """G-buffer pass: store the largest |motion.y| of every draw into a device uint32 (float bits; 0 disables)."""

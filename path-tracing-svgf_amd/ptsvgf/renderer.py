@@ -75,9 +75,19 @@ def acquire_stream(priority: int = 0):
 
 
 def release_stream(stream) -> None:
+    """Give a stream back to the pool; the library first drops what it holds for it (pt_stream_release: the
+    trace_fork side stream, merged-environment reader events), so the next holder starts afresh."""
+    from ._lib import check, pt
+
     key = getattr(stream, "_ptsvgf_key", None)
-    if key is not None:
-        _FREE_STREAMS.setdefault(key, []).append(stream)
+    if key is None:
+        return  # not from the pool
+    handle = getattr(stream, "cuda_stream", None)
+    if handle is not None:
+        rc = pt().pt_stream_release(handle)
+        if rc != -9:  # PT_ERR_STATE: the library was never initialised, so it holds nothing for the stream
+            check(rc)
+    _FREE_STREAMS.setdefault(key, []).append(stream)
 
 
 class Renderer:
@@ -770,7 +780,7 @@ class Renderer:
         self.flush()  # frames already issued are not counted
         torch.cuda.synchronize()
         for p, _ in self.pt_slots:
-            p.set_trace_stats(buf.data_ptr())
+            p.set_trace_stats(buf.data_ptr(), buf.numel())
         try:
             self.frame()
             self._issue_batch()  # this frame alone

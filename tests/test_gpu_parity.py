@@ -366,6 +366,33 @@ def test_merged_environment_equals_two_fetches(gpu, scene_small):
     assert not np.array_equal(outs[1][0], outs[1][1])
 
 
+def test_merged_environment_rebuilds_with_frames_in_flight(gpu, scene_small):
+    """The merged environment rebuilt twice (a new upload, then the first environment again) with four frames in flight
+    on four streams: a rebuild writes a retired buffer once its readers' events have completed, or a new one, and the
+    draws wait for the merge on their own streams (no device-wide wait); every frame equals the two-fetch path's."""
+    import torch
+
+    gl = gpu
+    W, H = 64, 48
+    envs = (scene_small.hdr, scene_small.hdr[::-1].copy())
+    outs = []
+    for merge in (0, 1):
+        r = _renderer(scene_small, W, H, mode="fast", run_taa=False, run_output=False, frames_in_flight=4)
+        r.pass_path_tracing.set_uniform_int("hdr_merge", merge)  # (every frame slot's pass)
+        got = []
+        for env in (1, 0, 1):
+            for _ in range(5):
+                r.frame()
+            got.append(gl.readback(r.planes()["color"]))
+            torch.cuda.synchronize()  # (GL orders an upload after the draws; here the host does)
+            gl.upload_rgb32f(r.hdrMap, envs[env])
+        r.close()
+        outs.append(got)
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+    assert not np.array_equal(outs[1][0], outs[1][1])
+
+
 def test_fast_driver_equals_reference_driver(gpu, scene_small):
     """Pointer-swapped fast driver == main.cpp call sequence with copies, bit for bit."""
     gl = gpu

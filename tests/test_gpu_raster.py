@@ -111,3 +111,37 @@ def test_primary_raster_equals_walk_bench_scene_1080p(gpu, scene_bench):
     got, st = _pt(gpu, scene_bench, W, H, 1, MOVES)
     print(st)
     _same(got, want, "bench1080")
+
+
+def test_trace_stats_buffer_length_is_respected(gpu, scene_small):
+    """pt_pass_set_trace_stats_n writes no counter past the caller's count, and the first-published entry point
+    (pt_pass_set_trace_stats) writes its 12 counters only (the buffer grew from 12 to 14 counters)."""
+    import ctypes as C
+
+    import torch
+
+    from ptsvgf._lib import pt
+    from ptsvgf.renderer import Renderer
+
+    assert pt().pt_trace_stats_count() == len(Renderer.STAT_KEYS) == 14
+    r = Renderer(scene_small, 64, 48, mode="fast", run_taa=False, run_output=False)
+    sentinel = -12345
+    try:
+        for n, setter in ((12, "v1"), (5, "n"), (14, "n")):
+            buf = torch.zeros(16, dtype=torch.int64, device="cuda")
+            buf[n:] = sentinel
+            torch.cuda.synchronize()
+            h = r.pass_path_tracing._handle()
+            if setter == "v1":
+                assert pt().pt_pass_set_trace_stats(h, C.c_void_p(buf.data_ptr())) == 0
+            else:
+                assert pt().pt_pass_set_trace_stats_n(h, C.c_void_p(buf.data_ptr()), n) == 0
+            r.frame()
+            r.flush()
+            torch.cuda.synchronize()
+            assert pt().pt_pass_set_trace_stats_n(h, None, 0) == 0
+            got = buf.cpu().tolist()
+            assert got[0] == 64 * 48, (n, got)  # primary rays
+            assert all(v == sentinel for v in got[n:]), (n, got)
+    finally:
+        r.close()
