@@ -1333,6 +1333,74 @@ class TileShardRenderer(BandRenderer):
         self._recv_stream = None
 
 
+class P2PRecorder:
+    """A torch.distributed stand-in that forwards everything and logs each batch_isend_irecv call: (site, group, frame,
+    ops) with ops = [(kind, peer, bytes)] in issue order. site = the function that issued the batch (halo_exchange,
+    exchange_window, exchange_tiles), group = "world" / "scatter" / "host" / "group", frame = frame_of() at the call
+    (the frame the host is issuing). check_p2p_logs compares the ranks' logs: what RCCL needs of point-to-point
+    traffic spread over two communicators (DESIGN.md "RCCL issue order")."""
+
+    def __init__(self, dist, frame_of=None):
+        self._dist = dist
+        self.frame_of = frame_of or (lambda: -1)
+        self.log = []
+
+    def __getattr__(self, name):
+        return getattr(self._dist, name)
+
+    def _group_name(self, group) -> str:
+        if group is None or group is self._dist.group.WORLD:
+            return "world"
+        if any(g is group for _, g in _SCATTER_GROUP.values()):
+            return "scatter"
+        if any(g is group for _, g in _HOST_GROUP.values()):
+            return "host"
+        return "group"
+
+    def batch_isend_irecv(self, ops):
+        import sys
+
+        site = sys._getframe(1).f_code.co_name
+        groups = {self._group_name(o.group) for o in ops}
+        if len(groups) != 1:
+            raise RuntimeError(f"a P2P batch spans several groups: {sorted(groups)}")
+        rec = [("send" if getattr(o.op, "__name__", "") == "isend" else "recv", int(o.peer),
+                int(o.tensor.numel() * o.tensor.element_size())) for o in ops]
+        self.log.append((site, groups.pop(), int(self.frame_of()), rec))
+        return self._dist.batch_isend_irecv(ops)
+
+
+def check_p2p_logs(logs) -> list:
+    """logs[r] = rank r's P2PRecorder.log. Returns the violations (empty: none) of the rule that keeps point-to-point
+    traffic on several communicators deadlock-free and correctly paired whatever the streams overlap: for every pair of
+    ranks (r, q), the batches in which r addresses q are, in issue order and over every group, the batches in which q
+    addresses r — same call site, same group, and r's sends to q (in order, by bytes) are q's receives from r and vice
+    versa. (Within one batch, one group call, sends and receives pair up in order among themselves: their interleaving
+    does not matter.)"""
+    bad = []
+    n = len(logs)
+
+    def batches(log, me, peer):
+        out = []
+        for site, g, _, ops in log:
+            snd = tuple(nb for kind, p, nb in ops if p == peer and kind == "send")
+            rcv = tuple(nb for kind, p, nb in ops if p == peer and kind == "recv")
+            if snd or rcv:
+                out.append((site, g, snd, rcv))
+        return out
+
+    for r in range(n):
+        for q in range(r + 1, n):
+            a = batches(logs[r], r, q)
+            b = [(site, g, rcv, snd) for site, g, snd, rcv in batches(logs[q], q, r)]
+            if a != b:
+                i = next((i for i, (x, y) in enumerate(zip(a, b)) if x != y), min(len(a), len(b)))
+                bad.append(f"ranks {r}<->{q}: batch {i} differs: {a[i] if i < len(a) else None} (rank {r}: site, group, "
+                           f"sends, receives) vs {b[i] if i < len(b) else None} (rank {q}, as seen from {r}); "
+                           f"{len(a)} vs {len(b)} batches")
+    return bad
+
+
 def gather_bands(owned: dict, plan: BandPlan, dist, dst: int = 0) -> dict | None:
     """Assemble full frames on rank `dst` from every rank's owned rows: owned maps plane names to (y1 - y0, W, C)
     float32 numpy arrays; returns {name: (H, W, C)} on dst, None elsewhere. Point-to-point sends of device tensors

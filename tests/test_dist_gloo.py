@@ -35,9 +35,12 @@ def _worker(rank, world, port, W, H, frames, moves, bounds=None, ghost=None, sha
     try:
         import oracle_ref as O
         from ptsvgf.camera import rigid_inverse
-        from ptsvgf.dist import (GHOST, GHOST_ZONE_GHOST, BandPlan, allreduce_motion, exchange_window, halo_exchange,
-                                 run_stage, svgf_margins)
+        from ptsvgf.dist import (GHOST, GHOST_ZONE_GHOST, BandPlan, P2PRecorder, allreduce_motion, exchange_window,
+                                 halo_exchange, run_stage, svgf_margins)
         from ptsvgf.scene import build_scene
+
+        cur = [0]
+        D = P2PRecorder(dist, frame_of=lambda: cur[0])  # every P2P batch logged (checked against the peers' below)
 
         scene = build_scene("table_clock_plant", hdr_size=(128, 64), plant_leaves=20)
         gz = shard == "frames_gz"  # ghost zone: passes draw margins, only the histories cross ranks
@@ -57,17 +60,18 @@ def _worker(rank, world, port, W, H, frames, moves, bounds=None, ghost=None, sha
             if gz:  # the histories only (BandRenderer ghost_zone)
                 t = {k: torch.from_numpy(a)[plan.row0:plan.row1] for k, a in arrays.items()}
                 if stage == "reproject":
-                    halo_exchange(plan.history_items(t, plan.motion), plan, dist)
+                    halo_exchange(plan.history_items(t, plan.motion), plan, D)
                 elif stage == "taa":
-                    halo_exchange([(t["prev_taa"], plan.motion)], plan, dist)
+                    halo_exchange([(t["prev_taa"], plan.motion)], plan, D)
                 return
-            run_stage(stage, {k: torch.from_numpy(a)[plan.row0:plan.row1] for k, a in arrays.items()}, plan, dist)
+            run_stage(stage, {k: torch.from_numpy(a)[plan.row0:plan.row1] for k, a in arrays.items()}, plan, D)
 
         nan = lambda: np.full((H, W, 4), np.nan, np.float32)  # noqa: E731
         prev_illum, prev_moments, prev_nd, prev_taa = nan(), nan(), nan(), nan()
         for q in (prev_illum, prev_moments, prev_nd, prev_taa):  # history starts as zeros (the build zero-fills)
             q[plan.row0:plan.row1] = 0.0
         for f in range(frames):
+            cur[0] = f
             mv = moves[f] if f < len(moves) else None
             if mv:
                 full.camera.orbit(*mv)
@@ -87,12 +91,12 @@ def _worker(rank, world, port, W, H, frames, moves, bounds=None, ghost=None, sha
                 col, em, al = band.os.path_trace(W, H, cam.frameCounter, cam.cam_position, rigid_inverse(view),
                                                  cfg.clamp_threshold, cfg.max_tracing_depth, band.aspect_corrected,
                                                  threads=2)
-                nbytes = exchange_window([(rank, [torch.from_numpy(a) for a in (col, em, al)])], plan, dist)
+                nbytes = exchange_window([(rank, [torch.from_numpy(a) for a in (col, em, al)])], plan, D)
                 assert nbytes == 3 * sum(plan.zone(k)[1] - plan.zone(k)[0] for k in range(world) if k != rank) * W * 16
             else:  # ... or receives its band's rows of the planes rank f % world traced
                 col, em, al = nan(), nan(), nan()
                 z0, z1 = plan.zone(rank)
-                exchange_window([(f % world, [torch.from_numpy(a)[z0:z1] for a in (col, em, al)])], plan, dist)
+                exchange_window([(f % world, [torch.from_numpy(a)[z0:z1] for a in (col, em, al)])], plan, D)
             for a in (col, em, al):
                 poison(a, *plan.zone(rank))
             # the motion bound the G-buffer kernel reduces (owned surface pixels), MAX over ranks
@@ -125,6 +129,7 @@ def _worker(rank, world, port, W, H, frames, moves, bounds=None, ghost=None, sha
                 o, w = v[plan.y0:plan.y1], want[k][plan.y0:plan.y1]
                 assert np.array_equal(np.isnan(o), np.isnan(w)), (rank, f, k, "NaN leaked into the band")
                 assert np.array_equal(np.nan_to_num(o), np.nan_to_num(w)), (rank, f, k)
+        _check_p2p(D, world, frames)
         if rank == 0:
             print("history rows per frame:", log)
         return log
@@ -163,6 +168,20 @@ def test_frame_shard_scatter_gloo(world, moves, bounds):
     mp.spawn(_worker, args=(world, _free_port(), W, H, 4, moves, bounds, None, "frames"), nprocs=world, join=True)
 
 
+def _check_p2p(D, world, frames=None):
+    """Every rank's P2P log (dist.P2PRecorder) against its peers': pairwise the same ops, bytes, groups and call sites
+    in the same order (dist.check_p2p_logs)."""
+    from ptsvgf.dist import check_p2p_logs
+
+    logs = [None] * world
+    dist.all_gather_object(logs, D.log)
+    bad = check_p2p_logs(logs)
+    assert not bad, bad[:4]
+    assert all(logs), "a rank issued no P2P batch"
+    if frames is not None:
+        assert {f for _, _, f, _ in logs[0]} <= set(range(frames))
+
+
 def _window_worker(rank, world, port, bounds, windows):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -170,7 +189,8 @@ def _window_worker(rank, world, port, bounds, windows):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from ptsvgf.dist import BandPlan, exchange_window
+        from ptsvgf.dist import BandPlan, P2PRecorder, exchange_window
+        D = P2PRecorder(dist)
         W, H = 8, bounds[-1]
         plan = BandPlan(W, H, rank, world, ghost=4, bounds=bounds, iterations=1)
 
@@ -187,13 +207,15 @@ def _window_worker(rank, world, port, bounds, windows):
                 else:
                     got[f] = [torch.full((plan.y1 - plan.y0, W, 4), float("nan")) for _ in range(3)]
                     window.append((f % world, got[f]))
-            sent = exchange_window(window, plan, dist)
+            sent = exchange_window(window, plan, D)
             mine = sum(1 for f in range(f0, f0 + n) if f % world == rank)
             assert sent == mine * 3 * (H - (plan.y1 - plan.y0)) * W * 16
             for f, planes in got.items():
                 for a, b in zip(planes, frame(f)):
                     assert torch.equal(a, b[plan.y0:plan.y1]), (rank, f)
             f0 += n
+        _check_p2p(D, world)
+        assert len(D.log) == len(windows) and {s for s, *_ in D.log} == {"exchange_window"}
     finally:
         dist.destroy_process_group()
 
@@ -470,3 +492,30 @@ def test_agree_bounds_gloo():
     """A band calibration ends in rank 0's plan on every rank (dist.agree_bounds): ranks whose own choices differ
     (their timings raced) would otherwise cut different bands and exchange halo rows their peers do not hold."""
     mp.spawn(_agree_worker, args=(3, _free_port()), nprocs=3, join=True)
+
+
+def test_check_p2p_logs_finds_mismatches():
+    """dist.check_p2p_logs: matched logs pass; a byte count, a group, a call site or a cross-group order that differs
+    between two peers is reported."""
+    from ptsvgf.dist import check_p2p_logs
+
+    r0 = [("halo_exchange", "world", 0, [("send", 1, 64), ("recv", 1, 32)]),
+          ("exchange_window", "scatter", 0, [("send", 1, 96), ("send", 2, 96)])]
+    # (within a batch the send / receive interleaving is free: one group call)
+    r1 = [("halo_exchange", "world", 0, [("send", 0, 32), ("recv", 0, 64)]),
+          ("exchange_window", "scatter", 0, [("recv", 0, 96)])]
+    r2 = [("exchange_window", "scatter", 0, [("recv", 0, 96)])]
+    assert check_p2p_logs([r0, r1, r2]) == []
+    bytes_off = [r0, [r1[0], ("exchange_window", "scatter", 0, [("recv", 0, 80)])], r2]
+    assert check_p2p_logs(bytes_off)
+    wrong_group = [r0, [("halo_exchange", "scatter", 0, r1[0][3]), r1[1]], r2]
+    assert check_p2p_logs(wrong_group)
+    swapped_sizes = [r0, [("halo_exchange", "world", 0, [("send", 0, 64), ("recv", 0, 32)]), r1[1]], r2]
+    assert check_p2p_logs(swapped_sizes)
+    split = [r0, [("halo_exchange", "world", 0, [("send", 0, 32)]), ("halo_exchange", "world", 0, [("recv", 0, 64)]),
+                  r1[1]], r2]  # the same ops in two batches: not one group call on both sides
+    assert check_p2p_logs(split)
+    reordered = [r0, [r1[1], r1[0]], r2]  # rank 1 issues the scatter receive before the world halo: cross-group order
+    assert any("0<->1" in m for m in check_p2p_logs(reordered))
+    missing = [r0, r1, []]
+    assert any("0<->2" in m for m in check_p2p_logs(missing))

@@ -135,3 +135,68 @@ def test_eight_bands_4k_moving_equal_full_frame(gpu):
     want = {k: gl.readback(full.planes()[k]) for k in KEYS}
     full.close()
     _compare(bands, want)
+
+
+def _p2p_worker(rank, world, port, outdir, window, burst, K, frames):
+    import json
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "path-tracing-svgf_amd"))
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ptsvgf import gl
+    from ptsvgf._lib import check, pt
+    from ptsvgf.camera import parameter_config
+    from ptsvgf.dist import FrameShardRenderer, P2PRecorder
+    torch.cuda.set_device(0)
+    gl.init(0)
+    check(pt().pt_set_stream(torch.cuda.current_stream().cuda_stream))
+    D = P2PRecorder(dist)
+    r = FrameShardRenderer(_scene(False), 320, 256, parameter_config(), rank, world, D, own_slots=max(2, burst),
+                           frames_in_flight=K, window=window, burst=burst)
+    D.frame_of = lambda: r.r.frame_index
+    for f in range(frames):
+        if f >= 3:  # static frames (3-row history reach), then an orbit (the ghost zone's capacity rows)
+            r.camera.orbit(1.0, 0.5)
+        r.frame()
+    r.planes()  # flush: the last window is cut short; every frame's device motion bound verified
+    torch.cuda.synchronize()
+    r.close()
+    logs = [None] * world
+    dist.all_gather_object(logs, D.log)
+    if rank == 0:
+        with open(os.path.join(outdir, "logs.json"), "w") as fh:
+            json.dump(logs, fh)
+    gl.shutdown()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,window,burst", [(3, 3, 1), (3, 2, 2), (4, 4, 1)])
+def test_frame_shard_p2p_issue_order(gpu, world, window, burst):
+    """the real FrameShardRenderer's point-to-point traffic over its two communicators — the history
+    exchange (halo_exchange on WORLD, issued early on the SVGF stream) and the window exchange (exchange_window on
+    scatter_group, on the receive stream) — logged per rank (dist.P2PRecorder) through static and moving frames, full
+    windows, a window cut short by flush() and bursts: for every pair of ranks the batches, groups, call sites and
+    byte counts match in issue order (dist.check_p2p_logs). gloo's blocking wait() hides a stream dependency RCCL would
+    need, but not an issue order that differs between ranks: that is what this checks, for the 8-GPU RCCL run."""
+    import json
+
+    import torch.multiprocessing as mp
+
+    from ptsvgf.dist import check_p2p_logs
+
+    frames = 3 * window + 2  # the last window holds 2 frames: cut short by flush()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_p2p_worker, args=(world, _port(), d, window, burst, 2 * window + 4, frames), nprocs=world, join=True)
+        with open(os.path.join(d, "logs.json")) as fh:
+            logs = json.load(fh)
+    bad = check_p2p_logs(logs)
+    assert not bad, bad[:4]
+    calls = {(site, g) for log in logs for site, g, _, _ in log}
+    assert calls == {("halo_exchange", "world"), ("exchange_window", "scatter")}, calls
+    windows = [sum(1 for site, *_ in log if site == "exchange_window") for log in logs]
+    assert min(windows) >= 3, windows
+    hist = [n for site, g, f, ops in logs[0] if site == "halo_exchange" for _, _, n in ops]
+    assert len(set(hist)) > 1, "static and moving frames exchange different history rows"
