@@ -457,10 +457,12 @@ def main():
         if world > 1:
             r.time_exchanges(True)  # HIP events around each halo stage on the back-end stream
         torch.cuda.synchronize()
+        torch.arange(3, device="cuda")  # kernel-trace marker: the timed frames start (tools/launch_diff.py)
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
         torch.cuda.synchronize()
+        torch.arange(3, device="cuda")  # kernel-trace marker: the timed frames have ended
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
