@@ -338,6 +338,18 @@ def camera_moved(cam, pre_viewproj) -> bool:
     return not np.array_equal(cur.view(np.uint32), np.asarray(pre_viewproj, np.float32).reshape(16).view(np.uint32))
 
 
+class MotionCheckError(RuntimeError):
+    """A frame's measured motion needed more history rows than its exchange carried. `frame` is the first such frame:
+    its SVGF output and every later frame's (the history carries it forward) are not the one-GPU frame's; discard them.
+    Raised after the fact (MotionCheck verifies once the device bound's copy has landed, frames later)."""
+
+    def __init__(self, frame: int, need: int, used: int):
+        super().__init__(f"frame {frame}: the G-buffer's motion needs {need} history rows but {used} were exchanged "
+                         f"(camera moved without the host seeing it: pre_viewproj and projection * view disagree); "
+                         f"frames {frame} and later are not the one-GPU frames")
+        self.frame, self.need, self.used = frame, need, used
+
+
 class MotionCheck:
     """The history rows of each frame from a bound the host holds when it issues the frame's back end — no wait for
     the G-buffer and no per-frame collective (round 4 synchronised on the G-buffer's motion bound and all-reduced it
@@ -348,8 +360,12 @@ class MotionCheck:
     Every rank derives the same count from the same camera path, so the exchanges pair up without communicating. The
     device bound the G-buffer kernel reduces (pt_pass_set_motion_bound) is still copied to pinned host memory behind
     each G-buffer and checked later, once its copy has landed (poll; never waited for unless a ring slot comes round
-    again), against the rows the frame used: a frame whose motion exceeded them raises (verify) — the bound is
-    verified, not trusted."""
+    again), against the rows the frame used: a frame whose motion exceeded them raises MotionCheckError (verify) — the
+    bound is verified, not trusted. The check runs AFTER the fact: by the time it raises, that frame and possibly
+    several later ones have been drawn with the short history; the error names the first bad frame (`frame`), from
+    which on the output is to be discarded. A moved camera exchanges capacity() rows (63 with the ghost zone, 96
+    without) whatever it actually moved: a host bound from the camera delta alone is not finite (a point at the near
+    plane moves without limit under any translation), so the rows are sized for the worst the ghost can hold."""
 
     RING = 64
 
@@ -364,6 +380,7 @@ class MotionCheck:
         self.moved = {}     # frame -> camera moved (host)
         self.used = {}      # frame -> history rows its exchange carried
         self.log = []       # (frame, rows the measured motion needs, rows used)
+        self.first_bad = None  # the first frame whose motion needed more rows than it exchanged (MotionCheckError)
 
     def note_camera(self, f: int, moved: bool) -> None:
         self.moved[f] = bool(moved)
@@ -420,12 +437,16 @@ class MotionCheck:
         need = motion_rows(m, self.plan.H)
         self.log.append((f, need, n))
         if need > n:
-            raise RuntimeError(f"frame {f}: the G-buffer's motion needs {need} history rows but {n} were exchanged "
-                               f"(camera moved without the host seeing it: pre_viewproj and projection * view disagree)")
+            if self.first_bad is None or f < self.first_bad[0]:
+                self.first_bad = (f, need, n)
+            raise MotionCheckError(*self.first_bad)
 
     def verify(self) -> None:
-        """Wait for every captured bound and check it (flush / close: the frames drawn so far)."""
+        """Wait for every captured bound and check it (flush / close: the frames drawn so far); raises
+        MotionCheckError naming the first frame whose exchange fell short."""
         self.poll(block=True)
+        if self.first_bad is not None:
+            raise MotionCheckError(*self.first_bad)
 
 
 class _StageFilter:

@@ -519,3 +519,44 @@ def test_check_p2p_logs_finds_mismatches():
     assert any("0<->1" in m for m in check_p2p_logs(reordered))
     missing = [r0, r1, []]
     assert any("0<->2" in m for m in check_p2p_logs(missing))
+
+
+def test_motion_check_names_first_bad_frame():
+    """MotionCheck verifies after the fact; MotionCheckError names the first frame whose exchanged history
+    rows fell short of its measured motion (that frame on is to be discarded), and verify() reports the earliest."""
+    import numpy as np
+
+    from ptsvgf.dist import REPROJ_REACH, BandPlan, MotionCheck, MotionCheckError
+
+    class Ev:
+        def query(self):
+            return True
+
+        def synchronize(self):
+            pass
+
+    mc = MotionCheck.__new__(MotionCheck)  # (the pinned host ring needs a device; a plain tensor stands in)
+    mc.plan = BandPlan(64, 400, 0, 2, ghost=40)
+    mc.host = torch.zeros(MotionCheck.RING, dtype=torch.int32)
+    mc.ev, mc.slot_frame = [None] * MotionCheck.RING, [None] * MotionCheck.RING
+    mc.pending, mc.moved, mc.used, mc.log, mc.first_bad = [], {}, {}, [], None
+
+    def frame(f, moved, motion_rows_measured):
+        j = f % MotionCheck.RING
+        mc.host[j:j + 1] = torch.from_numpy(np.array([motion_rows_measured / 400.0], np.float32).view(np.int32))
+        mc.ev[j], mc.slot_frame[j] = Ev(), f
+        mc.pending.append(j)
+        mc.note_camera(f, moved)
+
+    frame(0, False, 0.0)
+    frame(1, True, 30.0)  # moved: capacity rows, enough
+    assert mc.rows(0) == REPROJ_REACH and mc.rows(1) == mc.plan.capacity()
+    frame(2, False, 10.0)  # the host saw no move but the G-buffer measured 10 rows: short
+    frame(3, False, 12.0)
+    with pytest.raises(MotionCheckError) as e:
+        mc.rows(2)
+        mc.rows(3)
+    assert e.value.frame == 2 and e.value.need >= 10 + REPROJ_REACH and e.value.used == REPROJ_REACH
+    with pytest.raises(MotionCheckError) as e:
+        mc.verify()
+    assert e.value.frame == 2
