@@ -89,12 +89,31 @@ def summarize(path: str, frames: int, own_every: int):
         e[1] += d
         fk = family(n, g, full_grid)
         fam[fk] = fam.get(fk, 0.0) + d
+    # the SVGF chain of each frame (reproject, variance, five a-trous launches on one stream): its span from the
+    # reprojection's start to the last a-trous launch's end, against its kernels' summed time (the rest is waiting for
+    # CUs held by other streams' kernels, or for the chain's own inputs)
+    chains = []
+    svgf = [(a, b, n, q) for a, b, n, g, q in rows if any(k in n for k in SVGF)]
+    for i, (a, b, n, q) in enumerate(svgf):
+        if "reproject" not in n:
+            continue
+        same = [x for x in svgf[i:] if x[3] == q]
+        at = [x for x in same if "atrous" in x[2]][:5]
+        if len(at) == 5:
+            span = at[-1][1] - a
+            busy_k = sum(x[1] - x[0] for x in same if x[0] <= at[-1][0])
+            chains.append((span / 1e3, busy_k / 1e3))
     wall = (t1 - t0) / 1e3 / frames
     busy = union([(a, b) for a, b, *_ in rows]) / 1e3 / frames
     ksum = sum(d for _, d in per.values()) / frames
     print(f"== {os.path.basename(path.rstrip('/'))}: {frames} frames, {wall / 1e3:.3f} ms/frame wall, GPU busy "
           f"{busy / 1e3:.3f} ms/frame ({busy / wall:.0%}), kernel time {ksum / 1e3:.3f} ms/frame "
           f"({ksum / max(busy, 1e-9):.2f} kernels at once)")
+    if chains:
+        import statistics
+        print(f"   SVGF chain per frame: span {statistics.median(c[0] for c in chains) / 1e3:.3f} ms median "
+              f"(p90 {sorted(c[0] for c in chains)[int(0.9 * (len(chains) - 1))] / 1e3:.3f}), its kernels "
+              f"{statistics.median(c[1] for c in chains) / 1e3:.3f} ms ({len(chains)} chains)")
     for fk, d in sorted(fam.items(), key=lambda x: -x[1]):
         per_own = f" = {d / frames * own_every / 1e3:.3f} ms per own frame" if own_every > 1 and fk in (
             "path tracer", "G-buffer (whole frame)") else ""
