@@ -81,6 +81,13 @@ int pt_use_own_stream(void);                /* back to the library's own stream 
  * the merged environment's reader event) once that state's work is done, and
  * falls back to its own stream if this one is current. No GL counterpart. */
 int pt_stream_release(void* hip_stream);
+/* A new stream whose kernels run only on the CUs whose bits are set in
+ * mask[0..words) (hipExtStreamCreateWithCUMask; bit i of word w = CU 32 w + i),
+ * e.g. to keep a set of CUs free of long traversal launches for a latency-bound
+ * chain on another stream. Destroy with pt_stream_destroy. No GL counterpart. */
+int pt_stream_create_cu_masked(uint32_t words, const uint32_t* mask, void** out);
+int pt_stream_destroy(void* hip_stream);   /* release (above), wait for its work, destroy */
+int pt_device_cus(int* n);                 /* compute units of the library's device */
 int pt_sync(void);                          /* wait for all queued draws */
 const char* pt_last_error(void);
 int pt_version(void);

@@ -1370,7 +1370,17 @@ const ptk::WfFork* wf_fork(Pass* p, hipStream_t s, int* rc) {
   auto it = g.forks.find(s);
   if (it != g.forks.end()) return &it->second;
   ptk::WfFork f{};
-  hipError_t e = hipStreamCreateWithFlags(&f.side, hipStreamNonBlocking);
+  // the side stream runs on the draw stream's CUs (pt_stream_create_cu_masked): a CU mask that keeps CUs free of the
+  // traversal launches must hold for the forked walk too
+  hipError_t e = hipSuccess;
+  int ncu = 0;
+  uint32_t mask[16] = {};
+  bool masked = false;
+  if (s && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, g.device) == hipSuccess && ncu > 0 &&
+      ncu <= 512 && hipExtStreamGetCUMask(s, (uint32_t)((ncu + 31) / 32), mask) == hipSuccess)
+    for (int i = 0; i < ncu; ++i) masked = masked || !((mask[i / 32] >> (i % 32)) & 1u);
+  if (masked) e = hipExtStreamCreateWithCUMask(&f.side, (uint32_t)((ncu + 31) / 32), mask);
+  else e = hipStreamCreateWithFlags(&f.side, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&f.fork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&f.join, hipEventDisableTiming);
   if (e != hipSuccess) {
@@ -1815,6 +1825,34 @@ int pt_stream_release(void* s) {
     kv.second.uses.erase(u);
   }
   if (g.stream == st) g.stream = g.own;
+  return PT_OK;
+}
+
+int pt_stream_create_cu_masked(uint32_t words, const uint32_t* mask, void** out) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  if (!mask || !out || words == 0) return err(PT_ERR_ARG, "CU mask and output needed");
+  hipStream_t s = nullptr;
+  HIPCHK(hipExtStreamCreateWithCUMask(&s, words, mask));  // (the size counts uint32 words)
+  *out = (void*)s;
+  return PT_OK;
+}
+
+int pt_stream_destroy(void* s) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  if (!s) return err(PT_ERR_ARG, "null stream");
+  TRY(pt_stream_release(s));
+  HIPCHK(hipStreamSynchronize((hipStream_t)s));
+  HIPCHK(hipStreamDestroy((hipStream_t)s));
+  return PT_OK;
+}
+
+int pt_device_cus(int* n) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  if (!n) return err(PT_ERR_ARG, "null output");
+  HIPCHK(hipDeviceGetAttribute(n, hipDeviceAttributeMultiprocessorCount, g.device));
   return PT_OK;
 }
 

@@ -74,6 +74,9 @@ _PT_SIGS = [
     ("pt_set_stream", C.c_int, [_vp]),
     ("pt_use_own_stream", C.c_int, []),
     ("pt_stream_release", C.c_int, [_vp]),
+    ("pt_stream_create_cu_masked", C.c_int, [C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_void_p)]),
+    ("pt_stream_destroy", C.c_int, [_vp]),
+    ("pt_device_cus", C.c_int, [C.POINTER(C.c_int)]),
     ("pt_sync", C.c_int, []),
     ("pt_last_error", C.c_char_p, []),
     ("pt_version", C.c_int, []),

@@ -879,6 +879,24 @@ class FrameShardRenderer(BandRenderer):
         for p, _ in self.full.pt_slots:
             p.set_rows(0, H)
         self.own_slots = self.full.K
+        # experiment (PTSVGF_OWN_CU_RESERVE = R): the whole-frame path tracer's streams never use R CUs spread over the
+        # XCDs, so the band's G-buffer and SVGF chain (sequential through its history, a chain of short launches) always
+        # find free CUs beside the long traversal launches
+        self._masked = []
+        reserve = int(os.environ.get("PTSVGF_OWN_CU_RESERVE", "0"))
+        if reserve > 0:
+            import ctypes as C
+
+            from ._lib import check, pt
+            from .renderer import masked_stream, reserved_cus
+
+            n = C.c_int()
+            check(pt().pt_device_cus(C.byref(n)))
+            excl = reserved_cus(n.value, reserve)
+            for i in range(len(self.full._streams)):
+                st, h = masked_stream(excl)
+                self.full._streams[i] = st
+                self._masked.append(h)
         self._own_free = [None] * self.own_slots  # event: the window exchange that sent the slot's last frame is done
         self._win = []  # frames registered since the last window exchange
         kw.setdefault("front_streams", 1)  # band front ends are a G-buffer each: one stream, in order
@@ -1090,6 +1108,12 @@ class FrameShardRenderer(BandRenderer):
         self._full_tensors.clear()
         release_stream(self._recv_stream)
         self._recv_stream = None
+        if self._masked:
+            from ._lib import check, pt
+
+            for h in self._masked:
+                check(pt().pt_stream_destroy(h))
+            self._masked = []
 
 
 def tile_layout(plan: BandPlan, W: int, batch: int, count):

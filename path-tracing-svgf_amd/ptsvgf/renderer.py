@@ -90,6 +90,39 @@ def release_stream(stream) -> None:
     _FREE_STREAMS.setdefault(key, []).append(stream)
 
 
+def reserved_cus(ncu: int, reserve: int, xcds: int = 8) -> list:
+    """`reserve` CU indices spread evenly over the XCDs whether the CU mask numbers CUs XCD by XCD (XCD = i // (ncu /
+    xcds)) or round-robin (XCD = i % xcds): the j-th reserved CU sits in block j % xcds at residue j % xcds."""
+    per = ncu // xcds
+    out = []
+    for j in range(reserve):
+        b, k = j % xcds, j // xcds
+        out.append(b * per + (b + xcds * k) % per)
+    return sorted(set(out))
+
+
+def masked_stream(exclude: list):
+    """A stream whose kernels never run on the CUs in `exclude` (pt_stream_create_cu_masked), as a torch external
+    stream; returns (stream, raw handle) — destroy the handle with pt_stream_destroy after the last use."""
+    import ctypes as C
+
+    import torch
+
+    from ._lib import check, pt
+
+    n = C.c_int()
+    check(pt().pt_device_cus(C.byref(n)))
+    words = (n.value + 31) // 32
+    mask = (C.c_uint32 * words)(*([0xFFFFFFFF] * words))
+    for i in range(n.value, words * 32):
+        mask[i // 32] &= ~(1 << (i % 32)) & 0xFFFFFFFF
+    for i in exclude:
+        mask[i // 32] &= ~(1 << (i % 32)) & 0xFFFFFFFF
+    h = C.c_void_p()
+    check(pt().pt_stream_create_cu_masked(words, mask, C.byref(h)))
+    return torch.cuda.ExternalStream(h.value), h.value
+
+
 class Renderer:
     def __init__(self, scene: Scene, width: int, height: int, config: parameter_config | None = None,
                  mode: str = "fast", aspect_corrected: bool | None = None, band=None, prune: bool = True,

@@ -1,0 +1,79 @@
+"""The GPU's full-size bench frame against the independent float64 restatement of path_tracing.frag (VERDICT r05 weak
+1: the full-size 1080p / 4K checks compare the HIP path with the oracle only, and both share glsl_builtins.h).
+
+tests/test_independent_pt.py's Restatement (numpy float64 from the shader's text, numpy's own transcendentals,
+brute-force closest hits, nothing from glsl_builtins.h) traces 32 x 32 crops of the 4K bench frame the GPU rendered
+(aspect-corrected primary rays, the full 2048 x 1024 environment): on the default camera the crops holding the most
+wood (clearcoat), brass (metallic) and leaf (sheen) pixels, and on the surface-dominated camera the most leafy crop at
+frameCounter 3. Same bar as the oracle's: per channel within 1e-3 relative on all but 1 % of the pixels (branch flips
+between float64 and fp32 decisions), colour median relative difference at fp32 rounding (path_tracing.frag:1056-1128)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+MATERIALS = {"wood": (0.45, 0.28, 0.14), "brass": (0.80, 0.62, 0.35), "leaf": (0.16, 0.42, 0.12)}
+CROP = 32
+W, H = 3840, 2160
+
+
+def _best_crop(albedo, colour):
+    """The CROP x CROP window (on a CROP grid) holding the most pixels of this base colour."""
+    m = np.all(np.abs(albedo[..., :3] - np.asarray(colour, np.float32)) < 1e-3, -1)
+    g = m[:H - H % CROP, :W - W % CROP].reshape(H // CROP, CROP, W // CROP, CROP).sum((1, 3))
+    j, i = np.unravel_index(int(np.argmax(g)), g.shape)
+    return (int(i) * CROP, int(j) * CROP, CROP, CROP), int(g[j, i])
+
+
+# bench.py's VIEWS (orbit radius, elevation, azimuth, look-at: Utils/camera.h:14-38 parameters)
+VIEWS = {"default": None, "surface": dict(r_dis=0.8, upAngle=70.0, rotatAngle=180.0, move_vec=(0.4, -0.25, 0.0))}
+
+
+def _frame(gl, scene, view, frames):
+    from ptsvgf.camera import parameter_config, rigid_inverse
+    from ptsvgf.renderer import Renderer
+
+    r = Renderer(scene, W, H, parameter_config(), mode="fast", aspect_corrected=True, run_taa=False, run_output=False)
+    if VIEWS[view]:
+        for k, v in VIEWS[view].items():
+            setattr(r.camera, k, np.array(v, np.float32) if isinstance(v, tuple) else np.float32(v))
+        r.camera.dirty = True
+    for _ in range(frames):
+        r.frame()
+    cam = r.camera
+    fc = int(cam.frameCounter) - 1
+    eye, rot = cam.cam_position, rigid_inverse(cam.cam_view_mat)
+    pl = r.planes()
+    out = [gl.readback(pl[k]) for k in ("color", "emission", "albedo")]
+    r.close()
+    return out, fc, eye, rot
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("view,frames,materials", [("default", 1, ("wood", "brass", "leaf")),
+                                                   ("surface", 4, ("leaf",))])
+def test_gpu_4k_frame_matches_independent_restatement(gpu, scene_bench, view, frames, materials):
+    from test_independent_pt import Restatement, _compare
+
+    planes, fc, eye, rot = _frame(gpu, scene_bench, view, frames)
+    rs = Restatement(scene_bench, cull_group=32)
+    refs, mines = [[], [], []], [[], [], []]
+    for name in materials:
+        crop, n = _best_crop(planes[2], MATERIALS[name])
+        assert n >= 64, (view, name, n)  # the crop really holds that material
+        x0, y0, cw, ch = crop
+        mine = rs.frame(W, H, fc, eye, rot, crop=crop, aspect=True)
+        for j in range(3):
+            refs[j].append(planes[j][y0:y0 + ch, x0:x0 + cw])
+            mines[j].append(mine[j])
+        f1, m1, l1 = _compare([p[y0:y0 + ch, x0:x0 + cw] for p in planes], mine)
+        print(f"{view} fc {fc} {name} crop {crop} ({n} px): outside 1e-3 {f1:.4f}, median rel {m1:.2e}, "
+              f"beyond 1e-5 {l1:.4f}")
+    frac, med, loose = _compare([np.concatenate(a, 1) for a in refs], [np.concatenate(b, 1) for b in mines])
+    lit = float(np.mean(np.concatenate(refs[0], 1)[..., :3] > 0))
+    print(f"{view}: pixels outside 1e-3 {frac:.4f}, colour median relative difference {med:.2e}, beyond 1e-5 "
+          f"{loose:.4f}, lit {lit:.2f}")
+    assert lit > 0.5
+    assert frac <= 0.01, frac
+    assert med <= 1e-6, med
+    assert loose <= 0.05, loose

@@ -305,15 +305,18 @@ class Restatement:
         return np.where((xi3 <= pd)[:, None], Ld, np.where((xi3 <= pd + ps)[:, None], Ls, Lc))
 
     # ---------------------------------------------------------------- the frame ---
-    def frame(self, W, H, frameCounter, eye, camRot, clamp_threshold=10.0, max_depth=2, crop=None):
+    def frame(self, W, H, frameCounter, eye, camRot, clamp_threshold=10.0, max_depth=2, crop=None, aspect=False):
         """The W x H frame, or its crop = (x0, y0, cw, ch) (pixels keep their global coordinates: the ray and the RNG
-        seeds are the whole frame's)."""
+        seeds are the whole frame's). aspect: the build's aspect-corrected primary ray for W != H (pix.x scaled by
+        W / H; the reference's literal ray has no aspect term, DESIGN.md "Known deviations")."""
         x0, y0, cw, ch = crop if crop is not None else (0, 0, W, H)
         ys, xs = np.mgrid[y0:y0 + ch, x0:x0 + cw]
         x, y = xs.reshape(-1).astype(np.uint64), ys.reshape(-1).astype(np.uint64)
         R = x.size
         M = np.asarray(camRot, np.float64).reshape(4, 4)                   # column-major: M[col][row]
         pix = np.stack([(2.0 * x + 1.0) / W - 1.0, (2.0 * y + 1.0) / H - 1.0], -1)
+        if aspect:
+            pix[:, 0] *= W / H
         d = _norm(pix[:, :1] * M[0, :3] + pix[:, 1:] * M[1, :3] + (-1.0) * M[2, :3])  # cameraRotate * (pix, -1, 0)
         S = np.tile(np.asarray(eye, np.float64), (R, 1))
         seed = ((x * 1973 + y * 9277 + np.uint64(frameCounter) * 26699) & 0xFFFFFFFF) | 1   # :433-436
