@@ -314,9 +314,13 @@ class Restatement:
         x, y = xs.reshape(-1).astype(np.uint64), ys.reshape(-1).astype(np.uint64)
         R = x.size
         M = np.asarray(camRot, np.float64).reshape(4, 4)                   # column-major: M[col][row]
-        pix = np.stack([(2.0 * x + 1.0) / W - 1.0, (2.0 * y + 1.0) / H - 1.0], -1)
+        # pix: vert.vert's varying, which the rasteriser delivers in fp32 (the build's aspect term, W / H, in fp32 too)
+        f32 = np.float32
+        px = (f32(2) * x.astype(f32) + f32(1)) / f32(W) - f32(1)
+        py = (f32(2) * y.astype(f32) + f32(1)) / f32(H) - f32(1)
         if aspect:
-            pix[:, 0] *= W / H
+            px = px * (f32(W) / f32(H))
+        pix = np.stack([px.astype(np.float64), py.astype(np.float64)], -1)
         d = _norm(pix[:, :1] * M[0, :3] + pix[:, 1:] * M[1, :3] + (-1.0) * M[2, :3])  # cameraRotate * (pix, -1, 0)
         S = np.tile(np.asarray(eye, np.float64), (R, 1))
         seed = ((x * 1973 + y * 9277 + np.uint64(frameCounter) * 26699) & 0xFFFFFFFF) | 1   # :433-436
