@@ -758,3 +758,39 @@ def test_fused_modulate_equals_modulate_pass(gpu, scene_small, K):
         assert a.keys() == b.keys()
         for k in a:
             assert np.array_equal(a[k].view(np.uint32), b[k].view(np.uint32)), k
+
+
+def test_cu_masked_stream_same_bits(gpu, scene_small):
+    """pt_stream_create_cu_masked: frames drawn on a stream kept off 32 CUs (and the trace_fork side stream, which
+    inherits the mask) give the default stream's bits; pt_stream_destroy releases it."""
+    import ctypes as C
+
+    import torch
+
+    from ptsvgf._lib import check, pt
+    from ptsvgf.renderer import masked_stream, reserved_cus
+
+    gl = gpu
+    W, H = 64, 48
+    n = C.c_int()
+    check(pt().pt_device_cus(C.byref(n)))
+    assert n.value >= 64
+    excl = reserved_cus(n.value, 32)
+    assert len(excl) == 32 and len({i // (n.value // 8) for i in excl}) == 8
+    outs = []
+    for masked in (False, True):
+        st, h = masked_stream(excl) if masked else (torch.cuda.current_stream(), None)
+        with torch.cuda.stream(st):
+            r = _renderer(scene_small, W, H, mode="fast", run_taa=False, run_output=False)
+            r.pass_path_tracing.set_uniform_int("trace_fork", 1)
+            for f in range(3):
+                if f == 2:
+                    r.camera.orbit(1.0, 0.0)
+                r.frame()
+            outs.append({k: gl.readback(r.planes()[k]) for k in ("color", "atrous", "modulate")})
+            r.close()
+        torch.cuda.synchronize()
+        if h is not None:
+            check(pt().pt_stream_destroy(h))
+    for k in outs[0]:
+        assert np.array_equal(outs[0][k], outs[1][k]), k
