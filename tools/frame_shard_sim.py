@@ -184,6 +184,12 @@ def sim_rank(rk, bounds=None):
     for kv in filter(None, os.environ.get("PT_UNIFORMS", "").split(",")):  # name=value,... on the path tracer
         name, val = kv.split("=")
         r.pass_path_tracing.set_uniform_int(name, int(val))
+    rr = r.r  # SVGF_UNIFORMS=name:value;...: on the band's SVGF draws (as bench.py --svgf-uniform)
+    for kv in filter(None, os.environ.get("SVGF_UNIFORMS", "").split(";")):
+        name, val = kv.split(":")
+        for sp in [*rr.reproject, rr.variance_compute_pass, *rr.atrous_to.values(), *rr.atrous_mod_to.values(),
+                   rr.svgf_modulate_pass]:
+            sp.set_uniform_int(name, int(val))
     for _ in range(2 * K + N):  # every band slot and own slot used before timing (first use allocates)
         r.frame()
     r.r.flush()
