@@ -665,11 +665,13 @@ def main():
                                  "path_tracer": pt_rates(sv, sfps),
                                  "passes_ms": {k: round(v, 4) for k, v in sv["per_pass"].items()}}
 
-    if not args.no_extras and world == 1 and not args.moving:
-        # configs[4]'s temporal stress on one GPU: the camera orbits 1 deg every frame (Utils/camera.h:71 resets
-        # frameCounter on each move), so reprojection sees real motion, disocclusions fall back to the 3x3 search
-        # (svgf_reproject.frag:111-141) and young history takes the 7x7 variance (svgf_variance.frag:68-96)
-        mv = run(W, H, K, args.view, moving=True)
+    if not args.no_extras and not args.moving:
+        # configs[4]'s temporal stress: the camera orbits 1 deg every frame (Utils/camera.h:71 resets frameCounter on
+        # each move), so reprojection sees real motion, disocclusions fall back to the 3x3 search
+        # (svgf_reproject.frag:111-141) and young history takes the 7x7 variance (svgf_variance.frag:68-96). On N
+        # ranks (configs[4] names 8) the history exchanges carry the moved camera's rows (dist.MotionCheck) and the
+        # gathered bands are checked bitwise against a one-GPU render of the same orbit (band_parity)
+        mv = run(W, H, K, args.view, moving=True, parity=world > 1 and not args.no_band_parity)
         mfps = args.steps / mv["dt"]
         extra["moving"] = {"workload": f"{args.scene} {W}x{H} 1spp depth2 + 5-iter SVGF, orbit 1 deg/frame",
                            "fps": round(mfps, 3), "ms_per_step": round(mv["dt"] / args.steps * 1e3, 3),
@@ -678,7 +680,10 @@ def main():
                            "roofline": atrous_roofline(mv, W, mv["rows"], "moving"),
                            "path_tracer": pt_rates(mv, mfps),
                            "passes_ms": {k: round(v, 4) for k, v in mv["per_pass"].items()}}
-        if not args.no_1080p and (W, H) == (3840, 2160):
+        for key in ("bands", "band_parity", "max_history_rows"):
+            if mv.get(key) is not None:
+                extra["moving"][key] = mv[key]
+        if world == 1 and not args.no_1080p and (W, H) == (3840, 2160):
             mv2 = run(1920, 1080, k1080, args.view, probes=False, moving=True)
             extra["moving"]["fps_1080p"] = round(args.steps / mv2["dt"], 3)
 

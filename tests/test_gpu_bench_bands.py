@@ -114,3 +114,23 @@ def test_bench_frame_shard_8_ranks_gloo(W, H, balance):
         assert bands["bounds"] in [b for _, b in bands["calibration"]], bands
     else:
         assert bands["bounds"] == equal
+
+
+def test_bench_moving_extra_on_ranks_gloo():
+    """The driver's multi-GPU line carries configs[4] (moving camera, per-pass times) beside the static run: at N ranks
+    bench.py (extras on) draws the 1 deg/frame orbit through the frame shard and checks its gathered bands bitwise
+    against a one-GPU render of the same orbit (the history exchanges carry the moved camera's rows)."""
+    world = 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "bench.py"),
+           "--gpus", str(world), "--backend", "gloo", "--width", "320", "--height", "256", "--steps", "4",
+           "--warmup", "2", "--no-1080p", "--no-cpu-baseline", "--equal-bands", "1"]
+    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-4000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    mv = line["moving"]
+    print(json.dumps({k: mv[k] for k in ("fps", "history", "max_history_rows") if k in mv}), json.dumps(mv["band_parity"]))
+    assert line["band_parity"]["bit_exact"] and mv["band_parity"]["bit_exact"], mv["band_parity"]
+    assert mv["max_history_rows"] > 3  # the moved camera's history rows crossed ranks
+    assert {"reproject", "variance", "atrous"} <= set(mv["passes_ms"]) and mv["fps"] > 0
+    assert "history" in mv["bands"]["exchange_ms_per_frame"]
