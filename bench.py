@@ -510,9 +510,12 @@ def main():
             moves.append(None)  # trace_stats drew one frame (no camera move)
             out["stats"] = dict(zip(st, allsum([float(v) for v in st.values()])))
             r.profile(True)
-            step()
+            # on N ranks a frame's back end runs back_lag frames after its front end: profile that many more frames, so
+            # that at least one SVGF chain is timed (per_frame_passes: each pass per frame it served)
+            for _ in range(1 + (rr.lag if world > 1 else 0)):
+                step()
             torch.cuda.synchronize()
-            out["per_pass"] = r.pass_times()
+            out["per_pass"] = per_frame_passes(r)
             r.profile(False)
             if world > 1 and parity:
                 # the bands' rows before the a-trous replay below: a band's replay reads ghost rows the frame's later
@@ -610,6 +613,26 @@ def main():
                 "frac_pmc_traffic": round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
                 "frac_background_weighted": round(weighted / t / 1e9 / HBM_PEAK_GBS, 4),
                 "background_fraction": round(bgf, 4)}
+
+    def per_frame_passes(r):
+        """Per-pass ms per frame of the profiled frames (HIP events per draw): the SVGF passes over the frames whose
+        back end was drawn (a-trous: its four plain iterations, atrous_modulate the fused last one), the G-buffer over
+        the front ends drawn, the frame shard's whole-frame G-buffer / path tracer (full_*) over the frames this rank
+        traced; atrous_avg_ms = one a-trous launch; frame_sum_ms = the per-frame sum."""
+        rr = getattr(r, "r", r)
+        times = {k: list(v) for k, v in rr._times.items()}
+        full = getattr(r, "full", None)
+        if full is not None:
+            for k in ("gbuffer", "pathtrace"):
+                if full._times.get(k):
+                    times["full_" + k] = list(full._times[k])
+        nback = len(times.get("reproject", [])) or 1
+        back = ("reproject", "variance", "atrous", "atrous_modulate", "modulate", "taa")
+        out = {k: float(np.sum(v)) / (nback if k in back else max(1, len(v))) for k, v in times.items()}
+        if times.get("atrous"):
+            out["atrous_avg_ms"] = float(np.mean(times["atrous"]))
+        out["frame_sum_ms"] = float(sum(v for k, v in out.items() if k != "atrous_avg_ms"))
+        return out
 
     def shadow_split(st):
         return {"point_rays": int(st.get("shadow_point_rays", 0)), "occluded": int(st.get("shadow_occluded", 0))}
