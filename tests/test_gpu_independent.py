@@ -82,3 +82,82 @@ def test_gpu_4k_frame_matches_independent_restatement(gpu, scene_bench, view, fr
     # channels beyond 1e-5 relative: the brass's metallic GGX lobe (a sharp D term) amplifies fp32 rounding of N.H
     # (24-27 % of a brass crop's channels on the CPU oracle, 12 % of a leaf crop's)
     assert loose <= 0.2, loose
+
+
+@pytest.mark.timeout(900)
+def test_gpu_4k_svgf_matches_independent_restatement(gpu, scene_bench):
+    """The GPU's production SVGF chain at 4K against tests/test_independent_svgf.py's float64 restatement of the
+    shaders (numpy's pow / exp / sqrt, texture fetches written out; nothing from glsl_builtins.h): two static frames,
+    then an orbited frame whose history is reprojected with real sub-texel motion. On three 48 x 48 crops holding
+    surface pixels: the reprojection (svgf_reproject.frag:26-204) from the GPU's own previous-frame planes, per channel
+    within 1e-3 relative on all but 1 % of the pixels (a LINEAR tap on the sampler's 8-bit rounding boundary may round
+    either way in fp32 and float64); and the chain from the GPU's reprojected planes — variance (svgf_variance.frag),
+    a-trous iteration 1 (the next frame's history), all five a-trous iterations (svgf_Atrous.frag, 62 rows of
+    margin) and modulate — within north_star's 1e-3 per-channel L-inf (relative above 1)."""
+    from ptsvgf.camera import parameter_config
+    from ptsvgf.renderer import Renderer
+    from test_independent_svgf import atrous_ref, modulate_ref, reproject_ref, variance_ref
+
+    gl = gpu
+    r = Renderer(scene_bench, W, H, parameter_config(), mode="fast", aspect_corrected=True, run_taa=False,
+                 run_output=False)
+    for _ in range(2):
+        r.frame()
+    pl = r.planes()
+    prev = {k: gl.readback(pl[k]) for k in ("history_illum", "reproj_moments", "normal_depth")}
+    r.camera.orbit(1.0, 0.5)
+    r.frame()
+    pl = r.planes()
+    cur = {k: gl.readback(pl[k]) for k in ("velocity", "color", "albedo", "emission", "normal_depth", "fwidth",
+                                           "reproj_illum", "reproj_moments", "variance", "history_illum", "atrous",
+                                           "modulate")}
+    r.close()
+    surf = cur["normal_depth"][..., 3] != 1.0
+    M, C = 70, 48
+    # crops: the 48 x 48 windows (on a 48 grid, at least M from the frame edges) with the most surface pixels in three
+    # bands of columns (left, middle, right thirds)
+    g = surf[:H - H % C, :W - W % C].reshape(H // C, C, W // C, C).sum((1, 3))
+    crops = []
+    for third in range(3):
+        lo, hi = third * (W // C) // 3, (third + 1) * (W // C) // 3
+        best = None
+        for j in range(2, H // C - 2):
+            for i in range(max(lo, 2), min(hi, W // C - 2)):
+                if best is None or g[j, i] > g[best]:
+                    best = (j, i)
+        crops.append((best[1] * C, best[0] * C))
+    worst = {}
+
+    def rel(got, want, inner=None):
+        d = np.abs(got[..., :3].astype(np.float64) - want[..., :3]) / np.maximum(1.0, np.abs(want[..., :3]))
+        return float(np.nanmax(d)), float(np.mean(d.max(-1) > 1e-3))
+
+    for x0, y0 in crops:
+        assert surf[y0:y0 + C, x0:x0 + C].sum() >= 256, (x0, y0)
+        oi, om = reproject_ref(cur["velocity"], cur["color"], cur["albedo"], cur["emission"], prev["history_illum"],
+                               prev["reproj_moments"], cur["normal_depth"], prev["normal_depth"], cur["fwidth"],
+                               crop=(x0, y0, C, C))
+        inner = (slice(y0, y0 + C), slice(x0, x0 + C))
+        for name, got, want in (("reproj_illum", cur["reproj_illum"][inner], oi),
+                                ("reproj_moments", cur["reproj_moments"][inner], om)):
+            mx, frac = rel(got, want)
+            worst[name] = max(worst.get(name, (0, 0)), (frac, mx))
+            assert frac <= 0.01, (name, x0, y0, mx, frac)
+        sl = (slice(y0 - M, y0 + C + M), slice(x0 - M, x0 + C + M))
+        nd, fw = cur["normal_depth"][sl], cur["fwidth"][sl]
+        a = variance_ref(cur["reproj_illum"][sl], cur["reproj_moments"][sl], nd, fw)
+        chain = {"variance": a}
+        for i in range(5):
+            a = atrous_ref(a, nd, fw, 1 << i)
+            if i == 1:
+                chain["history_illum"] = a
+        chain["atrous"] = a
+        chain["modulate"] = modulate_ref(cur["albedo"][sl], cur["emission"][sl], a, nd)
+        cin = (slice(M, M + C), slice(M, M + C))
+        for name, want in chain.items():
+            mx, frac = rel(cur[name][inner], want[cin])
+            worst[name] = max(worst.get(name, (0, 0)), (frac, mx))
+            assert mx <= 1e-3, (name, x0, y0, mx)
+        young = int(np.sum((cur["reproj_moments"][inner][..., 2] < 4) & surf[inner]))
+        print(f"crop ({x0}, {y0}): {int(surf[inner].sum())} surface px, {young} young-history px")
+    print("worst (fraction beyond 1e-3, max relative):", {k: (round(f, 4), float(f"{m:.2e}")) for k, (f, m) in worst.items()})

@@ -183,22 +183,27 @@ def tex_linear(img, u, v):
 
 
 def reproject_ref(motion, color, albedo, emission, prev_illum, prev_moments, nd, prev_nd, fw, depth_thr=10.0,
-                  normal_thr=16.0):
+                  normal_thr=16.0, crop=None):
     """svgf_reproject.frag:26-204. Every history fetch (the four taps' previous normal / depth, illumination and
     moments, the 3x3 fallback, the history length at uv - motion) is a LINEAR texture fetch (tex_linear); the
-    current-frame planes are read at the pixel's own centre (plain texels)."""
+    current-frame planes are read at the pixel's own centre (plain texels). crop = (x0, y0, cw, ch): only those
+    pixels of the whole frame (outputs cw x ch)."""
+    H, W = color.shape[:2]
+    x0, y0, cw, ch = crop if crop is not None else (0, 0, W, H)
+    if crop is not None:  # the current-frame planes are read at the crop's pixels only; the history at any uv
+        sl = (slice(y0, y0 + ch), slice(x0, x0 + cw))
+        motion, color, albedo, emission, nd, fw = (a[sl] for a in (motion, color, albedo, emission, nd, fw))
     f = lambda a: a.astype(np.float64)  # noqa: E731
     motion, color, albedo, emission, prev_illum, prev_moments, nd, prev_nd, fw = map(
         f, (motion, color, albedo, emission, prev_illum, prev_moments, nd, prev_nd, fw))
-    H, W = color.shape[:2]
     iw, ih = 1.0 / W, 1.0 / H
-    oi, om = np.zeros((H, W, 4)), np.zeros((H, W, 4))
-    for y in range(H):
-        for x in range(W):
-            uv = np.array([(x + 0.5) * iw, (y + 0.5) * ih])
+    oi, om = np.zeros((ch, cw, 4)), np.zeros((ch, cw, 4))
+    for y in range(ch):
+        for x in range(cw):
+            uv = np.array([(x0 + x + 0.5) * iw, (y0 + y + 0.5) * ih])
             zc = nd[y, x, 3]
             if zc == 1.0:
-                oi[y, x], om[y, x] = color[y, x], prev_moments[y, x]
+                oi[y, x], om[y, x] = color[y, x], prev_moments[y0 + y, x0 + x]
                 continue
             with np.errstate(divide="ignore", invalid="ignore"):
                 ill = (color[y, x, :3] - emission[y, x, :3]) / np.maximum(albedo[y, x, :3], 0.001)
