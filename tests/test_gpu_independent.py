@@ -89,11 +89,12 @@ def test_gpu_4k_svgf_matches_independent_restatement(gpu, scene_bench):
     """The GPU's production SVGF chain at 4K against tests/test_independent_svgf.py's float64 restatement of the
     shaders (numpy's pow / exp / sqrt, texture fetches written out; nothing from glsl_builtins.h): two static frames,
     then an orbited frame whose history is reprojected with real sub-texel motion. On three 48 x 48 crops holding
-    surface pixels: the reprojection (svgf_reproject.frag:26-204) from the GPU's own previous-frame planes, per channel
-    within 1e-3 relative on all but 1 % of the pixels (a LINEAR tap on the sampler's 8-bit rounding boundary may round
-    either way in fp32 and float64); and the chain from the GPU's reprojected planes — variance (svgf_variance.frag),
-    a-trous iteration 1 (the next frame's history), all five a-trous iterations (svgf_Atrous.frag, 62 rows of
-    margin) and modulate — within north_star's 1e-3 per-channel L-inf (relative above 1)."""
+    surface pixels, within north_star's 1e-3 per-channel L-inf (relative above 1): the reprojection
+    (svgf_reproject.frag:26-204) from the GPU's own previous-frame planes, its texture coordinates in fp32 as GLSL's
+    vec2 computes them (in float64 a real motion's taps land on the other side of the sampler's 8-bit rounding steps
+    on ~0.5 % of the pixels); and the chain from the GPU's reprojected planes — variance (svgf_variance.frag), a-trous
+    iteration 1 (the next frame's history), all five a-trous iterations (svgf_Atrous.frag, 62 rows of margin) and
+    modulate."""
     from ptsvgf.camera import parameter_config
     from ptsvgf.renderer import Renderer
     from test_independent_svgf import atrous_ref, modulate_ref, reproject_ref, variance_ref
@@ -136,13 +137,13 @@ def test_gpu_4k_svgf_matches_independent_restatement(gpu, scene_bench):
         assert surf[y0:y0 + C, x0:x0 + C].sum() >= 256, (x0, y0)
         oi, om = reproject_ref(cur["velocity"], cur["color"], cur["albedo"], cur["emission"], prev["history_illum"],
                                prev["reproj_moments"], cur["normal_depth"], prev["normal_depth"], cur["fwidth"],
-                               crop=(x0, y0, C, C))
+                               crop=(x0, y0, C, C), coords32=True)
         inner = (slice(y0, y0 + C), slice(x0, x0 + C))
         for name, got, want in (("reproj_illum", cur["reproj_illum"][inner], oi),
                                 ("reproj_moments", cur["reproj_moments"][inner], om)):
             mx, frac = rel(got, want)
             worst[name] = max(worst.get(name, (0, 0)), (frac, mx))
-            assert frac <= 0.01, (name, x0, y0, mx, frac)
+            assert mx <= 1e-3, (name, x0, y0, mx, frac)
         sl = (slice(y0 - M, y0 + C + M), slice(x0 - M, x0 + C + M))
         nd, fw = cur["normal_depth"][sl], cur["fwidth"][sl]
         a = variance_ref(cur["reproj_illum"][sl], cur["reproj_moments"][sl], nd, fw)

@@ -171,8 +171,13 @@ def tex_linear(img, u, v):
     sub-texel weights in 8-bit fixed point, rounded (the texture-unit precision GL leaves to the implementation,
     SURVEY.md §7 hard part 3). A fetch at a texel centre returns that texel."""
     H, W = img.shape[:2]
-    qx = np.floor((u * W - 0.5) * 256.0 + 0.5)
-    qy = np.floor((v * H - 0.5) * 256.0 + 0.5)
+    if isinstance(u, np.float32):  # an fp32 coordinate (GLSL's vec2): its texel position in fp32 too
+        f = np.float32
+        qx = float(np.floor((u * f(W) - f(0.5)) * f(256.0) + f(0.5)))
+        qy = float(np.floor((v * f(H) - f(0.5)) * f(256.0) + f(0.5)))
+    else:
+        qx = np.floor((u * W - 0.5) * 256.0 + 0.5)
+        qy = np.floor((v * H - 0.5) * 256.0 + 0.5)
     x0, y0 = int(qx // 256), int(qy // 256)
     ax, ay = (qx - 256.0 * x0) / 256.0, (qy - 256.0 * y0) / 256.0
     xa, xb = min(max(x0, 0), W - 1), min(max(x0 + 1, 0), W - 1)
@@ -183,11 +188,13 @@ def tex_linear(img, u, v):
 
 
 def reproject_ref(motion, color, albedo, emission, prev_illum, prev_moments, nd, prev_nd, fw, depth_thr=10.0,
-                  normal_thr=16.0, crop=None):
+                  normal_thr=16.0, crop=None, coords32=False):
     """svgf_reproject.frag:26-204. Every history fetch (the four taps' previous normal / depth, illumination and
     moments, the 3x3 fallback, the history length at uv - motion) is a LINEAR texture fetch (tex_linear); the
     current-frame planes are read at the pixel's own centre (plain texels). crop = (x0, y0, cw, ch): only those
-    pixels of the whole frame (outputs cw x ch)."""
+    pixels of the whole frame (outputs cw x ch). coords32: the texture coordinates (uv, uv - motion, the taps, the
+    shader's "bilinear weights") in fp32 as GLSL's vec2 computes them (a frame's real motion puts taps on the
+    sampler's 8-bit rounding steps, where float64 coordinates round the other way); the rest stays float64."""
     H, W = color.shape[:2]
     x0, y0, cw, ch = crop if crop is not None else (0, 0, W, H)
     if crop is not None:  # the current-frame planes are read at the crop's pixels only; the history at any uv
@@ -200,7 +207,12 @@ def reproject_ref(motion, color, albedo, emission, prev_illum, prev_moments, nd,
     oi, om = np.zeros((ch, cw, 4)), np.zeros((ch, cw, 4))
     for y in range(ch):
         for x in range(cw):
-            uv = np.array([(x0 + x + 0.5) * iw, (y0 + y + 0.5) * ih])
+            if coords32:
+                f = np.float32
+                uv = np.array([(f(2 * (x0 + x) + 1) / f(W) - f(1)) * f(0.5) + f(0.5),
+                               (f(2 * (y0 + y) + 1) / f(H) - f(1)) * f(0.5) + f(0.5)], np.float32)
+            else:
+                uv = np.array([(x0 + x + 0.5) * iw, (y0 + y + 0.5) * ih])
             zc = nd[y, x, 3]
             if zc == 1.0:
                 oi[y, x], om[y, x] = color[y, x], prev_moments[y0 + y, x0 + x]
@@ -209,7 +221,7 @@ def reproject_ref(motion, color, albedo, emission, prev_illum, prev_moments, nd,
                 ill = (color[y, x, :3] - emission[y, x, :3]) / np.maximum(albedo[y, x, :3], 0.001)
             if np.isnan(ill).any():
                 ill = np.zeros(3)
-            prev = uv - motion[y, x, :2]
+            prev = uv - motion[y, x, :2].astype(np.float32) if coords32 else uv - motion[y, x, :2]
             fwn, fwz = fw[y, x, 0], fw[y, x, 1]
             ncur = nd[y, x, :3]
 
@@ -222,16 +234,24 @@ def reproject_ref(motion, color, albedo, emission, prev_illum, prev_moments, nd,
                 return not (np.linalg.norm(ncur - pnd[:3]) / (fwn + 1e-2) > normal_thr)
 
             offs = [(0.0, 0.0), (iw, 0.0), (0.0, ih), (iw, ih)]
-            v = [valid_at(prev + np.array(o)) for o in offs]
+            if coords32:
+                iw32, ih32 = np.float32(1.0) / np.float32(W), np.float32(1.0) / np.float32(H)
+                offs = [(0.0, 0.0), (iw32, 0.0), (0.0, ih32), (iw32, ih32)]
+            v = [valid_at(prev + np.array(o, prev.dtype)) for o in offs]
             pi, pm, ok = np.zeros(4), np.zeros(2), any(v)
             if ok:
-                fx = prev[0] - int(prev[0] / iw) * iw  # the shader's "bilinear weights" in UV units (:84-91)
-                fy = prev[1] - int(prev[1] / ih) * ih
+                if coords32:
+                    f, iw32, ih32 = np.float32, np.float32(1.0) / np.float32(W), np.float32(1.0) / np.float32(H)
+                    fx = float(prev[0] - f(int(prev[0] / iw32)) * iw32)
+                    fy = float(prev[1] - f(int(prev[1] / ih32)) * ih32)
+                else:
+                    fx = prev[0] - int(prev[0] / iw) * iw  # the shader's "bilinear weights" in UV units (:84-91)
+                    fy = prev[1] - int(prev[1] / ih) * ih
                 wts = [(1 - fx) * (1 - fy), fx * (1 - fy), (1 - fx) * fy, fx * fy]
                 sw = 0.0
                 for k, o in enumerate(offs):
                     if v[k]:
-                        loc = prev + np.array(o)
+                        loc = prev + np.array(o, prev.dtype)
                         pi += wts[k] * tex_linear(prev_illum, *loc)
                         pm += wts[k] * tex_linear(prev_moments, *loc)[:2]
                         sw += wts[k]
@@ -241,7 +261,9 @@ def reproject_ref(motion, color, albedo, emission, prev_illum, prev_moments, nd,
                 n = 0.0
                 for yy in (-1, 0, 1):
                     for xx in (-1, 0, 1):
-                        loc = prev + np.array([xx * iw, yy * ih])
+                        loc = (prev + np.array([xx, yy], np.float32) * np.array(
+                            [np.float32(1.0) / np.float32(W), np.float32(1.0) / np.float32(H)], np.float32)
+                            if coords32 else prev + np.array([xx * iw, yy * ih]))
                         if valid_at(loc):
                             pi += tex_linear(prev_illum, *loc)
                             pm += tex_linear(prev_moments, *loc)[:2]
