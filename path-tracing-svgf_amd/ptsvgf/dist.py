@@ -924,6 +924,7 @@ class FrameShardRenderer(BandRenderer):
         self._sgroup = scatter_group(dist) if world > 1 else None
         self._recv_stream = acquire_stream()
         self.scatter_log = []  # per exchange that carried a frame of this rank: bytes sent
+        self.own_events = None  # a list: (frame, start, end) HIP events of each own front end (diagnostics)
 
     def source(self, f: int) -> int:
         """The rank that traces frame f."""
@@ -1036,6 +1037,10 @@ class FrameShardRenderer(BandRenderer):
         st = fr._streams[o]
         if self._own_free[o] is not None:
             st.wait_event(self._own_free[o])
+        t0 = None
+        if self.own_events is not None:  # diagnostics: when this own front end starts and ends on its stream
+            t0 = torch.cuda.Event(enable_timing=True)
+            t0.record(st)
         fr._use_slot(o)
         fr._stream_to(st)
         fr.pre_viewproj = self.r.pre_viewproj
@@ -1044,8 +1049,10 @@ class FrameShardRenderer(BandRenderer):
         if self.ship_gbuffer:  # the whole frame's motion bound, checked here for every band (MotionCheck)
             self.mcheck.capture(f, self._fmb_dev[o:o + 1], st)
         fr._path_trace(fr.gbuf[o])
-        done = torch.cuda.Event()
+        done = torch.cuda.Event(enable_timing=t0 is not None)
         done.record(st)
+        if t0 is not None:
+            self.own_events.append((f, t0, done))
         return o, done
 
     def trace_stats(self) -> dict:

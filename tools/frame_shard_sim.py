@@ -198,6 +198,8 @@ def sim_rank(rk, bounds=None):
         LOG[k] = 0
     r.r.back_events = []
     r.r.latency_events = []
+    if hasattr(r, "own_events"):
+        r.own_events = []
     # host time in BandRenderer._motion (round 4: a wait for the G-buffer's bound + the per-frame all-reduce; round 5:
     # the host's own bound, MotionCheck) and in the host pacing (Renderer host_pace: frame f waits for SVGF(f - K))
     waits = []
@@ -224,6 +226,24 @@ def sim_rank(rk, bounds=None):
     D.BandRenderer._motion = orig_motion
     r.r.flush()
     torch.cuda.synchronize()
+    own = {}
+    if getattr(r, "own_events", None):
+        # the rank's own front ends (G-buffer + path tracer of a whole frame): their span on the GPU and how much of the
+        # time two or more of them ran at once
+        ref = r.own_events[0][1]
+        iv = [(ref.elapsed_time(a), ref.elapsed_time(b)) for _, a, b in r.own_events]
+        spans = [b - a for a, b in iv]
+        pts = sorted([(a, 1) for a, _ in iv] + [(b, -1) for _, b in iv])
+        cur, last, t2, tany = 0, None, 0.0, 0.0
+        for t, dlt in pts:
+            if last is not None:
+                tany += (t - last) if cur >= 1 else 0.0
+                t2 += (t - last) if cur >= 2 else 0.0
+            cur += dlt
+            last = t
+        own = dict(own_span=sum(spans) / len(spans), own_n=len(spans), own_busy_frac=tany / (pts[-1][0] - pts[0][0]),
+                   own_overlap_frac=t2 / max(tany, 1e-9))
+        r.own_events = None
     ev = [(a, b) for a, b in r.r.back_events if b is not None]
     r.r.back_events = None
     busy = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
@@ -239,7 +259,7 @@ def sim_rank(rk, bounds=None):
     out = dict(rows=(r.plan.y0, r.plan.y1), wall=wall * 1e3, issue=issue * 1e3, cpu=cpu * 1e3, back=busy,
                wait=sum(waits) / FRAMES * 1e3, pace=pace * 1e3, pp={k: v / N for k, v in pp.items()}, latency=lat,
                halo_mb=LOG["halo"] / FRAMES / 1e6, send_mb=LOG["send"] / FRAMES / 1e6,
-               recv_mb=LOG["recv"] / FRAMES / 1e6)
+               recv_mb=LOG["recv"] / FRAMES / 1e6, **own)
     r.close()
     return out
 
@@ -268,6 +288,9 @@ def report(tag, ranks, bounds):
                   f"camera-to-modulate {s['latency']:.2f} ms = {s['latency'] / s['wall']:.1f} frames", flush=True)
             print("   passes alone, ms per frame: " + " ".join(f"{k} {v:.3f}" for k, v in sorted(s["pp"].items())),
                   flush=True)
+            if "own_span" in s:
+                print(f"   own front ends: {s['own_n']}, span {s['own_span']:.3f} ms each, one or more running "
+                      f"{s['own_busy_frac']:.0%} of the time, two or more {s['own_overlap_frac']:.0%} of that", flush=True)
     res = []
     for rk in ranks:
         walls = sorted(s["wall"] for s in runs[rk])
