@@ -86,6 +86,12 @@ int pt_stream_release(void* hip_stream);
  * e.g. to keep a set of CUs free of long traversal launches for a latency-bound
  * chain on another stream. Destroy with pt_stream_destroy. No GL counterpart. */
 int pt_stream_create_cu_masked(uint32_t words, const uint32_t* mask, void** out);
+/* A new non-blocking stream at queue priority `priority` (hipStreamCreateWithPriority;
+ * numerically lower = higher, clamped into pt_stream_priority_range), e.g. to
+ * put long traversal launches below a latency-bound chain. A trace_fork side
+ * stream takes its draw stream's priority. Destroy with pt_stream_destroy. */
+int pt_stream_create_priority(int priority, void** out);
+int pt_stream_priority_range(int* least, int* greatest);
 int pt_stream_destroy(void* hip_stream);   /* release (above), wait for its work, destroy */
 int pt_device_cus(int* n);                 /* compute units of the library's device */
 int pt_sync(void);                          /* wait for all queued draws */

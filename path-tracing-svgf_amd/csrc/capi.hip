@@ -1379,8 +1379,11 @@ const ptk::WfFork* wf_fork(Pass* p, hipStream_t s, int* rc) {
   if (s && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, g.device) == hipSuccess && ncu > 0 &&
       ncu <= 512 && hipExtStreamGetCUMask(s, (uint32_t)((ncu + 31) / 32), mask) == hipSuccess)
     for (int i = 0; i < ncu; ++i) masked = masked || !((mask[i / 32] >> (i % 32)) & 1u);
+  // and at the draw stream's queue priority (pt_stream_create_priority)
+  int prio = 0;
+  if (s) (void)hipStreamGetPriority(s, &prio);
   if (masked) e = hipExtStreamCreateWithCUMask(&f.side, (uint32_t)((ncu + 31) / 32), mask);
-  else e = hipStreamCreateWithFlags(&f.side, hipStreamNonBlocking);
+  else e = hipStreamCreateWithPriority(&f.side, hipStreamNonBlocking, prio);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&f.fork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&f.join, hipEventDisableTiming);
   if (e != hipSuccess) {
@@ -1835,6 +1838,28 @@ int pt_stream_create_cu_masked(uint32_t words, const uint32_t* mask, void** out)
   hipStream_t s = nullptr;
   HIPCHK(hipExtStreamCreateWithCUMask(&s, words, mask));  // (the size counts uint32 words)
   *out = (void*)s;
+  return PT_OK;
+}
+
+int pt_stream_create_priority(int priority, void** out) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  if (!out) return err(PT_ERR_ARG, "output needed");
+  int least = 0, greatest = 0;
+  HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  // numerically lower = higher priority; clamp into [greatest, least]
+  priority = std::min(std::max(priority, std::min(least, greatest)), std::max(least, greatest));
+  hipStream_t s = nullptr;
+  HIPCHK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority));
+  *out = (void*)s;
+  return PT_OK;
+}
+
+int pt_stream_priority_range(int* least, int* greatest) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  TRY(ensure_init());
+  if (!least || !greatest) return err(PT_ERR_ARG, "null output");
+  HIPCHK(hipDeviceGetStreamPriorityRange(least, greatest));
   return PT_OK;
 }
 

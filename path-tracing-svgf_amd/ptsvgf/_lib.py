@@ -75,6 +75,8 @@ _PT_SIGS = [
     ("pt_use_own_stream", C.c_int, []),
     ("pt_stream_release", C.c_int, [_vp]),
     ("pt_stream_create_cu_masked", C.c_int, [C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_void_p)]),
+    ("pt_stream_create_priority", C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    ("pt_stream_priority_range", C.c_int, [C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("pt_stream_destroy", C.c_int, [_vp]),
     ("pt_device_cus", C.c_int, [C.POINTER(C.c_int)]),
     ("pt_sync", C.c_int, []),

@@ -888,13 +888,25 @@ class FrameShardRenderer(BandRenderer):
             import ctypes as C
 
             from ._lib import check, pt
-            from .renderer import masked_stream, reserved_cus
+            from .renderer import masked_stream, release_stream, reserved_cus
 
             n = C.c_int()
             check(pt().pt_device_cus(C.byref(n)))
             excl = reserved_cus(n.value, reserve)
             for i in range(len(self.full._streams)):
                 st, h = masked_stream(excl)
+                release_stream(self.full._streams[i])  # the pool's stream goes back unused
+                self.full._streams[i] = st
+                self._masked.append(h)
+        # experiment (PTSVGF_OWN_PRIORITY = P, e.g. 1 = HIP's low): the whole-frame path tracer's streams at queue
+        # priority P, below the band's G-buffer (normal) and SVGF chain (high)
+        own_prio = os.environ.get("PTSVGF_OWN_PRIORITY")
+        if own_prio is not None and reserve <= 0:
+            from .renderer import priority_stream, release_stream
+
+            for i in range(len(self.full._streams)):
+                st, h = priority_stream(int(own_prio))
+                release_stream(self.full._streams[i])  # the pool's stream goes back unused
                 self.full._streams[i] = st
                 self._masked.append(h)
         self._own_free = [None] * self.own_slots  # event: the window exchange that sent the slot's last frame is done

@@ -123,6 +123,21 @@ def masked_stream(exclude: list):
     return torch.cuda.ExternalStream(h.value), h.value
 
 
+def priority_stream(priority: int):
+    """A stream at HIP queue priority `priority` (pt_stream_create_priority: lower = higher; torch's pool stops at
+    0 and -1, this reaches HIP's low priority too), as a torch external stream; returns (stream, raw handle) — destroy
+    the handle with pt_stream_destroy after the last use."""
+    import ctypes as C
+
+    import torch
+
+    from ._lib import check, pt
+
+    h = C.c_void_p()
+    check(pt().pt_stream_create_priority(int(priority), C.byref(h)))
+    return torch.cuda.ExternalStream(h.value), h.value
+
+
 class Renderer:
     def __init__(self, scene: Scene, width: int, height: int, config: parameter_config | None = None,
                  mode: str = "fast", aspect_corrected: bool | None = None, band=None, prune: bool = True,

@@ -794,3 +794,37 @@ def test_cu_masked_stream_same_bits(gpu, scene_small):
             check(pt().pt_stream_destroy(h))
     for k in outs[0]:
         assert np.array_equal(outs[0][k], outs[1][k]), k
+
+
+def test_priority_stream_same_bits(gpu, scene_small):
+    """pt_stream_create_priority: frames drawn on a low-priority stream (and its trace_fork side stream, which takes
+    the draw stream's priority) give the default stream's bits; out-of-range priorities clamp."""
+    import ctypes as C
+
+    import torch
+
+    from ptsvgf._lib import check, pt
+    from ptsvgf.renderer import priority_stream
+
+    gl = gpu
+    lo, hi = C.c_int(), C.c_int()
+    check(pt().pt_stream_priority_range(C.byref(lo), C.byref(hi)))
+    assert hi.value <= 0 <= lo.value
+    W, H = 64, 48
+    outs = []
+    for prio in (None, lo.value + 5):  # clamped to the least priority
+        st, h = priority_stream(prio) if prio is not None else (torch.cuda.current_stream(), None)
+        with torch.cuda.stream(st):
+            r = _renderer(scene_small, W, H, mode="fast", run_taa=False, run_output=False)
+            r.pass_path_tracing.set_uniform_int("trace_fork", 1)
+            for f in range(3):
+                if f == 2:
+                    r.camera.orbit(1.0, 0.0)
+                r.frame()
+            outs.append({k: gl.readback(r.planes()[k]) for k in ("color", "atrous", "modulate")})
+            r.close()
+        torch.cuda.synchronize()
+        if h is not None:
+            check(pt().pt_stream_destroy(h))
+    for k in outs[0]:
+        assert np.array_equal(outs[0][k], outs[1][k]), k
