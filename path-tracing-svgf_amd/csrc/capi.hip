@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdio>
 #include <algorithm>
+#include <array>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -226,7 +227,7 @@ struct SceneGPU {
   int root_any = 0, need_any = 0;
   bool has4 = false;  // bvh4: the 4-wide form of bvh_any (pack_wide)
   bool nan4 = false;  // a child box of bvh4 has a NaN coordinate (PT_WIDE_SIGNED walks need lo <= hi: not walked)
-  int root4 = 0, need4 = 0;
+  int root4 = 0, need4 = 0, root4c = 0;  // root4c: the closest-hit walks' root (SceneDev::root4c)
   // refine_leaves' fine boxes are padded for rays whose origin lies within kFineEyeReach x the scene's largest vertex
   // coordinate; an eye further out (pt_params) walks the reference tree instead
   float fine_eye_limit = INFINITY;
@@ -644,8 +645,84 @@ static int ref_count_of(int ref) { return (-(ref + 1)) & 15; }
 // Layout (kWideStride x float4: 7 used = 112 B, padded to 128 B at 8): lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] refs[4]; refs >= 0 node index,
 // < 0 leaf, kNoneRef an empty slot. *need: the most stack entries a walk can hold (sum over a path of the
 // children pushed beside the one taken); the kernels check pushes against their stack anyway.
+// Which binary nodes a 4-wide node opens (PTSVGF_WIDE_COLLAPSE, read once): 0 = greedy (until round 6), the largest
+// interior child opened until four slots are used; 1 = SAH-optimal, a dynamic program over the binary tree that picks
+// the grouping with the least summed surface area of 4-wide nodes (each such node is one node step of a walk that
+// reaches it; the leaves, hence their triangle tests, are the same either way); 2 = SAH-optimal for the any-hit
+// (shadow) walks and greedy for the closest-hit walks, two trees in one buffer (SceneDev::root4c; the default);
+// 3 = the reverse. Every form keeps `keep` nodes closed, so each is result-preserving by the argument above.
+// Measured at 4K (profiles/r06/wide_collapse/, one box, two alternating repetitions): greedy 225.2 / 227.2 fps,
+// surface view 78.0 / 78.3; SAH-optimal for both 231.1 / 229.6 and 76.6 / 76.1 (shadow visits -1.5 % / -7.1 %, but
+// the surface view's closest-hit visits +7.8 %: the nearest-first, pruned walk is not what the area sum prices);
+// mode 2 228.0 / 228.4 and 79.3 / 78.7. Same bits in every mode (planes digest, the wide-tree parity tests).
+static int wide_collapse_mode() {
+  static const int m = [] {
+    const char* e = getenv("PTSVGF_WIDE_COLLAPSE");
+    return e ? atoi(e) : 2;
+  }();
+  return m;
+}
+
+// The dynamic program of wide_collapse_mode() 1. For a binary node x: best[x] = A(x) + D(x, 4) (x as a 4-wide node);
+// S(x, j) = the least cost of x's subtree given j slots of the enclosing 4-wide node (one slot: x itself, a leaf at
+// cost 0 or a 4-wide node at best[x]; more: opened, its children sharing the slots); D(x, i) = min over j of
+// S(left, j) + S(right, i - j). Children are stored after their parents (sah_build, fine_subtree), so one pass over
+// the ids from the last to the first sees every child before its parent.
+struct WideCollapse {
+  std::vector<float> best;
+  std::vector<std::array<float, 5>> S, D;
+  std::vector<std::array<signed char, 5>> dsplit;  // D(x, i): slots given to the left child
+  std::vector<std::array<bool, 5>> sopen;          // S(x, j): opened (else one slot)
+  explicit WideCollapse(const std::vector<SahNode>& nodes) {
+    const size_t n = nodes.size();
+    best.assign(n, 0.0f);
+    S.assign(n, {});
+    D.assign(n, {});
+    dsplit.assign(n, {});
+    sopen.assign(n, {});
+    for (size_t k = n; k-- > 0;) {
+      const SahNode& x = nodes[k];
+      const bool leaf = x.n > 0;
+      if (!leaf) {
+        for (int i = 2; i <= 4; ++i) {
+          float b = INFINITY;
+          int bj = 1;
+          for (int j = 1; j < i; ++j) {
+            const float c = S[x.left][j] + S[x.right][i - j];
+            if (c < b) { b = c; bj = j; }
+          }
+          D[k][i] = b;
+          dsplit[k][i] = (signed char)bj;
+        }
+        best[k] = sah_area(x.lo, x.hi) + D[k][4];
+      }
+      const float slot = leaf ? 0.0f : best[k];
+      for (int j = 1; j <= 4; ++j) {
+        const bool open = !leaf && !x.keep && j >= 2 && D[k][j] < slot;
+        S[k][j] = open ? D[k][j] : slot;
+        sopen[k][j] = open;
+      }
+    }
+  }
+  // the children of a 4-wide node rooted at binary node id
+  int children(const std::vector<SahNode>& nodes, int id, int* ch) const {
+    int nc = 0;
+    std::function<void(int, int)> cover = [&](int x, int j) {
+      if (!sopen[x][j]) { ch[nc++] = x; return; }
+      expand(nodes, x, j, cover);
+    };
+    expand(nodes, id, 4, cover);
+    return nc;
+  }
+  void expand(const std::vector<SahNode>& nodes, int x, int i, const std::function<void(int, int)>& cover) const {
+    const int j = dsplit[x][i];
+    cover(nodes[x].left, j);
+    cover(nodes[x].right, i - j);
+  }
+};
+
 static int pack_wide(const std::vector<SahNode>& nodes, const std::function<int(int, int)>& leaf_ref,
-                     std::vector<float4>& out, int* root_ref, int* need) {
+                     std::vector<float4>& out, int* root_ref, int* need, bool dp) {
   out.clear();
   *need = 0;
   auto ref_of = [&](const SahNode& L) { return L.direct ? L.ref : leaf_ref(L.first, L.n); };
@@ -653,10 +730,14 @@ static int pack_wide(const std::vector<SahNode>& nodes, const std::function<int(
     *root_ref = ref_of(nodes[0]);
     return PT_OK;
   }
+  std::unique_ptr<WideCollapse> wc(dp ? new WideCollapse(nodes) : nullptr);
+  double area_sum = 0.0;  // summed surface area of the 4-wide nodes (PTSVGF_WIDE_STATS)
   std::function<int(int, int)> build = [&](int id, int acc) -> int {
     int ch[4] = {nodes[id].left, nodes[id].right, -1, -1};
     int nc = 2;
-    while (nc < 4) {  // open the largest interior child that may be opened
+    area_sum += sah_area(nodes[id].lo, nodes[id].hi);
+    if (dp) nc = wc->children(nodes, id, ch);
+    while (!dp && nc < 4) {  // open the largest interior child that may be opened
       int best = -1;
       float ba = -1.0f;
       for (int c = 0; c < nc; ++c) {
@@ -704,6 +785,10 @@ static int pack_wide(const std::vector<SahNode>& nodes, const std::function<int(
   };
   build(0, 0);
   *root_ref = 0;
+  if (getenv("PTSVGF_WIDE_STATS"))
+    fprintf(stderr, "ptsvgf: 4-wide tree (%s collapse): %zu nodes, summed node area / root area %.4f, stack need %d\n",
+            dp ? "SAH-optimal" : "greedy", out.size() / ptk::kWideStride,
+            area_sum / std::max(1e-30, (double)sah_area(nodes[0].lo, nodes[0].hi)), *need);
   return PT_OK;
 }
 
@@ -810,7 +895,7 @@ static float refine_leaves(std::vector<SahNode>& nodes, const std::vector<SahPri
 // Any-hit tree over the leaves of the reference tree (see above), with fine leaves under them (refine_leaves).
 int build_anyhit_tree(const float* node_enc, int nnodes, int ntris, const float* tri_enc, std::vector<float4>& out,
                       int* root_ref, int* need, std::vector<float4>* wide = nullptr, int* root_wide = nullptr,
-                      int* need_wide = nullptr, float* fine_mag = nullptr) {
+                      int* need_wide = nullptr, float* fine_mag = nullptr, int* root_closest = nullptr) {
   std::vector<SahPrim> pr;
   for (int i = 1; i < nnodes; ++i) {
     const float* f = node_enc + (size_t)i * 12;
@@ -833,7 +918,27 @@ int build_anyhit_tree(const float* node_enc, int nnodes, int ntris, const float*
   auto leaf_ref = [&](int first, int) { return pr[first].ref; };
   const int rc = pack_sah(nodes, leaf_ref, out, root_ref, need);
   if (rc != PT_OK || !wide) return rc;
-  return pack_wide(nodes, leaf_ref, *wide, root_wide, need_wide);
+  const int mode = wide_collapse_mode();
+  const int rw = pack_wide(nodes, leaf_ref, *wide, root_wide, need_wide, mode == 1 || mode == 2);
+  if (root_closest) *root_closest = *root_wide;
+  if (rw != PT_OK || !root_closest || (mode != 2 && mode != 3) || *root_wide < 0) return rw;
+  // the closest-hit walks' tree, appended: its node indices shifted past the any-hit tree's
+  std::vector<float4> second;
+  int root2 = 0, need2 = 0;
+  const int r2 = pack_wide(nodes, leaf_ref, second, &root2, &need2, mode == 3);
+  if (r2 != PT_OK) return r2;
+  const int base = (int)(wide->size() / ptk::kWideStride);
+  for (size_t k = 0; k + ptk::kWideStride <= second.size(); k += ptk::kWideStride) {
+    int refs[4];
+    memcpy(refs, &second[k + 6], 16);
+    for (int c = 0; c < 4; ++c)
+      if (refs[c] >= 0) refs[c] += base;
+    memcpy(&second[k + 6], refs, 16);
+  }
+  *root_closest = root2 + base;
+  wide->insert(wide->end(), second.begin(), second.end());
+  *need_wide = std::max(*need_wide, need2);
+  return PT_OK;
 }
 
 void free_scene(SceneGPU& sg) {
@@ -889,7 +994,7 @@ int get_scene_lbvh(Texture* tris, Texture* nodes, SceneGPU& sg, SceneGPU** out) 
   for (auto b : opt)
     if (*b) { (void)hipFree(*b); *b = nullptr; }
   sg.has4 = false;
-  sg.need_any = sg.root_any = sg.need4 = sg.root4 = 0;  // no any-hit tree: its depth must not size the stack
+  sg.need_any = sg.root_any = sg.need4 = sg.root4 = sg.root4c = 0;  // no any-hit tree: its depth must not size the stack
   if (sg.geom) (void)hipFree(sg.geom);
   if (sg.shade) (void)hipFree(sg.shade);
   sg.geom = sg.shade = nullptr;
@@ -936,7 +1041,7 @@ int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU*
     s[8] = float4{f[40], f[41], 0.0f, 0.0f};
   }
   std::vector<float4> bvh, bvh4;
-  int root = 0, root4 = 0, need4 = 0;
+  int root = 0, root4 = 0, need4 = 0, root4c = 0;
   int rc = pack_bvh((const float*)nodes->host.data(), (int)nnodes, bvh, &root, (int)ntris, &sg.stack_need);
   if (rc != PT_OK) return rc;
   {  // optional: without it shadow and closest-hit rays walk the reference tree (binary, or its 4-wide form)
@@ -945,7 +1050,7 @@ int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU*
     float fine_mag = 0.0f;
     sg.fine_eye_limit = INFINITY;
     if (build_anyhit_tree((const float*)nodes->host.data(), (int)nnodes, (int)ntris, te, any, &sg.root_any,
-                          &sg.need_any, &bvh4, &root4, &need4, &fine_mag) == PT_OK) {
+                          &sg.need_any, &bvh4, &root4, &need4, &fine_mag, &root4c) == PT_OK) {
       if (fine_mag > 0.0f) sg.fine_eye_limit = kFineEyeReach * fine_mag;
       if (any.empty()) any.push_back(float4{0, 0, 0, 0});
       if ((rc = upload_vec(any, &sg.bvh_any)) != PT_OK) return rc;
@@ -953,6 +1058,7 @@ int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU*
       if ((rc = upload_vec(bvh4, &sg.bvh4)) != PT_OK) return rc;
       sg.has4 = true;
       sg.root4 = root4;
+      sg.root4c = root4c;
       sg.nan4 = false;
       for (size_t k = 0; k + ptk::kWideStride <= bvh4.size(); k += ptk::kWideStride) {
         const float* q = (const float*)&bvh4[k];
@@ -971,7 +1077,7 @@ int get_scene(Texture* tris, uint32_t th, Texture* nodes, uint32_t nh, SceneGPU*
     } else {
       for (float4** b : {&sg.bvh_any, &sg.bvh4})
         if (*b) { (void)hipFree(*b); *b = nullptr; }
-      sg.need_any = sg.root_any = sg.need4 = sg.root4 = 0;
+      sg.need_any = sg.root_any = sg.need4 = sg.root4 = sg.root4c = 0;
     }
   }
   if ((rc = upload_leaves((const float*)nodes->host.data(), nnodes, sg)) != PT_OK) return rc;
@@ -1222,6 +1328,7 @@ int pt_params(Pass* p, PTParams& k, SceneGPU*& sg) {
   k.scene.bvh4 = (k.scene.bvh_any && sg->has4 && !(PT_WIDE_SIGNED && sg->nan4) && ui(p, "wide_bvh", 1)) ? sg->bvh4
                                                                                                      : nullptr;
   k.scene.root4 = sg->root4;
+  k.scene.root4c = sg->root4c;
   k.scene.ntris = sg->ntris;
   k.scene.leaves = sg->leaves;
   k.scene.nleaves = sg->nleaves;

@@ -942,7 +942,7 @@ __global__ void __launch_bounds__(kTB) PT_TRACE_ATTR wf_trace_closest_refill(PTP
         d = xyz(dd);
         inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
         tree = p.scene.bvh_any;
-        node = WIDE ? p.scene.root4 : p.scene.root_any;
+        node = WIDE ? p.scene.root4c : p.scene.root_any;
         rewalk = false;
         ovf = WIDE && PT_WIDE_SIGNED && !finite3(inv);  // axis-parallel (wide_step's signed planes): the coop walk
         tbest = PT_INF;

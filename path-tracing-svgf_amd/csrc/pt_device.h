@@ -117,6 +117,7 @@ struct SceneDev {
   int root_ref;         // >= 0 interior node index, < 0 leaf ref
   const float4* bvh4;   // 4-wide collapse of bvh for any-hit rays (7 x float4 / node), may be null
   int root4;
+  int root4c;           // root of the closest-hit walks' 4-wide tree in bvh4 (= root4 unless PTSVGF_WIDE_COLLAPSE 2 / 3)
   const float4* bvh_any;  // binary any-hit tree over bvh's leaves (capi.hip build_anyhit_tree), may be null
   int root_any;
   int ntris;
