@@ -38,7 +38,8 @@ def main() -> None:
     h = hashlib.sha256()
     for k in ("color", "emission", "albedo"):
         h.update(gl.readback(r.planes()[k]).tobytes())
-    out = {"collapse": os.environ.get("PTSVGF_WIDE_COLLAPSE", "0"), "view": view, "W": W, "H": H,
+    out = {"collapse": os.environ.get("PTSVGF_WIDE_COLLAPSE", "default"),
+           "treelet": os.environ.get("PTSVGF_TREELET", "default"), "view": view, "W": W, "H": H,
            "bounce_visits": st["bounce_visits"], "shadow_visits": st["shadow_visits"],
            "bounce_rays": st["bounce_rays"], "shadow_rays": st["shadow_rays"], "planes_sha256": h.hexdigest()[:16]}
     print(json.dumps(out))
