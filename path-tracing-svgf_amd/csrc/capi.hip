@@ -656,7 +656,11 @@ static int tree_depth(const std::vector<SahNode>& nodes) {
 static void treelet_optimize(std::vector<SahNode>& nodes, const std::vector<SahPrim>& pr, int passes, int reserve) {
   if (passes <= 0 || nodes.empty() || nodes[0].n > 0) return;
   const std::vector<SahNode> orig = nodes;
-  constexpr int K = 7;
+  constexpr int KMAX = 10;
+  static const int K = [KMAX] {  // treelet leaves (PTSVGF_TREELET_LEAVES, 3..10, default 7)
+    const char* e = getenv("PTSVGF_TREELET_LEAVES");
+    return e ? std::min(KMAX, std::max(3, atoi(e))) : 7;
+  }();
   std::vector<double> cost;
   const double before = sah_tree_cost(nodes, pr, cost);
   std::vector<int> order;
@@ -667,7 +671,7 @@ static void treelet_optimize(std::vector<SahNode>& nodes, const std::vector<SahP
       if (nodes[r].n > 0) continue;
       // its subtree may have changed below (children come first in post order)
       cost[r] = sah_area(nodes[r].lo, nodes[r].hi) + cost[nodes[r].left] + cost[nodes[r].right];
-      int T[K], nt = 2, I[K], ni = 1;
+      int T[KMAX], nt = 2, I[KMAX], ni = 1;
       T[0] = nodes[r].left;
       T[1] = nodes[r].right;
       I[0] = r;
@@ -687,8 +691,8 @@ static void treelet_optimize(std::vector<SahNode>& nodes, const std::vector<SahP
       }
       if (nt < 3) continue;
       const int full = (1 << nt) - 1;
-      double area[1 << K], best[1 << K];
-      int split[1 << K];
+      static thread_local std::vector<double> area(1 << KMAX), best(1 << KMAX);
+      static thread_local std::vector<int> split(1 << KMAX);
       for (int S = 1; S <= full; ++S) {
         float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (int i = 0; i < nt; ++i)
