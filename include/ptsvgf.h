@@ -93,6 +93,22 @@ int pt_stream_create_cu_masked(uint32_t words, const uint32_t* mask, void** out)
 int pt_stream_create_priority(int priority, void** out);
 int pt_stream_priority_range(int* least, int* greatest);
 int pt_stream_destroy(void* hip_stream);   /* release (above), wait for its work, destroy */
+/* Host-only check of the trees the library derives from a reference tree
+ * (node_enc / tri_enc as pts_scene_encode writes them), built with 4-wide
+ * collapse mode `collapse` (0..3, PTSVGF_WIDE_COLLAPSE) and `treelet` passes of
+ * treelet restructuring (PTSVGF_TREELET). Needs no device and no pt_init.
+ * out[0..PT_TREE_CHECK_COUNT): 1/0 every reference-leaf triangle is held by
+ * exactly one leaf of the binary any-hit tree / the any-hit 4-wide tree / the
+ * closest-hit 4-wide tree (and no other triangle); 1/0 every child box lies
+ * inside its parent's box and every leaf box holds its triangles (boxes under a
+ * reference leaf's own box excepted: its fine boxes only cull); SAH cost / root
+ * area before and after the treelet passes; summed 4-wide node area / root area
+ * of the any-hit and closest-hit trees; 4-wide nodes (both trees); binary depth;
+ * 4-wide stack need; 1 when the closest-hit tree is a separate one.
+ * No GL counterpart: the reference walks its own tree only. */
+#define PT_TREE_CHECK_COUNT 12
+int pt_tree_check(const float* node_enc, int nnodes, const float* tri_enc, int ntris, int collapse, int treelet,
+                  double* out, int nout);
 int pt_device_cus(int* n);                 /* compute units of the library's device */
 int pt_sync(void);                          /* wait for all queued draws */
 const char* pt_last_error(void);

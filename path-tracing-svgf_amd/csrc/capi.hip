@@ -653,8 +653,15 @@ static int tree_depth(const std::vector<SahNode>& nodes) {
   return best;
 }
 
-static void treelet_optimize(std::vector<SahNode>& nodes, const std::vector<SahPrim>& pr, int passes, int reserve) {
-  if (passes <= 0 || nodes.empty() || nodes[0].n > 0) return;
+static void treelet_optimize(std::vector<SahNode>& nodes, const std::vector<SahPrim>& pr, int passes, int reserve,
+                             double* sah_before = nullptr, double* sah_after = nullptr) {
+  if (passes <= 0 || nodes.empty() || nodes[0].n > 0) {
+    std::vector<double> c;
+    const double v = nodes.empty() ? 0.0 : sah_tree_cost(nodes, pr, c) / std::max(1e-30, (double)sah_area(nodes[0].lo, nodes[0].hi));
+    if (sah_before) *sah_before = v;
+    if (sah_after) *sah_after = v;
+    return;
+  }
   const std::vector<SahNode> orig = nodes;
   constexpr int KMAX = 10;
   static const int K = [KMAX] {  // treelet leaves (PTSVGF_TREELET_LEAVES, 3..10, default 7)
@@ -752,6 +759,9 @@ static void treelet_optimize(std::vector<SahNode>& nodes, const std::vector<SahP
   const int depth = tree_depth(nodes);
   const bool keep = depth + reserve < kStack - 2;
   if (!keep) nodes = orig;
+  const double root_area = std::max(1e-30, (double)sah_area(orig[0].lo, orig[0].hi));
+  if (sah_before) *sah_before = before / root_area;
+  if (sah_after) *sah_after = (keep ? after : before) / root_area;
   if (getenv("PTSVGF_WIDE_STATS"))
     fprintf(stderr, "ptsvgf: treelet restructuring (%d passes): SAH cost / root area %.4f -> %.4f, depth %d%s\n", passes,
             before / std::max(1e-30, (double)sah_area(orig[0].lo, orig[0].hi)),
@@ -893,7 +903,7 @@ struct WideCollapse {
 };
 
 static int pack_wide(const std::vector<SahNode>& nodes, const std::function<int(int, int)>& leaf_ref,
-                     std::vector<float4>& out, int* root_ref, int* need, bool dp) {
+                     std::vector<float4>& out, int* root_ref, int* need, bool dp, double* area_out = nullptr) {
   out.clear();
   *need = 0;
   auto ref_of = [&](const SahNode& L) { return L.direct ? L.ref : leaf_ref(L.first, L.n); };
@@ -956,6 +966,7 @@ static int pack_wide(const std::vector<SahNode>& nodes, const std::function<int(
   };
   build(0, 0);
   *root_ref = 0;
+  if (area_out) *area_out = area_sum / std::max(1e-30, (double)sah_area(nodes[0].lo, nodes[0].hi));
   if (getenv("PTSVGF_WIDE_STATS"))
     fprintf(stderr, "ptsvgf: 4-wide tree (%s collapse): %zu nodes, summed node area / root area %.4f, stack need %d\n",
             dp ? "SAH-optimal" : "greedy", out.size() / ptk::kWideStride,
@@ -1066,7 +1077,14 @@ static float refine_leaves(std::vector<SahNode>& nodes, const std::vector<SahPri
 // Any-hit tree over the leaves of the reference tree (see above), with fine leaves under them (refine_leaves).
 int build_anyhit_tree(const float* node_enc, int nnodes, int ntris, const float* tri_enc, std::vector<float4>& out,
                       int* root_ref, int* need, std::vector<float4>* wide = nullptr, int* root_wide = nullptr,
-                      int* need_wide = nullptr, float* fine_mag = nullptr, int* root_closest = nullptr) {
+                      int* need_wide = nullptr, float* fine_mag = nullptr, int* root_closest = nullptr,
+                      int collapse = -1, int treelet = -1, double* stats = nullptr) {
+  // collapse / treelet: PTSVGF_WIDE_COLLAPSE / PTSVGF_TREELET when < 0; stats (pt_tree_check): SAH cost / root area
+  // before and after the treelet pass, summed 4-wide node area / root area of the any-hit and closest-hit trees
+  if (collapse < 0) collapse = wide_collapse_mode();
+  if (treelet < 0) treelet = treelet_passes();
+  double st_[4] = {0, 0, 0, 0};
+  double* st = stats ? stats : st_;
   std::vector<SahPrim> pr;
   for (int i = 1; i < nnodes; ++i) {
     const float* f = node_enc + (size_t)i * 12;
@@ -1084,20 +1102,21 @@ int build_anyhit_tree(const float* node_enc, int nnodes, int ntris, const float*
   nodes.reserve(2 * pr.size());
   const int F = fine_leaf_max();
   sah_build(pr, 0, (int)pr.size(), 1, nodes, 1, F > 0 ? ceil_log2(16) : 0);  // a fine subtree is <= 4 levels deep
-  treelet_optimize(nodes, pr, treelet_passes(), F > 0 ? ceil_log2(16) : 0);
+  treelet_optimize(nodes, pr, treelet, F > 0 ? ceil_log2(16) : 0, &st[0], &st[1]);
   const float mag = refine_leaves(nodes, pr, tri_enc, ntris, F);
   if (fine_mag) *fine_mag = mag;
   auto leaf_ref = [&](int first, int) { return pr[first].ref; };
   const int rc = pack_sah(nodes, leaf_ref, out, root_ref, need);
   if (rc != PT_OK || !wide) return rc;
-  const int mode = wide_collapse_mode();
-  const int rw = pack_wide(nodes, leaf_ref, *wide, root_wide, need_wide, mode == 1 || mode == 2);
+  const int mode = collapse;
+  const int rw = pack_wide(nodes, leaf_ref, *wide, root_wide, need_wide, mode == 1 || mode == 2, &st[2]);
+  st[3] = st[2];
   if (root_closest) *root_closest = *root_wide;
   if (rw != PT_OK || !root_closest || (mode != 2 && mode != 3) || *root_wide < 0) return rw;
   // the closest-hit walks' tree, appended: its node indices shifted past the any-hit tree's
   std::vector<float4> second;
   int root2 = 0, need2 = 0;
-  const int r2 = pack_wide(nodes, leaf_ref, second, &root2, &need2, mode == 3);
+  const int r2 = pack_wide(nodes, leaf_ref, second, &root2, &need2, mode == 3, &st[3]);
   if (r2 != PT_OK) return r2;
   const int base = (int)(wide->size() / ptk::kWideStride);
   for (size_t k = 0; k + ptk::kWideStride <= second.size(); k += ptk::kWideStride) {
@@ -1110,6 +1129,123 @@ int build_anyhit_tree(const float* node_enc, int nnodes, int ntris, const float*
   *root_closest = root2 + base;
   wide->insert(wide->end(), second.begin(), second.end());
   *need_wide = std::max(*need_wide, need2);
+  return PT_OK;
+}
+
+// pt_tree_check (include/ptsvgf.h): the trees build_anyhit_tree makes for a reference tree, checked on the host
+// against the properties the walks' result preservation rests on. Host only: no device, no pt_init.
+struct TreeCheck {
+  const float* node_enc;
+  int nnodes;
+  const float* tri_enc;
+  int ntris;
+  std::vector<int> cover;  // per triangle: leaves of the checked tree holding it
+  std::vector<char> inref; // per triangle: held by a reference leaf
+  std::map<std::array<uint32_t, 6>, int> refbox;  // reference leaf boxes (bits) -> triangle count
+  bool contain_ok = true, leaf_ok = true;
+  int depth = 0;
+  static std::array<uint32_t, 6> key(const float* lo, const float* hi) {
+    std::array<uint32_t, 6> k;
+    for (int a = 0; a < 3; ++a) { memcpy(&k[a], &lo[a], 4); memcpy(&k[3 + a], &hi[a], 4); }
+    return k;
+  }
+  void init() {
+    cover.assign((size_t)ntris, 0);
+    inref.assign((size_t)ntris, 0);
+    for (int i = 1; i < nnodes; ++i) {
+      const float* f = node_enc + (size_t)i * 12;
+      const int n = (int)f[3], first = (int)f[4];
+      if (n <= 0) continue;
+      for (int t = first; t < first + n && t < ntris; ++t) inref[(size_t)t] = 1;
+      refbox[key(f + 6, f + 9)] = n;
+    }
+  }
+  static bool inside(const float* lo, const float* hi, const float* plo, const float* phi) {
+    for (int a = 0; a < 3; ++a)
+      if (lo[a] < plo[a] || hi[a] > phi[a]) return false;
+    return true;
+  }
+  // a leaf ref below a box: its triangles marked; each triangle's vertex box inside the box
+  void leaf(int ref, const float* lo, const float* hi) {
+    const int first = ref_first_of(ref), cnt = ref_count_of(ref);
+    for (int t = first; t < first + cnt; ++t) {
+      if (t < 0 || t >= ntris) { leaf_ok = false; continue; }
+      ++cover[(size_t)t];
+      const float* v = tri_enc + (size_t)t * 45;
+      for (int a = 0; a < 3; ++a) {
+        const float tl = std::min(v[a], std::min(v[3 + a], v[6 + a])), th = std::max(v[a], std::max(v[3 + a], v[6 + a]));
+        if (std::isfinite(tl) && std::isfinite(th) && (tl < lo[a] || th > hi[a])) contain_ok = false;
+      }
+    }
+  }
+  // a child slot box (lo, hi) holding a subtree; `fine`: the box is a reference leaf's (its fine boxes, widened, need
+  // not lie inside it: each fine leaf's box must hold its triangles instead)
+  bool is_ref_leaf_box(const float* lo, const float* hi) const { return refbox.count(key(lo, hi)) != 0; }
+  bool partition_ok() const {
+    for (int t = 0; t < ntris; ++t)
+      if (cover[(size_t)t] != (inref[(size_t)t] ? 1 : 0)) return false;
+    return true;
+  }
+  void walk_binary(const std::vector<float4>& bvh, int ref, const float* lo, const float* hi, bool fine, int d) {
+    depth = std::max(depth, d);
+    if (ref < 0) { leaf(ref, lo, hi); return; }
+    const float* q = (const float*)&bvh[4 * (size_t)ref];
+    const float L0[3] = {q[0], q[1], q[2]}, L1[3] = {q[3], q[4], q[5]};
+    const float R0[3] = {q[6], q[7], q[8]}, R1[3] = {q[9], q[10], q[11]};
+    int rl, rr;
+    memcpy(&rl, &q[12], 4);
+    memcpy(&rr, &q[13], 4);
+    for (int s = 0; s < 2; ++s) {
+      const float* cl = s ? R0 : L0;
+      const float* ch = s ? R1 : L1;
+      if (!fine && lo && !inside(cl, ch, lo, hi)) contain_ok = false;
+      walk_binary(bvh, s ? rr : rl, cl, ch, fine || is_ref_leaf_box(cl, ch), d + 1);
+    }
+  }
+  void walk_wide(const std::vector<float4>& w, int ref, const float* lo, const float* hi, bool fine, int d) {
+    depth = std::max(depth, d);
+    if (ref < 0) { leaf(ref, lo, hi); return; }
+    const float* q = (const float*)&w[(size_t)ptk::kWideStride * ref];
+    int refs[4];
+    memcpy(refs, q + 24, 16);
+    for (int c = 0; c < 4; ++c) {
+      if (refs[c] == kNoneRef) continue;
+      const float cl[3] = {q[c], q[8 + c], q[16 + c]}, ch[3] = {q[4 + c], q[12 + c], q[20 + c]};
+      if (!fine && lo && !inside(cl, ch, lo, hi)) contain_ok = false;
+      walk_wide(w, refs[c], cl, ch, fine || is_ref_leaf_box(cl, ch), d + 1);
+    }
+  }
+};
+
+int tree_check(const float* node_enc, int nnodes, const float* tri_enc, int ntris, int collapse, int treelet,
+               double* out, int nout) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!node_enc || !tri_enc || !out || nnodes < 2 || ntris < 1) return err(PT_ERR_ARG, "trees and output needed");
+  if (nout < PT_TREE_CHECK_COUNT) return err(PT_ERR_ARG, "output holds fewer than PT_TREE_CHECK_COUNT values");
+  if (collapse < 0 || collapse > 3 || treelet < 0) return err(PT_ERR_ARG, "collapse in 0..3, treelet >= 0");
+  std::vector<float4> bin, wide;
+  int root_any = 0, need_any = 0, root4 = 0, need4 = 0, root4c = 0;
+  float mag = 0.0f;
+  double st[4] = {0, 0, 0, 0};
+  const int rc = build_anyhit_tree(node_enc, nnodes, ntris, tri_enc, bin, &root_any, &need_any, &wide, &root4, &need4,
+                                   &mag, &root4c, collapse, treelet, st);
+  if (rc != PT_OK) return rc;
+  double ok[3];
+  int depth[3];
+  bool contain = true;
+  for (int k = 0; k < 3; ++k) {
+    TreeCheck tc{node_enc, nnodes, tri_enc, ntris};
+    tc.init();
+    if (k == 0) tc.walk_binary(bin, root_any, nullptr, nullptr, false, 1);
+    else tc.walk_wide(wide, k == 1 ? root4 : root4c, nullptr, nullptr, false, 1);
+    ok[k] = tc.partition_ok() && tc.leaf_ok ? 1.0 : 0.0;
+    depth[k] = tc.depth;
+    contain = contain && tc.contain_ok;
+  }
+  const double vals[PT_TREE_CHECK_COUNT] = {ok[0], ok[1], ok[2], contain ? 1.0 : 0.0, st[0], st[1], st[2], st[3],
+                                            (double)(wide.size() / ptk::kWideStride), (double)depth[0],
+                                            (double)need4, root4c != root4 ? 1.0 : 0.0};
+  for (int i = 0; i < PT_TREE_CHECK_COUNT; ++i) out[i] = vals[i];
   return PT_OK;
 }
 
@@ -2012,6 +2148,11 @@ static int texbuffer_take(Texture* t, const void* dev_src, size_t bytes) {
 }
 
 extern "C" {
+
+int pt_tree_check(const float* node_enc, int nnodes, const float* tri_enc, int ntris, int collapse, int treelet,
+                  double* out, int nout) {
+  return tree_check(node_enc, nnodes, tri_enc, ntris, collapse, treelet, out, nout);
+}
 
 const char* pt_last_error(void) { return g_err.c_str(); }
 int pt_version(void) { return 1; }

@@ -78,6 +78,8 @@ _PT_SIGS = [
     ("pt_stream_create_priority", C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
     ("pt_stream_priority_range", C.c_int, [C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("pt_stream_destroy", C.c_int, [_vp]),
+    ("pt_tree_check", C.c_int, [C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_float), C.c_int, C.c_int, C.c_int,
+                                C.POINTER(C.c_double), C.c_int]),
     ("pt_device_cus", C.c_int, [C.POINTER(C.c_int)]),
     ("pt_sync", C.c_int, []),
     ("pt_last_error", C.c_char_p, []),
