@@ -223,11 +223,15 @@ __device__ __forceinline__ v3 primary_dir(const PTParams& p, int x, int y) {
 constexpr int kTieFix = -2;  // hit.x of a pixel wf_primary_raster leaves to the walk (two triangles share its t)
 
 // 16x16 screen tiles, each wave an 8x8 sub-tile: coherent camera rays.
+// nslots: the subset's tiles; a block walks slots blockIdx.x, + gridDim.x, ... (the full launch: one slot per block;
+// the fix-up launch after wf_primary_raster, whose work is almost always none, a few hundred blocks: a grid of one
+// block per tile, each reading one flag and leaving, held its stream for 0.1-0.6 ms of a frame at 4K)
 template <int KS, bool DEEP>
-__global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
+__global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p, int nslots) {
   __shared__ int stk[KS * 256];
+  for (int slot = blockIdx.x; slot < nslots; slot += gridDim.x) {
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-  const int tile = sched_tile(p.tiles, blockIdx.x);  // cost-ordered dispatch (subset slot)
+  const int tile = sched_tile(p.tiles, slot);  // cost-ordered dispatch (subset slot)
   const int gt = tile * p.tile_stride + p.tile_offset, ntx = (p.W + 15) / 16;
   const int tx = gt % ntx, ty = gt / ntx;
   const int x = tx * 16 + (wv & 1) * 8 + (ln & 7);
@@ -241,13 +245,13 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
       // its stride group (the last slot also the band's tail), so every band tile is cleared once
       if (threadIdx.x == 0) {
         const int all = ntx * ((p.y1 - p.y0 + 15) / 16), lo = tile * p.tile_stride;
-        const int hi = tile + 1 == (int)gridDim.x ? all : min(all, lo + p.tile_stride);
+        const int hi = tile + 1 == nslots ? all : min(all, lo + p.tile_stride);
         for (int j = lo; j < hi; ++j) p.leaf_bins.tile_count[j] = 0;
       }
     } else {
       if (p.closest_tree) return;  // the flagged pixels went to wf_primary_coop
       valid = valid && ldnt(&p.wf.hit[pid]).x == kTieFix;
-      if (!__any(valid)) return;
+      if (!__any(valid)) continue;
       count_ray = false;  // counted by the rasteriser
     }
   }
@@ -291,6 +295,7 @@ __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p) {
   stat_add(p, kStatSpills, spill ? 1u : 0u);
   sched_cost(p.tiles, tile, steps);
   if (valid) add_row_cost(p, y - p.y0, pid, steps);
+  }
 }
 
 // ------------------------------------------------ primaries by tile binning ---
@@ -1351,6 +1356,15 @@ int wf_subset_tiles(int W, int rows, int stride, int offset) {
 // launch per bounce for the list-driven traversals of every frame's rays (lane-refill kernels; the one-ray-per-lane
 // kernels run per frame). Frame b's wavefront state lies at pid offset b * N of ps[0]'s, its counters at
 // ps[0].wf.counters + b * kWfCounters; the batched launches use frame 0's work-queue heads and straggler lists.
+// wf_primary's fix-up grid after wf_primary_raster with closest_tree on (PTSVGF_PRIMARY_FIX_BLOCKS, read once; 0 = one
+// block per tile, as until round 6)
+static int primary_fix_blocks() {
+  static const int n = [] {
+    const char* e = getenv("PTSVGF_PRIMARY_FIX_BLOCKS");
+    return e ? std::max(0, atoi(e)) : 512;
+  }();
+  return n;
+}
 template <int KS, bool DEEP>
 int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, const WfFork* fk) {
   const PTParams& p = ps[0];
@@ -1374,9 +1388,12 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, const WfFork* fk
                            (const int*)(f.wf.counters + kCtrStragC));
       PTParams q = f;
       q.pr_fix = f.leaf_bins.ctr;  // ties (and an overflow) walked
-      hipLaunchKernelGGL((wf_primary<KS, DEEP>), dim3(ntiles), dim3(256), 0, s, q);
+      // with closest_tree the flagged pixels went to wf_primary_coop: this launch has work only after a list
+      // overflow, so a few blocks striding over the tiles
+      const int gfix = f.closest_tree && primary_fix_blocks() > 0 ? std::min(ntiles, primary_fix_blocks()) : ntiles;
+      hipLaunchKernelGGL((wf_primary<KS, DEEP>), dim3(gfix), dim3(256), 0, s, q, ntiles);
     } else {
-      hipLaunchKernelGGL((wf_primary<KS, DEEP>), dim3(ntiles), dim3(256), 0, s, f);
+      hipLaunchKernelGGL((wf_primary<KS, DEEP>), dim3(ntiles), dim3(256), 0, s, f, ntiles);
     }
     if (f.tiles.cost) {  // this frame's primary costs -> tile order of the bounce-0 shade and the next frame
       const int rc = launch_tile_sort(f.tiles.cost, f.tiles.perm_next, f.tiles.ntiles, s);

@@ -111,6 +111,10 @@ def test_primary_raster_equals_walk_bench_scene_1080p(gpu, scene_bench):
     got, st = _pt(gpu, scene_bench, W, H, 1, MOVES)
     print(st)
     _same(got, want, "bench1080")
+    # every subset's pair list overflows: wf_primary walks all 8 160 tiles from its fix-up grid of a few hundred
+    # blocks striding over them (kernels_wavefront.hip primary_fix_blocks)
+    over, _ = _pt(gpu, scene_bench, W, H, 1, MOVES, cap=4)
+    _same(over, want, "bench1080/overflow")
 
 
 def test_trace_stats_buffer_length_is_respected(gpu, scene_small):
