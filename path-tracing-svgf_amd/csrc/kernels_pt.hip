@@ -264,18 +264,20 @@ __device__ __forceinline__ void gb_finish(const GBufParams& p, int x, int y, boo
   if (p.tflags && lz != 1.0f && y >= p.tf_y0 && y < p.tf_y1) atrous_mark_tiles(p.tflags, p.tf_off, p.W, x, y - p.tf_y0);
 }
 
+// One 16 x 16 tile per slot; a block takes slots blockIdx.x, + gridDim.x, ... (ntx tiles per row, nslots tiles). As
+// the rasteriser's overflow fallback (p.bins.ctr set) it has work only after an overflow and launches a few hundred
+// blocks (launch_gbuffer): one block per tile, each reading one flag and leaving, held its stream for ~0.14 ms of a
+// 4K frame.
 template <int KS>
-__global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
+__global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p, int ntx, int nslots) {
   __shared__ int stk[KS * kBlock];
-  if (p.bins.ctr) {  // launched as the rasteriser's overflow fallback
-    if (p.bins.ctr[2] == 0) return;  // not needed
-    // the overflowed frame skipped the scatter, which returns every tile count to zero: clear them here
-    const int b = blockIdx.y * gridDim.x + blockIdx.x;
-    if (threadIdx.x == 0) p.bins.tile_count[b] = 0;
-  }
+  if (p.bins.ctr && p.bins.ctr[2] == 0) return;  // the rasteriser's fallback, not needed
+  for (int b = blockIdx.x; b < nslots; b += gridDim.x) {
+  // the overflowed frame skipped the scatter, which returns every tile count to zero: clear them here
+  if (p.bins.ctr && threadIdx.x == 0) p.bins.tile_count[b] = 0;
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-  const int tile = sched_tile(p.tiles, blockIdx.y * gridDim.x + blockIdx.x);  // cost-ordered dispatch
-  const int tx = tile % gridDim.x, ty = tile / gridDim.x;
+  const int tile = sched_tile(p.tiles, b);  // cost-ordered dispatch
+  const int tx = tile % ntx, ty = tile / ntx;
   const int x = tx * 16 + (wv & 1) * 8 + (ln & 7);
   const int y = p.y0 + ty * 16 + (wv >> 1) * 8 + (ln >> 3);
   const bool valid = x < p.W && y < p.y1;
@@ -347,6 +349,7 @@ __global__ void __launch_bounds__(kBlock) gbuffer_kernel(GBufParams p) {
   }
   sched_cost(p.tiles, tile, steps);
   gb_finish(p, x, y, valid, ln, o, d, best, bests, bu, bv);
+  }
 }
 
 // ------------------------------------------------------- tile binning ---
@@ -586,11 +589,22 @@ int launch_pathtrace(const PTParams& p, hipStream_t s) {
   hipLaunchKernelGGL(pathtrace_kernel, grid, dim3(kBlock), 0, s, p);
   return (int)hipGetLastError();
 }
+// the fallback's grid (PTSVGF_GBUFFER_FIX_BLOCKS, read once; 0 = one block per tile, as until round 6)
+static int gbuffer_fix_blocks() {
+  static const int n = [] {
+    const char* e = getenv("PTSVGF_GBUFFER_FIX_BLOCKS");
+    return e ? std::max(0, atoi(e)) : 512;
+  }();
+  return n;
+}
 int launch_gbuffer(const GBufParams& p, hipStream_t s) {
   if (p.y1 <= p.y0) return 0;
-  dim3 grid((p.W + 15) / 16, (p.y1 - p.y0 + 15) / 16);
-  if (p.stack_need <= kStackSmall) hipLaunchKernelGGL(gbuffer_kernel<kStackSmall>, grid, dim3(kBlock), 0, s, p);
-  else hipLaunchKernelGGL(gbuffer_kernel<kStack>, grid, dim3(kBlock), 0, s, p);
+  const int ntx = (p.W + 15) / 16, nslots = ntx * ((p.y1 - p.y0 + 15) / 16);
+  const int fix = p.bins.ctr ? gbuffer_fix_blocks() : 0;
+  const dim3 grid(fix > 0 ? std::min(nslots, fix) : nslots);
+  if (p.stack_need <= kStackSmall)
+    hipLaunchKernelGGL(gbuffer_kernel<kStackSmall>, grid, dim3(kBlock), 0, s, p, ntx, nslots);
+  else hipLaunchKernelGGL(gbuffer_kernel<kStack>, grid, dim3(kBlock), 0, s, p, ntx, nslots);
   return (int)hipGetLastError();
 }
 
