@@ -635,13 +635,32 @@ __device__ __forceinline__ int batch_frame(const int* tot, int nb, int* k) {
 // each with its own head word (one returning atomic per grab of kGrab items; a per-XCD head keeps the grabs of
 // 256 CUs off one word, MI355X_MICROARCH.md "dequeue"). A wave drains its XCD's region first, then the others;
 // regions seen exhausted (a relaxed load of the head) are skipped without an atomic. Wave-uniform.
+#ifndef PT_REFILL_QUEUE
+#define PT_REFILL_QUEUE 0
+#endif
 constexpr int kGrab = 64;
 struct WaveQueue {
   int* heads;
   int total, xcd;
   unsigned done;  // regions known exhausted
   int next, end;  // current grab [next, end)
+  // static chunks (PT_REFILL_QUEUE 0): this wave's virtual wave index, the grid's waves, chunk rounds, big waves
+  int vw, gw, R, big;
+  __device__ __forceinline__ void chunk() {
+    if (vw < big) {
+      next = vw * 64 * R;
+      end = next + 64 * R;
+    } else {
+      next = min(big * 64 * R + (vw - big) * 64, total);
+      end = min(next + 64, total);
+    }
+  }
   __device__ __forceinline__ bool grab() {
+    if (!PT_REFILL_QUEUE) {  // static chunks: the chunk of virtual wave vw + the grid's waves, if any
+      vw += gw;
+      chunk();
+      return next < end;
+    }
     for (int t = 0; t < 8; ++t) {
       const int r = (xcd + t) & 7;
       if ((done >> r) & 1u) continue;
@@ -683,9 +702,6 @@ constexpr int kRefillBlocks = 256 * 10;
 #ifndef PT_REFILL_MIN
 #define PT_REFILL_MIN 16
 #endif
-#ifndef PT_REFILL_QUEUE
-#define PT_REFILL_QUEUE 0
-#endif
 constexpr int kRefillRounds = PT_REFILL_ROUNDS, kRefillMin = PT_REFILL_MIN;
 // Chunk rounds per big wave, from the list length: a big wave lasts about R one-ray waves, which pays only when the
 // launch spans several rounds of resident waves anyway (at 1080p the lists are too short: refill there measured
@@ -710,27 +726,33 @@ __device__ __forceinline__ int refill_rounds(int total, int waves) {
   return r < 1 ? 1 : (r > kRefillRounds ? kRefillRounds : r);
 }
 __device__ __forceinline__ WaveQueue refill_queue(int* heads, int total, int big_pct, int waves) {
-  WaveQueue q{heads, total, (int)(blockIdx.x & 7), 0u, 0, 0};
+  WaveQueue q{heads, total, (int)(blockIdx.x & 7), 0u, 0, 0, 0, 0, 1, 0};
   if (PT_REFILL_QUEUE) {
     q.grab();
   } else {
-    const int wave = blockIdx.x * (kTB / 64) + (threadIdx.x >> 6);
-    const int R = refill_rounds(total, waves);
-    const int big = R > 1 ? (int)((long long)total * big_pct / 100) / (64 * R) : 0;  // waves with big chunks
-    if (wave < big) {
-      q.next = wave * 64 * R;
-      q.end = q.next + 64 * R;
-    } else {
-      q.next = min(big * 64 * R + (wave - big) * 64, total);
-      q.end = min(q.next + 64, total);
-    }
-    q.done = 0xffu;  // no grabs beyond the chunk
+    q.vw = blockIdx.x * (kTB / 64) + (threadIdx.x >> 6);
+    q.gw = gridDim.x * (kTB / 64);
+    q.R = refill_rounds(total, waves);
+    q.big = q.R > 1 ? (int)((long long)total * big_pct / 100) / (64 * q.R) : 0;  // waves with big chunks
+    q.chunk();
+    q.done = 0xffu;
   }
   return q;
 }
-__host__ __device__ constexpr int refill_blocks(int items_max) {
-  return PT_REFILL_QUEUE ? (items_max + kTB - 1) / kTB < kRefillBlocks ? (items_max + kTB - 1) / kTB : kRefillBlocks
-                         : (items_max + kTB - 1) / kTB;  // enough 64-item waves for every item (spare waves exit)
+// The static chunks' grid. Until round 6 it had a wave for every 64 items the lists could hold (2 per pixel for the
+// shadow rays: 129 600 blocks at 4K) while the frame's lists hold a fraction of that: every wave past the work read
+// the list counts and left, ~250 000 of them per shadow launch, at the launch's end. Now at most
+// PTSVGF_REFILL_GRID blocks (read once; default 256 CUs x 26 waves x 2 rounds / 2 waves per block; 0 = unbounded),
+// and a wave whose chunk is done takes the chunk of its virtual wave + the grid's waves (WaveQueue::grab): the same
+// chunks, hence the same per-ray walks and results.
+inline int refill_blocks(int items_max) {
+  static const int cap = [] {
+    const char* e = getenv("PTSVGF_REFILL_GRID");
+    return e ? std::max(0, atoi(e)) : kResidentWaves * 2 / (kTB / 64);
+  }();
+  const int need = (items_max + kTB - 1) / kTB;
+  if (PT_REFILL_QUEUE) return need < kRefillBlocks ? need : kRefillBlocks;
+  return cap > 0 && need > cap ? cap : need;
 }
 
 // Traversal counters only (PTParams::wf.stats set): of one frame's shadow rays of a bounce, those toward point lights
