@@ -114,7 +114,7 @@ __device__ __forceinline__ bool seg_get(const int* __restrict__ items, const int
 constexpr int kLists = kLiveBins + 1 + kPointBins;
 __device__ __forceinline__ void block_push_shade(bool p_live, int lbin, bool p_h, bool p_p, int bin, int v,
                                                  int* __restrict__ live, int* live_counts, int* __restrict__ shadow,
-                                                 int* shadow_counts, int cap) {
+                                                 int* shadow_counts, int cap, int chunk) {
   __shared__ int wc[kLists][4];
   __shared__ int base[kLists];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -128,7 +128,7 @@ __device__ __forceinline__ void block_push_shade(bool p_live, int lbin, bool p_h
 #pragma unroll
     for (int l = 0; l < kLists; ++l) wc[l][wv] = __popcll(m[l]);
   __syncthreads();
-  const int seg = blockIdx.x % kSeg;
+  const int seg = chunk % kSeg;  // the chunk's segment (wf_list_capacity: at most 256 items per chunk)
   if (threadIdx.x < kLists) {
     const int l = threadIdx.x;
     const int t = (wc[l][0] + wc[l][1]) + (wc[l][2] + wc[l][3]);
@@ -1192,136 +1192,148 @@ __global__ void __launch_bounds__(256) PT_SHADE_ATTR wf_shade(PTParams p, int bo
                                                 const int* __restrict__ counts_in, int* __restrict__ list_out,
                                                 int* __restrict__ counts_out, int* __restrict__ shadow_out,
                                                 int* __restrict__ shadow_counts, int cap) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  int pid = 0;
-  bool valid;
-  if (bounce == 0) {
-    // one 16 x 16 primary tile per block, in descending order of this frame's primary-ray cost
-    // (tiles.perm_next, sorted right after wf_primary): the rays of expensive tiles are appended to
-    // the lists first, so every later list-driven trace launch starts its slowest rays first
-    const int ntx = (p.W + 15) / 16;
-    const int tile = (p.tiles.cost ? p.tiles.perm_next[blockIdx.x] : (int)blockIdx.x) * p.tile_stride + p.tile_offset;
-    const int x = (tile % ntx) * 16 + (threadIdx.x & 15), ly = (tile / ntx) * 16 + (threadIdx.x >> 4);
-    valid = x < p.W && ly < p.y1 - p.y0;
-    pid = ly * p.W + x;
-  } else {
-    valid = bins_get(list_in, counts_in, kLiveBins, cap, k, &pid);
-  }
-  bool push = false, need_h = false, need_p = false;
-  int pbin = 0;  // point-light list of this ray (light index mod kPointBins)
-  int lbin = 0;  // live list of the continuing ray (direction octant)
-  if (valid) {
-    int x, y;
-    pix_xy(p, pid, &x, &y);
-    int2 hr = ldnt(&p.wf.hit[pid]);
-    v3 S, d;
-    uint32_t seed;
-    v3 light, red;
+  // bounce 0: one tile per block. Later bounces: 256 list items per chunk, a block taking chunks blockIdx.x,
+  // + gridDim.x, ... (a grid a multiple of kSeg: chunk c appends to segment c % kSeg, as one block per chunk did)
+  int total = 0;
+  if (bounce > 0)
+    for (int i = 0; i < kLiveBins * kSeg; ++i) total += counts_in[i];
+  for (int c = blockIdx.x; bounce == 0 || c * 256 < total; c += gridDim.x) {
+    const int k = c * 256 + threadIdx.x;
+    int pid = 0;
+    bool valid;
     if (bounce == 0) {
-      S = mk(p.eye[0], p.eye[1], p.eye[2]);
-      d = primary_dir(p, x, y);
-      seed = ((uint32_t)x * 1973u + (uint32_t)y * 9277u + p.frameCounter * 26699u) | 1u;  // :433-436
-      wang_hash(&seed);  // AA jitter rand() x2 (:1060), never applied
-      wang_hash(&seed);
-      light = splat(0.0f);
-      red = splat(1.0f);
+      // one 16 x 16 primary tile per block, in descending order of this frame's primary-ray cost
+      // (tiles.perm_next, sorted right after wf_primary): the rays of expensive tiles are appended to
+      // the lists first, so every later list-driven trace launch starts its slowest rays first
+      const int ntx = (p.W + 15) / 16;
+      const int tile = (p.tiles.cost ? p.tiles.perm_next[blockIdx.x] : (int)blockIdx.x) * p.tile_stride + p.tile_offset;
+      const int x = (tile % ntx) * 16 + (threadIdx.x & 15), ly = (tile / ntx) * 16 + (threadIdx.x >> 4);
+      valid = x < p.W && ly < p.y1 - p.y0;
+      pid = ly * p.W + x;
     } else {
-      S = xyz(ldnt(&p.wf.ray_o[pid]));
-      d = xyz(ldnt(&p.wf.ray_d[pid]));
-      seed = ldnt(&p.wf.seed[pid]);
-      light = xyz(ldnt(&p.wf.light[pid]));
-      red = xyz(ldnt(&p.wf.red[pid]));
+      valid = bins_get(list_in, counts_in, kLiveBins, cap, k, &pid);
     }
-    if (hr.x < 0) {  // miss (:1084-1087)
-      light = add(light, mul(hdr_color(p, d), red));
+    bool push = false, need_h = false, need_p = false;
+    int pbin = 0;  // point-light list of this ray (light index mod kPointBins)
+    int lbin = 0;  // live list of the continuing ray (direction octant)
+    if (valid) {
+      int x, y;
+      pix_xy(p, pid, &x, &y);
+      int2 hr = ldnt(&p.wf.hit[pid]);
+      v3 S, d;
+      uint32_t seed;
+      v3 light, red;
       if (bounce == 0) {
-        pst(p.emission, x, y, f4(0.0f, 0.0f, 0.0f, 1.0f));
-        pst(p.albedo, x, y, f4(0.0f, 0.0f, 0.0f, 1.0f));
+        S = mk(p.eye[0], p.eye[1], p.eye[2]);
+        d = primary_dir(p, x, y);
+        seed = ((uint32_t)x * 1973u + (uint32_t)y * 9277u + p.frameCounter * 26699u) | 1u;  // :433-436
+        wang_hash(&seed);  // AA jitter rand() x2 (:1060), never applied
+        wang_hash(&seed);
+        light = splat(0.0f);
+        red = splat(1.0f);
+      } else {
+        S = xyz(ldnt(&p.wf.ray_o[pid]));
+        d = xyz(ldnt(&p.wf.ray_d[pid]));
+        seed = ldnt(&p.wf.seed[pid]);
+        light = xyz(ldnt(&p.wf.light[pid]));
+        red = xyz(ldnt(&p.wf.red[pid]));
       }
-    } else {
-      Hit h = decode_hit(p.scene, hr.x, __int_as_float(hr.y), S, d);
-      if (bounce == 0) {
-        pst(p.emission, x, y, f4(h.m.emissive.x, h.m.emissive.y, h.m.emissive.z, 1.0f));
-        pst(p.albedo, x, y, f4(h.m.baseColor.x, h.m.baseColor.y, h.m.baseColor.z, 1.0f));
-      }
-      uint32_t ps = ((uint32_t)x * 1973u + (uint32_t)y * 9277u + (uint32_t)(114514 / 1919) * 26699u) | 1u;
-      float cpu = u32_to_unit(wang_hash(&ps));
-      float cpv = u32_to_unit(wang_hash(&ps));
-      float xi1 = p.sobol_u[bounce] + cpu;
-      if (xi1 > 1.0f) xi1 -= 1.0f;
-      if (xi1 < 0.0f) xi1 += 1.0f;
-      float xi2 = p.sobol_v[bounce] + cpv;
-      if (xi2 > 1.0f) xi2 -= 1.0f;
-      if (xi2 < 0.0f) xi2 += 1.0f;
-      float xi3 = u32_to_unit(wang_hash(&seed));
-      v3 V = neg(h.viewDir);
-      v3 L = sample_brdf(xi1, xi2, xi3, V, h.normal, h.m);
-      if (dot(h.normal, L) > 0.0f) {
-        push = true;
-                v3 brdf = brdf_eval(V, h.normal, L, h.m);
-        float bpdf = brdf_pdf(V, h.normal, L, h.m);
-        // hdriLight, evaluated as if unoccluded (:922-946)
-        float r1 = u32_to_unit(wang_hash(&seed));
-        float r2 = u32_to_unit(wang_hash(&seed));
-        v3 hd = sample_hdr(p, r1, r2);
-        float hpdf;
-        v3 hv = hdr_color_pdf(p, hd, &hpdf);
-        v3 hb = brdf_eval(V, h.normal, hd, h.m);
-        v3 hcalc = divs(mul(muls(hb, f_abs(dot(hd, h.normal))), hv), hpdf);
-        // calculatePointLight, as if unoccluded (:884-919)
-        v3 pcalc = splat(0.0f);
-        float4 shp = f4(0.0f, 0.0f, 0.0f, -1.0f);
-        if (p.pointLightSize != 0) {
-          float ppdf = (2.0f * PT_PI) / (float)p.pointLightSize;
-          int li = (int)(u32_to_unit(wang_hash(&seed)) * (float)p.pointLightSize);
-          pbin = li & (kPointBins - 1);
-          v3 lpos = splat(0.0f), lrad = splat(0.0f);
-          if (li >= 0 && li < p.scene.nlights_buf) {
-            const float* lp = p.scene.lights + 6 * li;
-            lpos = mk(lp[0], lp[1], lp[2]);
-            lrad = mk(lp[3], lp[4], lp[5]);
-          }
-          v3 ld = normalize(sub(lpos, h.P));
-          float dist = length(sub(lpos, h.P));
-          v3 plv = divs(lrad, dist * dist);
-          v3 pb = brdf_eval(V, h.normal, ld, h.m);
-          pcalc = divs(muls(mul(plv, pb), f_abs(dot(ld, h.normal))), ppdf);
-          shp = f4(ld.x, ld.y, ld.z, dist);
+      if (hr.x < 0) {  // miss (:1084-1087)
+        light = add(light, mul(hdr_color(p, d), red));
+        if (bounce == 0) {
+          pst(p.emission, x, y, f4(0.0f, 0.0f, 0.0f, 1.0f));
+          pst(p.albedo, x, y, f4(0.0f, 0.0f, 0.0f, 1.0f));
         }
-        v3 cosb = muls(brdf, f_abs(dot(L, h.normal)));
-        v3 bcalc = divs(mul(h.m.emissive, cosb), bpdf);
-        // A verdict only zeroes terms: with the point value exactly +0 (light below the
-        // surface: zero BRDF) its ray cannot change a bit; the HDR verdict also moves the
-        // MIS weights, so it is dropped only when every term is +0 and every pdf finite.
-        const bool pz = zero_bits(pcalc);
-        need_p = shp.w >= 0.0f && !pz;
-        need_h = !(pz && zero_bits(hcalc) && zero_bits(bcalc) && __builtin_isfinite(hpdf) && __builtin_isfinite(bpdf));
-        stnt(&p.wf.pend0[pid], f4(hcalc.x, hcalc.y, hcalc.z, hpdf));
-        stnt(&p.wf.pend1[pid], f4(pcalc.x, pcalc.y, pcalc.z, bpdf));
-        stnt(&p.wf.pend2[pid], f4(bcalc.x, bcalc.y, bcalc.z, 0.0f));
-        stnt(&p.wf.pend3[pid], f4(cosb.x, cosb.y, cosb.z, 0.0f));
-        stnt(&p.wf.sh_h[pid], f4(hd.x, hd.y, hd.z, 0.0f));
-        stnt(&p.wf.sh_p[pid], shp);
-        stnt(&p.wf.ray_o[pid], f4(h.P.x, h.P.y, h.P.z, 0.0f));
-        stnt(&p.wf.ray_d[pid], f4(L.x, L.y, L.z, 0.0f));
-        stnt(&p.wf.red[pid], f4(red.x, red.y, red.z, 0.0f));
-        stnt(&p.wf.occ_h[pid], (uint8_t)0);
-        stnt(&p.wf.occ_p[pid], (uint8_t)0);
+      } else {
+        Hit h = decode_hit(p.scene, hr.x, __int_as_float(hr.y), S, d);
+        if (bounce == 0) {
+          pst(p.emission, x, y, f4(h.m.emissive.x, h.m.emissive.y, h.m.emissive.z, 1.0f));
+          pst(p.albedo, x, y, f4(h.m.baseColor.x, h.m.baseColor.y, h.m.baseColor.z, 1.0f));
+        }
+        uint32_t ps = ((uint32_t)x * 1973u + (uint32_t)y * 9277u + (uint32_t)(114514 / 1919) * 26699u) | 1u;
+        float cpu = u32_to_unit(wang_hash(&ps));
+        float cpv = u32_to_unit(wang_hash(&ps));
+        float xi1 = p.sobol_u[bounce] + cpu;
+        if (xi1 > 1.0f) xi1 -= 1.0f;
+        if (xi1 < 0.0f) xi1 += 1.0f;
+        float xi2 = p.sobol_v[bounce] + cpv;
+        if (xi2 > 1.0f) xi2 -= 1.0f;
+        if (xi2 < 0.0f) xi2 += 1.0f;
+        float xi3 = u32_to_unit(wang_hash(&seed));
+        v3 V = neg(h.viewDir);
+        v3 L = sample_brdf(xi1, xi2, xi3, V, h.normal, h.m);
+        if (dot(h.normal, L) > 0.0f) {
+          push = true;
+                  v3 brdf = brdf_eval(V, h.normal, L, h.m);
+          float bpdf = brdf_pdf(V, h.normal, L, h.m);
+          // hdriLight, evaluated as if unoccluded (:922-946)
+          float r1 = u32_to_unit(wang_hash(&seed));
+          float r2 = u32_to_unit(wang_hash(&seed));
+          v3 hd = sample_hdr(p, r1, r2);
+          float hpdf;
+          v3 hv = hdr_color_pdf(p, hd, &hpdf);
+          v3 hb = brdf_eval(V, h.normal, hd, h.m);
+          v3 hcalc = divs(mul(muls(hb, f_abs(dot(hd, h.normal))), hv), hpdf);
+          // calculatePointLight, as if unoccluded (:884-919)
+          v3 pcalc = splat(0.0f);
+          float4 shp = f4(0.0f, 0.0f, 0.0f, -1.0f);
+          if (p.pointLightSize != 0) {
+            float ppdf = (2.0f * PT_PI) / (float)p.pointLightSize;
+            int li = (int)(u32_to_unit(wang_hash(&seed)) * (float)p.pointLightSize);
+            pbin = li & (kPointBins - 1);
+            v3 lpos = splat(0.0f), lrad = splat(0.0f);
+            if (li >= 0 && li < p.scene.nlights_buf) {
+              const float* lp = p.scene.lights + 6 * li;
+              lpos = mk(lp[0], lp[1], lp[2]);
+              lrad = mk(lp[3], lp[4], lp[5]);
+            }
+            v3 ld = normalize(sub(lpos, h.P));
+            float dist = length(sub(lpos, h.P));
+            v3 plv = divs(lrad, dist * dist);
+            v3 pb = brdf_eval(V, h.normal, ld, h.m);
+            pcalc = divs(muls(mul(plv, pb), f_abs(dot(ld, h.normal))), ppdf);
+            shp = f4(ld.x, ld.y, ld.z, dist);
+          }
+          v3 cosb = muls(brdf, f_abs(dot(L, h.normal)));
+          v3 bcalc = divs(mul(h.m.emissive, cosb), bpdf);
+          // A verdict only zeroes terms: with the point value exactly +0 (light below the
+          // surface: zero BRDF) its ray cannot change a bit; the HDR verdict also moves the
+          // MIS weights, so it is dropped only when every term is +0 and every pdf finite.
+          const bool pz = zero_bits(pcalc);
+          need_p = shp.w >= 0.0f && !pz;
+          need_h = !(pz && zero_bits(hcalc) && zero_bits(bcalc) && __builtin_isfinite(hpdf) && __builtin_isfinite(bpdf));
+          stnt(&p.wf.pend0[pid], f4(hcalc.x, hcalc.y, hcalc.z, hpdf));
+          stnt(&p.wf.pend1[pid], f4(pcalc.x, pcalc.y, pcalc.z, bpdf));
+          stnt(&p.wf.pend2[pid], f4(bcalc.x, bcalc.y, bcalc.z, 0.0f));
+          stnt(&p.wf.pend3[pid], f4(cosb.x, cosb.y, cosb.z, 0.0f));
+          stnt(&p.wf.sh_h[pid], f4(hd.x, hd.y, hd.z, 0.0f));
+          stnt(&p.wf.sh_p[pid], shp);
+          stnt(&p.wf.ray_o[pid], f4(h.P.x, h.P.y, h.P.z, 0.0f));
+          stnt(&p.wf.ray_d[pid], f4(L.x, L.y, L.z, 0.0f));
+          stnt(&p.wf.red[pid], f4(red.x, red.y, red.z, 0.0f));
+          stnt(&p.wf.occ_h[pid], (uint8_t)0);
+          stnt(&p.wf.occ_p[pid], (uint8_t)0);
+        }
       }
+      stnt(&p.wf.seed[pid], seed);
+      stnt(&p.wf.light[pid], f4(light.x, light.y, light.z, 0.0f));
     }
-    stnt(&p.wf.seed[pid], seed);
-    stnt(&p.wf.light[pid], f4(light.x, light.y, light.z, 0.0f));
+    // HDR and point-light shadow rays go to separate lists so trace waves stay homogeneous
+
+    block_push_shade(push, lbin, need_h, need_p, pbin, pid, list_out, counts_out, shadow_out, shadow_counts, cap, c);
+    if (bounce == 0) break;
+    __syncthreads();  // the next chunk's push reuses block_push_shade's shared counters
   }
-  // HDR and point-light shadow rays go to separate lists so trace waves stay homogeneous
-  block_push_shade(push, lbin, need_h, need_p, pbin, pid, list_out, counts_out, shadow_out, shadow_counts, cap);
 }
 
 // ----------------------------------------------------------------- finish ---
 __global__ void __launch_bounds__(256) wf_finish(PTParams p, const int* __restrict__ list,
                                                  const int* __restrict__ counts, int cap) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
+  int total = 0;
+  for (int i = 0; i < kLiveBins * kSeg; ++i) total += counts[i];
+  for (int k = blockIdx.x * 256 + threadIdx.x; k < total; k += gridDim.x * 256) {
   int pid;
-  if (!bins_get(list, counts, kLiveBins, cap, k, &pid)) return;
+  if (!bins_get(list, counts, kLiveBins, cap, k, &pid)) continue;
   float4 q0 = ldnt(&p.wf.pend0[pid]), q1 = ldnt(&p.wf.pend1[pid]), q2 = ldnt(&p.wf.pend2[pid]), q3 = ldnt(&p.wf.pend3[pid]);
   NeeTerms nt;
   nt.hcalc = xyz(q0); nt.pcalc = xyz(q1); nt.bcalc = xyz(q2);
@@ -1334,6 +1346,7 @@ __global__ void __launch_bounds__(256) wf_finish(PTParams p, const int* __restri
   light = add(light, hitLight);
   stnt(&p.wf.red[pid], f4(red.x, red.y, red.z, 0.0f));
   stnt(&p.wf.light[pid], f4(light.x, light.y, light.z, 0.0f));
+  }
 }
 
 // --------------------------------------------------------------- finalize ---
@@ -1378,6 +1391,18 @@ int wf_subset_tiles(int W, int rows, int stride, int offset) {
 // launch per bounce for the list-driven traversals of every frame's rays (lane-refill kernels; the one-ray-per-lane
 // kernels run per frame). Frame b's wavefront state lies at pid offset b * N of ps[0]'s, its counters at
 // ps[0].wf.counters + b * kWfCounters; the batched launches use frame 0's work-queue heads and straggler lists.
+// Grid of the list-driven shade (bounces > 0) and finish launches: until round 6 one block per 256 pixels (32 400 at
+// 4K), most of them past the list's end, reading its counts and leaving. Now at most PTSVGF_LIST_BLOCKS (read once;
+// default 2 048, a multiple of kSeg; 0 = one per 256 pixels) striding over 256-item chunks.
+static int list_blocks(int n_items_max) {
+  static const int cap = [] {
+    const char* e = getenv("PTSVGF_LIST_BLOCKS");
+    const int v = e ? std::max(0, atoi(e)) : 2048;
+    return (v + kSeg - 1) / kSeg * kSeg;
+  }();
+  const int need = (n_items_max + 255) / 256;
+  return cap > 0 && need > cap ? cap : need;
+}
 // wf_primary's fix-up grid after wf_primary_raster with closest_tree on (PTSVGF_PRIMARY_FIX_BLOCKS, read once; 0 = one
 // block per tile, as until round 6)
 static int primary_fix_blocks() {
@@ -1423,6 +1448,7 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, const WfFork* fk
     }
   }
   const int gN = (N + 255) / 256, gT = (N + kTB - 1) / kTB, gT2 = (2 * N + kTB - 1) / kTB;
+  const int gL = list_blocks(N);  // list-driven shade / finish: at most list_blocks() blocks striding
   const int gS0 = ntiles;  // bounce-0 shade: one block per primary tile
   auto lst = [&](const PTParams& f, int i) { return (i & 1) ? f.wf.list1 : f.wf.list0; };  // bounce i's live list
   const bool refill_closest = p.refill && p.closest_tree && p.prune && p.scene.bvh_any;
@@ -1463,7 +1489,7 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, const WfFork* fk
     for (int b = 0; b < nb; ++b) {
       const PTParams& f = ps[b];
       const int* live_in = f.wf.counters + kWfCtr * (i > 0 ? i - 1 : 0);
-      hipLaunchKernelGGL(wf_shade, dim3(i == 0 ? gS0 : gN), dim3(256), 0, s, f, i, (const int*)lst(f, i + 1), live_in,
+      hipLaunchKernelGGL(wf_shade, dim3(i == 0 ? gS0 : gL), dim3(256), 0, s, f, i, (const int*)lst(f, i + 1), live_in,
                          lst(f, i), f.wf.counters + kWfCtr * i, f.wf.shadow_list, f.wf.counters + kWfCtr * i + kCtrHdr,
                          cap);
     }
@@ -1511,7 +1537,7 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, const WfFork* fk
         hipLaunchKernelGGL(wf_shadow_stats, dim3(gN), dim3(256), 0, ss, ps[b], (const int*)ps[b].wf.shadow_list,
                            (const int*)(ps[b].wf.counters + kWfCtr * i + kCtrHdr), cap);
     for (int b = 0; b < nb; ++b)
-      hipLaunchKernelGGL(wf_finish, dim3(gN), dim3(256), 0, ss, ps[b], (const int*)lst(ps[b], i),
+      hipLaunchKernelGGL(wf_finish, dim3(gL), dim3(256), 0, ss, ps[b], (const int*)lst(ps[b], i),
                          (const int*)(ps[b].wf.counters + kWfCtr * i), cap);
     if (i == 0 && split) {
       const hipError_t e = hipEventRecord(fk->join, ss);
