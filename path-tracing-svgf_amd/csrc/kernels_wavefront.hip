@@ -223,9 +223,7 @@ __device__ __forceinline__ v3 primary_dir(const PTParams& p, int x, int y) {
 constexpr int kTieFix = -2;  // hit.x of a pixel wf_primary_raster leaves to the walk (two triangles share its t)
 
 // 16x16 screen tiles, each wave an 8x8 sub-tile: coherent camera rays.
-// nslots: the subset's tiles; a block walks slots blockIdx.x, + gridDim.x, ... (the full launch: one slot per block;
-// the fix-up launch after wf_primary_raster, whose work is almost always none, a few hundred blocks: a grid of one
-// block per tile, each reading one flag and leaving, held its stream for 0.1-0.6 ms of a frame at 4K)
+// nslots: the subset's tiles; a block walks slots blockIdx.x, + gridDim.x, ... (launched with one slot per block)
 template <int KS, bool DEEP>
 __global__ void __launch_bounds__(256) PT_TRACE_ATTR wf_primary(PTParams p, int nslots) {
   __shared__ int stk[KS * 256];
@@ -1134,9 +1132,37 @@ __global__ void __launch_bounds__(64 * kCoopWaves) wf_closest_coop(PTParams p, c
 
 // The primary rays wf_primary_raster flagged (an exact-t tie, or no hit below the G-buffer bound): one wave per ray
 // (closest_coop_walk: closest_hit's answer, unbounded, ties walked on the reference tree).
+// After a pair-list overflow (leaf_bins.ctr[2]: the rasteriser skipped the frame) every pixel of the subset's tiles is
+// walked here the same way, and the tile counts the skipped scatter left are cleared; until round 6 a wf_primary
+// launch of one block per tile did that, and every frame paid for its launch.
 __global__ void __launch_bounds__(64 * kCoopWaves) wf_primary_coop(PTParams p, const int* __restrict__ strag_count) {
   __shared__ int st[kCoopWaves][kCoopCap];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (p.leaf_bins.ctr && p.leaf_bins.ctr[2]) {
+    const int ntx = (p.W + 15) / 16, all = ntx * ((p.y1 - p.y0 + 15) / 16);
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < all; j += gridDim.x * blockDim.x)
+      p.leaf_bins.tile_count[j] = 0;
+    const int nsub = all / p.tile_stride + (all % p.tile_stride > p.tile_offset ? 1 : 0);  // the subset's tiles
+    uint32_t nrays = 0, nrewalk = 0;
+    for (int r = blockIdx.x * kCoopWaves + wv; r < nsub * 256; r += gridDim.x * kCoopWaves) {
+      const int gt = (r >> 8) * p.tile_stride + p.tile_offset, i = r & 255;
+      const int x = (gt % ntx) * 16 + (i & 15), y = p.y0 + (gt / ntx) * 16 + (i >> 4);
+      if (x >= p.W || y >= p.y1) continue;  // wave-uniform
+      const int pid = (y - p.y0) * p.W + x;
+      float t;
+      bool rw;
+      const int tri = closest_coop_walk(p.scene, st[wv], kCoopCap, mk(p.eye[0], p.eye[1], p.eye[2]),
+                                        primary_dir(p, x, y), &t, &rw);
+      if ((threadIdx.x & 63) == 0) {
+        stnt(&p.wf.hit[pid], make_int2(tri, __float_as_int(t)));
+        nrewalk += rw ? 1u : 0u;
+        ++nrays;
+      }
+    }
+    stat_add(p, kStatPrimRays, nrays);
+    stat_add(p, kStatTieRewalks, nrewalk);
+    return;
+  }
   const int n = *strag_count;
   uint32_t nrewalk = 0, nretry = 0;
   for (int r = blockIdx.x * kCoopWaves + wv; r < n; r += gridDim.x * kCoopWaves) {
@@ -1403,15 +1429,6 @@ static int list_blocks(int n_items_max) {
   const int need = (n_items_max + 255) / 256;
   return cap > 0 && need > cap ? cap : need;
 }
-// wf_primary's fix-up grid after wf_primary_raster with closest_tree on (PTSVGF_PRIMARY_FIX_BLOCKS, read once; 0 = one
-// block per tile, as until round 6)
-static int primary_fix_blocks() {
-  static const int n = [] {
-    const char* e = getenv("PTSVGF_PRIMARY_FIX_BLOCKS");
-    return e ? std::max(0, atoi(e)) : 512;
-  }();
-  return n;
-}
 template <int KS, bool DEEP>
 int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, const WfFork* fk) {
   const PTParams& p = ps[0];
@@ -1433,12 +1450,16 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, const WfFork* fk
       if (f.closest_tree)
         hipLaunchKernelGGL(wf_primary_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, s, f,
                            (const int*)(f.wf.counters + kCtrStragC));
-      PTParams q = f;
-      q.pr_fix = f.leaf_bins.ctr;  // ties (and an overflow) walked
-      // with closest_tree the flagged pixels went to wf_primary_coop: this launch has work only after a list
-      // overflow, so a few blocks striding over the tiles
-      const int gfix = f.closest_tree && primary_fix_blocks() > 0 ? std::min(ntiles, primary_fix_blocks()) : ntiles;
-      hipLaunchKernelGGL((wf_primary<KS, DEEP>), dim3(gfix), dim3(256), 0, s, q, ntiles);
+      static const bool fix_launch = [] {  // A/B only: PTSVGF_PRIMARY_FIX_LAUNCH=1 launches it anyway (512 blocks)
+        const char* e = getenv("PTSVGF_PRIMARY_FIX_LAUNCH");
+        return e && atoi(e) != 0;
+      }();
+      if (!f.closest_tree || fix_launch) {  // the flagged pixels (and, after an overflow, all) by the per-pixel walk
+        PTParams q = f;
+        q.pr_fix = f.leaf_bins.ctr;
+        hipLaunchKernelGGL((wf_primary<KS, DEEP>), dim3(f.closest_tree ? std::min(ntiles, 512) : ntiles), dim3(256), 0,
+                           s, q, ntiles);
+      }
     } else {
       hipLaunchKernelGGL((wf_primary<KS, DEEP>), dim3(ntiles), dim3(256), 0, s, f, ntiles);
     }
