@@ -137,10 +137,16 @@ __device__ __forceinline__ void block_push_shade(bool p_live, int lbin, bool p_h
   }
   __syncthreads();
   const unsigned long long lt = (1ull << lane) - 1ull;
+  // this lane's masks by constant indices and selects: a per-lane index into m[] put it in scratch (or LDS) memory
+  unsigned long long mlive = m[0], mpoint = m[kLiveBins + 1];
+#pragma unroll
+  for (int j = 1; j < kLiveBins; ++j) mlive = lbin == j ? m[j] : mlive;
+#pragma unroll
+  for (int j = 1; j < kPointBins; ++j) mpoint = bin == j ? m[kLiveBins + 1 + j] : mpoint;
   if (p_live) {
     int o = base[lbin];
     for (int w = 0; w < wv; ++w) o += wc[lbin][w];
-    live[((size_t)lbin * kSeg + seg) * cap + o + __popcll(m[lbin] & lt)] = v;
+    live[((size_t)lbin * kSeg + seg) * cap + o + __popcll(mlive & lt)] = v;
   }
   if (p_h) {
     int o = base[kLiveBins];
@@ -151,7 +157,7 @@ __device__ __forceinline__ void block_push_shade(bool p_live, int lbin, bool p_h
     const int li = kLiveBins + 1 + bin;
     int o = base[li];
     for (int w = 0; w < wv; ++w) o += wc[li][w];
-    shadow[(size_t)(1 + bin) * kSeg * cap + seg * cap + o + __popcll(m[li] & lt)] = v;
+    shadow[(size_t)(1 + bin) * kSeg * cap + seg * cap + o + __popcll(mpoint & lt)] = v;
   }
 }
 
