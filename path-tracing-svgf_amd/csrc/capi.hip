@@ -912,6 +912,19 @@ static int pack_wide(const std::vector<SahNode>& nodes, const std::function<int(
     return PT_OK;
   }
   std::unique_ptr<WideCollapse> wc(dp ? new WideCollapse(nodes) : nullptr);
+  static const int order_key = [] {
+    const char* e = getenv("PTSVGF_WIDE_ORDER_KEY");
+    return e ? atoi(e) : 0;
+  }();
+  std::vector<double> tris_below(nodes.size(), 0.0);  // triangles in each subtree (order_key 1 / 2)
+  if (order_key) {
+    std::vector<int> po;
+    post_order(nodes, 0, po);
+    for (int id : po) {
+      const SahNode& x = nodes[id];
+      tris_below[id] = x.n > 0 ? (double)ref_count_of(ref_of(x)) : tris_below[x.left] + tris_below[x.right];
+    }
+  }
   double area_sum = 0.0;  // summed surface area of the 4-wide nodes (PTSVGF_WIDE_STATS)
   std::function<int(int, int)> build = [&](int id, int acc) -> int {
     int ch[4] = {nodes[id].left, nodes[id].right, -1, -1};
@@ -938,8 +951,12 @@ static int pack_wide(const std::vector<SahNode>& nodes, const std::function<int(
     // second cache line of this node's fetch holds most of it. Put the child a ray most likely enters there (largest
     // surface area). Slots only order ties between equally near children; the candidates, hence every result, are
     // the same.
+    // PTSVGF_WIDE_ORDER_KEY (read once; A/B): 0 = area (default), 1 = triangles below, 2 = area x triangles below
     std::stable_sort(ch, ch + nc, [&](int x, int y) {
-      return sah_area(nodes[x].lo, nodes[x].hi) > sah_area(nodes[y].lo, nodes[y].hi);
+      const double ax = sah_area(nodes[x].lo, nodes[x].hi), ay = sah_area(nodes[y].lo, nodes[y].hi);
+      if (order_key == 1) return tris_below[x] > tris_below[y];
+      if (order_key == 2) return ax * tris_below[x] > ay * tris_below[y];
+      return ax > ay;
     });
 #endif
     const int k = (int)(out.size() / ptk::kWideStride);
