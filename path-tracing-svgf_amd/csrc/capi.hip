@@ -1781,6 +1781,8 @@ int pt_wf_setup(Pass* p, PTParams& k, SceneGPU* sg, const WFState& st) {
     // sets it then), 0 (default) keeps the shortest single-frame latency
     k.refill = std::min(100, std::max(0, ui(p, "trace_refill", 0)));
     k.refill_waves = std::max(0, ui(p, "refill_waves", 0));
+    k.refill_grid = std::max(0, ui(p, "refill_grid", 0));
+    k.list_grid = std::max(0, ui(p, "list_grid", 0));
     const int ntiles = wf_subset_tiles(k.W, std::max(0, k.y1 - k.y0), k.tile_stride, k.tile_offset);  // wf_primary's grid
     TRY(tile_order_begin(p, ntiles, &k.tiles));
     // primary rays by tile-binned rasterisation of the reference leaves (default; 0 = the per-pixel walk); the leaves
@@ -1878,7 +1880,7 @@ int draw_pathtrace_batch(Pass** ps, int n) {
     // compared at its effective value (the default pt_params / pt_wf_setup apply when a pass never set it)
     struct Same { const char* name; int dflt; };
     const Same same[] = {{"trace_refill", 0}, {"shadow_budget", 0}, {"closest_budget", 0}, {"wide_bvh", 1},
-                         {"refill_waves", 0}, {"trace_fork", 0}};
+                         {"refill_waves", 0}, {"trace_fork", 0}, {"refill_grid", 0}, {"list_grid", 0}};
     bool agree = true;
     for (const Same& u : same) agree = agree && ui(ps[b], u.name, u.dflt) == ui(ps[0], u.name, u.dflt);
     if (sb != sg || k[b].W != k[0].W || k[b].y0 != k[0].y0 || k[b].y1 != k[0].y1 || k[b].max_depth != k[0].max_depth ||

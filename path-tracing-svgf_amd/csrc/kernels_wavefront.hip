@@ -749,14 +749,15 @@ __device__ __forceinline__ WaveQueue refill_queue(int* heads, int total, int big
 // PTSVGF_REFILL_GRID blocks (read once; default 256 CUs x 26 waves x 2 rounds / 2 waves per block; 0 = unbounded),
 // and a wave whose chunk is done takes the chunk of its virtual wave + the grid's waves (WaveQueue::grab): the same
 // chunks, hence the same per-ray walks and results.
-inline int refill_blocks(int items_max) {
+inline int refill_blocks(int items_max, int grid = 0) {
   static const int cap = [] {
     const char* e = getenv("PTSVGF_REFILL_GRID");
     return e ? std::max(0, atoi(e)) : kResidentWaves * 2 / (kTB / 64);
   }();
   const int need = (items_max + kTB - 1) / kTB;
   if (PT_REFILL_QUEUE) return need < kRefillBlocks ? need : kRefillBlocks;
-  return cap > 0 && need > cap ? cap : need;
+  const int c = grid > 0 ? grid : cap;
+  return c > 0 && need > c ? c : need;
 }
 
 // Traversal counters only (PTParams::wf.stats set): of one frame's shadow rays of a bounce, those toward point lights
@@ -1426,14 +1427,15 @@ int wf_subset_tiles(int W, int rows, int stride, int offset) {
 // Grid of the list-driven shade (bounces > 0) and finish launches: until round 6 one block per 256 pixels (32 400 at
 // 4K), most of them past the list's end, reading its counts and leaving. Now at most PTSVGF_LIST_BLOCKS (read once;
 // default 2 048, a multiple of kSeg; 0 = one per 256 pixels) striding over 256-item chunks.
-static int list_blocks(int n_items_max) {
+static int list_blocks(int n_items_max, int grid = 0) {
   static const int cap = [] {
     const char* e = getenv("PTSVGF_LIST_BLOCKS");
     const int v = e ? std::max(0, atoi(e)) : 2048;
     return (v + kSeg - 1) / kSeg * kSeg;
   }();
   const int need = (n_items_max + 255) / 256;
-  return cap > 0 && need > cap ? cap : need;
+  const int c = grid > 0 ? (grid + kSeg - 1) / kSeg * kSeg : cap;
+  return c > 0 && need > c ? c : need;
 }
 template <int KS, bool DEEP>
 int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, const WfFork* fk) {
@@ -1475,7 +1477,7 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, const WfFork* fk
     }
   }
   const int gN = (N + 255) / 256, gT = (N + kTB - 1) / kTB, gT2 = (2 * N + kTB - 1) / kTB;
-  const int gL = list_blocks(N);  // list-driven shade / finish: at most list_blocks() blocks striding
+  const int gL = list_blocks(N, p.list_grid);  // list-driven shade / finish: at most list_blocks() blocks striding
   const int gS0 = ntiles;  // bounce-0 shade: one block per primary tile
   auto lst = [&](const PTParams& f, int i) { return (i & 1) ? f.wf.list1 : f.wf.list0; };  // bounce i's live list
   const bool refill_closest = p.refill && p.closest_tree && p.prune && p.scene.bvh_any;
@@ -1491,11 +1493,11 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, const WfFork* fk
       int* strag = p.wf.counters + kWfCtr * i + kCtrStragC;
       if constexpr (!DEEP)
         if (wide) {
-          hipLaunchKernelGGL((wf_trace_closest_refill<kWideKS, false, true>), dim3(refill_blocks(nb * N)), dim3(kTB), 0, st,
+          hipLaunchKernelGGL((wf_trace_closest_refill<kWideKS, false, true>), dim3(refill_blocks(nb * N, p.refill_grid)), dim3(kTB), 0, st,
                              p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQClosest, strag);
         }
       if (!wide)
-        hipLaunchKernelGGL((wf_trace_closest_refill<KS, DEEP, false>), dim3(refill_blocks(nb * N)), dim3(kTB), 0, st,
+        hipLaunchKernelGGL((wf_trace_closest_refill<KS, DEEP, false>), dim3(refill_blocks(nb * N, p.refill_grid)), dim3(kTB), 0, st,
                            p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQClosest, strag);
       if (p.wf.closest_budget || wide)  // (4-wide: ties and stack overflows go there too)
         hipLaunchKernelGGL(wf_closest_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, st, p, (const int*)strag);
@@ -1536,11 +1538,11 @@ int launch_wavefront(const PTParams* ps, int nb, hipStream_t s, const WfFork* fk
       int* strag = p.wf.counters + kWfCtr * i + kCtrStrag;  // shadow rays handed to the cooperative walk
       if constexpr (!DEEP)
         if (wide) {
-          hipLaunchKernelGGL((wf_trace_shadow_refill<kWideKS, false, true>), dim3(refill_blocks(2 * nb * N)), dim3(kTB), 0,
+          hipLaunchKernelGGL((wf_trace_shadow_refill<kWideKS, false, true>), dim3(refill_blocks(2 * nb * N, p.refill_grid)), dim3(kTB), 0,
                              ss, p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQShadow, strag);
         }
       if (!wide)
-        hipLaunchKernelGGL((wf_trace_shadow_refill<KS, DEEP, false>), dim3(refill_blocks(2 * nb * N)), dim3(kTB), 0, ss,
+        hipLaunchKernelGGL((wf_trace_shadow_refill<KS, DEEP, false>), dim3(refill_blocks(2 * nb * N, p.refill_grid)), dim3(kTB), 0, ss,
                            p, lb, cap, p.wf.counters + kWfCtr * i + kCtrQShadow, strag);
       if (p.wf.shadow_budget || wide)
         hipLaunchKernelGGL(wf_shadow_coop, dim3(kCoopBlocks), dim3(64 * kCoopWaves), 0, ss, p, (const int*)strag);

@@ -221,6 +221,8 @@ struct PTParams {
   int stack_need;       // deepest interior level of the binary BVH (selects the LDS stack size)
   int refill;           // > 0: percent of each bounce/shadow list traced by lane-refill waves (kernels_wavefront.hip)
   int refill_waves;     // resident waves a refill launch is sized for (0: the whole chip, kResidentWaves)
+  int refill_grid;      // most blocks of a refill launch (uniform refill_grid; 0: PTSVGF_REFILL_GRID / its default)
+  int list_grid;        // most blocks of the list-driven shade / finish (uniform list_grid; 0: PTSVGF_LIST_BLOCKS)
   float sobol_u[4], sobol_v[4];  // sobolVec2(frameCounter+1, b): uniform across pixels
   WFState wf;
   // optional bound for the primary rays from this frame's G-buffer (world position + normal/linearZ planes,

@@ -828,3 +828,29 @@ def test_priority_stream_same_bits(gpu, scene_small):
             check(pt().pt_stream_destroy(h))
     for k in outs[0]:
         assert np.array_equal(outs[0][k], outs[1][k]), k
+
+
+@pytest.mark.parametrize("scene_name", ["scene_small", "scene_cornell"])
+def test_strided_launch_grids_are_result_preserving(gpu, scene_name, request):
+    """The refill traversal launches with a grid far below their waves (uniform refill_grid = 3 blocks: every wave
+    walks many static chunks in turn, WaveQueue::grab) and the list-driven shade / finish with 8 blocks striding over
+    256-item chunks (uniform list_grid) give the default grids' bits, through a camera move and frames in flight."""
+    gl = gpu
+    scene = request.getfixturevalue(scene_name)
+    W, H = 96, 64
+    outs = []
+    for grid in (0, 3):
+        r = _renderer(scene, W, H, mode="fast", run_taa=False, run_output=False, frames_in_flight=2)
+        r.pass_path_tracing.set_uniform_int("refill_grid", grid)
+        r.pass_path_tracing.set_uniform_int("list_grid", 8 if grid else 0)
+        frames = []
+        for f in range(4):
+            if f == 2:
+                r.camera.orbit(2.0, 1.0)
+            r.frame()
+            frames.append({k: gl.readback(r.planes()[k]) for k in ("color", "emission", "albedo", "modulate")})
+        outs.append(frames)
+        r.close()
+    for a, b in zip(*outs):
+        for k in a:
+            assert np.array_equal(a[k].view(np.uint32), b[k].view(np.uint32)), k
